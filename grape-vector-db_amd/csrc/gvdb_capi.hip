@@ -1,0 +1,1201 @@
+// gvdb_capi.hip — the C ABI (include/gvdb.h) over the gfx950 kernels.
+//
+// Owns: the index object (HBM-resident rows / codes / norms / ids for one
+// shard), the per-call workspace pool (reentrant searches), the BQ search
+// orchestration (stage 1 fast path + exact slow path, stage 2, final sort)
+// and the error contract (thread-local last error, VectorDbError codes).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gvdb.h"
+#include "gvdb_internal.h"
+
+using namespace gvdb;
+
+// ============================================================================
+// errors
+// ============================================================================
+namespace {
+thread_local std::string t_err = "";
+thread_local uint64_t t_dim_expected = 0, t_dim_actual = 0;
+
+gvdb_status fail(gvdb_status s, const std::string& msg) {
+    t_err = msg;
+    return s;
+}
+gvdb_status dev_fail(hipError_t e, const char* where) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+        return fail(GVDB_ERR_OUT_OF_MEMORY, std::string(where) + ": " + hipGetErrorString(e));
+    return fail(GVDB_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
+}
+gvdb_status dim_mismatch(uint64_t expected, uint64_t actual) {
+    t_dim_expected = expected;
+    t_dim_actual = actual;
+    char b[128];
+    snprintf(b, sizeof b, "Dimension mismatch: expected %llu, actual %llu", (unsigned long long)expected,
+             (unsigned long long)actual);
+    return fail(GVDB_ERR_DIMENSION_MISMATCH, b);
+}
+
+#define HIP_TRY(expr, where)                          \
+    do {                                              \
+        hipError_t e_ = (expr);                       \
+        if (e_ != hipSuccess) return dev_fail(e_, where); \
+    } while (0)
+
+// Rust `f32 as usize` (saturating; NaN -> 0).
+uint64_t rust_f32_as_usize(float v) {
+    if (!(v == v) || v <= 0.0f) return 0;
+    if (v >= 18446744073709551615.0f) return UINT64_MAX;
+    return (uint64_t)v;
+}
+
+// ============================================================================
+// Kernel timing (HIP events around the launches, read after the batch's
+// stream sync; enabled by gvdb_timing_enable, used by bench.py)
+// ============================================================================
+enum { kTimSampleHist = 0, kTimScan = 1, kTimSelect = 2, kTimRerank = 3, kTimFinal = 4, kTimN = 5 };
+struct Timing {
+    std::mutex mu;
+    bool on = false;
+    double ms[kTimN] = {0};
+    uint64_t n[kTimN] = {0};
+};
+Timing& timing() {
+    static Timing t;
+    return t;
+}
+struct EvSet {
+    hipEvent_t e[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool ok = false;
+    void create() {
+        ok = true;
+        for (auto& x : e)
+            if (hipEventCreate(&x) != hipSuccess) ok = false;
+    }
+    ~EvSet() {
+        for (auto& x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+};
+
+// ============================================================================
+// device buffers
+// ============================================================================
+struct DBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) n = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    template <class T>
+    T* as() const {
+        return (T*)p;
+    }
+};
+
+struct Workspace {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DBuf q, qnorm, qcodes, hist, thr, counts, buf, fail, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow,
+        sort_tmp, flags, rows, norms, codes, misc;
+    uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
+    EvSet ev;                     // timing events (created on first timed call)
+    ~Workspace() {
+        for (DBuf* b : {&q, &qnorm, &qcodes, &hist, &thr, &counts, &buf, &fail, &s1_rows, &s1_dist, &scores, &out_ids,
+                        &out_scores, &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc})
+            b->release();
+        if (h_flags) (void)hipHostFree(h_flags);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+struct WsPool {
+    std::mutex mu;
+    std::vector<std::unique_ptr<Workspace>> free;
+    Workspace* acquire(int device) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            for (size_t i = 0; i < free.size(); ++i) {
+                if (free[i]->device == device) {
+                    Workspace* w = free[i].release();
+                    free.erase(free.begin() + i);
+                    return w;
+                }
+            }
+        }
+        auto* w = new Workspace();
+        w->device = device;
+        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipHostMalloc((void**)&w->h_flags, 16, hipHostMallocDefault) != hipSuccess) {
+            delete w;
+            return nullptr;
+        }
+        return w;
+    }
+    void release(Workspace* w) {
+        std::lock_guard<std::mutex> g(mu);
+        free.emplace_back(w);
+    }
+};
+
+WsPool& global_pool() {
+    static WsPool p;
+    return p;
+}
+
+struct WsGuard {
+    Workspace* w;
+    explicit WsGuard(int dev) : w(global_pool().acquire(dev)) {}
+    ~WsGuard() {
+        if (w) global_pool().release(w);
+    }
+};
+
+// ============================================================================
+// BQ search on one shard view (stage 1 + stage 2 + final ordering)
+// ============================================================================
+struct ShardView {
+    const float* rows;      // [N][clen]
+    uint64_t clen;
+    const float* norms;     // [N]
+    const uint4* codes;     // [W4][cap]
+    uint64_t cap;
+    uint32_t N;
+    uint32_t D;             // candidate dimension (bits)
+    const uint64_t* ids;    // row -> id or nullptr
+    uint64_t row_offset;
+};
+
+constexpr uint32_t kExactN = 262144;  // below this the "sample" is the whole shard
+
+// Stage-1 sampling plan: S rows in 4096-row chunks spread over the shard.
+void plan_sampling(uint32_t N, uint32_t R, uint32_t& chunks, uint32_t& stride, uint32_t& target, uint32_t& bufcap) {
+    if (N <= kExactN) {
+        chunks = (N + 4095u) / 4096u;
+        stride = 4096u;
+        target = R;  // exact threshold: count(d <= T) >= R guaranteed
+        bufcap = std::min<uint64_t>(N, 8ull * R + 2048ull);
+        return;
+    }
+    uint64_t S = std::max<uint64_t>(kExactN, N / 32u);
+    chunks = (uint32_t)(S / 4096u);
+    stride = N / chunks;  // >= 4096: chunks never overlap
+    S = (uint64_t)chunks * 4096u;
+    const double m = (double)R * (double)S / (double)N;  // expected sample hits of the top-R set
+    target = (uint32_t)std::ceil(m + 4.0 * std::sqrt(m) + 4.0);
+    const double expect_full = (double)target * (double)N / (double)S;
+    bufcap = (uint32_t)std::min<double>((double)N, 8.0 * expect_full + 2048.0);
+}
+
+struct BqSearchArgs {
+    ShardView v;
+    const float* d_q;       // [B][qlen]
+    uint64_t qlen;
+    uint32_t B;
+    const uint32_t* d_qwords;  // optional pre-packed query codes [B][4*W4] (else packed from d_q)
+    float thr;              // packing threshold
+    bool dims_match;        // binary query dim == candidate dim
+    uint32_t R;
+    uint32_t kout;
+    int kind;
+    int descending;
+    uint64_t* d_out_ids;
+    float* d_out_scores;
+    uint32_t* d_out_n;
+    uint32_t* d_out_dist;   // candidates mode: stage-1 order, no final sort
+};
+
+gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
+    const ShardView& v = a.v;
+    const uint32_t B = a.B, R = a.R;
+    if (B == 0) return GVDB_OK;
+    if (R == 0) {
+        if (a.d_out_n) HIP_TRY(hipMemsetAsync(a.d_out_n, 0, (size_t)B * 4, s), "memset out_n");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        return GVDB_OK;
+    }
+    const uint32_t W4 = code_w4(v.D);
+    HIP_TRY(ws.qnorm.ensure((size_t)B * 4), "alloc qnorm");
+    HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
+    HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
+    HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
+    HIP_TRY(ws.scores.ensure((size_t)B * R * 4), "alloc scores");
+    HIP_TRY(ws.fail.ensure((size_t)B * 4), "alloc fail");
+    HIP_TRY(ws.flags.ensure(16), "alloc flags");
+    uint32_t* d_flags = ws.flags.as<uint32_t>();
+    HIP_TRY(hipMemsetAsync(d_flags, 0, 16, s), "memset flags");
+    HIP_TRY(launch_row_norms(a.d_q, B, (uint32_t)a.qlen, ws.qnorm.as<float>(), s), "qnorm");
+
+    std::vector<uint32_t> slow_q;
+    bool fast_ran = false;
+    bool timed = false;
+    {
+        std::lock_guard<std::mutex> g(timing().mu);
+        timed = timing().on;
+    }
+    if (timed && !ws.ev.ok) ws.ev.create();
+    timed = timed && ws.ev.ok;
+    if (!a.dims_match || v.D == 0) {
+        HIP_TRY(launch_iota_rows(ws.s1_rows.as<uint32_t>(), B, R, s), "iota");
+    } else {
+        if (a.d_qwords) {
+            HIP_TRY(hipMemcpyAsync(ws.qcodes.p, a.d_qwords, (size_t)B * W4 * 16, hipMemcpyDeviceToDevice, s), "qcopy");
+        } else {
+            HIP_TRY(launch_pack(a.d_q, B, v.D, a.thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
+        }
+        if (R <= kSelectLdsCap) {
+            Stage1Args s1{};
+            s1.codes = v.codes;
+            s1.cap = v.cap;
+            s1.N = v.N;
+            s1.D = v.D;
+            s1.qcodes = ws.qcodes.as<uint4>();
+            s1.B = B;
+            s1.R = R;
+            plan_sampling(v.N, R, s1.sample_chunks, s1.sample_stride, s1.target, s1.bufcap);
+            HIP_TRY(ws.hist.ensure((size_t)B * (v.D + 1) * 4), "alloc hist");
+            HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
+            HIP_TRY(ws.counts.ensure((size_t)B * 4), "alloc counts");
+            HIP_TRY(ws.buf.ensure((size_t)B * s1.bufcap * 8), "alloc candidate buffer");
+            HIP_TRY(hipMemsetAsync(ws.hist.p, 0, (size_t)B * (v.D + 1) * 4, s), "memset hist");
+            HIP_TRY(hipMemsetAsync(ws.counts.p, 0, (size_t)B * 4, s), "memset counts");
+            HIP_TRY(hipMemsetAsync(ws.fail.p, 0, (size_t)B * 4, s), "memset fail");
+            s1.hist = ws.hist.as<uint32_t>();
+            s1.thr = ws.thr.as<uint32_t>();
+            s1.counts = ws.counts.as<uint32_t>();
+            s1.buf = ws.buf.as<uint64_t>();
+            s1.fail = ws.fail.as<uint32_t>();
+            s1.s1_rows = ws.s1_rows.as<uint32_t>();
+            s1.s1_dist = ws.s1_dist.as<uint32_t>();
+            s1.ev = timed ? ws.ev.e : nullptr;
+            HIP_TRY(launch_stage1_fast(s1, s), "stage1");
+            fast_ran = true;
+        } else {
+            for (uint32_t q = 0; q < B; ++q) slow_q.push_back(q);
+        }
+    }
+
+    auto run_stage2 = [&](uint32_t q0, uint32_t nq) -> gvdb_status {
+        RerankArgs rr{};
+        rr.rows = v.rows;
+        rr.clen = v.clen;
+        rr.norms = v.norms;
+        rr.q = a.d_q + (uint64_t)q0 * a.qlen;
+        rr.qlen = a.qlen;
+        rr.qnorm = ws.qnorm.as<float>() + q0;
+        rr.s1_rows = ws.s1_rows.as<uint32_t>() + (uint64_t)q0 * R;
+        rr.B = nq;
+        rr.R = R;
+        rr.kind = a.kind;
+        rr.scores = ws.scores.as<float>() + (uint64_t)q0 * R;
+        HIP_TRY(launch_rerank(rr, s), "rerank");
+        if (a.d_out_dist) {
+            HIP_TRY(launch_emit_candidates(rr.s1_rows, ws.s1_dist.as<uint32_t>() + (uint64_t)q0 * R, rr.scores, nq, R,
+                                           v.ids, a.d_out_ids + (uint64_t)q0 * R, a.d_out_dist + (uint64_t)q0 * R,
+                                           a.d_out_scores + (uint64_t)q0 * R, s),
+                    "emit candidates");
+            return GVDB_OK;
+        }
+        FinalArgs fa{};
+        fa.scores = rr.scores;
+        fa.s1_rows = rr.s1_rows;
+        fa.B = nq;
+        fa.R = R;
+        fa.kout = a.kout;
+        fa.descending = a.descending;
+        fa.ids = v.ids;
+        fa.row_offset = v.row_offset;
+        fa.out_ids = a.d_out_ids + (uint64_t)q0 * a.kout;
+        fa.out_scores = a.d_out_scores + (uint64_t)q0 * a.kout;
+        fa.out_n = a.d_out_n ? a.d_out_n + q0 : nullptr;
+        fa.nan_flag = d_flags + 1;
+        if (R <= kSortLdsCap) {
+            HIP_TRY(launch_final_sort(fa, s), "final sort");
+        } else {
+            const size_t need = final_sort_global_bytes(R);
+            HIP_TRY(ws.sort_tmp.ensure(need), "alloc sort tmp");
+            HIP_TRY(launch_final_sort_global(fa, ws.sort_tmp.p, ws.sort_tmp.n, s), "final sort (global)");
+        }
+        return GVDB_OK;
+    };
+
+    if (slow_q.size() < B) {
+        gvdb_status st = run_stage2(0, B);
+        if (st != GVDB_OK) return st;
+        if (timed) HIP_TRY(hipEventRecord(ws.ev.e[5], s), "event");
+    }
+    // One host sync per batch: did any query leave the certified fast path?
+    std::vector<uint32_t> fails;
+    if (fast_ran) {
+        fails.resize(B);
+        HIP_TRY(hipMemcpyAsync(fails.data(), ws.fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, s), "read fail");
+    }
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    if (timed && fast_ran && slow_q.size() < B) {
+        float t[4] = {0, 0, 0, 0};
+        (void)hipEventElapsedTime(&t[0], ws.ev.e[0], ws.ev.e[1]);
+        (void)hipEventElapsedTime(&t[1], ws.ev.e[1], ws.ev.e[2]);
+        (void)hipEventElapsedTime(&t[2], ws.ev.e[2], ws.ev.e[3]);
+        (void)hipEventElapsedTime(&t[3], ws.ev.e[3], ws.ev.e[5]);
+        std::lock_guard<std::mutex> g(timing().mu);
+        for (int i = 0; i < 4; ++i) {
+            timing().ms[i] += t[i];
+            timing().n[i] += 1;
+        }
+    }
+    for (uint32_t q = 0; q < fails.size(); ++q)
+        if (fails[q]) slow_q.push_back(q);
+    if (!slow_q.empty()) {
+        const size_t need = stage1_slow_bytes(v.N);
+        HIP_TRY(ws.slow.ensure(need), "alloc slow path");
+        for (uint32_t q : slow_q) {
+            HIP_TRY(launch_stage1_slow(v.codes, v.cap, v.N, v.D, ws.qcodes.as<uint4>() + (uint64_t)q * W4, R,
+                                       ws.s1_rows.as<uint32_t>() + (uint64_t)q * R,
+                                       ws.s1_dist.as<uint32_t>() + (uint64_t)q * R, ws.slow.p, ws.slow.n, s),
+                    "stage1 slow");
+            gvdb_status st = run_stage2(q, 1);
+            if (st != GVDB_OK) return st;
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(ws.h_flags, d_flags, 8, hipMemcpyDeviceToHost, s), "read flags");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    if (ws.h_flags[1])
+        return fail(GVDB_ERR_QUANTIZATION, "NaN score: the reference's partial_cmp().unwrap() sort would panic");
+    return GVDB_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// index object
+// ============================================================================
+struct gvdb_index {
+    int device = 0;
+    uint32_t dim = 0;  // 0 = not fixed yet
+    float thr = 0.0f;
+    uint64_t n = 0, cap = 0;
+    float* rows = nullptr;
+    uint4* codes = nullptr;
+    float* norms = nullptr;
+    uint64_t* ids = nullptr;
+    std::vector<uint64_t> h_ids;                      // row -> id (kOrphan for shadowed rows)
+    std::unordered_map<uint64_t, uint64_t> id_row;    // live id -> row
+    hipStream_t stream = nullptr;                     // mutations
+    uint64_t capacity_hint = 0;
+
+    uint32_t w4() const { return code_w4(dim); }
+    size_t device_bytes() const {
+        return cap * ((size_t)dim * 4 + (size_t)w4() * 16 + 4 + 8);
+    }
+    void free_all() {
+        for (void* p : {(void*)rows, (void*)codes, (void*)norms, (void*)ids})
+            if (p) (void)hipFree(p);
+        rows = nullptr;
+        codes = nullptr;
+        norms = nullptr;
+        ids = nullptr;
+        n = cap = 0;
+    }
+};
+
+namespace {
+
+gvdb_status set_device(int dev) {
+    hipError_t e = hipSetDevice(dev);
+    if (e != hipSuccess) return dev_fail(e, "hipSetDevice");
+    return GVDB_OK;
+}
+
+// Grow HBM storage to hold `need` rows (copies the live rows; planes are
+// re-strided because the SoA plane stride is the capacity).
+gvdb_status ensure_capacity(gvdb_index* ix, uint64_t need) {
+    if (need <= ix->cap) return GVDB_OK;
+    uint64_t ncap = std::max<uint64_t>({need, ix->cap * 2, ix->capacity_hint, 1024});
+    const uint32_t D = ix->dim, W4 = ix->w4();
+    float* nrows = nullptr;
+    uint4* ncodes = nullptr;
+    float* nnorms = nullptr;
+    uint64_t* nids = nullptr;
+    hipError_t e = hipMalloc((void**)&nrows, ncap * D * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&ncodes, ncap * W4 * 16);
+    if (e == hipSuccess) e = hipMalloc((void**)&nnorms, ncap * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&nids, ncap * 8);
+    if (e != hipSuccess) {
+        for (void* p : {(void*)nrows, (void*)ncodes, (void*)nnorms, (void*)nids})
+            if (p) (void)hipFree(p);
+        return dev_fail(e, "grow index");
+    }
+    if (ix->n) {
+        HIP_TRY(hipMemcpyAsync(nrows, ix->rows, ix->n * D * 4, hipMemcpyDeviceToDevice, ix->stream), "grow rows");
+        for (uint32_t w = 0; w < W4; ++w)
+            HIP_TRY(hipMemcpyAsync(ncodes + w * ncap, ix->codes + w * ix->cap, ix->n * 16, hipMemcpyDeviceToDevice,
+                                   ix->stream),
+                    "grow codes");
+        HIP_TRY(hipMemcpyAsync(nnorms, ix->norms, ix->n * 4, hipMemcpyDeviceToDevice, ix->stream), "grow norms");
+        HIP_TRY(hipMemcpyAsync(nids, ix->ids, ix->n * 8, hipMemcpyDeviceToDevice, ix->stream), "grow ids");
+        HIP_TRY(hipStreamSynchronize(ix->stream), "grow sync");
+    }
+    uint64_t n = ix->n;
+    ix->free_all();
+    ix->rows = nrows;
+    ix->codes = ncodes;
+    ix->norms = nnorms;
+    ix->ids = nids;
+    ix->cap = ncap;
+    ix->n = n;
+    return GVDB_OK;
+}
+
+// Host bookkeeping for appended ids (HashMap insert semantics, index.rs:175-176:
+// a re-added id shadows its old row, which stays in the corpus but can no
+// longer be returned).  Returns the rows whose id must become kOrphan on device.
+std::vector<uint64_t> register_ids(gvdb_index* ix, const uint64_t* h_new_ids, uint64_t n) {
+    std::vector<uint64_t> orphaned;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t row = ix->n + i;
+        const uint64_t id = h_new_ids[i];
+        auto it = ix->id_row.find(id);
+        if (it != ix->id_row.end()) {
+            ix->h_ids[it->second] = kOrphan;
+            orphaned.push_back(it->second);
+            it->second = row;
+        } else {
+            ix->id_row.emplace(id, row);
+        }
+        ix->h_ids.push_back(id);
+    }
+    return orphaned;
+}
+
+gvdb_status finish_add(gvdb_index* ix, uint64_t n, const std::vector<uint64_t>& orphaned) {
+    const uint64_t r0 = ix->n;
+    HIP_TRY(launch_pack(ix->rows + r0 * ix->dim, n, ix->dim, ix->thr, ix->codes, kPackSoA, ix->cap, r0, ix->stream),
+            "pack rows");
+    HIP_TRY(launch_row_norms(ix->rows + r0 * ix->dim, n, ix->dim, ix->norms + r0, ix->stream), "row norms");
+    // rows shadowed inside this batch live at >= r0: fix them after the id upload
+    static const uint64_t orphan = kOrphan;
+    for (uint64_t row : orphaned)
+        HIP_TRY(hipMemcpyAsync(ix->ids + row, &orphan, 8, hipMemcpyHostToDevice, ix->stream), "orphan id");
+    HIP_TRY(hipStreamSynchronize(ix->stream), "add sync");
+    ix->n += n;
+    return GVDB_OK;
+}
+
+gvdb_status check_add_dim(gvdb_index* ix, uint32_t dim) {
+    if (dim == 0) return fail(GVDB_ERR_INVALID_VECTOR_DIMENSION, "vector dimension 0");
+    if (ix->dim == 0) {
+        ix->dim = dim;  // dimension fixed by the first vector (index.rs:169-171)
+    } else if (dim != ix->dim) {
+        return dim_mismatch(ix->dim, dim);
+    }
+    return GVDB_OK;
+}
+
+uint32_t effective_R(const gvdb_index* ix, const gvdb_search_params* sp, uint64_t k) {
+    uint64_t R = sp->rescore_count ? sp->rescore_count : rust_f32_as_usize((float)ix->n * sp->rescore_ratio);
+    R = std::max<uint64_t>(R, k);  // search(k) returns k hits like HnswMap::search().take(k)
+    R = std::min<uint64_t>(R, ix->n);
+    return (uint32_t)R;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+uint32_t gvdb_abi_version(void) { return GVDB_ABI_VERSION; }
+
+const char* gvdb_last_error(void) { return t_err.c_str(); }
+
+const char* gvdb_status_string(gvdb_status s) {
+    switch (s) {
+        case GVDB_OK: return "ok";
+        case GVDB_ERR_INDEX_NOT_BUILT: return "IndexNotBuilt";
+        case GVDB_ERR_DIMENSION_MISMATCH: return "DimensionMismatch";
+        case GVDB_ERR_INVALID_VECTOR_DIMENSION: return "InvalidVectorDimension";
+        case GVDB_ERR_QUANTIZATION: return "QuantizationError";
+        case GVDB_ERR_INDEX: return "IndexError";
+        case GVDB_ERR_INVALID_ARGUMENT: return "InvalidArgument";
+        case GVDB_ERR_DEVICE: return "DeviceError";
+        case GVDB_ERR_OUT_OF_MEMORY: return "OutOfMemory";
+    }
+    return "unknown";
+}
+
+void gvdb_last_dimension_mismatch(uint64_t* expected, uint64_t* actual) {
+    if (expected) *expected = t_dim_expected;
+    if (actual) *actual = t_dim_actual;
+}
+
+int32_t gvdb_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+gvdb_status gvdb_index_create(const gvdb_params* params, gvdb_index** out) {
+    if (!out) return fail(GVDB_ERR_INVALID_ARGUMENT, "out is null");
+    *out = nullptr;
+    gvdb_params p{};
+    if (params) p = *params;
+    gvdb_status st = set_device(p.device);
+    if (st != GVDB_OK) return st;
+    auto* ix = new gvdb_index();
+    ix->device = p.device;
+    ix->dim = p.dimension;
+    ix->thr = p.bq_threshold;
+    ix->capacity_hint = p.capacity_hint;
+    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ix;
+        return fail(GVDB_ERR_DEVICE, "hipStreamCreate failed");
+    }
+    *out = ix;
+    return GVDB_OK;
+}
+
+void gvdb_index_destroy(gvdb_index* ix) {
+    if (!ix) return;
+    (void)hipSetDevice(ix->device);
+    (void)hipStreamSynchronize(ix->stream);
+    ix->free_all();
+    (void)hipStreamDestroy(ix->stream);
+    delete ix;
+}
+
+gvdb_status gvdb_index_add(gvdb_index* ix, const float* rows, uint64_t n, uint32_t dim, const uint64_t* ids) {
+    if (!ix || (n && (!rows || !ids))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if (n == 0) return GVDB_OK;
+    gvdb_status st = set_device(ix->device);
+    if (st != GVDB_OK) return st;
+    if ((st = check_add_dim(ix, dim)) != GVDB_OK) return st;
+    if ((st = ensure_capacity(ix, ix->n + n)) != GVDB_OK) return st;
+    HIP_TRY(hipMemcpyAsync(ix->rows + ix->n * dim, rows, n * dim * 4, hipMemcpyHostToDevice, ix->stream), "upload rows");
+    HIP_TRY(hipMemcpyAsync(ix->ids + ix->n, ids, n * 8, hipMemcpyHostToDevice, ix->stream), "upload ids");
+    std::vector<uint64_t> orphaned = register_ids(ix, ids, n);
+    return finish_add(ix, n, orphaned);
+}
+
+gvdb_status gvdb_index_add_device(gvdb_index* ix, const float* d_rows, uint64_t n, uint32_t dim, const uint64_t* d_ids,
+                                  void* stream) {
+    if (!ix || (n && (!d_rows || !d_ids))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if (n == 0) return GVDB_OK;
+    gvdb_status st = set_device(ix->device);
+    if (st != GVDB_OK) return st;
+    if ((st = check_add_dim(ix, dim)) != GVDB_OK) return st;
+    if ((st = ensure_capacity(ix, ix->n + n)) != GVDB_OK) return st;
+    if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "caller stream");
+    HIP_TRY(hipMemcpyAsync(ix->rows + ix->n * dim, d_rows, n * dim * 4, hipMemcpyDeviceToDevice, ix->stream),
+            "copy rows");
+    HIP_TRY(hipMemcpyAsync(ix->ids + ix->n, d_ids, n * 8, hipMemcpyDeviceToDevice, ix->stream), "copy ids");
+    std::vector<uint64_t> h(n);
+    HIP_TRY(hipMemcpyAsync(h.data(), d_ids, n * 8, hipMemcpyDeviceToHost, ix->stream), "ids to host");
+    HIP_TRY(hipStreamSynchronize(ix->stream), "sync");
+    std::vector<uint64_t> orphaned = register_ids(ix, h.data(), n);
+    return finish_add(ix, n, orphaned);
+}
+
+gvdb_status gvdb_index_build(gvdb_index* ix) {
+    if (!ix) return fail(GVDB_ERR_INVALID_ARGUMENT, "null index");
+    return GVDB_OK;  // codes and norms are maintained on every add
+}
+
+gvdb_status gvdb_index_optimize(gvdb_index* ix) { return gvdb_index_build(ix); }
+
+static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
+                                     const gvdb_search_params* sp_in, uint64_t* d_ids, float* d_scores, uint32_t* d_n,
+                                     Workspace& ws, hipStream_t s) {
+    gvdb_search_params sp{};
+    sp.mode = GVDB_SEARCH_BQ_RERANK;
+    sp.metric = GVDB_METRIC_COSINE;
+    sp.rescore_ratio = 0.1f;
+    if (sp_in) sp = *sp_in;
+    const int kind = sp.metric == GVDB_METRIC_L2 ? kScoreL2
+                     : sp.metric == GVDB_METRIC_COSINE_DISTANCE ? kScoreCosineDistance
+                                                                 : kScoreCosine;
+    const int descending = kind == kScoreCosine;
+    if (sp.mode == GVDB_SEARCH_FLAT) {
+        HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
+        HIP_TRY(ws.scores.ensure(B * ix->n * 4), "alloc flat scores");
+        HIP_TRY(ws.flags.ensure(16), "alloc flags");
+        HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
+        HIP_TRY(launch_row_norms(d_q, B, dim, ws.qnorm.as<float>(), s), "qnorm");
+        HIP_TRY(launch_flat_scores(d_q, (uint32_t)B, ws.qnorm.as<float>(), ix->rows, (uint32_t)ix->n, dim, ix->norms,
+                                   kind, ws.scores.as<float>(), s),
+                "flat scores");
+        const size_t need = flat_select_bytes((uint32_t)ix->n);
+        HIP_TRY(ws.sort_tmp.ensure(need), "alloc sort tmp");
+        HIP_TRY(launch_flat_select(ws.scores.as<float>(), (uint32_t)B, (uint32_t)ix->n, (uint32_t)k, descending, 0, 0.0f,
+                                   ix->ids, d_ids, d_scores, d_n, ws.sort_tmp.p, ws.sort_tmp.n,
+                                   ws.flags.as<uint32_t>() + 1, s),
+                "flat select");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        return GVDB_OK;
+    }
+    BqSearchArgs a{};
+    a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
+    a.d_q = d_q;
+    a.qlen = dim;
+    a.B = (uint32_t)B;
+    a.thr = ix->thr;
+    a.dims_match = true;
+    a.R = effective_R(ix, &sp, k);
+    a.kout = (uint32_t)k;
+    a.kind = kind;
+    a.descending = descending;
+    a.d_out_ids = d_ids;
+    a.d_out_scores = d_scores;
+    a.d_out_n = d_n;
+    return bq_search(a, ws, s);
+}
+
+static gvdb_status check_search(const gvdb_index* ix, uint32_t dim, uint64_t B, uint64_t k) {
+    if (!ix) return fail(GVDB_ERR_INVALID_ARGUMENT, "null index");
+    if (ix->n == 0) return fail(GVDB_ERR_INDEX_NOT_BUILT, "Index not built");
+    if (dim != ix->dim) return dim_mismatch(ix->dim, dim);
+    if (ix->n > 0xFFFFFFFFull) return fail(GVDB_ERR_INDEX, "shard exceeds 2^32 rows");
+    if (B > 0xFFFFFFFFull || k > 0xFFFFFFFFull) return fail(GVDB_ERR_INVALID_ARGUMENT, "batch or k too large");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64_t B, uint32_t dim, uint64_t k,
+                              const gvdb_search_params* sp, uint64_t* out_ids, float* out_scores, uint32_t* out_n) {
+    gvdb_status st = check_search(ix, dim, B, k);
+    if (st != GVDB_OK) return st;
+    if (B == 0) return GVDB_OK;
+    if (!queries || !out_n || (k && (!out_ids || !out_scores))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if ((st = set_device(ix->device)) != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    hipStream_t s = ws.stream;
+    const uint64_t kk = k ? k : 1;
+    HIP_TRY(ws.q.ensure(B * dim * 4), "alloc queries");
+    HIP_TRY(ws.out_ids.ensure(B * kk * 8), "alloc out");
+    HIP_TRY(ws.out_scores.ensure(B * kk * 4), "alloc out");
+    HIP_TRY(ws.out_n.ensure(B * 4), "alloc out");
+    HIP_TRY(hipMemcpyAsync(ws.q.p, queries, B * dim * 4, hipMemcpyHostToDevice, s), "upload queries");
+    if (k == 0) {
+        memset(out_n, 0, B * 4);
+        return GVDB_OK;
+    }
+    st = index_search_impl(ix, ws.q.as<float>(), B, dim, k, sp, ws.out_ids.as<uint64_t>(), ws.out_scores.as<float>(),
+                           ws.out_n.as<uint32_t>(), ws, s);
+    if (st != GVDB_OK) return st;
+    HIP_TRY(hipMemcpyAsync(out_ids, ws.out_ids.p, B * k * 8, hipMemcpyDeviceToHost, s), "download ids");
+    HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
+    HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download n");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_index_search_device(const gvdb_index* ix, const float* d_queries, uint64_t B, uint32_t dim, uint64_t k,
+                                     const gvdb_search_params* sp, uint64_t* d_out_ids, float* d_out_scores,
+                                     uint32_t* d_out_n, void* stream) {
+    gvdb_status st = check_search(ix, dim, B, k);
+    if (st != GVDB_OK) return st;
+    if (B == 0 || k == 0) return GVDB_OK;
+    if (!d_queries || !d_out_ids || !d_out_scores) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if ((st = set_device(ix->device)) != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    hipStream_t s = stream ? (hipStream_t)stream : g.w->stream;
+    return index_search_impl(ix, d_queries, B, dim, k, sp, d_out_ids, d_out_scores, d_out_n, *g.w, s);
+}
+
+gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queries, uint64_t B, uint32_t dim, uint64_t R,
+                                      uint64_t* d_out_rows, uint32_t* d_out_dist, void* stream) {
+    gvdb_status st = check_search(ix, dim, B, R);
+    if (st != GVDB_OK) return st;
+    if (B == 0 || R == 0) return GVDB_OK;
+    if (R > ix->n) return fail(GVDB_ERR_INVALID_ARGUMENT, "R exceeds the number of rows");
+    if (!d_queries || !d_out_rows || !d_out_dist) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if ((st = set_device(ix->device)) != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+    const uint32_t W4 = code_w4(dim);
+    const uint32_t RR = (uint32_t)R;
+    HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc");
+    HIP_TRY(ws.s1_rows.ensure(B * R * 4), "alloc");
+    HIP_TRY(ws.s1_dist.ensure(B * R * 4), "alloc");
+    HIP_TRY(ws.fail.ensure(B * 4), "alloc");
+    HIP_TRY(launch_pack(d_queries, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
+    std::vector<uint32_t> fails(B, 1u);
+    if (RR <= kSelectLdsCap) {
+        Stage1Args s1{};
+        s1.codes = ix->codes;
+        s1.cap = ix->cap;
+        s1.N = (uint32_t)ix->n;
+        s1.D = dim;
+        s1.qcodes = ws.qcodes.as<uint4>();
+        s1.B = (uint32_t)B;
+        s1.R = RR;
+        plan_sampling(s1.N, RR, s1.sample_chunks, s1.sample_stride, s1.target, s1.bufcap);
+        HIP_TRY(ws.hist.ensure(B * (dim + 1) * 4), "alloc");
+        HIP_TRY(ws.thr.ensure(B * 4), "alloc");
+        HIP_TRY(ws.counts.ensure(B * 4), "alloc");
+        HIP_TRY(ws.buf.ensure(B * (size_t)s1.bufcap * 8), "alloc");
+        HIP_TRY(hipMemsetAsync(ws.hist.p, 0, B * (dim + 1) * 4, s), "memset");
+        HIP_TRY(hipMemsetAsync(ws.counts.p, 0, B * 4, s), "memset");
+        HIP_TRY(hipMemsetAsync(ws.fail.p, 0, B * 4, s), "memset");
+        s1.hist = ws.hist.as<uint32_t>();
+        s1.thr = ws.thr.as<uint32_t>();
+        s1.counts = ws.counts.as<uint32_t>();
+        s1.buf = ws.buf.as<uint64_t>();
+        s1.fail = ws.fail.as<uint32_t>();
+        s1.s1_rows = ws.s1_rows.as<uint32_t>();
+        s1.s1_dist = ws.s1_dist.as<uint32_t>();
+        HIP_TRY(launch_stage1_fast(s1, s), "stage1");
+        HIP_TRY(hipMemcpyAsync(fails.data(), ws.fail.p, B * 4, hipMemcpyDeviceToHost, s), "read fail");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+    }
+    bool any_slow = false;
+    for (uint64_t q = 0; q < B; ++q) {
+        if (!fails[q]) continue;
+        if (!any_slow) {
+            HIP_TRY(ws.slow.ensure(stage1_slow_bytes((uint32_t)ix->n)), "alloc slow");
+            any_slow = true;
+        }
+        HIP_TRY(launch_stage1_slow(ix->codes, ix->cap, (uint32_t)ix->n, dim, ws.qcodes.as<uint4>() + q * W4, RR,
+                                   ws.s1_rows.as<uint32_t>() + q * R, ws.s1_dist.as<uint32_t>() + q * R, ws.slow.p,
+                                   ws.slow.n, s),
+                "stage1 slow");
+    }
+    HIP_TRY(launch_widen(ws.s1_rows.as<uint32_t>(), d_out_rows, B * R, s), "widen rows");
+    HIP_TRY(hipMemcpyAsync(d_out_dist, ws.s1_dist.p, B * R * 4, hipMemcpyDeviceToDevice, s), "dist");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_index_remove(gvdb_index* ix, uint64_t id, int32_t* removed) {
+    if (!ix) return fail(GVDB_ERR_INVALID_ARGUMENT, "null index");
+    if (removed) *removed = 0;
+    auto it = ix->id_row.find(id);
+    if (it == ix->id_row.end()) return GVDB_OK;  // Ok(false) (index.rs:282-284)
+    gvdb_status st = set_device(ix->device);
+    if (st != GVDB_OK) return st;
+    const uint64_t gone = it->second;
+    ix->id_row.erase(it);
+    // Keep rows that still map to an id, in order (index.rs:248-258: orphans
+    // have no id and vanish too).
+    std::vector<uint64_t> map;
+    map.reserve(ix->n);
+    for (uint64_t r = 0; r < ix->n; ++r)
+        if (r != gone && ix->h_ids[r] != kOrphan) map.push_back(r);
+    const uint64_t m = map.size();
+    if (m == 0) {  // all vectors deleted: index unbuilt (index.rs:271-274)
+        (void)hipStreamSynchronize(ix->stream);
+        uint32_t dim = ix->dim;
+        ix->free_all();
+        ix->dim = dim;
+        ix->h_ids.clear();
+        ix->id_row.clear();
+        if (removed) *removed = 1;
+        return GVDB_OK;
+    }
+    const uint64_t cap = std::max<uint64_t>(m, 1024);
+    const uint32_t D = ix->dim, W4 = ix->w4();
+    float *nrows = nullptr, *nnorms = nullptr;
+    uint4* ncodes = nullptr;
+    uint64_t *nids = nullptr, *dmap = nullptr;
+    hipError_t e = hipMalloc((void**)&nrows, cap * D * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&ncodes, cap * W4 * 16);
+    if (e == hipSuccess) e = hipMalloc((void**)&nnorms, cap * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&nids, cap * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&dmap, m * 8);
+    if (e != hipSuccess) {
+        for (void* p : {(void*)nrows, (void*)ncodes, (void*)nnorms, (void*)nids, (void*)dmap})
+            if (p) (void)hipFree(p);
+        return dev_fail(e, "remove: allocation");
+    }
+    HIP_TRY(hipMemcpyAsync(dmap, map.data(), m * 8, hipMemcpyHostToDevice, ix->stream), "remove map");
+    // codes: plane stride changes from old cap to new cap
+    HIP_TRY(launch_gather(ix->rows, nrows, ix->codes, ncodes, ix->norms, nnorms, ix->ids, nids, dmap, m, cap, D,
+                          ix->stream),
+            "remove gather");
+    HIP_TRY(hipStreamSynchronize(ix->stream), "remove sync");
+    (void)hipFree(dmap);
+    std::vector<uint64_t> nh(m);
+    for (uint64_t i = 0; i < m; ++i) nh[i] = ix->h_ids[map[i]];
+    ix->free_all();
+    ix->rows = nrows;
+    ix->codes = ncodes;
+    ix->norms = nnorms;
+    ix->ids = nids;
+    ix->cap = cap;
+    ix->n = m;
+    ix->h_ids.swap(nh);
+    ix->id_row.clear();
+    for (uint64_t r = 0; r < m; ++r) ix->id_row.emplace(ix->h_ids[r], r);
+    if (removed) *removed = 1;
+    return GVDB_OK;
+}
+
+uint64_t gvdb_index_len(const gvdb_index* ix) { return ix ? ix->id_row.size() : 0; }
+
+int32_t gvdb_index_is_empty(const gvdb_index* ix) { return gvdb_index_len(ix) == 0; }
+
+void gvdb_index_clear(gvdb_index* ix) {
+    if (!ix) return;
+    (void)hipSetDevice(ix->device);
+    (void)hipStreamSynchronize(ix->stream);
+    ix->free_all();
+    ix->dim = 0;  // dimension = None (index.rs:304-309)
+    ix->h_ids.clear();
+    ix->id_row.clear();
+}
+
+gvdb_status gvdb_index_get_stats(const gvdb_index* ix, gvdb_index_stats* out) {
+    if (!ix || !out) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    out->vector_count = gvdb_index_len(ix);
+    out->dimension = ix->dim;
+    out->memory_usage = ix->n * (uint64_t)ix->dim * 4;  // vectors.len() * dim * 4 (index.rs:318-320)
+    out->device_bytes = ix->device_bytes();
+    return GVDB_OK;
+}
+
+const float* gvdb_index_device_rows(const gvdb_index* ix) { return ix ? ix->rows : nullptr; }
+
+// ---- kernel timing -------------------------------------------------------------------
+void gvdb_timing_enable(int32_t on) {
+    std::lock_guard<std::mutex> g(timing().mu);
+    timing().on = on != 0;
+}
+
+void gvdb_timing_reset(void) {
+    std::lock_guard<std::mutex> g(timing().mu);
+    for (int i = 0; i < kTimN; ++i) {
+        timing().ms[i] = 0;
+        timing().n[i] = 0;
+    }
+}
+
+gvdb_status gvdb_timing_read(uint32_t which, double* total_ms, uint64_t* launches) {
+    if (which >= (uint32_t)kTimN || !total_ms || !launches) return fail(GVDB_ERR_INVALID_ARGUMENT, "bad timing slot");
+    std::lock_guard<std::mutex> g(timing().mu);
+    *total_ms = timing().ms[which];
+    *launches = timing().n[which];
+    return GVDB_OK;
+}
+
+// ---- BinaryQuantizer ---------------------------------------------------------------
+gvdb_status gvdb_bq_quantize_device(const float* d_rows, uint64_t n, uint32_t D, float threshold, uint8_t* d_out,
+                                    void* stream) {
+    if (n == 0) return GVDB_OK;
+    if (!d_rows || !d_out) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(launch_pack(d_rows, n, D, threshold, d_out, kPackBytesAoS, 0, 0, (hipStream_t)stream), "pack");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_bq_quantize(const float* rows, uint64_t n, uint32_t D, float threshold, uint8_t* out) {
+    if (n == 0 || D == 0) return GVDB_OK;
+    if (!rows || !out) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    WsGuard g(0);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    const size_t nb = (D + 7u) / 8u;
+    HIP_TRY(ws.rows.ensure(n * D * 4), "alloc");
+    HIP_TRY(ws.misc.ensure(n * nb), "alloc");
+    HIP_TRY(hipMemcpyAsync(ws.rows.p, rows, n * D * 4, hipMemcpyHostToDevice, ws.stream), "upload");
+    HIP_TRY(launch_pack(ws.rows.as<float>(), n, D, threshold, ws.misc.p, kPackBytesAoS, 0, 0, ws.stream), "pack");
+    HIP_TRY(hipMemcpyAsync(out, ws.misc.p, n * nb, hipMemcpyDeviceToHost, ws.stream), "download");
+    HIP_TRY(hipStreamSynchronize(ws.stream), "sync");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_bq_hamming(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t D, uint32_t* out) {
+    if (n == 0) return GVDB_OK;
+    if (!a || !b || !out) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    WsGuard g(0);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    const size_t nb = (D + 7u) / 8u;
+    HIP_TRY(ws.misc.ensure(2 * n * nb + n * 4 + 512), "alloc");
+    uint8_t* da = ws.misc.as<uint8_t>();
+    uint8_t* db = da + n * nb;
+    uint32_t* dout = (uint32_t*)(((uintptr_t)(db + n * nb) + 255) & ~(uintptr_t)255);
+    HIP_TRY(hipMemcpyAsync(da, a, n * nb, hipMemcpyHostToDevice, ws.stream), "upload");
+    HIP_TRY(hipMemcpyAsync(db, b, n * nb, hipMemcpyHostToDevice, ws.stream), "upload");
+    HIP_TRY(launch_hamming_pairs(da, db, n, D, dout, ws.stream), "hamming");
+    HIP_TRY(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, ws.stream), "download");
+    HIP_TRY(hipStreamSynchronize(ws.stream), "sync");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_bq_multi_stage_search(const uint8_t* q_bits, uint32_t qdim, const uint8_t* c_bits, uint32_t cdim,
+                                       uint64_t N, const float* q, uint64_t qlen, const float* cands, uint64_t clen,
+                                       float rescore_ratio, uint64_t* out_idx, float* out_cos, uint64_t* out_n) {
+    if (!out_n) return fail(GVDB_ERR_INVALID_ARGUMENT, "out_n is null");
+    *out_n = 0;
+    if (N > 0xFFFFFFFFull) return fail(GVDB_ERR_INVALID_ARGUMENT, "more than 2^32 candidates");
+    // len check (quantization.rs:158-162) is structural here: one N for both.
+    const bool dims_match = qdim == cdim;
+    if (dims_match && cdim == 0 && N >= 2)
+        return fail(GVDB_ERR_QUANTIZATION, "dimension 0: similarity is NaN and the reference sort panics");
+    uint64_t R = std::min<uint64_t>(rust_f32_as_usize((float)N * rescore_ratio), N);
+    if (R == 0 || N == 0) return GVDB_OK;
+    if (!q_bits || !c_bits || !q || !cands || !out_idx || !out_cos)
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    WsGuard g(0);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    hipStream_t s = ws.stream;
+    const uint32_t W4 = code_w4(cdim);
+    const size_t nb = (cdim + 7u) / 8u;
+    // upload: candidate rows + norms, codes (SoA from Msb0 bytes), query
+    HIP_TRY(ws.rows.ensure(std::max<size_t>(N * clen * 4, 4)), "alloc rows");
+    HIP_TRY(ws.norms.ensure(N * 4), "alloc norms");
+    HIP_TRY(ws.codes.ensure(N * W4 * 16 + N * nb + 16), "alloc codes");
+    HIP_TRY(ws.q.ensure(std::max<size_t>(qlen * 4, 4)), "alloc q");
+    HIP_TRY(ws.out_ids.ensure(R * 8), "alloc out");
+    HIP_TRY(ws.out_scores.ensure(R * 4), "alloc out");
+    HIP_TRY(ws.misc.ensure(W4 * 16 + nb + 16), "alloc qbits");
+    if (clen) HIP_TRY(hipMemcpyAsync(ws.rows.p, cands, N * clen * 4, hipMemcpyHostToDevice, s), "upload cands");
+    if (qlen) HIP_TRY(hipMemcpyAsync(ws.q.p, q, qlen * 4, hipMemcpyHostToDevice, s), "upload q");
+    HIP_TRY(launch_row_norms(ws.rows.as<float>(), N, (uint32_t)clen, ws.norms.as<float>(), s), "norms");
+    uint32_t* d_qwords = nullptr;
+    if (dims_match && cdim) {
+        uint8_t* cbytes = ws.codes.as<uint8_t>() + N * W4 * 16;
+        HIP_TRY(hipMemcpyAsync(cbytes, c_bits, N * nb, hipMemcpyHostToDevice, s), "upload codes");
+        HIP_TRY(launch_bytes_to_soa(cbytes, N, cdim, ws.codes.as<uint4>(), N, 0, s), "codes to SoA");
+        uint8_t* qb = ws.misc.as<uint8_t>() + W4 * 16;
+        HIP_TRY(hipMemcpyAsync(qb, q_bits, nb, hipMemcpyHostToDevice, s), "upload qbits");
+        HIP_TRY(launch_bytes_to_words(qb, 1, cdim, ws.misc.as<uint32_t>(), s), "qbits to words");
+        d_qwords = ws.misc.as<uint32_t>();
+    }
+    BqSearchArgs a{};
+    a.v = ShardView{ws.rows.as<float>(), clen, ws.norms.as<float>(), ws.codes.as<uint4>(), N, (uint32_t)N, cdim,
+                    nullptr, 0};
+    a.d_q = ws.q.as<float>();
+    a.qlen = qlen;
+    a.B = 1;
+    a.d_qwords = d_qwords;
+    a.dims_match = dims_match && cdim;
+    a.R = (uint32_t)R;
+    a.kout = (uint32_t)R;
+    a.kind = kScoreCosine;
+    a.descending = 1;
+    a.d_out_ids = ws.out_ids.as<uint64_t>();
+    a.d_out_scores = ws.out_scores.as<float>();
+    a.d_out_n = nullptr;
+    gvdb_status st = bq_search(a, ws, s);
+    if (st != GVDB_OK) return st;
+    HIP_TRY(hipMemcpyAsync(out_idx, ws.out_ids.p, R * 8, hipMemcpyDeviceToHost, s), "download idx");
+    HIP_TRY(hipMemcpyAsync(out_cos, ws.out_scores.p, R * 4, hipMemcpyDeviceToHost, s), "download cos");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    *out_n = R;
+    return GVDB_OK;
+}
+
+// ---- flat scan -----------------------------------------------------------------
+gvdb_status gvdb_flat_search(const float* queries, uint64_t B, const float* rows, uint64_t N, uint32_t D, uint64_t limit,
+                             uint32_t metric, int32_t has_threshold, float threshold, uint64_t* out_idx,
+                             float* out_scores, uint32_t* out_n) {
+    if (B == 0) return GVDB_OK;
+    if (!queries || !out_n || (N && !rows) || (limit && (!out_idx || !out_scores)))
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if (N > 0xFFFFFFFFull) return fail(GVDB_ERR_INVALID_ARGUMENT, "more than 2^32 rows");
+    if (N == 0 || limit == 0) {
+        memset(out_n, 0, B * 4);
+        return GVDB_OK;
+    }
+    WsGuard g(0);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    hipStream_t s = ws.stream;
+    const int kind = metric == GVDB_METRIC_L2 ? kScoreL2
+                     : metric == GVDB_METRIC_COSINE_DISTANCE ? kScoreCosineDistance
+                                                             : kScoreCosine;
+    HIP_TRY(ws.rows.ensure(N * D * 4 + 4), "alloc rows");
+    HIP_TRY(ws.norms.ensure(N * 4), "alloc norms");
+    HIP_TRY(ws.q.ensure(B * D * 4 + 4), "alloc q");
+    HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
+    HIP_TRY(ws.scores.ensure(B * N * 4), "alloc scores");
+    HIP_TRY(ws.out_ids.ensure(B * limit * 8), "alloc out");
+    HIP_TRY(ws.out_scores.ensure(B * limit * 4), "alloc out");
+    HIP_TRY(ws.out_n.ensure(B * 4), "alloc out");
+    HIP_TRY(ws.flags.ensure(16), "alloc flags");
+    HIP_TRY(ws.sort_tmp.ensure(flat_select_bytes((uint32_t)N)), "alloc sort");
+    HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset");
+    if (D) HIP_TRY(hipMemcpyAsync(ws.rows.p, rows, N * D * 4, hipMemcpyHostToDevice, s), "upload rows");
+    if (D) HIP_TRY(hipMemcpyAsync(ws.q.p, queries, B * D * 4, hipMemcpyHostToDevice, s), "upload q");
+    HIP_TRY(launch_row_norms(ws.rows.as<float>(), N, D, ws.norms.as<float>(), s), "norms");
+    HIP_TRY(launch_row_norms(ws.q.as<float>(), B, D, ws.qnorm.as<float>(), s), "qnorm");
+    HIP_TRY(launch_flat_scores(ws.q.as<float>(), (uint32_t)B, ws.qnorm.as<float>(), ws.rows.as<float>(), (uint32_t)N, D,
+                               ws.norms.as<float>(), kind, ws.scores.as<float>(), s),
+            "flat scores");
+    HIP_TRY(launch_flat_select(ws.scores.as<float>(), (uint32_t)B, (uint32_t)N, (uint32_t)limit, kind == kScoreCosine,
+                               has_threshold && kind == kScoreCosine, threshold, nullptr, ws.out_ids.as<uint64_t>(),
+                               ws.out_scores.as<float>(), ws.out_n.as<uint32_t>(), ws.sort_tmp.p, ws.sort_tmp.n,
+                               ws.flags.as<uint32_t>() + 1, s),
+            "flat select");
+    HIP_TRY(hipMemcpyAsync(out_idx, ws.out_ids.p, B * limit * 8, hipMemcpyDeviceToHost, s), "download");
+    HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * limit * 4, hipMemcpyDeviceToHost, s), "download");
+    HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* ix, const float* d_queries, uint64_t B, uint32_t dim,
+                                            uint64_t R, uint64_t* d_out_ids, uint32_t* d_out_dist,
+                                            float* d_out_scores, void* stream) {
+    gvdb_status st = check_search(ix, dim, B, R);
+    if (st != GVDB_OK) return st;
+    if (B == 0 || R == 0) return GVDB_OK;
+    if (R > ix->n) return fail(GVDB_ERR_INVALID_ARGUMENT, "R exceeds the number of rows");
+    if (!d_queries || !d_out_ids || !d_out_dist || !d_out_scores) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if ((st = set_device(ix->device)) != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    hipStream_t s = stream ? (hipStream_t)stream : g.w->stream;
+    BqSearchArgs a{};
+    a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
+    a.d_q = d_queries;
+    a.qlen = dim;
+    a.B = (uint32_t)B;
+    a.thr = ix->thr;
+    a.dims_match = true;
+    a.R = (uint32_t)R;
+    a.kout = (uint32_t)R;
+    a.kind = kScoreCosine;
+    a.descending = 1;
+    a.d_out_ids = d_out_ids;
+    a.d_out_scores = d_out_scores;
+    a.d_out_dist = d_out_dist;
+    return bq_search(a, *g.w, s);
+}
+
+gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d_dist, const float* d_cos,
+                                       const uint32_t* d_counts, uint64_t G, uint64_t B, uint64_t stride, uint64_t R,
+                                       uint64_t k, uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
+                                       void* stream) {
+    if (B == 0) return GVDB_OK;
+    if (G * stride > kSortLdsCap) return fail(GVDB_ERR_INVALID_ARGUMENT, "G*stride exceeds 4096");
+    if (!d_gids || !d_dist || !d_cos || !d_counts || !d_out_ids || !d_out_scores)
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    WsGuard g(0);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    hipStream_t s = stream ? (hipStream_t)stream : g.w->stream;
+    HIP_TRY(g.w->flags.ensure(16), "alloc flags");
+    HIP_TRY(hipMemsetAsync(g.w->flags.p, 0, 16, s), "memset flags");
+    HIP_TRY(launch_bq_shard_merge(d_gids, d_dist, d_cos, d_counts, (uint32_t)G, (uint32_t)B, (uint32_t)stride,
+                                  (uint32_t)R, (uint32_t)k, d_out_ids, d_out_scores, d_out_n,
+                                  g.w->flags.as<uint32_t>() + 1, s),
+            "shard merge");
+    HIP_TRY(hipMemcpyAsync(g.w->h_flags, g.w->flags.p, 8, hipMemcpyDeviceToHost, s), "flags");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    if (g.w->h_flags[1]) return fail(GVDB_ERR_QUANTIZATION, "NaN score in merge");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cosv, const uint32_t* counts,
+                                uint64_t G, uint64_t B, uint64_t stride, uint64_t R, uint64_t k, uint64_t* out_ids,
+                                float* out_scores, uint32_t* out_n) {
+    // Host form of the same merge (used where the gathered lists are on the host).
+    if (B == 0) return GVDB_OK;
+    if (!gids || !dist || !cosv || !counts || !out_n || (k && (!out_ids || !out_scores)))
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    struct E {
+        uint32_t d;
+        uint64_t gid;
+        float c;
+    };
+    std::vector<E> all;
+    for (uint64_t q = 0; q < B; ++q) {
+        all.clear();
+        for (uint64_t g = 0; g < G; ++g) {
+            const uint64_t c = std::min<uint64_t>(counts[g * B + q], stride);
+            for (uint64_t i = 0; i < c; ++i) {
+                const uint64_t at = (g * B + q) * stride + i;
+                all.push_back({dist[at], gids[at], cosv[at]});
+            }
+        }
+        std::stable_sort(all.begin(), all.end(),
+                         [](const E& a, const E& b) { return a.d != b.d ? a.d < b.d : a.gid < b.gid; });
+        const uint64_t r = std::min<uint64_t>(R, all.size());
+        all.resize(r);
+        for (const E& e : all)
+            if (e.c != e.c && r >= 2) return fail(GVDB_ERR_QUANTIZATION, "NaN score in merge");
+        std::stable_sort(all.begin(), all.end(), [](const E& a, const E& b) { return a.c > b.c; });
+        const uint64_t take = std::min<uint64_t>(k, r);
+        for (uint64_t i = 0; i < take; ++i) {
+            out_ids[q * k + i] = all[i].gid;
+            out_scores[q * k + i] = all[i].c;
+        }
+        out_n[q] = (uint32_t)take;
+    }
+    return GVDB_OK;
+}
+
+// ---- shard merge -----------------------------------------------------------------
+gvdb_status gvdb_topk_merge(const uint64_t* ids, const float* scores, const uint32_t* counts, uint64_t n_shards,
+                            uint64_t B, uint64_t stride, uint64_t limit, int32_t descending, uint64_t* out_ids,
+                            float* out_scores, uint32_t* out_n) {
+    // Host merge: the reference's merge is host-side too (shard.rs:776-784).
+    if (B == 0) return GVDB_OK;
+    if (!ids || !scores || !counts || !out_n || (limit && (!out_ids || !out_scores)))
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    std::vector<std::pair<float, uint64_t>> all;
+    for (uint64_t q = 0; q < B; ++q) {
+        all.clear();
+        for (uint64_t s = 0; s < n_shards; ++s) {
+            const uint64_t c = std::min<uint64_t>(counts[s * B + q], stride);
+            for (uint64_t i = 0; i < c; ++i) {
+                const uint64_t at = (s * B + q) * stride + i;
+                all.push_back({scores[at], ids[at]});
+            }
+        }
+        auto cmp = [descending](const std::pair<float, uint64_t>& a, const std::pair<float, uint64_t>& b) {
+            return descending ? a.first > b.first : a.first < b.first;  // NaN compares as Equal
+        };
+        std::stable_sort(all.begin(), all.end(), cmp);
+        const uint64_t n = std::min<uint64_t>(limit, all.size());
+        for (uint64_t i = 0; i < n; ++i) {
+            out_ids[q * limit + i] = all[i].second;
+            out_scores[q * limit + i] = all[i].first;
+        }
+        out_n[q] = (uint32_t)n;
+    }
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_topk_merge_device(const uint64_t* d_ids, const float* d_scores, const uint32_t* d_counts,
+                                   uint64_t n_shards, uint64_t B, uint64_t stride, uint64_t limit, int32_t descending,
+                                   uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n, void* stream) {
+    if (B == 0) return GVDB_OK;
+    if (n_shards * stride > kSortLdsCap) return fail(GVDB_ERR_INVALID_ARGUMENT, "n_shards*stride exceeds 4096");
+    if (!d_ids || !d_scores || !d_counts || !d_out_n || (limit && (!d_out_ids || !d_out_scores)))
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(launch_topk_merge(d_ids, d_scores, d_counts, (uint32_t)n_shards, (uint32_t)B, (uint32_t)stride,
+                              (uint32_t)limit, descending, d_out_ids, d_out_scores, d_out_n, s),
+            "merge");
+    return GVDB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,160 @@
+// gvdb_internal.h — internal launch interface between the C ABI layer
+// (gvdb_capi.hip) and the gfx950 kernels (gvdb_kernels.hip).
+//
+// HBM layout of one index shard:
+//   rows  : float [cap][D]            row-major f32 corpus (rerank gathers rows)
+//   codes : uint4 [W4][cap]           BQ codes, word-major SoA: plane w4 holds
+//                                     code words 4*w4 .. 4*w4+3 of every row;
+//                                     word w = little-endian u32 of Msb0 bytes
+//                                     4w..4w+3 (quantization.rs:97-101 packing),
+//                                     pad bytes 0.  Lane n reads row n: every
+//                                     wave-load is 1 KiB contiguous.
+//   norms : float [cap]               sqrt(sequential sum x*x) per row
+//   ids   : uint64 [cap]              caller ids; GVDB_ORPHAN = shadowed row
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gvdb {
+
+constexpr uint64_t kOrphan = ~0ull;       // row whose id was re-added (index.rs:175-176)
+constexpr uint32_t kSelectLdsCap = 8192;  // stage-1 select: keys sorted in LDS
+constexpr uint32_t kSortLdsCap = 4096;    // stage-2 sort: keys sorted in LDS
+
+__host__ __device__ inline uint32_t code_words(uint32_t D) { return (((D + 7u) / 8u) + 3u) / 4u; }  // u32 words
+// uint4 planes per row, rounded up to a width the scan kernel is instantiated
+// for (pad planes hold zero bits in query and rows alike: no distance change).
+__host__ __device__ inline uint32_t code_w4(uint32_t D) {
+    const uint32_t raw = (code_words(D) + 3u) / 4u;
+    const uint32_t set[10] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32};
+    for (int i = 0; i < 10; ++i)
+        if (raw <= set[i]) return set[i];
+    return raw;
+}
+
+enum PackLayout : int {
+    kPackBytesAoS = 0,  // Msb0 bytes, row stride ceil(D/8)           (BinaryVector::to_bytes)
+    kPackWordsAoS = 1,  // u32 words, row stride 4*W4 words           (query codes)
+    kPackSoA = 2,       // uint4 planes [W4][cap] (index codes)
+};
+
+enum ScoreKind : int { kScoreCosine = 0, kScoreL2 = 1, kScoreCosineDistance = 2 };
+
+// ---- K1 pack ----------------------------------------------------------------
+hipError_t launch_pack(const float* rows, uint64_t n, uint32_t D, float thr, void* out, int layout,
+                       uint64_t cap, uint64_t row0, hipStream_t s);
+hipError_t launch_bytes_to_soa(const uint8_t* bytes, uint64_t n, uint32_t D, uint4* codes, uint64_t cap,
+                               uint64_t row0, hipStream_t s);
+hipError_t launch_bytes_to_words(const uint8_t* bytes, uint64_t n, uint32_t D, uint32_t* words, hipStream_t s);
+hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t D, uint32_t* out,
+                                hipStream_t s);
+
+// ---- exact sequential norms (bit-identical to the reference's fold) -----------
+hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t D, float* out, hipStream_t s);
+
+// ---- K2 stage 1: BQ Hamming top-R -----------------------------------------------
+struct Stage1Args {
+    const uint4* codes;      // [W4][cap]
+    uint64_t cap;
+    uint32_t N;              // rows scanned
+    uint32_t D;              // dimension (bits)
+    const uint4* qcodes;     // [B][W4]
+    uint32_t B;
+    uint32_t R;
+    // sampling for the threshold estimate
+    uint32_t sample_chunks;  // number of contiguous 4096-row chunks
+    uint32_t sample_stride;  // rows between chunk starts
+    uint32_t target;         // sample count that defines the threshold
+    // workspace
+    uint32_t* hist;          // [B][D+1]
+    uint32_t* thr;           // [B]
+    uint32_t* counts;        // [B]
+    uint64_t* buf;           // [B][bufcap]
+    uint32_t bufcap;
+    uint32_t* fail;          // [B]  (1 = fast path could not certify the top-R)
+    uint32_t* s1_rows;       // [B][R]
+    uint32_t* s1_dist;       // [B][R]
+    hipEvent_t* ev;          // optional [4]: before hist, before scan, after scan, after select
+};
+// hist/counts/fail must be zeroed by the caller on stream s.
+hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s);
+// Exact slow path for ONE query: all N distances + stable radix sort.
+// tmp buffers sized by stage1_slow_bytes().
+size_t stage1_slow_bytes(uint32_t N);
+hipError_t launch_stage1_slow(const uint4* codes, uint64_t cap, uint32_t N, uint32_t D, const uint4* qcode,
+                              uint32_t R, uint32_t* out_rows, uint32_t* out_dist, void* tmp, size_t tmp_bytes,
+                              hipStream_t s);
+// Stage 1 when the query dimension differs from the candidates' (every
+// similarity is 0.0, quantization.rs:168): rows 0..R-1 in order.
+hipError_t launch_iota_rows(uint32_t* rows, uint32_t B, uint32_t R, hipStream_t s);
+
+// ---- K3 stage 2: exact rerank of the stage-1 list ------------------------------
+struct RerankArgs {
+    const float* rows;       // [*][clen]
+    uint64_t clen;
+    const float* norms;      // [*]
+    const float* q;          // [B][qlen]
+    uint64_t qlen;
+    const float* qnorm;      // [B]
+    const uint32_t* s1_rows; // [B][R]
+    uint32_t B, R;
+    int kind;                // ScoreKind
+    float* scores;           // [B][R]
+};
+hipError_t launch_rerank(const RerankArgs& a, hipStream_t s);
+
+// Final ordering of each query's R scores (stable: ties keep stage-1 rank),
+// truncated to kout; rows -> ids (ids==nullptr: emit row numbers); orphans
+// dropped after truncation.  R <= kSortLdsCap: one workgroup per query.
+struct FinalArgs {
+    const float* scores;     // [B][R]
+    const uint32_t* s1_rows; // [B][R]
+    uint32_t B, R, kout;
+    int descending;
+    const uint64_t* ids;     // row -> id, or nullptr
+    uint64_t row_offset;     // added to emitted row numbers when ids == nullptr
+    uint64_t* out_ids;       // [B][kout]
+    float* out_scores;       // [B][kout]
+    uint32_t* out_n;         // [B] or nullptr
+    uint32_t* nan_flag;      // set to 1 if a NaN score would make the reference panic
+};
+hipError_t launch_final_sort(const FinalArgs& a, hipStream_t s);
+size_t final_sort_global_bytes(uint32_t R);
+hipError_t launch_final_sort_global(const FinalArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s);
+
+// ---- flat exact scan (storage.rs:296-339, index.rs:620-640) --------------------
+hipError_t launch_flat_scores(const float* q, uint32_t B, const float* qnorm, const float* rows, uint32_t N,
+                              uint32_t D, const float* norms, int kind, float* scores /*[B][N]*/, hipStream_t s);
+size_t flat_select_bytes(uint32_t N);
+// per query: keep score >= threshold when has_threshold (cosine), stable sort,
+// first `limit`.
+// ids: row -> id with orphans skipped (nullptr: emit row numbers).
+hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint32_t limit, int descending,
+                              int has_threshold, float threshold, const uint64_t* ids, uint64_t* out_idx,
+                              float* out_scores, uint32_t* out_n, void* tmp, size_t tmp_bytes, uint32_t* nan_flag,
+                              hipStream_t s);
+
+// ---- shard merge (shard.rs:776-784) --------------------------------------------
+hipError_t launch_topk_merge(const uint64_t* ids, const float* scores, const uint32_t* counts, uint32_t n_shards,
+                             uint32_t B, uint32_t stride, uint32_t limit, int descending, uint64_t* out_ids,
+                             float* out_scores, uint32_t* out_n, hipStream_t s);
+
+hipError_t launch_widen(const uint32_t* a, uint64_t* b, uint64_t n, hipStream_t s);
+
+hipError_t launch_emit_candidates(const uint32_t* s1_rows, const uint32_t* s1_dist, const float* scores, uint32_t B,
+                                  uint32_t R, const uint64_t* ids, uint64_t* out_ids, uint32_t* out_dist,
+                                  float* out_scores, hipStream_t s);
+// Exact sharded multi-stage merge (one exchange): see gvdb_kernels.hip.
+// G*stride <= kSortLdsCap.
+hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cosv, const uint32_t* counts,
+                                 uint32_t G, uint32_t B, uint32_t stride, uint32_t R, uint32_t kout, uint64_t* out_ids,
+                                 float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s);
+
+// ---- index maintenance -----------------------------------------------------------
+// Order-preserving gather of rows/codes/norms/ids: new row r <- old row map[r]
+// (remove_vector compaction, index.rs:245-266).
+hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, uint4* ncodes, const float* norms,
+                         float* nnorms, const uint64_t* ids, uint64_t* nids, const uint64_t* map, uint64_t m,
+                         uint64_t cap, uint32_t D, hipStream_t s);
+
+}  // namespace gvdb

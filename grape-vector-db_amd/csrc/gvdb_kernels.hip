@@ -1,0 +1,1230 @@
+// gvdb_kernels.hip — gfx950 (MI355X, CDNA4) kernels of the grape-vector-db
+// ANN hot path.  Wave64 throughout; no CUDA-isms, no dual paths.
+//
+//   K1  k_pack / k_bytes_to_*        BinaryQuantizer::quantize  (quantization.rs:86-122)
+//   K2  k_sample_hist, k_threshold,  multi_stage_search stage 1 (quantization.rs:165-179):
+//       k_scan (hot), k_select       exact top-R by (Hamming asc, row asc) == the
+//                                    reference's stable sort by similarity desc
+//   K3  k_rerank, k_final_sort       stage 2 (quantization.rs:177-190) with
+//                                    cosine_similarity_manual (206-216) computed in
+//                                    the reference's exact sequential f32 order
+//   flat k_flat_scores              storage.rs:296-339 / index.rs:620-640
+//   merge k_topk_merge               shard.rs:776-784
+//
+// Floating point: this file is compiled with -ffp-contract=off and without
+// fast-math; every f32 reduction that produces a reported score runs
+// sequentially in one lane, in the reference's order, so scores are
+// bit-identical to the Rust fold (sum starts at -0.0f, `impl Sum for f32`).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "gvdb_internal.h"
+
+namespace gvdb {
+
+#define GVDB_LAUNCH_CHECK() \
+    do {                    \
+        hipError_t e__ = hipGetLastError(); \
+        if (e__ != hipSuccess) return e__;  \
+    } while (0)
+
+// ============================================================================
+// K1: sign/threshold packing
+// ============================================================================
+// A ballot over 64 consecutive dims gives bit l = dim (base + l), LSB-first.
+// Msb0 (bitvec::order::Msb0) stores dim 8b+i at bit (7-i) of byte b; read as
+// a little-endian u32 that is a per-byte bit reversal.
+__device__ __forceinline__ uint32_t msb0_word(uint32_t lsb) { return __builtin_bswap32(__builtin_bitreverse32(lsb)); }
+
+__global__ __launch_bounds__(256) void k_pack(const float* __restrict__ rows, uint64_t n, uint32_t D, float thr,
+                                              void* __restrict__ out, int layout, uint64_t cap, uint64_t row0,
+                                              uint32_t W4) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t chunks = (D + 63u) / 64u;             // 64-dim units per row
+    const uint32_t nbytes = (D + 7u) / 8u;
+    const uint32_t nwords_pad = 4u * W4;                 // padded u32 words per row
+    const uint64_t units = n * (uint64_t)chunks;
+    for (uint64_t u = wave; u < units; u += nwaves) {
+        const uint64_t r = u / chunks;
+        const uint32_t c = (uint32_t)(u - r * chunks);
+        const uint32_t dim = c * 64u + lane;
+        // NaN > thr is false, like Rust's `value > threshold`.
+        const bool bit = dim < D && rows[r * D + dim] > thr;
+        const uint64_t m = __ballot(bit);
+        if (lane < 2) {
+            const uint32_t w = 2u * c + lane;
+            const uint32_t word = msb0_word(lane == 0 ? (uint32_t)m : (uint32_t)(m >> 32));
+            if (layout == kPackBytesAoS) {
+                uint8_t* o = (uint8_t*)out + r * nbytes;
+                for (uint32_t b = 0; b < 4; ++b)
+                    if (4u * w + b < nbytes) o[4u * w + b] = (uint8_t)(word >> (8u * b));
+            } else if (layout == kPackWordsAoS) {
+                if (w < nwords_pad) ((uint32_t*)out)[r * nwords_pad + w] = word;
+            } else {
+                if (w < nwords_pad) {
+                    uint32_t* planes = (uint32_t*)out;
+                    planes[(((uint64_t)(w >> 2) * cap) + row0 + r) * 4u + (w & 3u)] = word;
+                }
+            }
+        }
+        // zero the pad words beyond the last 64-dim unit (SoA / words layouts)
+        if (c == chunks - 1 && layout != kPackBytesAoS) {
+            for (uint32_t w = 2u * chunks + lane; w < nwords_pad; w += 64u) {
+                if (layout == kPackWordsAoS) ((uint32_t*)out)[r * nwords_pad + w] = 0u;
+                else ((uint32_t*)out)[(((uint64_t)(w >> 2) * cap) + row0 + r) * 4u + (w & 3u)] = 0u;
+            }
+        }
+    }
+}
+
+hipError_t launch_pack(const float* rows, uint64_t n, uint32_t D, float thr, void* out, int layout, uint64_t cap,
+                       uint64_t row0, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t units = n * ((D + 63u) / 64u);
+    uint64_t blocks = (units + 3) / 4;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_pack, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, D, thr, out, layout, cap, row0,
+                       code_w4(D));
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+__global__ void k_bytes_to_soa(const uint8_t* __restrict__ bytes, uint64_t n, uint32_t nbytes, uint32_t nwords,
+                               uint32_t* __restrict__ planes, uint64_t cap, uint64_t row0) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= n * nwords) return;
+    const uint64_t r = t / nwords;
+    const uint32_t w = (uint32_t)(t - r * nwords);
+    uint32_t word = 0;
+    for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t idx = 4u * w + b;
+        if (idx < nbytes) word |= (uint32_t)bytes[r * nbytes + idx] << (8u * b);
+    }
+    planes[(((uint64_t)(w >> 2) * cap) + row0 + r) * 4u + (w & 3u)] = word;
+}
+
+hipError_t launch_bytes_to_soa(const uint8_t* bytes, uint64_t n, uint32_t D, uint4* codes, uint64_t cap,
+                               uint64_t row0, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t nwords = 4u * code_w4(D);
+    const uint64_t total = n * nwords;
+    hipLaunchKernelGGL(k_bytes_to_soa, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, bytes, n,
+                       (D + 7u) / 8u, nwords, (uint32_t*)codes, cap, row0);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+__global__ void k_bytes_to_words(const uint8_t* __restrict__ bytes, uint64_t n, uint32_t nbytes, uint32_t nwords,
+                                 uint32_t* __restrict__ words) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (t >= n * nwords) return;
+    const uint64_t r = t / nwords;
+    const uint32_t w = (uint32_t)(t - r * nwords);
+    uint32_t word = 0;
+    for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t idx = 4u * w + b;
+        if (idx < nbytes) word |= (uint32_t)bytes[r * nbytes + idx] << (8u * b);
+    }
+    words[r * nwords + w] = word;
+}
+
+hipError_t launch_bytes_to_words(const uint8_t* bytes, uint64_t n, uint32_t D, uint32_t* words, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t nwords = 4u * code_w4(D);
+    const uint64_t total = n * nwords;
+    hipLaunchKernelGGL(k_bytes_to_words, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, bytes, n,
+                       (D + 7u) / 8u, nwords, words);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// hamming 0.1.3 distance over byte slices (quantization.rs:139).
+__global__ void k_hamming_pairs(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, uint64_t n,
+                                uint32_t nbytes, uint32_t* __restrict__ out) {
+    const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    uint32_t d = 0;
+    const uint8_t* pa = a + r * nbytes;
+    const uint8_t* pb = b + r * nbytes;
+    for (uint32_t i = 0; i < nbytes; ++i) d += __builtin_popcount((uint32_t)(pa[i] ^ pb[i]));
+    out[r] = d;
+}
+
+hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t D, uint32_t* out,
+                                hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hamming_pairs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a, b, n, (D + 7u) / 8u,
+                       out);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ============================================================================
+// Sequential-order f32 reductions through an LDS row tile.
+//
+// One lane owns one row and folds it left to right, exactly like Rust's
+// `iter().map(..).sum::<f32>()`.  To keep the HBM reads coalesced, each wave
+// first stages a [64 rows][32 dims] tile in LDS (16-B loads, 8 lanes per
+// 128-B row segment), then every lane reads its own row back with
+// ds_read_b128.  Row stride 36 floats: conflict-free for both the
+// ds_write_b128 (8-lane groups) and the ds_read_b128 (16-lane groups).
+// ============================================================================
+constexpr int kCh = 32;        // dims per staged chunk
+constexpr int kTileLd = 36;    // padded LDS row stride (floats)
+
+// Stage rows[row_of(r)][c0 .. c0+32) for r = 0..63 into tile[r][0..32).
+// row_base[r] = element offset of row r, or UINT64_MAX for an absent row.
+// Elements at/after `len` are written as 0 (never read by the fold).
+__device__ __forceinline__ void stage_tile(float* tile, const float* __restrict__ src, const uint64_t* row_base,
+                                           uint64_t c0, uint64_t len, bool vec4, uint32_t lane) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const uint32_t idx = it * 64u + lane;
+        const uint32_t r = idx >> 3;
+        const uint32_t c4 = idx & 7u;
+        const uint64_t base = row_base[r];
+        const uint64_t j = c0 + 4u * c4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (base != ~0ull) {
+            if (vec4 && j + 3 < len) {
+                v = *(const float4*)(src + base + j);
+            } else {
+                if (j + 0 < len) v.x = src[base + j + 0];
+                if (j + 1 < len) v.y = src[base + j + 1];
+                if (j + 2 < len) v.z = src[base + j + 2];
+                if (j + 3 < len) v.w = src[base + j + 3];
+            }
+        }
+        *(float4*)(tile + r * kTileLd + 4u * c4) = v;
+    }
+}
+
+// sqrt(sum x*x) per row, bit-identical to `a.iter().map(|x| x*x).sum::<f32>().sqrt()`.
+__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ rows, uint64_t n, uint32_t D,
+                                                   float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float tiles[4][64 * kTileLd];
+    __shared__ uint64_t bases[4][64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    float* tile = tiles[wv];
+    const uint64_t r0 = ((uint64_t)blockIdx.x * 4u + wv) * 64u;
+    const uint64_t myrow = r0 + lane;
+    bases[wv][lane] = myrow < n ? myrow * D : ~0ull;
+    __syncthreads();
+    const bool vec4 = (D & 3u) == 0;
+    float s = -0.0f;
+    for (uint64_t c0 = 0; c0 < D; c0 += kCh) {
+        stage_tile(tile, rows, bases[wv], c0, D, vec4, lane);
+        __syncthreads();
+        const uint32_t m = (uint32_t)((D - c0) < (uint64_t)kCh ? (D - c0) : kCh);
+        const float* tr = tile + lane * kTileLd;
+        if (m == kCh) {
+#pragma unroll
+            for (int j = 0; j < kCh; j += 4) {
+                const float4 v = *(const float4*)(tr + j);
+                s = s + v.x * v.x;
+                s = s + v.y * v.y;
+                s = s + v.z * v.z;
+                s = s + v.w * v.w;
+            }
+        } else {
+            for (uint32_t j = 0; j < m; ++j) s = s + tr[j] * tr[j];
+        }
+        __syncthreads();
+    }
+    if (myrow < n) out[myrow] = sqrtf(s);
+}
+
+hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t D, float* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_row_norms, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, D, out);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ============================================================================
+// K2: BQ Hamming stage 1
+// ============================================================================
+// popcount(x) + acc as ONE v_bcnt_u32_b32 (the accumulate form).  Written as
+// inline asm because LLVM otherwise re-associates the chain into
+// v_bcnt(x, 0) + v_add3 trees: +1 VALU op per 2 words on the hot loop.
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ uint32_t ham4(const uint4& c, const uint4& q, uint32_t acc) {
+    acc = bcnt_acc(c.x ^ q.x, acc);
+    acc = bcnt_acc(c.y ^ q.y, acc);
+    acc = bcnt_acc(c.z ^ q.z, acc);
+    acc = bcnt_acc(c.w ^ q.w, acc);
+    return acc;
+}
+
+// Sample histogram: blockIdx.x = sample chunk (4096 contiguous rows starting
+// at chunk*stride), blockIdx.y = query tile of QT queries.  LDS histogram per
+// query, flushed with global atomics (non-zero bins only).
+template <int W4>
+__global__ __launch_bounds__(256) void k_sample_hist(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                     uint32_t D, uint32_t stride, const uint4* __restrict__ qcodes,
+                                                     uint32_t B, uint32_t QT, uint32_t* __restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lh[];
+    const uint32_t nb = D + 1u;
+    for (uint32_t i = threadIdx.x; i < QT * nb; i += 256) lh[i] = 0u;
+    __syncthreads();
+    const uint64_t start = (uint64_t)blockIdx.x * stride;
+    const uint32_t q0 = blockIdx.y * QT;
+    const uint32_t qn = (B - q0) < QT ? (B - q0) : QT;
+    for (uint32_t it = 0; it < 16; ++it) {
+        const uint64_t row = start + it * 256u + threadIdx.x;
+        if (row >= N) break;
+        uint4 c[W4];
+#pragma unroll
+        for (int w = 0; w < W4; ++w) c[w] = codes[(uint64_t)w * cap + row];
+        for (uint32_t qi = 0; qi < qn; ++qi) {
+            const uint4* qc = qcodes + (uint64_t)(q0 + qi) * W4;
+            uint32_t d = 0;
+#pragma unroll
+            for (int w = 0; w < W4; ++w) d = ham4(c[w], qc[w], d);
+            atomicAdd(&lh[qi * nb + d], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < qn * nb; i += 256) {
+        const uint32_t v = lh[i];
+        if (v) atomicAdd(&hist[(uint64_t)(q0 + i / nb) * nb + (i % nb)], v);
+    }
+}
+
+// T[q] = smallest t with (sample count of d <= t) >= target; D if never.
+// Also emits T into counts' companion (thr) and resets nothing else.
+__global__ void k_threshold(const uint32_t* __restrict__ hist, uint32_t B, uint32_t D, uint32_t target,
+                            uint32_t* __restrict__ thr) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= B) return;
+    const uint32_t* h = hist + (uint64_t)q * (D + 1u);
+    uint32_t cum = 0, t = D;
+    for (uint32_t i = 0; i <= D; ++i) {
+        cum += h[i];
+        if (cum >= target) {
+            t = i;
+            break;
+        }
+    }
+    thr[q] = t;
+}
+
+// The hot loop.  Each lane holds CPL rows' codes in VGPRs (coalesced 16-B
+// loads from the SoA planes); the batch's query codes are wave-uniform and
+// arrive through scalar loads, so one pair costs W4*4 x (v_xor_b32 +
+// v_bcnt_u32_b32) plus one compare per CPL rows.  Rows with d <= T[q] are
+// appended to the query's candidate buffer as (d << 32 | row).
+template <int W4, int CPL>
+__global__ __launch_bounds__(256) void k_scan(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                              const uint4* __restrict__ qcodes, const uint32_t* __restrict__ thr,
+                                              uint32_t B, uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                              uint32_t bufcap) {
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * (256u * CPL);
+    uint4 c[CPL][W4];
+    uint32_t bias[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const uint64_t n = base + (uint64_t)k * 256u + tid;
+        const bool ok = n < N;
+        const uint64_t nc = ok ? n : (uint64_t)(N - 1);
+        bias[k] = ok ? 0u : 0x01000000u;  // out-of-range rows never pass the threshold
+#pragma unroll
+        for (int w = 0; w < W4; ++w) c[k][w] = codes[(uint64_t)w * cap + nc];
+    }
+    // query codes are wave-uniform: scalar loads.  For narrow codes the next
+    // query is prefetched into SGPRs so the s_load latency hides under the
+    // current query's VALU work; wide codes would not fit the SGPR file.
+    constexpr bool kPrefetch = W4 <= 6;
+    uint4 qw[W4];
+    uint32_t T = thr[0];
+#pragma unroll
+    for (int w = 0; w < W4; ++w) qw[w] = qcodes[w];
+    for (uint32_t q = 0; q < B; ++q) {
+        const uint32_t qnext = (q + 1 < B) ? q + 1 : q;
+        uint4 qn[W4];
+        uint32_t Tn = 0;
+        if constexpr (kPrefetch) {
+#pragma unroll
+            for (int w = 0; w < W4; ++w) qn[w] = qcodes[(uint64_t)qnext * W4 + w];
+            Tn = thr[qnext];
+        } else {
+#pragma unroll
+            for (int w = 0; w < W4; ++w) qw[w] = qcodes[(uint64_t)q * W4 + w];
+            T = thr[q];
+        }
+        uint32_t d[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) d[k] = bias[k];
+#pragma unroll
+        for (int w = 0; w < W4; ++w) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) d[k] = ham4(c[k][w], qw[w], d[k]);
+        }
+        uint32_t dmin = d[0];
+#pragma unroll
+        for (int k = 1; k < CPL; ++k) dmin = min(dmin, d[k]);
+        if (dmin <= T) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                if (d[k] <= T) {
+                    const uint32_t pos = atomicAdd(&counts[q], 1u);
+                    if (pos < bufcap)
+                        buf[(uint64_t)q * bufcap + pos] =
+                            ((uint64_t)d[k] << 32) | (uint32_t)(base + (uint64_t)k * 256u + tid);
+                }
+            }
+        }
+        if constexpr (kPrefetch) {
+#pragma unroll
+            for (int w = 0; w < W4; ++w) qw[w] = qn[w];
+            T = Tn;
+        }
+    }
+}
+
+// Generic scan for codes wider than the templated set: codes re-read per
+// query (L1/L2 resident within the block).
+__global__ __launch_bounds__(256) void k_scan_generic(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                      uint32_t W4, const uint4* __restrict__ qcodes,
+                                                      const uint32_t* __restrict__ thr, uint32_t B,
+                                                      uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                      uint32_t bufcap) {
+    const uint64_t n = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (n >= N) return;
+    for (uint32_t q = 0; q < B; ++q) {
+        const uint4* qc = qcodes + (uint64_t)q * W4;
+        uint32_t d = 0;
+        for (uint32_t w = 0; w < W4; ++w) d = ham4(codes[(uint64_t)w * cap + n], qc[w], d);
+        if (d <= thr[q]) {
+            const uint32_t pos = atomicAdd(&counts[q], 1u);
+            if (pos < bufcap) buf[(uint64_t)q * bufcap + pos] = ((uint64_t)d << 32) | (uint32_t)n;
+        }
+    }
+}
+
+__global__ void k_sample_hist_generic(const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t D,
+                                      uint32_t W4, uint32_t stride, const uint4* __restrict__ qcodes, uint32_t B,
+                                      uint32_t* __restrict__ hist) {
+    const uint64_t start = (uint64_t)blockIdx.x * stride;
+    const uint32_t q = blockIdx.y;
+    const uint4* qc = qcodes + (uint64_t)q * W4;
+    for (uint32_t it = 0; it < 16; ++it) {
+        const uint64_t row = start + it * 256u + threadIdx.x;
+        if (row >= N) break;
+        uint32_t d = 0;
+        for (uint32_t w = 0; w < W4; ++w) d = ham4(codes[(uint64_t)w * cap + row], qc[w], d);
+        atomicAdd(&hist[(uint64_t)q * (D + 1u) + d], 1u);
+    }
+}
+
+// In-LDS bitonic sort (ascending) of P = power-of-two u64 keys by a whole
+// workgroup.
+__device__ void bitonic_sort_lds(uint64_t* s, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        s[i] = b;
+                        s[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// Exact top-R from the candidate buffer: histogram -> T_R (R-th smallest d),
+// gather every key with d <= T_R, sort (d, row) ascending, keep R.  Any
+// uncertainty (too few keys: threshold estimate too tight; buffer overflow;
+// too many ties for LDS) raises fail[q] and the host reruns that query on the
+// exact slow path.
+__global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ counts, const uint64_t* __restrict__ buf,
+                                                uint32_t bufcap, uint32_t D, uint32_t R, uint32_t* __restrict__ fail,
+                                                uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist
+    uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
+    __shared__ uint32_t s_T, s_n;
+    const uint32_t q = blockIdx.x;
+    const uint32_t cnt = counts[q];
+    if (cnt < R || cnt > bufcap) {
+        if (threadIdx.x == 0) fail[q] = 1u;
+        return;
+    }
+    const uint64_t* b = buf + (uint64_t)q * bufcap;
+    for (uint32_t i = threadIdx.x; i <= D; i += 256) hist[i] = 0u;
+    if (threadIdx.x == 0) s_n = 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += 256) atomicAdd(&hist[(uint32_t)(b[i] >> 32)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t cum = 0, t = D;
+        for (uint32_t i = 0; i <= D; ++i) {
+            cum += hist[i];
+            if (cum >= R) {
+                t = i;
+                break;
+            }
+        }
+        s_T = t;
+    }
+    __syncthreads();
+    const uint32_t T = s_T;
+    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+        const uint64_t key = b[i];
+        if ((uint32_t)(key >> 32) <= T) {
+            const uint32_t pos = atomicAdd(&s_n, 1u);
+            if (pos < kSelectLdsCap) sk[pos] = key;
+        }
+    }
+    __syncthreads();
+    const uint32_t n = s_n;
+    if (n > kSelectLdsCap) {
+        if (threadIdx.x == 0) fail[q] = 1u;
+        return;
+    }
+    const uint32_t P = next_pow2(n);
+    for (uint32_t i = n + threadIdx.x; i < P; i += 256) sk[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_lds(sk, P);
+    for (uint32_t i = threadIdx.x; i < R; i += 256) {
+        const uint64_t key = sk[i];
+        s1_rows[(uint64_t)q * R + i] = (uint32_t)key;
+        s1_dist[(uint64_t)q * R + i] = (uint32_t)(key >> 32);
+    }
+}
+
+template <int W4, int CPL>
+static void launch_scan_t(const Stage1Args& a, hipStream_t s) {
+    const uint64_t per_block = 256ull * CPL;
+    const uint32_t blocks = (uint32_t)((a.N + per_block - 1) / per_block);
+    hipLaunchKernelGGL((k_scan<W4, CPL>), dim3(blocks), dim3(256), 0, s, a.codes, a.cap, a.N, a.qcodes, a.thr, a.B,
+                       a.counts, a.buf, a.bufcap);
+}
+
+template <int W4>
+static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
+    uint32_t QT = 12288u / (a.D + 1u);
+    if (QT < 1) QT = 1;
+    if (QT > 32) QT = 32;
+    if (QT > a.B) QT = a.B;
+    const size_t lds = (size_t)QT * (a.D + 1u) * 4u;
+    hipLaunchKernelGGL((k_sample_hist<W4>), dim3(a.sample_chunks, (a.B + QT - 1) / QT), dim3(256), lds, s, a.codes,
+                       a.cap, a.N, a.D, a.sample_stride, a.qcodes, a.B, QT, a.hist);
+}
+
+hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
+    const uint32_t W4 = code_w4(a.D);
+    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+    switch (W4) {
+#define GVDB_CASE(w, cpl)            \
+    case w:                          \
+        launch_hist_t<w>(a, s);      \
+        break;
+        GVDB_CASE(1, 8)
+        GVDB_CASE(2, 8)
+        GVDB_CASE(3, 8)
+        GVDB_CASE(4, 4)
+        GVDB_CASE(6, 4)
+        GVDB_CASE(8, 2)
+        GVDB_CASE(12, 2)
+        GVDB_CASE(16, 1)
+        GVDB_CASE(24, 1)
+        GVDB_CASE(32, 1)
+#undef GVDB_CASE
+        default:
+            hipLaunchKernelGGL(k_sample_hist_generic, dim3(a.sample_chunks, a.B), dim3(256), 0, s, a.codes, a.cap,
+                               a.N, a.D, W4, a.sample_stride, a.qcodes, a.B, a.hist);
+    }
+    GVDB_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_threshold, dim3((a.B + 255) / 256), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
+    GVDB_LAUNCH_CHECK();
+    if (a.ev) (void)hipEventRecord(a.ev[1], s);
+    switch (W4) {
+#define GVDB_CASE(w, cpl)             \
+    case w:                           \
+        launch_scan_t<w, cpl>(a, s);  \
+        break;
+        GVDB_CASE(1, 8)
+        GVDB_CASE(2, 8)
+        GVDB_CASE(3, 8)
+        GVDB_CASE(4, 4)
+        GVDB_CASE(6, 4)
+        GVDB_CASE(8, 2)
+        GVDB_CASE(12, 2)
+        GVDB_CASE(16, 1)
+        GVDB_CASE(24, 1)
+        GVDB_CASE(32, 1)
+#undef GVDB_CASE
+        default:
+            hipLaunchKernelGGL(k_scan_generic, dim3((a.N + 255) / 256), dim3(256), 0, s, a.codes, a.cap, a.N, W4,
+                               a.qcodes, a.thr, a.B, a.counts, a.buf, a.bufcap);
+    }
+    GVDB_LAUNCH_CHECK();
+    if (a.ev) (void)hipEventRecord(a.ev[2], s);
+    const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)(a.D + 1u) * 4u;
+    hipLaunchKernelGGL(k_select, dim3(a.B), dim3(256), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R, a.fail,
+                       a.s1_rows, a.s1_dist);
+    GVDB_LAUNCH_CHECK();
+    if (a.ev) (void)hipEventRecord(a.ev[3], s);
+    return hipSuccess;
+}
+
+// ---- exact slow path (one query) --------------------------------------------------
+__global__ void k_dist_all(const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t W4,
+                           const uint4* __restrict__ qc, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const uint64_t n = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    uint32_t d = 0;
+    for (uint32_t w = 0; w < W4; ++w) d = ham4(codes[(uint64_t)w * cap + n], qc[w], d);
+    keys[n] = d;
+    vals[n] = (uint32_t)n;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static size_t cub_pairs_u32_bytes(uint32_t N) {
+    size_t bytes = 0;
+    hipcub::DoubleBuffer<uint32_t> k(nullptr, nullptr), v(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k, v, (int)N, 0, 32);
+    return bytes;
+}
+
+size_t stage1_slow_bytes(uint32_t N) { return 4 * align256((size_t)N * 4) + align256(cub_pairs_u32_bytes(N)); }
+
+hipError_t launch_stage1_slow(const uint4* codes, uint64_t cap, uint32_t N, uint32_t D, const uint4* qcode, uint32_t R,
+                              uint32_t* out_rows, uint32_t* out_dist, void* tmp, size_t tmp_bytes, hipStream_t s) {
+    char* p = (char*)tmp;
+    const size_t a = align256((size_t)N * 4);
+    uint32_t* k0 = (uint32_t*)p;
+    uint32_t* k1 = (uint32_t*)(p + a);
+    uint32_t* v0 = (uint32_t*)(p + 2 * a);
+    uint32_t* v1 = (uint32_t*)(p + 3 * a);
+    void* ctmp = p + 4 * a;
+    size_t cbytes = tmp_bytes - 4 * a;
+    hipLaunchKernelGGL(k_dist_all, dim3((N + 255) / 256), dim3(256), 0, s, codes, cap, N, code_w4(D), qcode, k0, v0);
+    GVDB_LAUNCH_CHECK();
+    int end_bit = 1;
+    while ((1u << end_bit) <= D) ++end_bit;
+    hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(ctmp, cbytes, kb, vb, (int)N, 0, end_bit, s);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(out_rows, vb.Current(), (size_t)R * 4, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+    return hipMemcpyAsync(out_dist, kb.Current(), (size_t)R * 4, hipMemcpyDeviceToDevice, s);
+}
+
+__global__ void k_iota_rows(uint32_t* rows, uint32_t B, uint32_t R) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)B * R) return;
+    rows[t] = (uint32_t)(t % R);
+}
+
+hipError_t launch_iota_rows(uint32_t* rows, uint32_t B, uint32_t R, hipStream_t s) {
+    const uint64_t total = (uint64_t)B * R;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_iota_rows, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, rows, B, R);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ============================================================================
+// K3: exact rerank.  Block = 4 waves of one query; lane = one stage-1
+// candidate; the lane folds q . x (or sum (q-x)^2) over the dims in order.
+// ============================================================================
+__global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ rows, uint64_t clen,
+                                                const float* __restrict__ norms, const float* __restrict__ q,
+                                                uint64_t qlen, const float* __restrict__ qnorm,
+                                                const uint32_t* __restrict__ s1_rows, uint32_t R, int kind,
+                                                float* __restrict__ scores) {
+    __shared__ __attribute__((aligned(16))) float tiles[4][64 * kTileLd];
+    __shared__ __attribute__((aligned(16))) float qs[kCh];
+    __shared__ uint64_t bases[4][64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t qi = blockIdx.y;
+    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+    const bool valid = r < R;
+    const uint32_t row = valid ? s1_rows[(uint64_t)qi * R + r] : 0u;
+    bases[wv][lane] = valid ? (uint64_t)row * clen : ~0ull;
+    const float* qv = q + (uint64_t)qi * qlen;
+    float* tile = tiles[wv];
+    // dot: zip(query, cand) truncates to min(qlen, clen); L2 uses the same length.
+    const uint64_t len = qlen < clen ? qlen : clen;
+    const bool vec4 = (clen & 3u) == 0;
+    float acc = -0.0f;
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 < len; c0 += kCh) {
+        stage_tile(tile, rows, bases[wv], c0, len, vec4, lane);
+        if (threadIdx.x < kCh) qs[threadIdx.x] = (c0 + threadIdx.x < len) ? qv[c0 + threadIdx.x] : 0.0f;
+        __syncthreads();
+        const uint32_t m = (uint32_t)((len - c0) < (uint64_t)kCh ? (len - c0) : kCh);
+        const float* tr = tile + lane * kTileLd;
+        if (kind == kScoreL2) {
+            for (uint32_t j = 0; j < m; ++j) {
+                const float d = qs[j] - tr[j];
+                acc = acc + d * d;
+            }
+        } else if (m == kCh) {
+#pragma unroll
+            for (int j = 0; j < kCh; j += 4) {
+                const float4 v = *(const float4*)(tr + j);
+                const float4 w = *(const float4*)(qs + j);
+                acc = acc + w.x * v.x;
+                acc = acc + w.y * v.y;
+                acc = acc + w.z * v.z;
+                acc = acc + w.w * v.w;
+            }
+        } else {
+            for (uint32_t j = 0; j < m; ++j) acc = acc + qs[j] * tr[j];
+        }
+        __syncthreads();
+    }
+    if (!valid) return;
+    float score;
+    if (kind == kScoreL2) {
+        score = sqrtf(acc);
+    } else {
+        const float na = qnorm[qi], nb = norms[row];
+        if (kind == kScoreCosine) {
+            score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+        } else {
+            score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+        }
+    }
+    scores[(uint64_t)qi * R + r] = score;
+}
+
+hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
+    if (a.B == 0 || a.R == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rerank, dim3((a.R + 255) / 256, a.B), dim3(256), 0, s, a.rows, a.clen, a.norms, a.q, a.qlen,
+                       a.qnorm, a.s1_rows, a.R, a.kind, a.scores);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// Total order key for f32 scores: -0.0 == +0.0 (Rust partial_cmp), ascending.
+__device__ __forceinline__ uint32_t f32_order(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (u == 0x80000000u) u = 0u;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(256) void k_final_sort(const float* __restrict__ scores,
+                                                    const uint32_t* __restrict__ s1_rows, uint32_t R, uint32_t kout,
+                                                    int descending, const uint64_t* __restrict__ ids,
+                                                    uint64_t row_offset, uint64_t* __restrict__ out_ids,
+                                                    float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
+                                                    uint32_t* __restrict__ nan_flag) {
+    __shared__ uint64_t sk[kSortLdsCap];
+    __shared__ uint32_t s_nan;
+    const uint32_t q = blockIdx.x;
+    const float* sc = scores + (uint64_t)q * R;
+    if (threadIdx.x == 0) s_nan = 0u;
+    __syncthreads();
+    const uint32_t P = next_pow2(R);
+    for (uint32_t i = threadIdx.x; i < P; i += 256) {
+        uint64_t key = ~0ull;
+        if (i < R) {
+            const float f = sc[i];
+            if (f != f) s_nan = 1u;
+            uint32_t o = f32_order(f);
+            if (descending) o = ~o;
+            key = ((uint64_t)o << 32) | i;  // ties: stage-1 rank ascending (stable sort)
+        }
+        sk[i] = key;
+    }
+    __syncthreads();
+    if (s_nan && R >= 2) {
+        if (threadIdx.x == 0) atomicOr(nan_flag, 1u);
+    }
+    bitonic_sort_lds(sk, P);
+    const uint32_t take = kout < R ? kout : R;
+    // take(k) then drop orphan rows (index.rs:217-228); order-preserving
+    // compaction by wave 0 with a ballot prefix.
+    if (threadIdx.x < 64) {
+        uint32_t o = 0;
+        for (uint32_t i0 = 0; i0 < take; i0 += 64) {
+            const uint32_t i = i0 + threadIdx.x;
+            uint64_t id = kOrphan;
+            uint32_t rank = 0;
+            if (i < take) {
+                rank = (uint32_t)sk[i];
+                const uint32_t row = s1_rows[(uint64_t)q * R + rank];
+                id = ids ? ids[row] : (uint64_t)row + row_offset;
+            }
+            const bool keep = i < take && id != kOrphan;
+            const uint64_t m = __ballot(keep);
+            const uint32_t before = __popcll(m & ((1ull << threadIdx.x) - 1ull));
+            if (keep) {
+                out_ids[(uint64_t)q * kout + o + before] = id;
+                out_scores[(uint64_t)q * kout + o + before] = sc[rank];
+            }
+            o += __popcll(m);
+        }
+        if (threadIdx.x == 0 && out_n) out_n[q] = o;
+    }
+}
+
+hipError_t launch_final_sort(const FinalArgs& a, hipStream_t s) {
+    if (a.B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_final_sort, dim3(a.B), dim3(256), 0, s, a.scores, a.s1_rows, a.R, a.kout, a.descending, a.ids,
+                       a.row_offset, a.out_ids, a.out_scores, a.out_n, a.nan_flag);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// Large-R variant: per query, radix-sort (order key, rank) pairs in HBM.
+__global__ void k_make_keys(const float* __restrict__ sc, uint32_t R, int descending, uint32_t* __restrict__ keys,
+                            uint32_t* __restrict__ vals, uint32_t* __restrict__ nan_flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    const float f = sc[i];
+    if (f != f && R >= 2) atomicOr(nan_flag, 1u);
+    uint32_t o = f32_order(f);
+    keys[i] = descending ? ~o : o;
+    vals[i] = i;
+}
+
+__global__ void k_emit_sorted(const uint32_t* __restrict__ ranks, const float* __restrict__ sc,
+                              const uint32_t* __restrict__ s1_rows, uint32_t take, const uint64_t* __restrict__ ids,
+                              uint64_t row_offset, uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
+                              uint32_t* __restrict__ out_n) {
+    // single wave: order-preserving compaction of orphans via ballot prefix.
+    uint32_t o = 0;
+    for (uint32_t i0 = 0; i0 < take; i0 += 64) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint64_t id = kOrphan;
+        uint32_t rank = 0;
+        if (i < take) {
+            rank = ranks[i];
+            const uint32_t row = s1_rows[rank];
+            id = ids ? ids[row] : (uint64_t)row + row_offset;
+        }
+        const bool keep = i < take && id != kOrphan;
+        const uint64_t m = __ballot(keep);
+        const uint32_t before = __popcll(m & ((1ull << threadIdx.x) - 1ull));
+        if (keep) {
+            out_ids[o + before] = id;
+            out_scores[o + before] = sc[rank];
+        }
+        o += __popcll(m);
+    }
+    if (threadIdx.x == 0 && out_n) *out_n = o;
+}
+
+static size_t cub_pairs_bytes_u32(uint32_t n) { return cub_pairs_u32_bytes(n); }
+
+size_t final_sort_global_bytes(uint32_t R) { return 4 * align256((size_t)R * 4) + align256(cub_pairs_bytes_u32(R)); }
+
+hipError_t launch_final_sort_global(const FinalArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s) {
+    char* p = (char*)tmp;
+    const size_t al = align256((size_t)a.R * 4);
+    uint32_t* k0 = (uint32_t*)p;
+    uint32_t* k1 = (uint32_t*)(p + al);
+    uint32_t* v0 = (uint32_t*)(p + 2 * al);
+    uint32_t* v1 = (uint32_t*)(p + 3 * al);
+    void* ctmp = p + 4 * al;
+    const uint32_t take = a.kout < a.R ? a.kout : a.R;
+    for (uint32_t q = 0; q < a.B; ++q) {
+        size_t cbytes = tmp_bytes - 4 * al;
+        const float* sc = a.scores + (uint64_t)q * a.R;
+        hipLaunchKernelGGL(k_make_keys, dim3((a.R + 255) / 256), dim3(256), 0, s, sc, a.R, a.descending, k0, v0,
+                           a.nan_flag);
+        GVDB_LAUNCH_CHECK();
+        hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
+        hipError_t e = hipcub::DeviceRadixSort::SortPairs(ctmp, cbytes, kb, vb, (int)a.R, 0, 32, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_emit_sorted, dim3(1), dim3(64), 0, s, vb.Current(), sc, a.s1_rows + (uint64_t)q * a.R,
+                           take, a.ids, a.row_offset, a.out_ids + (uint64_t)q * a.kout,
+                           a.out_scores + (uint64_t)q * a.kout, a.out_n ? a.out_n + q : nullptr);
+        GVDB_LAUNCH_CHECK();
+    }
+    return hipSuccess;
+}
+
+// ============================================================================
+// Flat exact scan: scores[q][row] for a tile of QT queries per block, each
+// lane folding its row in order (bit-identical to storage.rs:851-865 /
+// index.rs:686-700 / index.rs:69-78).
+// ============================================================================
+constexpr int kFlatQT = 16;
+
+__global__ __launch_bounds__(256) void k_flat_scores(const float* __restrict__ q, uint32_t B,
+                                                     const float* __restrict__ qnorm, const float* __restrict__ rows,
+                                                     uint32_t N, uint32_t D, const float* __restrict__ norms, int kind,
+                                                     float* __restrict__ scores) {
+    __shared__ __attribute__((aligned(16))) float tiles[4][64 * kTileLd];
+    __shared__ __attribute__((aligned(16))) float qs[kFlatQT][kCh];
+    __shared__ uint64_t bases[4][64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t row = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t q0 = blockIdx.y * kFlatQT;
+    const uint32_t qn = (B - q0) < (uint32_t)kFlatQT ? (B - q0) : (uint32_t)kFlatQT;
+    bases[wv][lane] = row < N ? row * D : ~0ull;
+    float* tile = tiles[wv];
+    const bool vec4 = (D & 3u) == 0;
+    float acc[kFlatQT];
+#pragma unroll
+    for (int i = 0; i < kFlatQT; ++i) acc[i] = -0.0f;
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 < D; c0 += kCh) {
+        stage_tile(tile, rows, bases[wv], c0, D, vec4, lane);
+        for (uint32_t t = threadIdx.x; t < kFlatQT * kCh; t += 256) {
+            const uint32_t qi = t / kCh, j = t % kCh;
+            qs[qi][j] = (qi < qn && c0 + j < D) ? q[(uint64_t)(q0 + qi) * D + c0 + j] : 0.0f;
+        }
+        __syncthreads();
+        const uint32_t m = (uint32_t)((D - c0) < (uint64_t)kCh ? (D - c0) : kCh);
+        const float* tr = tile + lane * kTileLd;
+        for (uint32_t j = 0; j < m; ++j) {
+            const float x = tr[j];
+            if (kind == kScoreL2) {
+#pragma unroll
+                for (int i = 0; i < kFlatQT; ++i) {
+                    const float d = qs[i][j] - x;
+                    acc[i] = acc[i] + d * d;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < kFlatQT; ++i) acc[i] = acc[i] + qs[i][j] * x;
+            }
+        }
+        __syncthreads();
+    }
+    if (row >= N) return;
+    const float nb = norms ? norms[row] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < kFlatQT; ++i) {
+        if ((uint32_t)i >= qn) break;
+        float score;
+        if (kind == kScoreL2) {
+            score = sqrtf(acc[i]);
+        } else {
+            const float na = qnorm[q0 + i];
+            if (kind == kScoreCosine)
+                score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc[i] / (na * nb);
+            else
+                score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc[i] / (na * nb));
+        }
+        scores[(uint64_t)(q0 + i) * N + row] = score;
+    }
+}
+
+hipError_t launch_flat_scores(const float* q, uint32_t B, const float* qnorm, const float* rows, uint32_t N, uint32_t D,
+                              const float* norms, int kind, float* scores, hipStream_t s) {
+    if (B == 0 || N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_flat_scores, dim3((N + 255) / 256, (B + kFlatQT - 1) / kFlatQT), dim3(256), 0, s, q, B, qnorm,
+                       rows, N, D, norms, kind, scores);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+size_t flat_select_bytes(uint32_t N) { return final_sort_global_bytes(N); }
+
+__global__ void k_emit_flat(const uint32_t* __restrict__ ranks, const float* __restrict__ sc, uint32_t N,
+                            uint32_t limit, int has_threshold, float threshold, const uint64_t* __restrict__ ids,
+                            uint64_t* __restrict__ out_idx, float* __restrict__ out_scores,
+                            uint32_t* __restrict__ out_n) {
+    // Walk the sorted list; rows without an id are skipped BEFORE truncation
+    // (index.rs:626-631 iterates only mapped rows); with a threshold the
+    // sorted-descending list is cut at the first score < threshold
+    // (storage.rs:313-317 drops them before sorting: same survivors, same order).
+    uint32_t o = 0;
+    for (uint32_t i0 = 0; i0 < N && o < limit; i0 += 64) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool keep = false;
+        float f = 0.f;
+        uint64_t id = 0;
+        if (i < N) {
+            const uint32_t rank = ranks[i];
+            f = sc[rank];
+            id = ids ? ids[rank] : (uint64_t)rank;
+            keep = (!has_threshold || !(f < threshold)) && id != kOrphan;
+        }
+        const uint64_t m = __ballot(keep);
+        const uint32_t before = __popcll(m & ((1ull << threadIdx.x) - 1ull));
+        if (keep && o + before < limit) {
+            out_idx[o + before] = id;
+            out_scores[o + before] = f;
+        }
+        o += __popcll(m);
+    }
+    if (threadIdx.x == 0) *out_n = o < limit ? o : limit;
+}
+
+hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint32_t limit, int descending,
+                              int has_threshold, float threshold, const uint64_t* ids, uint64_t* out_idx,
+                              float* out_scores, uint32_t* out_n, void* tmp, size_t tmp_bytes, uint32_t* nan_flag,
+                              hipStream_t s) {
+    char* p = (char*)tmp;
+    const size_t al = align256((size_t)N * 4);
+    uint32_t* k0 = (uint32_t*)p;
+    uint32_t* k1 = (uint32_t*)(p + al);
+    uint32_t* v0 = (uint32_t*)(p + 2 * al);
+    uint32_t* v1 = (uint32_t*)(p + 3 * al);
+    void* ctmp = p + 4 * al;
+    for (uint32_t q = 0; q < B; ++q) {
+        size_t cbytes = tmp_bytes - 4 * al;
+        const float* sc = scores + (uint64_t)q * N;
+        hipLaunchKernelGGL(k_make_keys, dim3((N + 255) / 256), dim3(256), 0, s, sc, N, descending, k0, v0, nan_flag);
+        GVDB_LAUNCH_CHECK();
+        hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
+        hipError_t e = hipcub::DeviceRadixSort::SortPairs(ctmp, cbytes, kb, vb, (int)N, 0, 32, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_emit_flat, dim3(1), dim3(64), 0, s, vb.Current(), sc, N, limit, has_threshold, threshold,
+                           ids, out_idx + (uint64_t)q * limit, out_scores + (uint64_t)q * limit, out_n + q);
+        GVDB_LAUNCH_CHECK();
+    }
+    return hipSuccess;
+}
+
+// ============================================================================
+// Shard merge (shard.rs:776-784): per query concat the shards' lists in shard
+// order, stable sort by score, truncate.  One workgroup per query, LDS sort.
+// ============================================================================
+__global__ __launch_bounds__(256) void k_topk_merge(const uint64_t* __restrict__ ids, const float* __restrict__ scores,
+                                                    const uint32_t* __restrict__ counts, uint32_t n_shards, uint32_t B,
+                                                    uint32_t stride, uint32_t limit, int descending,
+                                                    uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
+                                                    uint32_t* __restrict__ out_n) {
+    __shared__ uint64_t sk[kSortLdsCap];
+    __shared__ uint32_t s_n;
+    const uint32_t q = blockIdx.x;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    // position in the concatenation = shard * stride + i (monotone in concat order)
+    for (uint32_t t = threadIdx.x; t < n_shards * stride; t += 256) {
+        const uint32_t sh = t / stride, i = t % stride;
+        if (i < counts[(uint64_t)sh * B + q]) {
+            const float f = scores[((uint64_t)sh * B + q) * stride + i];
+            uint32_t o = f32_order(f);
+            if (descending) o = ~o;
+            const uint32_t pos = atomicAdd(&s_n, 1u);
+            sk[pos] = ((uint64_t)o << 32) | t;
+        }
+    }
+    __syncthreads();
+    const uint32_t n = s_n;
+    const uint32_t P = next_pow2(n);
+    for (uint32_t i = n + threadIdx.x; i < P; i += 256) sk[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_lds(sk, P);
+    const uint32_t take = limit < n ? limit : n;
+    for (uint32_t i = threadIdx.x; i < take; i += 256) {
+        const uint32_t t = (uint32_t)sk[i];
+        const uint32_t sh = t / stride, j = t % stride;
+        out_ids[(uint64_t)q * limit + i] = ids[((uint64_t)sh * B + q) * stride + j];
+        out_scores[(uint64_t)q * limit + i] = scores[((uint64_t)sh * B + q) * stride + j];
+    }
+    if (threadIdx.x == 0) out_n[q] = take;
+}
+
+hipError_t launch_topk_merge(const uint64_t* ids, const float* scores, const uint32_t* counts, uint32_t n_shards,
+                             uint32_t B, uint32_t stride, uint32_t limit, int descending, uint64_t* out_ids,
+                             float* out_scores, uint32_t* out_n, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_topk_merge, dim3(B), dim3(256), 0, s, ids, scores, counts, n_shards, B, stride, limit,
+                       descending, out_ids, out_scores, out_n);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+__global__ void k_widen(const uint32_t* __restrict__ a, uint64_t* __restrict__ b, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[i] = a[i];
+}
+
+hipError_t launch_widen(const uint32_t* a, uint64_t* b, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_widen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a, b, n);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// Stage-1-ordered candidate list with exact scores (sharded search input).
+__global__ void k_emit_candidates(const uint32_t* __restrict__ s1_rows, const uint32_t* __restrict__ s1_dist,
+                                  const float* __restrict__ scores, uint32_t B, uint32_t R,
+                                  const uint64_t* __restrict__ ids, uint64_t* __restrict__ out_ids,
+                                  uint32_t* __restrict__ out_dist, float* __restrict__ out_scores) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)B * R) return;
+    out_ids[t] = ids ? ids[s1_rows[t]] : (uint64_t)s1_rows[t];
+    out_dist[t] = s1_dist[t];
+    out_scores[t] = scores[t];
+}
+
+hipError_t launch_emit_candidates(const uint32_t* s1_rows, const uint32_t* s1_dist, const float* scores, uint32_t B,
+                                  uint32_t R, const uint64_t* ids, uint64_t* out_ids, uint32_t* out_dist,
+                                  float* out_scores, hipStream_t s) {
+    const uint64_t total = (uint64_t)B * R;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_emit_candidates, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, s1_rows, s1_dist,
+                       scores, B, R, ids, out_ids, out_dist, out_scores);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ============================================================================
+// Exact sharded multi-stage merge.  Each shard sends, per query, its LOCAL
+// stage-1 top-R (Hamming d, global id) with the exact cosine of each; the
+// union of the local top-R lists contains the global top-R, so one exchange
+// suffices.  Per query: sort the union by (d asc, gid asc) == the reference's
+// stable stage-1 sort over the concatenated corpus, keep R, then sort those by
+// (cosine desc, global stage-1 rank asc), keep k.  Bit-identical to running
+// multi_stage_search on one device over all shards (ids = global row numbers).
+// ============================================================================
+__device__ void bitonic_sort_pairs_lds(uint64_t* s, uint32_t* v, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        s[i] = b;
+                        s[ixj] = a;
+                        const uint32_t t = v[i];
+                        v[i] = v[ixj];
+                        v[ixj] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restrict__ gids,
+                                                        const uint32_t* __restrict__ dist,
+                                                        const float* __restrict__ cosv,
+                                                        const uint32_t* __restrict__ counts, uint32_t G, uint32_t B,
+                                                        uint32_t stride, uint32_t R, uint32_t kout,
+                                                        uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
+                                                        uint32_t* __restrict__ out_n, uint32_t* __restrict__ nan_flag) {
+    __shared__ uint64_t sk[kSortLdsCap];
+    __shared__ uint32_t sv[kSortLdsCap];
+    __shared__ uint32_t s_n;
+    const uint32_t q = blockIdx.x;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < G * stride; t += 256) {
+        const uint32_t g = t / stride, i = t % stride;
+        if (i < counts[(uint64_t)g * B + q]) {
+            const uint64_t at = ((uint64_t)g * B + q) * stride + i;
+            const uint32_t pos = atomicAdd(&s_n, 1u);
+            sk[pos] = ((uint64_t)dist[at] << 40) | (gids[at] & ((1ull << 40) - 1));
+            sv[pos] = t;
+        }
+    }
+    __syncthreads();
+    const uint32_t n = s_n;
+    uint32_t P = next_pow2(n);
+    for (uint32_t i = n + threadIdx.x; i < P; i += 256) {
+        sk[i] = ~0ull;
+        sv[i] = 0;
+    }
+    __syncthreads();
+    bitonic_sort_pairs_lds(sk, sv, P);
+    const uint32_t r = R < n ? R : n;
+    // second key: cosine desc, then global stage-1 rank
+    __shared__ uint32_t s_nan;
+    if (threadIdx.x == 0) s_nan = 0;
+    __syncthreads();
+    const uint32_t P2 = next_pow2(r);
+    for (uint32_t i = threadIdx.x; i < P2; i += 256) {
+        uint64_t key = ~0ull;
+        uint32_t val = 0;
+        if (i < r) {
+            const uint32_t t = sv[i];
+            const uint32_t g = t / stride, j = t % stride;
+            const float f = cosv[((uint64_t)g * B + q) * stride + j];
+            if (f != f) s_nan = 1u;
+            key = ((uint64_t)(~f32_order(f)) << 32) | i;
+            val = t;
+        }
+        sk[i] = key;  // thread i reads and rewrites only slot i
+        sv[i] = val;
+    }
+    __syncthreads();
+    if (s_nan && r >= 2 && threadIdx.x == 0) atomicOr(nan_flag, 1u);
+    bitonic_sort_pairs_lds(sk, sv, P2);
+    const uint32_t take = kout < r ? kout : r;
+    for (uint32_t i = threadIdx.x; i < take; i += 256) {
+        const uint32_t t = sv[i];
+        const uint32_t g = t / stride, j = t % stride;
+        const uint64_t at = ((uint64_t)g * B + q) * stride + j;
+        out_ids[(uint64_t)q * kout + i] = gids[at];
+        out_scores[(uint64_t)q * kout + i] = cosv[at];
+    }
+    if (threadIdx.x == 0 && out_n) out_n[q] = take;
+}
+
+hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cosv, const uint32_t* counts,
+                                 uint32_t G, uint32_t B, uint32_t stride, uint32_t R, uint32_t kout, uint64_t* out_ids,
+                                 float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bq_shard_merge, dim3(B), dim3(256), 0, s, gids, dist, cosv, counts, G, B, stride, R, kout,
+                       out_ids, out_scores, out_n, nan_flag);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ============================================================================
+// Order-preserving gather (remove_vector compaction, index.rs:245-266)
+// ============================================================================
+__global__ void k_gather_rows(const float* __restrict__ src, float* __restrict__ dst, const uint64_t* __restrict__ map,
+                              uint64_t m, uint32_t D) {
+    const uint64_t r = blockIdx.y * (uint64_t)gridDim.x + blockIdx.x;
+    if (r >= m) return;
+    const float* s = src + map[r] * D;
+    float* d = dst + r * D;
+    for (uint32_t j = threadIdx.x; j < D; j += blockDim.x) d[j] = s[j];
+}
+
+__global__ void k_gather_meta(const uint4* __restrict__ codes, uint4* __restrict__ ncodes, const float* __restrict__ norms,
+                              float* __restrict__ nnorms, const uint64_t* __restrict__ ids, uint64_t* __restrict__ nids,
+                              const uint64_t* __restrict__ map, uint64_t m, uint64_t cap, uint32_t W4) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const uint64_t o = map[r];
+    for (uint32_t w = 0; w < W4; ++w) ncodes[(uint64_t)w * cap + r] = codes[(uint64_t)w * cap + o];
+    nnorms[r] = norms[o];
+    nids[r] = ids[o];
+}
+
+hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, uint4* ncodes, const float* norms,
+                         float* nnorms, const uint64_t* ids, uint64_t* nids, const uint64_t* map, uint64_t m,
+                         uint64_t cap, uint32_t D, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    const uint32_t gx = (uint32_t)(m < 65535 ? m : 65535);
+    const uint32_t gy = (uint32_t)((m + gx - 1) / gx);
+    hipLaunchKernelGGL(k_gather_rows, dim3(gx, gy), dim3(256), 0, s, rows, nrows, map, m, D);
+    GVDB_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_gather_meta, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, codes, ncodes, norms, nnorms,
+                       ids, nids, map, m, cap, code_w4(D));
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+}  // namespace gvdb

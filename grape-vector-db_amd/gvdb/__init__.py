@@ -1,0 +1,405 @@
+"""gvdb — host-side mirror of grape-vector-db's vector hot-path API over the
+MI355X C ABI (include/gvdb.h, libgvdb.so).
+
+Reference interfaces mirrored (reference snapshot 2025-08-24, Rust):
+  * ``VectorIndex`` trait                    src/index.rs:35-62
+    -> :class:`GpuVectorIndex` (alias ``HnswVectorIndex``: the drop-in for
+       HnswVectorIndex, index.rs:91-310)
+  * ``IndexStats``                           src/index.rs:83-88
+  * ``BinaryQuantizationConfig``             src/quantization.rs:10-31
+  * ``BinaryVector``                         src/quantization.rs:35-63
+  * ``BinaryQuantizer``                      src/quantization.rs:67-216
+  * ``VectorStore::vector_search`` (flat)    src/storage.rs:296-339 -> :func:`flat_search`
+  * ``ShardManager::search_vectors`` merge   src/distributed/shard.rs:776-784 -> :func:`topk_merge`
+  * ``VectorDbError``                        src/types.rs:859-920
+
+String ids stay on the host: each distinct string gets a stable u64; the C
+ABI reproduces HashMap-insert shadowing for a re-added id.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import lib, ptr
+
+__all__ = [
+    "VectorDbError", "IndexNotBuilt", "DimensionMismatch", "InvalidVectorDimension", "QuantizationError",
+    "IndexError_", "DeviceError", "BinaryQuantizationConfig", "BinaryVector", "BinaryQuantizer",
+    "IndexStats", "GpuVectorIndex", "HnswVectorIndex", "SearchParams", "flat_search", "topk_merge", "lib",
+]
+
+
+# ---------------------------------------------------------------------------
+# errors (VectorDbError, types.rs:859-920)
+# ---------------------------------------------------------------------------
+class VectorDbError(Exception):
+    code = -1
+
+
+class IndexNotBuilt(VectorDbError):
+    code = _ffi.GVDB_ERR_INDEX_NOT_BUILT
+
+
+class DimensionMismatch(VectorDbError):
+    code = _ffi.GVDB_ERR_DIMENSION_MISMATCH
+
+    def __init__(self, msg: str, expected: int = 0, actual: int = 0):
+        super().__init__(msg)
+        self.expected = expected
+        self.actual = actual
+
+
+class InvalidVectorDimension(VectorDbError):
+    code = _ffi.GVDB_ERR_INVALID_VECTOR_DIMENSION
+
+
+class QuantizationError(VectorDbError):
+    code = _ffi.GVDB_ERR_QUANTIZATION
+
+
+class IndexError_(VectorDbError):
+    code = _ffi.GVDB_ERR_INDEX
+
+
+class InvalidArgument(VectorDbError):
+    code = _ffi.GVDB_ERR_INVALID_ARGUMENT
+
+
+class DeviceError(VectorDbError):
+    code = _ffi.GVDB_ERR_DEVICE
+
+
+class OutOfMemory(DeviceError):
+    code = _ffi.GVDB_ERR_OUT_OF_MEMORY
+
+
+_ERRORS = {c.code: c for c in (IndexNotBuilt, DimensionMismatch, InvalidVectorDimension, QuantizationError,
+                               IndexError_, InvalidArgument, DeviceError, OutOfMemory)}
+
+
+def check(status: int) -> None:
+    if status == _ffi.GVDB_OK:
+        return
+    L = lib()
+    msg = (L.gvdb_last_error() or b"").decode(errors="replace")
+    cls = _ERRORS.get(status, VectorDbError)
+    if cls is DimensionMismatch:
+        e, a = C.c_uint64(), C.c_uint64()
+        L.gvdb_last_dimension_mismatch(C.byref(e), C.byref(a))
+        raise DimensionMismatch(msg, e.value, a.value)
+    raise cls(msg)
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+# ---------------------------------------------------------------------------
+# BinaryQuantizer (quantization.rs)
+# ---------------------------------------------------------------------------
+@dataclass
+class BinaryQuantizationConfig:
+    """quantization.rs:10-31 (defaults 22-30)."""
+    threshold: float = 0.0
+    enable_simd: bool = True
+    rescore_ratio: float = 0.1
+    enable_cache: bool = True
+
+
+@dataclass
+class BinaryVector:
+    """quantization.rs:35-63: BitVec<u8, Msb0> bytes + original dimension."""
+    data: bytes
+    dimension: int
+
+    def byte_size(self) -> int:
+        return (self.dimension + 7) // 8
+
+    def to_bytes(self) -> bytes:
+        return bytes(self.data)
+
+    @staticmethod
+    def from_bytes(b: bytes, dimension: int) -> "BinaryVector":
+        return BinaryVector(bytes(b), dimension)
+
+    def bits(self) -> List[bool]:
+        return [bool(self.data[i >> 3] & (0x80 >> (i & 7))) for i in range(self.dimension)]
+
+
+class BinaryQuantizer:
+    """quantization.rs:67-216, computed on the GPU through the C ABI.
+
+    The reference's cache (89-109) memoises identical bits; it changes no
+    result, so this mirror keeps only its statistics surface.
+    """
+
+    def __init__(self, config: Optional[BinaryQuantizationConfig] = None):
+        self.config = config or BinaryQuantizationConfig()
+
+    def quantize(self, vector: Sequence[float]) -> BinaryVector:
+        v = _f32(vector).reshape(1, -1)
+        return self.quantize_batch(v)[0]
+
+    def quantize_batch(self, vectors) -> List[BinaryVector]:
+        rows = [_f32(v).reshape(-1) for v in vectors]
+        if not rows:
+            return []
+        dims = {len(r) for r in rows}
+        out: List[BinaryVector] = []
+        if len(dims) == 1:
+            D = dims.pop()
+            m = np.stack(rows) if D else np.zeros((len(rows), 0), np.float32)
+            nb = (D + 7) // 8
+            o = np.zeros((len(rows), nb), np.uint8)
+            if D:
+                check(lib().gvdb_bq_quantize(ptr(m), len(rows), D, self.config.threshold, ptr(o)))
+            return [BinaryVector(o[i].tobytes(), D) for i in range(len(rows))]
+        for r in rows:
+            out.extend(self.quantize_batch([r]))
+        return out
+
+    def hamming_distance(self, a: BinaryVector, b: BinaryVector) -> float:
+        """quantization.rs:130-141 (Err(InvalidVectorDimension) on mismatch)."""
+        if a.dimension != b.dimension:
+            raise InvalidVectorDimension("binary vectors of different dimension")
+        nb = a.byte_size()
+        if nb == 0:
+            return 0.0
+        A = np.frombuffer(a.data, np.uint8).copy()
+        B = np.frombuffer(b.data, np.uint8).copy()
+        out = np.zeros(1, np.uint32)
+        check(lib().gvdb_bq_hamming(ptr(A), ptr(B), 1, a.dimension, ptr(out)))
+        return float(np.float32(out[0]))
+
+    def similarity(self, a: BinaryVector, b: BinaryVector) -> float:
+        """quantization.rs:144-148: 1 - d/D in f32."""
+        d = np.float32(self.hamming_distance(a, b))
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return float(np.float32(1.0) - (d / np.float32(a.dimension)))
+
+    def multi_stage_search(self, query_binary: BinaryVector, candidates_binary: Sequence[BinaryVector],
+                           original_query: Sequence[float], original_candidates) -> List[Tuple[int, float]]:
+        """quantization.rs:151-193 on the GPU: BQ stage 1 + exact cosine rescore."""
+        if len(candidates_binary) != len(original_candidates):
+            raise QuantizationError("Mismatch between binary and original candidate counts")
+        N = len(candidates_binary)
+        q = _f32(original_query).reshape(-1)
+        if N == 0:
+            return []
+        cdims = {c.dimension for c in candidates_binary}
+        if len(cdims) != 1:
+            raise InvalidArgument("the C ABI takes candidates of one dimension")
+        cdim = cdims.pop()
+        nb = (cdim + 7) // 8
+        cb = np.zeros((N, max(nb, 1)), np.uint8)
+        for i, c in enumerate(candidates_binary):
+            cb[i, :nb] = np.frombuffer(c.data[:nb], np.uint8)
+        cb = np.ascontiguousarray(cb[:, :nb]) if nb else np.zeros((N, 1), np.uint8)
+        cands = np.stack([_f32(c).reshape(-1) for c in original_candidates])
+        qb = np.frombuffer(query_binary.data, np.uint8).copy() if query_binary.data else np.zeros(1, np.uint8)
+        R = N  # capacity upper bound
+        out_idx = np.zeros(R, np.uint64)
+        out_cos = np.zeros(R, np.float32)
+        n = C.c_uint64()
+        check(lib().gvdb_bq_multi_stage_search(ptr(qb), query_binary.dimension, ptr(cb), cdim, N, ptr(q), q.size,
+                                               ptr(cands), cands.shape[1], self.config.rescore_ratio, ptr(out_idx),
+                                               ptr(out_cos), C.byref(n)))
+        return [(int(out_idx[i]), float(out_cos[i])) for i in range(n.value)]
+
+    def get_cache_stats(self):
+        return {"enabled": self.config.enable_cache, "size": 0, "capacity": 10000 if self.config.enable_cache else 0}
+
+
+# ---------------------------------------------------------------------------
+# VectorIndex (index.rs:35-62)
+# ---------------------------------------------------------------------------
+@dataclass
+class IndexStats:
+    """index.rs:83-88."""
+    vector_count: int
+    dimension: int
+    index_type: str
+    memory_usage: int
+    device_bytes: int = 0
+
+
+@dataclass
+class SearchParams:
+    """Explicit knobs of the GPU search (the reference hard-codes them)."""
+    mode: int = _ffi.GVDB_SEARCH_BQ_RERANK
+    metric: int = _ffi.GVDB_METRIC_COSINE
+    rescore_count: int = 0          # R; 0 -> (len as f32 * rescore_ratio) as usize
+    rescore_ratio: float = 0.1      # BinaryQuantizationConfig.rescore_ratio default
+
+    def to_c(self) -> _ffi.gvdb_search_params:
+        return _ffi.gvdb_search_params(self.mode, self.metric, self.rescore_count, self.rescore_ratio, 0)
+
+
+class GpuVectorIndex:
+    """MI355X drop-in for HnswVectorIndex (index.rs:91-310).
+
+    ``search`` runs BQ Hamming stage 1 + exact rerank on the GPU
+    (:class:`SearchParams`); scores follow ``params.metric`` (cosine by default,
+    ``GVDB_METRIC_L2`` reproduces HnswVectorIndex's L2 distances).
+    """
+
+    index_type = "GPU-BQ"
+
+    def __init__(self, dimension: int = 0, threshold: float = 0.0, device: int = 0, capacity_hint: int = 0,
+                 params: Optional[SearchParams] = None):
+        self._lib = lib()
+        h = C.c_void_p()
+        p = _ffi.gvdb_params(dimension, threshold, device, 0, capacity_hint)
+        check(self._lib.gvdb_index_create(C.byref(p), C.byref(h)))
+        self._h = h
+        self.device = device
+        self.params = params or SearchParams()
+        self._id_of: dict = {}       # str -> u64
+        self._str_of: List[str] = []  # u64 -> str
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.gvdb_index_destroy(h)
+            self._h = None
+
+    # -- id table -----------------------------------------------------------
+    def _u64(self, sid: str) -> int:
+        u = self._id_of.get(sid)
+        if u is None:
+            u = len(self._str_of)
+            self._id_of[sid] = u
+            self._str_of.append(sid)
+        return u
+
+    # -- trait methods ------------------------------------------------------
+    def add_vector(self, id: str, vector: Sequence[float]) -> None:
+        self.add_vectors([(id, vector)])
+
+    def add_vectors(self, vectors: Iterable[Tuple[str, Sequence[float]]]) -> None:
+        """index.rs:187-210: rows before a dimension mismatch are kept."""
+        items = list(vectors)
+        i = 0
+        while i < len(items):
+            D = len(items[i][1])
+            j = i
+            while j < len(items) and len(items[j][1]) == D:
+                j += 1
+            rows = np.stack([_f32(v).reshape(-1) for _, v in items[i:j]]) if D else np.zeros((j - i, 0), np.float32)
+            ids = np.array([self._u64(s) for s, _ in items[i:j]], np.uint64)
+            self.add_batch(ids, rows)
+            i = j
+
+    def add_batch(self, ids: np.ndarray, rows: np.ndarray) -> None:
+        rows = _f32(rows)
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        check(self._lib.gvdb_index_add(self._h, ptr(rows), rows.shape[0], rows.shape[1] if rows.ndim == 2 else 0,
+                                       ptr(ids)))
+
+    def add_device(self, rows, ids, stream: int = 0) -> None:
+        """rows: torch cuda float32 [n, D]; ids: torch cuda int64/uint64 [n]."""
+        check(self._lib.gvdb_index_add_device(self._h, rows.data_ptr(), rows.shape[0], rows.shape[1],
+                                              ids.data_ptr(), stream or None))
+
+    def search(self, query: Sequence[float], k: int) -> List[Tuple[str, float]]:
+        q = _f32(query).reshape(1, -1)
+        ids, scores, n = self.search_batch(q, k)
+        return [(self._str_of[int(ids[0, i])] if int(ids[0, i]) < len(self._str_of) else str(int(ids[0, i])),
+                 float(scores[0, i])) for i in range(int(n[0]))]
+
+    def search_batch(self, queries: np.ndarray, k: int, params: Optional[SearchParams] = None):
+        q = _f32(queries)
+        if q.ndim == 1:
+            q = q.reshape(1, -1)
+        B, D = q.shape
+        sp = (params or self.params).to_c()
+        ids = np.zeros((B, max(k, 1)), np.uint64)
+        sc = np.zeros((B, max(k, 1)), np.float32)
+        n = np.zeros(B, np.uint32)
+        check(self._lib.gvdb_index_search(self._h, ptr(q), B, D, k, C.byref(sp), ptr(ids), ptr(sc), ptr(n)))
+        return ids[:, :k], sc[:, :k], n
+
+    def search_device(self, queries, k: int, out_ids, out_scores, out_n=None, params: Optional[SearchParams] = None,
+                      stream: int = 0) -> None:
+        sp = (params or self.params).to_c()
+        check(self._lib.gvdb_index_search_device(self._h, queries.data_ptr(), queries.shape[0], queries.shape[1], k,
+                                                 C.byref(sp), out_ids.data_ptr(), out_scores.data_ptr(),
+                                                 out_n.data_ptr() if out_n is not None else None, stream or None))
+
+    def bq_topr_device(self, queries, R: int, out_rows, out_dist, stream: int = 0) -> None:
+        check(self._lib.gvdb_index_bq_topr_device(self._h, queries.data_ptr(), queries.shape[0], queries.shape[1], R,
+                                                  out_rows.data_ptr(), out_dist.data_ptr(), stream or None))
+
+    def remove_vector(self, id: str) -> bool:
+        u = self._id_of.get(id)
+        if u is None:
+            return False
+        r = C.c_int32()
+        check(self._lib.gvdb_index_remove(self._h, u, C.byref(r)))
+        return bool(r.value)
+
+    def len(self) -> int:
+        return int(self._lib.gvdb_index_len(self._h))
+
+    def __len__(self) -> int:
+        return self.len()
+
+    def is_empty(self) -> bool:
+        return bool(self._lib.gvdb_index_is_empty(self._h))
+
+    def optimize(self) -> None:
+        check(self._lib.gvdb_index_optimize(self._h))
+
+    def build_index(self) -> None:
+        check(self._lib.gvdb_index_build(self._h))
+
+    def clear(self) -> None:
+        self._lib.gvdb_index_clear(self._h)
+
+    def get_stats(self) -> IndexStats:
+        s = _ffi.gvdb_index_stats()
+        check(self._lib.gvdb_index_get_stats(self._h, C.byref(s)))
+        return IndexStats(int(s.vector_count), int(s.dimension), self.index_type, int(s.memory_usage),
+                          int(s.device_bytes))
+
+
+HnswVectorIndex = GpuVectorIndex
+
+
+# ---------------------------------------------------------------------------
+# flat scan and shard merge
+# ---------------------------------------------------------------------------
+def flat_search(queries, rows, limit: int, metric: int = _ffi.GVDB_METRIC_COSINE, threshold: Optional[float] = None):
+    """storage.rs:296-339 (cosine, optional threshold) / index.rs:620-640
+    (cosine distance) / exact L2, for a batch of queries over host rows."""
+    q = _f32(queries)
+    if q.ndim == 1:
+        q = q.reshape(1, -1)
+    x = _f32(rows)
+    B, D = q.shape
+    N = x.shape[0]
+    idx = np.zeros((B, max(limit, 1)), np.uint64)
+    sc = np.zeros((B, max(limit, 1)), np.float32)
+    n = np.zeros(B, np.uint32)
+    check(lib().gvdb_flat_search(ptr(q), B, ptr(x), N, D, limit, metric, int(threshold is not None),
+                                 float(threshold or 0.0), ptr(idx), ptr(sc), ptr(n)))
+    return idx[:, :limit], sc[:, :limit], n
+
+
+def topk_merge(ids: np.ndarray, scores: np.ndarray, counts: np.ndarray, limit: int, descending: bool = True):
+    """shard.rs:776-784.  ids/scores: [n_shards, B, stride]; counts [n_shards, B]."""
+    ids = np.ascontiguousarray(ids, np.uint64)
+    scores = np.ascontiguousarray(scores, np.float32)
+    counts = np.ascontiguousarray(counts, np.uint32)
+    S, B, stride = ids.shape
+    oi = np.zeros((B, max(limit, 1)), np.uint64)
+    os_ = np.zeros((B, max(limit, 1)), np.float32)
+    on = np.zeros(B, np.uint32)
+    check(lib().gvdb_topk_merge(ptr(ids), ptr(scores), ptr(counts), S, B, stride, limit, int(descending), ptr(oi),
+                                ptr(os_), ptr(on)))
+    return oi[:, :limit], os_[:, :limit], on

@@ -1,0 +1,224 @@
+/*
+ * gvdb.h — C ABI of the MI355X-native ANN search path for grape-vector-db.
+ *
+ * Drop-in boundary for the reference's vector hot path (reference snapshot
+ * 2025-08-24, Rust):
+ *   - trait VectorIndex                      src/index.rs:35-62
+ *   - HnswVectorIndex (search via HNSW)      src/index.rs:91-310
+ *   - BinaryQuantizer::{quantize, hamming_distance, similarity,
+ *                       multi_stage_search} src/quantization.rs:86-193
+ *   - VectorStore::vector_search (flat)      src/storage.rs:296-339
+ *   - FaissVectorIndex::search (Flat)        src/index.rs:620-640
+ *   - ShardManager::search_vectors merge     src/distributed/shard.rs:776-784
+ *
+ * Rules of the boundary:
+ *   - plain pointers and sizes only; no exceptions cross it;
+ *   - caller-owned output buffers;
+ *   - string ids never enter the library: the host keeps a String <-> u64
+ *     table (see grape-vector-db_amd/host/gvdb.hpp and INTEGRATION.md);
+ *   - gvdb_index_search* are reentrant for concurrent readers (each call
+ *     takes its own stream + workspace from a pool); add/build/remove/clear
+ *     need the caller's exclusive lock, mirroring Arc<RwLock<dyn VectorIndex>>
+ *     (src/lib.rs:238);
+ *   - errors: gvdb_status codes 1:1 with VectorDbError (src/types.rs:859-920)
+ *     plus GVDB_ERR_DEVICE; details via gvdb_last_error() (thread-local).
+ *   - functions suffixed _device take DEVICE pointers (HBM-resident inputs
+ *     and outputs) and an optional hipStream_t passed as void* (NULL = the
+ *     library's own stream for that call).  They are the zero-copy form used
+ *     when the caller already keeps data on the GPU.
+ */
+#ifndef GVDB_H_
+#define GVDB_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GVDB_ABI_VERSION 1
+
+typedef enum gvdb_status {
+    GVDB_OK = 0,
+    GVDB_ERR_INDEX_NOT_BUILT = 1,          /* VectorDbError::IndexNotBuilt               */
+    GVDB_ERR_DIMENSION_MISMATCH = 2,       /* VectorDbError::DimensionMismatch{exp,act}  */
+    GVDB_ERR_INVALID_VECTOR_DIMENSION = 3, /* VectorDbError::InvalidVectorDimension      */
+    GVDB_ERR_QUANTIZATION = 4,             /* VectorDbError::QuantizationError(String)   */
+    GVDB_ERR_INDEX = 5,                    /* VectorDbError::IndexError(String)          */
+    GVDB_ERR_INVALID_ARGUMENT = 6,         /* null pointer / bad size at the ABI          */
+    GVDB_ERR_DEVICE = 7,                   /* HIP runtime / kernel failure                */
+    GVDB_ERR_OUT_OF_MEMORY = 8             /* device allocation failed                    */
+} gvdb_status;
+
+/* Scores reported by gvdb_index_search*. */
+typedef enum gvdb_metric {
+    /* cosine similarity, descending: multi_stage_search stage 2
+     * (quantization.rs:181-190) and storage.rs:296-339 */
+    GVDB_METRIC_COSINE = 0,
+    /* Euclidean distance, ascending: VectorPoint::distance (index.rs:69-78),
+     * the score HnswVectorIndex::search returns (index.rs:212-231) */
+    GVDB_METRIC_L2 = 1,
+    /* 1 - cosine, ascending: cosine_distance (index.rs:686-700), the score
+     * FaissVectorIndex::search returns */
+    GVDB_METRIC_COSINE_DISTANCE = 2
+} gvdb_metric;
+
+typedef enum gvdb_search_mode {
+    /* BQ Hamming top-R prefilter then exact rerank of the R candidates
+     * (multi_stage_search semantics, quantization.rs:151-193) */
+    GVDB_SEARCH_BQ_RERANK = 0,
+    /* exact scan of every live row (storage.rs:296-339 / index.rs:620-640) */
+    GVDB_SEARCH_FLAT = 1
+} gvdb_search_mode;
+
+typedef struct gvdb_params {
+    uint32_t dimension;       /* 0: fixed by the first add (index.rs:160-170) */
+    float bq_threshold;       /* BinaryQuantizationConfig.threshold, default 0.0 (quantization.rs:25) */
+    int32_t device;           /* HIP device ordinal                                     */
+    uint32_t reserved;
+    uint64_t capacity_hint;   /* rows to pre-reserve in HBM (0 = grow on demand)         */
+} gvdb_params;
+
+typedef struct gvdb_search_params {
+    uint32_t mode;            /* gvdb_search_mode                                        */
+    uint32_t metric;          /* gvdb_metric                                             */
+    uint64_t rescore_count;   /* R; 0 => R = (len as f32 * rescore_ratio) as usize       */
+    float rescore_ratio;      /* BinaryQuantizationConfig.rescore_ratio, default 0.1     */
+    uint32_t reserved;
+} gvdb_search_params;
+
+typedef struct gvdb_index_stats {  /* IndexStats, index.rs:83-88 */
+    uint64_t vector_count;
+    uint64_t dimension;
+    uint64_t memory_usage;    /* bytes of f32 rows, as the reference reports             */
+    uint64_t device_bytes;    /* total HBM held by the index (rows + codes + norms + ids)*/
+} gvdb_index_stats;
+
+typedef struct gvdb_index gvdb_index;
+
+/* ---- library ------------------------------------------------------------ */
+uint32_t gvdb_abi_version(void);
+const char* gvdb_last_error(void);                  /* thread-local, never NULL */
+const char* gvdb_status_string(gvdb_status s);
+/* Detail of the last GVDB_ERR_DIMENSION_MISMATCH on this thread. */
+void gvdb_last_dimension_mismatch(uint64_t* expected, uint64_t* actual);
+int32_t gvdb_device_count(void);
+/* Kernel timing with HIP events recorded around the launches on the stream
+ * they run on (read after each batch's own stream sync).  Slots:
+ * 0 = stage-1 sample histogram + threshold, 1 = k_scan (the BQ Hamming hot
+ * loop), 2 = stage-1 select, 3 = stage 2 (rerank + final sort). */
+void gvdb_timing_enable(int32_t on);
+void gvdb_timing_reset(void);
+gvdb_status gvdb_timing_read(uint32_t which, double* total_ms, uint64_t* launches);
+
+/* ---- VectorIndex (index.rs:35-62) --------------------------------------- */
+/* HnswVectorIndex::new / with_config (index.rs:100-117) */
+gvdb_status gvdb_index_create(const gvdb_params* params, gvdb_index** out);
+void gvdb_index_destroy(gvdb_index* index);
+/* add_vectors (index.rs:187-210): n rows of `dim` f32, row-major, host memory.
+ * Dimension check per row order; on mismatch nothing after the failing row
+ * is added (rows before it stay, as in the reference loop).  The index
+ * becomes searchable at once (the reference rebuilds after every add). */
+gvdb_status gvdb_index_add(gvdb_index* index, const float* rows, uint64_t n, uint32_t dim,
+                           const uint64_t* ids);
+/* Same, rows already in HBM on the index's device (copied into the index). */
+gvdb_status gvdb_index_add_device(gvdb_index* index, const float* d_rows, uint64_t n, uint32_t dim,
+                                  const uint64_t* d_ids, void* stream);
+/* build_index / optimize (index.rs:140-154, 299-302): re-derives codes and
+ * norms; a no-op when they are current. */
+gvdb_status gvdb_index_build(gvdb_index* index);
+/* search (index.rs:212-231) for a batch of B queries (B x dim, host memory).
+ * Per query q, up to k results: out_ids[q*k + i], out_scores[q*k + i],
+ * count out_n[q].  IndexNotBuilt when the index is empty (index.rs:213). */
+gvdb_status gvdb_index_search(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
+                              uint64_t k, const gvdb_search_params* sp, uint64_t* out_ids,
+                              float* out_scores, uint32_t* out_n);
+/* Same with queries and outputs in HBM.  out_n may be NULL.  Synchronises
+ * the stream before returning (the fallback decision reads a device flag). */
+gvdb_status gvdb_index_search_device(const gvdb_index* index, const float* d_queries, uint64_t B,
+                                     uint32_t dim, uint64_t k, const gvdb_search_params* sp,
+                                     uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
+                                     void* stream);
+/* Stage-1 only (BQ top-R, quantization.rs:165-179) into device buffers:
+ * out_rows[q*R + i] = row index (ascending Hamming, ascending row on ties),
+ * out_dist[q*R + i] = Hamming distance.  For sharded search / tests. */
+gvdb_status gvdb_index_bq_topr_device(const gvdb_index* index, const float* d_queries, uint64_t B,
+                                      uint32_t dim, uint64_t R, uint64_t* d_out_rows,
+                                      uint32_t* d_out_dist, void* stream);
+/* Sharded-search building block: stage 1 (local top-R) + exact cosine of
+ * every candidate, in stage-1 order (Hamming asc, row asc), no final sort.
+ * out_ids[q*R + i] = ids[row] (callers use global row numbers as ids),
+ * out_dist = Hamming distance, out_scores = cosine (quantization.rs:181-187). */
+gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* index, const float* d_queries, uint64_t B,
+                                            uint32_t dim, uint64_t R, uint64_t* d_out_ids,
+                                            uint32_t* d_out_dist, float* d_out_scores, void* stream);
+/* remove_vector (index.rs:233-285): order-preserving compaction. *removed=1
+ * if the id was present. */
+gvdb_status gvdb_index_remove(gvdb_index* index, uint64_t id, int32_t* removed);
+uint64_t gvdb_index_len(const gvdb_index* index);
+int32_t gvdb_index_is_empty(const gvdb_index* index);
+gvdb_status gvdb_index_optimize(gvdb_index* index);
+void gvdb_index_clear(gvdb_index* index);
+gvdb_status gvdb_index_get_stats(const gvdb_index* index, gvdb_index_stats* out);
+/* Device pointers of the resident corpus, for sharded drivers and tests. */
+const float* gvdb_index_device_rows(const gvdb_index* index);
+
+/* ---- BinaryQuantizer (quantization.rs:67-216) --------------------------- */
+/* quantize / quantize_batch (86-127): n rows of D f32 -> n rows of
+ * ceil(D/8) bytes, BitVec<u8, Msb0> packing, bit = x > threshold. */
+gvdb_status gvdb_bq_quantize(const float* rows, uint64_t n, uint32_t D, float threshold, uint8_t* out);
+gvdb_status gvdb_bq_quantize_device(const float* d_rows, uint64_t n, uint32_t D, float threshold,
+                                    uint8_t* d_out, void* stream);
+/* hamming_distance (130-141) for n pairs (a[i], b[i]) of ceil(D/8) bytes. */
+gvdb_status gvdb_bq_hamming(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t D, uint32_t* out);
+/* multi_stage_search (151-193).  q_bits: ceil(qdim/8) bytes; c_bits: N rows
+ * of ceil(cdim/8) bytes; q: qlen f32; cands: N rows of clen f32.
+ * Writes min(R, N) entries (R = (N as f32 * rescore_ratio) as usize) to
+ * out_idx/out_cos, sorted like the reference; *out_n = that count.
+ * Capacity of out_idx/out_cos must be >= min(R, N). */
+gvdb_status gvdb_bq_multi_stage_search(const uint8_t* q_bits, uint32_t qdim, const uint8_t* c_bits,
+                                       uint32_t cdim, uint64_t N, const float* q, uint64_t qlen,
+                                       const float* cands, uint64_t clen, float rescore_ratio,
+                                       uint64_t* out_idx, float* out_cos, uint64_t* out_n);
+
+/* ---- flat scan (storage.rs:296-339, index.rs:620-640) ------------------- */
+/* Exact scan over N rows (host memory) for B queries: metric COSINE keeps
+ * scores >= threshold when has_threshold (storage.rs:313-317), descending;
+ * COSINE_DISTANCE ascending; L2 ascending. limit results per query. */
+gvdb_status gvdb_flat_search(const float* queries, uint64_t B, const float* rows, uint64_t N, uint32_t D,
+                             uint64_t limit, uint32_t metric, int32_t has_threshold, float threshold,
+                             uint64_t* out_idx, float* out_scores, uint32_t* out_n);
+
+/* ---- shard merge (shard.rs:776-784) ------------------------------------- */
+/* Per query: concat n_shards lists (stride entries each, counts[s*B + q]
+ * valid), stable sort by score (descending if `descending`), truncate to
+ * limit.  Layout: ids[(s*B + q)*stride + i].  Host memory. */
+gvdb_status gvdb_topk_merge(const uint64_t* ids, const float* scores, const uint32_t* counts,
+                            uint64_t n_shards, uint64_t B, uint64_t stride, uint64_t limit,
+                            int32_t descending, uint64_t* out_ids, float* out_scores, uint32_t* out_n);
+/* Same on device buffers (all-gathered shard results stay in HBM). */
+gvdb_status gvdb_topk_merge_device(const uint64_t* d_ids, const float* d_scores, const uint32_t* d_counts,
+                                   uint64_t n_shards, uint64_t B, uint64_t stride, uint64_t limit,
+                                   int32_t descending, uint64_t* d_out_ids, float* d_out_scores,
+                                   uint32_t* d_out_n, void* stream);
+
+/* ---- exact sharded multi-stage merge (shard.rs:776-784 + quantization.rs:
+ * 165-190 over the concatenated shards) ------------------------------------ */
+/* Inputs gathered from G shards, layout [(g*B + q)*stride + i], counts[g*B+q]
+ * valid entries each, as produced by gvdb_index_bq_candidates_device with
+ * global ids.  Per query: union sorted by (dist asc, gid asc) -> first R ->
+ * sorted by (cosine desc, that rank asc) -> first k.  Identical to one
+ * multi_stage_search over all shards.  Device form needs G*stride <= 4096. */
+gvdb_status gvdb_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cos,
+                                const uint32_t* counts, uint64_t G, uint64_t B, uint64_t stride, uint64_t R,
+                                uint64_t k, uint64_t* out_ids, float* out_scores, uint32_t* out_n);
+gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d_dist, const float* d_cos,
+                                       const uint32_t* d_counts, uint64_t G, uint64_t B, uint64_t stride,
+                                       uint64_t R, uint64_t k, uint64_t* d_out_ids, float* d_out_scores,
+                                       uint32_t* d_out_n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GVDB_H_ */

@@ -1,0 +1,282 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact bytes / ids / Hamming distances, and bit-exact f32 scores
+(the rerank folds each row in the reference's sequential order, so cosine
+scores match to the last bit; the north-star tolerance 1e-5 is asserted as
+well for documentation).  Sizes stay where the oracle finishes in seconds.
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+COS_TOL = 1e-5  # north_star: "cosine scores within 1e-5"
+
+
+@pytest.fixture(scope="module")
+def g(gvdb_mod):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return gvdb_mod
+
+
+def rng_rows(seed, n, d, dup=0):
+    r = np.random.default_rng(seed)
+    x = r.standard_normal((n, d)).astype(np.float32)
+    for i in range(dup):  # duplicate rows -> equal Hamming AND equal cosine ties
+        x[(7 * i + 11) % n] = x[(13 * i + 3) % n]
+    return x
+
+
+def same_f32(a, b):
+    return np.array(a, np.float32).tobytes() == np.array(b, np.float32).tobytes()
+
+
+# --------------------------------------------------------------------------- K1
+def test_quantize_kat(g):
+    q = g.BinaryQuantizer()
+    assert q.quantize([0.5, -0.3, 0.8, -0.1, 0.2]).data == bytes([0xA8])  # quantization.rs:361-372
+    a = q.quantize([1.0, -1.0, 1.0, -1.0])
+    b = q.quantize([1.0, 1.0, -1.0, -1.0])
+    assert (a.data, b.data) == (bytes([0xA0]), bytes([0xC0]))
+    assert q.hamming_distance(a, b) == 2.0 and q.similarity(a, b) == 0.5  # quantization.rs:375-386
+
+
+@pytest.mark.parametrize("D", [1, 5, 8, 31, 63, 64, 65, 100, 128, 129, 768, 1000, 3072])
+def test_quantize_matches_oracle(g, oracle_mod, D):
+    x = rng_rows(D, 257, D)
+    x[0, 0] = np.nan
+    x[1, : min(D, 4)] = -0.0
+    x[2, : min(D, 4)] = 0.0
+    for thr in (0.0, 0.25):
+        got = g.BinaryQuantizer(g.BinaryQuantizationConfig(threshold=thr)).quantize_batch(x)
+        ref = oracle_mod.quantize(x, thr)
+        assert all(got[i].data == ref[i].tobytes() for i in range(len(x)))
+
+
+def test_hamming_matches_oracle(g, oracle_mod):
+    q = g.BinaryQuantizer()
+    for D in (3, 64, 768):
+        x = rng_rows(D + 1, 20, D)
+        bv = q.quantize_batch(x)
+        ref = oracle_mod.quantize(x)
+        for i in range(0, 20, 2):
+            assert q.hamming_distance(bv[i], bv[i + 1]) == oracle_mod.hamming(ref[i], ref[i + 1])
+    with pytest.raises(g.InvalidVectorDimension):
+        q.hamming_distance(q.quantize([1.0, 2.0]), q.quantize([1.0]))
+
+
+# --------------------------------------------------------------------------- K2+K3 (multi_stage_search)
+@pytest.mark.parametrize("N,D,ratio", [(1, 8, 1.0), (2, 8, 1.0), (10, 16, 0.5), (1000, 100, 0.1), (5000, 128, 0.02),
+                                       (3000, 768, 0.05), (2000, 3072, 0.01), (4000, 64, 1.0)])
+def test_multi_stage_matches_oracle(g, oracle_mod, N, D, ratio):
+    x = rng_rows(N * 7 + D, N, D, dup=min(N // 4, 40))
+    qv = rng_rows(D, 1, D)[0]
+    bq = g.BinaryQuantizer(g.BinaryQuantizationConfig(rescore_ratio=ratio))
+    cb = bq.quantize_batch(x)
+    qb = bq.quantize(qv)
+    got = bq.multi_stage_search(qb, cb, qv, x)
+    ri, rc = oracle_mod.multi_stage_search(oracle_mod.quantize(qv)[0], D, oracle_mod.quantize(x), D, qv, x, ratio)
+    assert [i for i, _ in got] == [int(i) for i in ri]
+    assert same_f32([c for _, c in got], rc)  # bit-exact cosine
+    assert np.max(np.abs(np.array([c for _, c in got]) - rc), initial=0.0) <= COS_TOL
+
+
+def test_multi_stage_dimension_mismatch(g, oracle_mod):
+    x = rng_rows(1, 50, 16)
+    qv = rng_rows(2, 1, 8)[0]
+    bq = g.BinaryQuantizer(g.BinaryQuantizationConfig(rescore_ratio=0.5))
+    got = bq.multi_stage_search(bq.quantize(qv), bq.quantize_batch(x), qv, x)
+    ri, rc = oracle_mod.multi_stage_search(oracle_mod.quantize(qv)[0], 8, oracle_mod.quantize(x), 16, qv, x, 0.5)
+    assert [i for i, _ in got] == [int(i) for i in ri] and same_f32([c for _, c in got], rc)
+
+
+def test_multi_stage_errors(g):
+    bq = g.BinaryQuantizer()
+    with pytest.raises(g.QuantizationError):  # quantization.rs:158-162
+        bq.multi_stage_search(bq.quantize([1.0]), [bq.quantize([1.0])], [1.0], [[1.0], [2.0]])
+    assert bq.multi_stage_search(bq.quantize([1.0]), [], [1.0], []) == []
+
+
+# --------------------------------------------------------------------------- stage 1 at scale (sampling path)
+def topr(g, ix, Q, R):
+    import torch
+
+    q = torch.from_numpy(Q).cuda()
+    rows = torch.zeros((Q.shape[0], R), dtype=torch.int64, device="cuda")
+    dist = torch.zeros((Q.shape[0], R), dtype=torch.int32, device="cuda")
+    ix.bq_topr_device(q, R, rows, dist)
+    torch.cuda.synchronize()
+    return rows.cpu().numpy().astype(np.uint64), dist.cpu().numpy().astype(np.uint32)
+
+
+@pytest.mark.parametrize("N,D,B,R,dup", [(600_000, 128, 6, 100, 0), (300_000, 768, 4, 64, 0),
+                                          (100_000, 64, 5, 1000, 2000), (50_000, 128, 3, 5000, 0),
+                                          (40_000, 32, 3, 9000, 0)])
+def test_stage1_topr_matches_oracle(g, oracle_mod, N, D, B, R, dup):
+    x = rng_rows(N + D, N, D)
+    if dup:  # a block of identical rows: massive ties at one distance
+        x[1000:1000 + dup] = x[5]
+    Q = rng_rows(D + 99, B, D)
+    Q[0] = x[5]
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    gi, gd = topr(g, ix, Q, R)
+    ri, rd = oracle_mod.bq_topr_batch(oracle_mod.quantize(Q), oracle_mod.quantize(x), D, R)
+    assert (gd == rd).all()
+    assert (gi == ri).all()
+
+
+def test_stage1_massive_ties_fallback(g, oracle_mod):
+    # 12k identical nearest rows > the 8192-key LDS select: exact slow path
+    N, D, R = 30_000, 64, 500
+    x = rng_rows(3, N, D)
+    x[100:12_100] = x[1]
+    Q = x[1:2].copy()
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    gi, gd = topr(g, ix, Q, R)
+    ri, rd = oracle_mod.bq_topr_batch(oracle_mod.quantize(Q), oracle_mod.quantize(x), D, R)
+    assert (gi == ri).all() and (gd == rd).all()
+
+
+# --------------------------------------------------------------------------- index search (VectorIndex)
+@pytest.mark.parametrize("N,D,B,R,k,metric", [(20_000, 128, 16, 100, 10, 0), (20_000, 128, 8, 100, 10, 1),
+                                               (20_000, 96, 8, 64, 64, 2), (300_000, 768, 4, 100, 10, 0),
+                                               (5_000, 256, 4, 4500, 20, 0)])
+def test_index_search_matches_oracle(g, oracle_mod, N, D, B, R, k, metric):
+    x = rng_rows(N + 1, N, D, dup=50)
+    Q = rng_rows(D + 5, B, D)
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64) * 3 + 7, x)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(metric=metric, rescore_count=R))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R, kind=metric)
+    kk = min(k, R, N)
+    assert (n == kk).all()
+    assert (ids[:, :kk] == ri[:, :kk] * 3 + 7).all()
+    assert same_f32(sc[:, :kk], rs[:, :kk])
+
+
+def test_index_semantics(g):
+    ix = g.GpuVectorIndex()
+    with pytest.raises(g.IndexNotBuilt):  # index.rs:213
+        ix.search([1.0, 0.0, 0.0], 5)
+    ix.add_vector("test1", [1.0, 0.0, 0.0])  # query.rs:428-483 KAT
+    assert ix.search([1.0, 0.1, 0.0], 5)[0][0] == "test1"
+    with pytest.raises(g.DimensionMismatch) as e:  # index.rs:160-168
+        ix.add_vector("bad", [1.0, 2.0])
+    assert (e.value.expected, e.value.actual) == (3, 2)
+    ix.add_vectors([("a", [0.0, 1.0, 0.0]), ("b", [0.0, 0.0, 1.0])])
+    assert ix.len() == 3 and not ix.is_empty()
+    # re-adding an id shadows the old row (HashMap insert, index.rs:175-176)
+    ix.add_vector("a", [0.9, 0.1, 0.0])
+    assert ix.len() == 3 and ix.get_stats().memory_usage == 4 * 3 * 4
+    res = ix.search_batch(np.array([[1.0, 0, 0]], np.float32), 10, g.SearchParams(rescore_count=4))
+    ids = [int(i) for i in res[0][0, :res[2][0]]]
+    assert len(ids) == 3  # the orphaned row is dropped after take(k)
+    assert ix.remove_vector("b") is True and ix.remove_vector("zzz") is False
+    assert ix.len() == 2 and ix.get_stats().memory_usage == 2 * 3 * 4  # orphans compacted away
+    hits = ix.search([1.0, 0.0, 0.0], 5)
+    assert [h[0] for h in hits] == ["test1", "a"]
+    ix.clear()
+    assert ix.is_empty() and ix.get_stats().dimension == 0
+    with pytest.raises(g.IndexNotBuilt):
+        ix.search([1.0], 1)
+
+
+def test_index_flat_mode_matches_oracle(g, oracle_mod):
+    N, D = 3000, 64
+    x = rng_rows(9, N, D, dup=30)
+    x[17] = 0.0  # zero-norm row
+    Q = rng_rows(10, 5, D)
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    ids, sc, n = ix.search_batch(Q, 25, g.SearchParams(mode=1, metric=0))
+    for b in range(5):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], x, 25)
+        assert list(ids[b, :n[b]]) == list(ri) and same_f32(sc[b, :n[b]], rs)
+    ids, sc, n = ix.search_batch(Q, 25, g.SearchParams(mode=1, metric=2))
+    for b in range(5):
+        ri, rs = oracle_mod.flat_cosine_distance_search(Q[b], x, 25)
+        assert list(ids[b, :n[b]]) == list(ri) and same_f32(sc[b, :n[b]], rs)
+
+
+def test_flat_search_threshold(g, oracle_mod):
+    N, D = 2000, 32
+    x = rng_rows(11, N, D)
+    Q = rng_rows(12, 3, D)
+    idx, sc, n = g.flat_search(Q, x, 50, threshold=0.3)
+    for b in range(3):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], x, 50, threshold=0.3)
+        assert list(idx[b, :n[b]]) == list(ri) and same_f32(sc[b, :n[b]], rs)
+
+
+# --------------------------------------------------------------------------- merges
+def test_topk_merge_device_matches_host(g):
+    import torch
+
+    rng = np.random.default_rng(0)
+    S, B, stride, limit = 4, 9, 50, 30
+    ids = rng.integers(0, 10**9, (S, B, stride)).astype(np.uint64)
+    sc = (rng.integers(0, 16, (S, B, stride)) / 16).astype(np.float32)
+    cnt = rng.integers(0, stride + 1, (S, B)).astype(np.uint32)
+    hi, hs, hn = g.topk_merge(ids, sc, cnt, limit)
+    d = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32) if a.dtype == np.uint32 else a).cuda()
+    oi = torch.zeros((B, limit), dtype=torch.int64, device="cuda")
+    os_ = torch.zeros((B, limit), dtype=torch.float32, device="cuda")
+    on = torch.zeros(B, dtype=torch.int32, device="cuda")
+    st = g.lib().gvdb_topk_merge_device(d(ids).data_ptr(), d(sc).data_ptr(), d(cnt).data_ptr(), S, B, stride, limit, 1,
+                                        oi.data_ptr(), os_.data_ptr(), on.data_ptr(), None)
+    assert st == 0
+    torch.cuda.synchronize()
+    n = on.cpu().numpy()
+    assert (n == hn).all()
+    for q in range(B):
+        assert (oi.cpu().numpy()[q, :n[q]].view(np.uint64) == hi[q, :n[q]]).all()
+        assert same_f32(os_.cpu().numpy()[q, :n[q]], hs[q, :n[q]])
+
+
+def test_sharded_candidates_merge_equals_single_device(g, oracle_mod):
+    """Exact sharded mode: per-shard candidates + one merge == one device."""
+    import torch
+
+    N, D, B, R, k, G = 40_000, 128, 8, 100, 10, 4
+    x = rng_rows(21, N, D, dup=100)
+    Q = rng_rows(22, B, D)
+    bounds = [N * s // G for s in range(G + 1)]
+    gids = np.zeros((G, B, R), np.uint64)
+    dist = np.zeros((G, B, R), np.uint32)
+    cosv = np.zeros((G, B, R), np.float32)
+    counts = np.zeros((G, B), np.uint32)
+    q = torch.from_numpy(Q).cuda()
+    for s in range(G):
+        lo, hi = bounds[s], bounds[s + 1]
+        ix = g.GpuVectorIndex(dimension=D)
+        ix.add_batch(np.arange(lo, hi, dtype=np.uint64), x[lo:hi])
+        oi = torch.zeros((B, R), dtype=torch.int64, device="cuda")
+        od = torch.zeros((B, R), dtype=torch.int32, device="cuda")
+        oc = torch.zeros((B, R), dtype=torch.float32, device="cuda")
+        st = g.lib().gvdb_index_bq_candidates_device(ix._h, q.data_ptr(), B, D, R, oi.data_ptr(), od.data_ptr(),
+                                                      oc.data_ptr(), None)
+        assert st == 0
+        torch.cuda.synchronize()
+        gids[s], dist[s], cosv[s] = oi.cpu().numpy().view(np.uint64), od.cpu().numpy().view(np.uint32), oc.cpu().numpy()
+        counts[s] = R
+    # device merge
+    dg = torch.from_numpy(gids.view(np.int64)).cuda()
+    dd = torch.from_numpy(dist.view(np.int32)).cuda()
+    dc = torch.from_numpy(cosv).cuda()
+    dn = torch.from_numpy(counts.view(np.int32)).cuda()
+    mi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+    ms = torch.zeros((B, k), dtype=torch.float32, device="cuda")
+    mn = torch.zeros(B, dtype=torch.int32, device="cuda")
+    st = g.lib().gvdb_bq_shard_merge_device(dg.data_ptr(), dd.data_ptr(), dc.data_ptr(), dn.data_ptr(), G, B, R, R, k,
+                                            mi.data_ptr(), ms.data_ptr(), mn.data_ptr(), None)
+    assert st == 0
+    torch.cuda.synchronize()
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R, kind=0)
+    assert (mi.cpu().numpy().view(np.uint64) == ri[:, :k]).all()
+    assert same_f32(ms.cpu().numpy(), rs[:, :k])
