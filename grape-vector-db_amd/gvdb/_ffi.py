@@ -115,6 +115,15 @@ def lib() -> C.CDLL:
                     f"libgvdb.so not found at {LIB_PATH}: run __graft_entry__.build() "
                     "(there is no CPU fallback for the GPU search path)"
                 )
+            # One HIP runtime per process: PyTorch-ROCm bundles its own
+            # libamdhip64 (SONAME libamdhip64.so.7, NEEDED as "libamdhip64.so").
+            # Loading torch first makes libgvdb bind to that same copy; loading
+            # libgvdb first would pull /opt/rocm's copy and torch would then
+            # load a second runtime that sees no device.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             L = C.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(L, name)

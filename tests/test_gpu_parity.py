@@ -228,7 +228,9 @@ def test_topk_merge_device_matches_host(g):
     oi = torch.zeros((B, limit), dtype=torch.int64, device="cuda")
     os_ = torch.zeros((B, limit), dtype=torch.float32, device="cuda")
     on = torch.zeros(B, dtype=torch.int32, device="cuda")
-    st = g.lib().gvdb_topk_merge_device(d(ids).data_ptr(), d(sc).data_ptr(), d(cnt).data_ptr(), S, B, stride, limit, 1,
+    t_ids, t_sc, t_cnt = d(ids), d(sc), d(cnt)  # keep the device copies alive across the call
+    torch.cuda.synchronize()
+    st = g.lib().gvdb_topk_merge_device(t_ids.data_ptr(), t_sc.data_ptr(), t_cnt.data_ptr(), S, B, stride, limit, 1,
                                         oi.data_ptr(), os_.data_ptr(), on.data_ptr(), None)
     assert st == 0
     torch.cuda.synchronize()
