@@ -156,32 +156,16 @@ def main():
         def step():
             ix.search_device(q, k, out_ids, out_sc, out_n, sp)
     else:
-        import torch.distributed as dist
+        from gvdb.sharded import ShardedBQSearch, gpu_candidates_fn, shard_bounds
 
-        R_l = min(R, n_local)
-        c_ids = torch.zeros((B, R), dtype=torch.int64, device=dev)
-        c_d = torch.zeros((B, R), dtype=torch.int32, device=dev)
-        c_c = torch.zeros((B, R), dtype=torch.float32, device=dev)
-        pack = torch.zeros((B, R, 4), dtype=torch.int32, device=dev)
-        gathered = torch.zeros((world, B, R, 4), dtype=torch.int32, device=dev)
-        counts = torch.full((world, B), R_l, dtype=torch.int32, device=dev)
-        sync = torch.cuda.current_stream().cuda_stream
+        b = shard_bounds(N, world)
+        sharded = ShardedBQSearch(gpu_candidates_fn(ix), [b[g + 1] - b[g] for g in range(world)], B, R, k, dev)
 
         def step():
-            st = L.gvdb_index_bq_candidates_device(ix._h, q.data_ptr(), B, D, R_l, c_ids.data_ptr(), c_d.data_ptr(),
-                                                   c_c.data_ptr(), sync)
-            gvdb.check(st)
-            pack[:, :R_l, 0:2] = c_ids[:, :R_l].view(torch.int32).view(B, R_l, 2)
-            pack[:, :R_l, 2] = c_d[:, :R_l]
-            pack[:, :R_l, 3] = c_c[:, :R_l].view(torch.int32)
-            dist.all_gather_into_tensor(gathered, pack)  # RCCL over xGMI: B*R*16 bytes per rank
-            g_ids = gathered[..., 0:2].contiguous().view(torch.int64).view(world, B, R)
-            g_d = gathered[..., 2].contiguous()
-            g_c = gathered[..., 3].contiguous().view(torch.float32)
-            st = L.gvdb_bq_shard_merge_device(g_ids.data_ptr(), g_d.data_ptr(), g_c.data_ptr(), counts.data_ptr(),
-                                              world, B, R, R, k, out_ids.data_ptr(), out_sc.data_ptr(),
-                                              out_n.data_ptr(), sync)
-            gvdb.check(st)
+            ids, sc, n = sharded.search(q)
+            out_ids.copy_(ids)
+            out_sc.copy_(sc)
+            out_n.copy_(n)
 
     def barrier():
         torch.cuda.synchronize()

@@ -118,13 +118,13 @@ struct DBuf {
 struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
-    DBuf q, qnorm, qcodes, hist, thr, counts, buf, fail, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow,
-        sort_tmp, flags, rows, norms, codes, misc;
+    DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
+        rows, norms, codes, misc;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     ~Workspace() {
-        for (DBuf* b : {&q, &qnorm, &qcodes, &hist, &thr, &counts, &buf, &fail, &s1_rows, &s1_dist, &scores, &out_ids,
-                        &out_scores, &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc})
+        for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
+                        &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -209,6 +209,31 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t& chunks, uint32_t& stride, u
     bufcap = (uint32_t)std::min<double>((double)N, 8.0 * expect_full + 2048.0);
 }
 
+// Stage-1 workspace: ONE memset zeroes flags | counts | fail | hist, which
+// sit contiguously in ws.zero (flags[0] = any stage-1 failure, flags[1] = NaN).
+gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D, uint32_t R, uint32_t N,
+                           hipStream_t s) {
+    plan_sampling(N, R, s1.sample_chunks, s1.sample_stride, s1.target, s1.bufcap);
+    const size_t nb = (size_t)D + 1u;
+    const size_t words = 4 + 2 * (size_t)B + (size_t)B * nb;
+    HIP_TRY(ws.zero.ensure(words * 4 + 16), "alloc stage-1 state");
+    HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
+    HIP_TRY(ws.buf.ensure((size_t)B * s1.bufcap * 8), "alloc candidate buffer");
+    HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
+    HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
+    HIP_TRY(hipMemsetAsync(ws.zero.p, 0, ((words * 4 + 15) / 16) * 16, s), "memset stage-1 state");
+    uint32_t* z = ws.zero.as<uint32_t>();
+    s1.any_fail = z;
+    s1.counts = z + 4;
+    s1.fail = z + 4 + B;
+    s1.hist = z + 4 + 2 * (size_t)B;
+    s1.thr = ws.thr.as<uint32_t>();
+    s1.buf = ws.buf.as<uint64_t>();
+    s1.s1_rows = ws.s1_rows.as<uint32_t>();
+    s1.s1_dist = ws.s1_dist.as<uint32_t>();
+    return GVDB_OK;
+}
+
 struct BqSearchArgs {
     ShardView v;
     const float* d_q;       // [B][qlen]
@@ -239,13 +264,11 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     const uint32_t W4 = code_w4(v.D);
     HIP_TRY(ws.qnorm.ensure((size_t)B * 4), "alloc qnorm");
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
-    HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
-    HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
     HIP_TRY(ws.scores.ensure((size_t)B * R * 4), "alloc scores");
-    HIP_TRY(ws.fail.ensure((size_t)B * 4), "alloc fail");
-    HIP_TRY(ws.flags.ensure(16), "alloc flags");
-    uint32_t* d_flags = ws.flags.as<uint32_t>();
-    HIP_TRY(hipMemsetAsync(d_flags, 0, 16, s), "memset flags");
+    Stage1Args s1{};
+    gvdb_status pst = prepare_stage1(ws, s1, B, v.D, R, v.N, s);
+    if (pst != GVDB_OK) return pst;
+    uint32_t* d_flags = s1.any_fail;  // [0] any stage-1 failure, [1] NaN
     HIP_TRY(launch_row_norms(a.d_q, B, (uint32_t)a.qlen, ws.qnorm.as<float>(), s), "qnorm");
 
     std::vector<uint32_t> slow_q;
@@ -266,7 +289,6 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             HIP_TRY(launch_pack(a.d_q, B, v.D, a.thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
         }
         if (R <= kSelectLdsCap) {
-            Stage1Args s1{};
             s1.codes = v.codes;
             s1.cap = v.cap;
             s1.N = v.N;
@@ -274,21 +296,6 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             s1.qcodes = ws.qcodes.as<uint4>();
             s1.B = B;
             s1.R = R;
-            plan_sampling(v.N, R, s1.sample_chunks, s1.sample_stride, s1.target, s1.bufcap);
-            HIP_TRY(ws.hist.ensure((size_t)B * (v.D + 1) * 4), "alloc hist");
-            HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
-            HIP_TRY(ws.counts.ensure((size_t)B * 4), "alloc counts");
-            HIP_TRY(ws.buf.ensure((size_t)B * s1.bufcap * 8), "alloc candidate buffer");
-            HIP_TRY(hipMemsetAsync(ws.hist.p, 0, (size_t)B * (v.D + 1) * 4, s), "memset hist");
-            HIP_TRY(hipMemsetAsync(ws.counts.p, 0, (size_t)B * 4, s), "memset counts");
-            HIP_TRY(hipMemsetAsync(ws.fail.p, 0, (size_t)B * 4, s), "memset fail");
-            s1.hist = ws.hist.as<uint32_t>();
-            s1.thr = ws.thr.as<uint32_t>();
-            s1.counts = ws.counts.as<uint32_t>();
-            s1.buf = ws.buf.as<uint64_t>();
-            s1.fail = ws.fail.as<uint32_t>();
-            s1.s1_rows = ws.s1_rows.as<uint32_t>();
-            s1.s1_dist = ws.s1_dist.as<uint32_t>();
             s1.ev = timed ? ws.ev.e : nullptr;
             HIP_TRY(launch_stage1_fast(s1, s), "stage1");
             fast_ran = true;
@@ -346,12 +353,9 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         if (st != GVDB_OK) return st;
         if (timed) HIP_TRY(hipEventRecord(ws.ev.e[5], s), "event");
     }
-    // One host sync per batch: did any query leave the certified fast path?
-    std::vector<uint32_t> fails;
-    if (fast_ran) {
-        fails.resize(B);
-        HIP_TRY(hipMemcpyAsync(fails.data(), ws.fail.p, (size_t)B * 4, hipMemcpyDeviceToHost, s), "read fail");
-    }
+    // One host sync per batch: flags[0] says whether any query left the
+    // certified fast path, flags[1] whether a NaN score appeared.
+    HIP_TRY(hipMemcpyAsync(ws.h_flags, d_flags, 8, hipMemcpyDeviceToHost, s), "read flags");
     HIP_TRY(hipStreamSynchronize(s), "sync");
     if (timed && fast_ran && slow_q.size() < B) {
         float t[4] = {0, 0, 0, 0};
@@ -365,8 +369,12 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             timing().n[i] += 1;
         }
     }
-    for (uint32_t q = 0; q < fails.size(); ++q)
-        if (fails[q]) slow_q.push_back(q);
+    if (fast_ran && ws.h_flags[0]) {
+        std::vector<uint32_t> fails(B);
+        HIP_TRY(hipMemcpy(fails.data(), s1.fail, (size_t)B * 4, hipMemcpyDeviceToHost), "read fail");
+        for (uint32_t q = 0; q < B; ++q)
+            if (fails[q]) slow_q.push_back(q);
+    }
     if (!slow_q.empty()) {
         const size_t need = stage1_slow_bytes(v.N);
         HIP_TRY(ws.slow.ensure(need), "alloc slow path");
@@ -378,9 +386,9 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             gvdb_status st = run_stage2(q, 1);
             if (st != GVDB_OK) return st;
         }
+        HIP_TRY(hipMemcpyAsync(ws.h_flags, d_flags, 8, hipMemcpyDeviceToHost, s), "read flags");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
     }
-    HIP_TRY(hipMemcpyAsync(ws.h_flags, d_flags, 8, hipMemcpyDeviceToHost, s), "read flags");
-    HIP_TRY(hipStreamSynchronize(s), "sync");
     if (ws.h_flags[1])
         return fail(GVDB_ERR_QUANTIZATION, "NaN score: the reference's partial_cmp().unwrap() sort would panic");
     return GVDB_OK;
@@ -607,7 +615,8 @@ gvdb_status gvdb_index_add_device(gvdb_index* ix, const float* d_rows, uint64_t 
     if (st != GVDB_OK) return st;
     if ((st = check_add_dim(ix, dim)) != GVDB_OK) return st;
     if ((st = ensure_capacity(ix, ix->n + n)) != GVDB_OK) return st;
-    if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "caller stream");
+    // the rows were produced on the caller's stream (NULL = default stream): wait for them
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "caller stream");
     HIP_TRY(hipMemcpyAsync(ix->rows + ix->n * dim, d_rows, n * dim * 4, hipMemcpyDeviceToDevice, ix->stream),
             "copy rows");
     HIP_TRY(hipMemcpyAsync(ix->ids + ix->n, d_ids, n * 8, hipMemcpyDeviceToDevice, ix->stream), "copy ids");
@@ -722,7 +731,7 @@ gvdb_status gvdb_index_search_device(const gvdb_index* ix, const float* d_querie
     if ((st = set_device(ix->device)) != GVDB_OK) return st;
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
-    hipStream_t s = stream ? (hipStream_t)stream : g.w->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
     return index_search_impl(ix, d_queries, B, dim, k, sp, d_out_ids, d_out_scores, d_out_n, *g.w, s);
 }
 
@@ -737,17 +746,16 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
-    hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream
     const uint32_t W4 = code_w4(dim);
     const uint32_t RR = (uint32_t)R;
     HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc");
-    HIP_TRY(ws.s1_rows.ensure(B * R * 4), "alloc");
-    HIP_TRY(ws.s1_dist.ensure(B * R * 4), "alloc");
-    HIP_TRY(ws.fail.ensure(B * 4), "alloc");
+    Stage1Args s1{};
+    st = prepare_stage1(ws, s1, (uint32_t)B, dim, RR, (uint32_t)ix->n, s);
+    if (st != GVDB_OK) return st;
     HIP_TRY(launch_pack(d_queries, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
     std::vector<uint32_t> fails(B, 1u);
     if (RR <= kSelectLdsCap) {
-        Stage1Args s1{};
         s1.codes = ix->codes;
         s1.cap = ix->cap;
         s1.N = (uint32_t)ix->n;
@@ -755,23 +763,8 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
         s1.qcodes = ws.qcodes.as<uint4>();
         s1.B = (uint32_t)B;
         s1.R = RR;
-        plan_sampling(s1.N, RR, s1.sample_chunks, s1.sample_stride, s1.target, s1.bufcap);
-        HIP_TRY(ws.hist.ensure(B * (dim + 1) * 4), "alloc");
-        HIP_TRY(ws.thr.ensure(B * 4), "alloc");
-        HIP_TRY(ws.counts.ensure(B * 4), "alloc");
-        HIP_TRY(ws.buf.ensure(B * (size_t)s1.bufcap * 8), "alloc");
-        HIP_TRY(hipMemsetAsync(ws.hist.p, 0, B * (dim + 1) * 4, s), "memset");
-        HIP_TRY(hipMemsetAsync(ws.counts.p, 0, B * 4, s), "memset");
-        HIP_TRY(hipMemsetAsync(ws.fail.p, 0, B * 4, s), "memset");
-        s1.hist = ws.hist.as<uint32_t>();
-        s1.thr = ws.thr.as<uint32_t>();
-        s1.counts = ws.counts.as<uint32_t>();
-        s1.buf = ws.buf.as<uint64_t>();
-        s1.fail = ws.fail.as<uint32_t>();
-        s1.s1_rows = ws.s1_rows.as<uint32_t>();
-        s1.s1_dist = ws.s1_dist.as<uint32_t>();
         HIP_TRY(launch_stage1_fast(s1, s), "stage1");
-        HIP_TRY(hipMemcpyAsync(fails.data(), ws.fail.p, B * 4, hipMemcpyDeviceToHost, s), "read fail");
+        HIP_TRY(hipMemcpyAsync(fails.data(), s1.fail, B * 4, hipMemcpyDeviceToHost, s), "read fail");
         HIP_TRY(hipStreamSynchronize(s), "sync");
     }
     bool any_slow = false;
@@ -1072,7 +1065,7 @@ gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* ix, const float* d
     if ((st = set_device(ix->device)) != GVDB_OK) return st;
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
-    hipStream_t s = stream ? (hipStream_t)stream : g.w->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
     BqSearchArgs a{};
     a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
     a.d_q = d_queries;
@@ -1100,7 +1093,7 @@ gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d
         return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     WsGuard g(0);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
-    hipStream_t s = stream ? (hipStream_t)stream : g.w->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
     HIP_TRY(g.w->flags.ensure(16), "alloc flags");
     HIP_TRY(hipMemsetAsync(g.w->flags.p, 0, 16, s), "memset flags");
     HIP_TRY(launch_bq_shard_merge(d_gids, d_dist, d_cos, d_counts, (uint32_t)G, (uint32_t)B, (uint32_t)stride,

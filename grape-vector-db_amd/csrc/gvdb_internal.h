@@ -72,6 +72,7 @@ struct Stage1Args {
     uint64_t* buf;           // [B][bufcap]
     uint32_t bufcap;
     uint32_t* fail;          // [B]  (1 = fast path could not certify the top-R)
+    uint32_t* any_fail;      // [1]  OR of fail[]
     uint32_t* s1_rows;       // [B][R]
     uint32_t* s1_dist;       // [B][R]
     hipEvent_t* ev;          // optional [4]: before hist, before scan, after scan, after select

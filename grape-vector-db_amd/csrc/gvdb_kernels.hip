@@ -461,6 +461,7 @@ __device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
 // exact slow path.
 __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ counts, const uint64_t* __restrict__ buf,
                                                 uint32_t bufcap, uint32_t D, uint32_t R, uint32_t* __restrict__ fail,
+                                                uint32_t* __restrict__ any_fail,
                                                 uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist
     uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
@@ -468,7 +469,13 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
     const uint32_t q = blockIdx.x;
     const uint32_t cnt = counts[q];
     if (cnt < R || cnt > bufcap) {
-        if (threadIdx.x == 0) fail[q] = 1u;
+        // keep the stage-2 launch that still runs over this query in bounds;
+        // the host reruns the query on the exact slow path
+        for (uint32_t i = threadIdx.x; i < R; i += 256) s1_rows[(uint64_t)q * R + i] = 0u;
+        if (threadIdx.x == 0) {
+            fail[q] = 1u;
+            atomicOr(any_fail, 1u);
+        }
         return;
     }
     const uint64_t* b = buf + (uint64_t)q * bufcap;
@@ -500,7 +507,13 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
     __syncthreads();
     const uint32_t n = s_n;
     if (n > kSelectLdsCap) {
-        if (threadIdx.x == 0) fail[q] = 1u;
+        // keep the stage-2 launch that still runs over this query in bounds;
+        // the host reruns the query on the exact slow path
+        for (uint32_t i = threadIdx.x; i < R; i += 256) s1_rows[(uint64_t)q * R + i] = 0u;
+        if (threadIdx.x == 0) {
+            fail[q] = 1u;
+            atomicOr(any_fail, 1u);
+        }
         return;
     }
     const uint32_t P = next_pow2(n);
@@ -584,7 +597,7 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
     const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)(a.D + 1u) * 4u;
     hipLaunchKernelGGL(k_select, dim3(a.B), dim3(256), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R, a.fail,
-                       a.s1_rows, a.s1_dist);
+                       a.any_fail, a.s1_rows, a.s1_dist);
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[3], s);
     return hipSuccess;

@@ -95,6 +95,16 @@ def check(status: int) -> None:
     raise cls(msg)
 
 
+def _stream(stream: Optional[int]):
+    """The HIP stream for a _device call: the given handle, else torch's current
+    stream (the inputs were produced there)."""
+    if stream is not None:
+        return stream or None
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream or None
+
+
 def _f32(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
 
@@ -301,10 +311,10 @@ class GpuVectorIndex:
         check(self._lib.gvdb_index_add(self._h, ptr(rows), rows.shape[0], rows.shape[1] if rows.ndim == 2 else 0,
                                        ptr(ids)))
 
-    def add_device(self, rows, ids, stream: int = 0) -> None:
-        """rows: torch cuda float32 [n, D]; ids: torch cuda int64/uint64 [n]."""
+    def add_device(self, rows, ids, stream: Optional[int] = None) -> None:
+        """rows: torch cuda float32 [n, D]; ids: torch cuda int64/uint64 [n] (copied into the index)."""
         check(self._lib.gvdb_index_add_device(self._h, rows.data_ptr(), rows.shape[0], rows.shape[1],
-                                              ids.data_ptr(), stream or None))
+                                              ids.data_ptr(), _stream(stream)))
 
     def search(self, query: Sequence[float], k: int) -> List[Tuple[str, float]]:
         q = _f32(query).reshape(1, -1)
@@ -325,15 +335,15 @@ class GpuVectorIndex:
         return ids[:, :k], sc[:, :k], n
 
     def search_device(self, queries, k: int, out_ids, out_scores, out_n=None, params: Optional[SearchParams] = None,
-                      stream: int = 0) -> None:
+                      stream: Optional[int] = None) -> None:
         sp = (params or self.params).to_c()
         check(self._lib.gvdb_index_search_device(self._h, queries.data_ptr(), queries.shape[0], queries.shape[1], k,
                                                  C.byref(sp), out_ids.data_ptr(), out_scores.data_ptr(),
-                                                 out_n.data_ptr() if out_n is not None else None, stream or None))
+                                                 out_n.data_ptr() if out_n is not None else None, _stream(stream)))
 
-    def bq_topr_device(self, queries, R: int, out_rows, out_dist, stream: int = 0) -> None:
+    def bq_topr_device(self, queries, R: int, out_rows, out_dist, stream: Optional[int] = None) -> None:
         check(self._lib.gvdb_index_bq_topr_device(self._h, queries.data_ptr(), queries.shape[0], queries.shape[1], R,
-                                                  out_rows.data_ptr(), out_dist.data_ptr(), stream or None))
+                                                  out_rows.data_ptr(), out_dist.data_ptr(), _stream(stream)))
 
     def remove_vector(self, id: str) -> bool:
         u = self._id_of.get(id)

@@ -1,0 +1,104 @@
+"""Exact sharded BQ multi-stage search over torch.distributed.
+
+Replaces ``ShardManager::search_vectors`` (src/distributed/shard.rs:760-786:
+scatter to shards, concat, sort, truncate) inside one node.  Each rank owns a
+contiguous row range whose ids are global row numbers.  Per batch:
+
+1. the rank computes its LOCAL stage-1 top-R (Hamming asc, row asc) and the
+   exact cosine of each candidate (``gvdb_index_bq_candidates_device``);
+2. ONE all-gather moves the (id, Hamming, cosine) triplets — B*R*16 bytes per
+   rank — over RCCL/xGMI (gloo on CPU in the tests);
+3. every rank merges: union sorted by (Hamming, id) -> first R -> stable sort by
+   cosine desc -> first k (``gvdb_bq_shard_merge[_device]``).
+
+The union of local top-R lists contains the global top-R, so the result is
+bit-identical to one multi_stage_search over the concatenated corpus.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import check
+from ._ffi import lib
+
+# candidates_fn(queries, R_local) -> (gids int64 [B,R_local], dist int32 [B,R_local], cos f32 [B,R_local])
+CandidatesFn = Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]
+
+
+def shard_bounds(n: int, world: int) -> List[int]:
+    return [n * g // world for g in range(world + 1)]
+
+
+class ShardedBQSearch:
+    def __init__(self, candidates_fn: CandidatesFn, shard_rows: Sequence[int], B: int, R: int, k: int,
+                 device: torch.device, group=None):
+        self.cand = candidates_fn
+        self.world = len(shard_rows)
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.B, self.R, self.k = B, R, k
+        self.dev = device
+        self.group = group
+        self.on_gpu = device.type == "cuda"
+        self.r_local = [min(R, n) for n in shard_rows]
+        self.pack = torch.zeros((B, R, 4), dtype=torch.int32, device=device)
+        self.gathered = torch.zeros((self.world, B, R, 4), dtype=torch.int32, device=device)
+        self.counts = torch.tensor([[r] * B for r in self.r_local], dtype=torch.int32, device=device)
+        self.out_ids = torch.zeros((B, k), dtype=torch.int64, device=device)
+        self.out_scores = torch.zeros((B, k), dtype=torch.float32, device=device)
+        self.out_n = torch.zeros(B, dtype=torch.int32, device=device)
+
+    def search(self, q: torch.Tensor):
+        B, R, k = self.B, self.R, self.k
+        rl = self.r_local[self.rank]
+        gids, d, c = self.cand(q, rl)
+        self.pack[:, :rl, 0:2] = gids[:, :rl].contiguous().view(torch.int32).view(B, rl, 2)
+        self.pack[:, :rl, 2] = d[:, :rl]
+        self.pack[:, :rl, 3] = c[:, :rl].contiguous().view(torch.int32)
+        if self.world > 1:
+            if self.on_gpu:
+                dist.all_gather_into_tensor(self.gathered, self.pack, group=self.group)
+            else:
+                parts = list(self.gathered.unbind(0))
+                dist.all_gather(parts, self.pack, group=self.group)
+                self.gathered = torch.stack(parts)
+        else:
+            self.gathered[0].copy_(self.pack)
+        g_ids = self.gathered[..., 0:2].contiguous().view(torch.int64).view(self.world, B, R)
+        g_d = self.gathered[..., 2].contiguous()
+        g_c = self.gathered[..., 3].contiguous().view(torch.float32)
+        L = lib()
+        if self.on_gpu:
+            stream = torch.cuda.current_stream(self.dev).cuda_stream or None
+            check(L.gvdb_bq_shard_merge_device(g_ids.data_ptr(), g_d.data_ptr(), g_c.data_ptr(),
+                                               self.counts.data_ptr(), self.world, B, R, R, k,
+                                               self.out_ids.data_ptr(), self.out_scores.data_ptr(),
+                                               self.out_n.data_ptr(), stream))
+        else:
+            check(L.gvdb_bq_shard_merge(g_ids.data_ptr(), g_d.data_ptr(), g_c.data_ptr(), self.counts.data_ptr(),
+                                        self.world, B, R, R, k, self.out_ids.data_ptr(),
+                                        self.out_scores.data_ptr(), self.out_n.data_ptr()))
+        return self.out_ids, self.out_scores, self.out_n
+
+
+def gpu_candidates_fn(index) -> CandidatesFn:
+    """Local candidates from a GpuVectorIndex whose ids are global row numbers."""
+    bufs = {}
+
+    def fn(q: torch.Tensor, r: int):
+        B = q.shape[0]
+        key = (B, r)
+        if key not in bufs:
+            bufs[key] = (torch.zeros((B, r), dtype=torch.int64, device=q.device),
+                         torch.zeros((B, r), dtype=torch.int32, device=q.device),
+                         torch.zeros((B, r), dtype=torch.float32, device=q.device))
+        ids, d, c = bufs[key]
+        stream = torch.cuda.current_stream(q.device).cuda_stream or None
+        check(lib().gvdb_index_bq_candidates_device(index._h, q.data_ptr(), B, q.shape[1], r, ids.data_ptr(),
+                                                     d.data_ptr(), c.data_ptr(), stream))
+        return ids, d, c
+
+    return fn

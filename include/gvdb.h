@@ -23,9 +23,9 @@
  *   - errors: gvdb_status codes 1:1 with VectorDbError (src/types.rs:859-920)
  *     plus GVDB_ERR_DEVICE; details via gvdb_last_error() (thread-local).
  *   - functions suffixed _device take DEVICE pointers (HBM-resident inputs
- *     and outputs) and an optional hipStream_t passed as void* (NULL = the
- *     library's own stream for that call).  They are the zero-copy form used
- *     when the caller already keeps data on the GPU.
+ *     and outputs) and the hipStream_t (as void*) the caller produced them on
+ *     and wants the work ordered on; NULL = the legacy default stream.  They
+ *     are the zero-copy form used when the caller keeps data on the GPU.
  */
 #ifndef GVDB_H_
 #define GVDB_H_

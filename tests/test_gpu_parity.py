@@ -143,6 +143,19 @@ def test_stage1_massive_ties_fallback(g, oracle_mod):
     assert (gi == ri).all() and (gd == rd).all()
 
 
+def test_index_search_after_fallback(g, oracle_mod):
+    # a batch where one query leaves the fast path (12k ties) and the others do not
+    N, D, R, k = 30_000, 64, 500, 10
+    x = rng_rows(4, N, D)
+    x[100:12_100] = x[1]
+    Q = np.concatenate([x[1:2], rng_rows(5, 3, D)])
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_count=R))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (ids == ri[:, :k]).all() and same_f32(sc, rs[:, :k])
+
+
 # --------------------------------------------------------------------------- index search (VectorIndex)
 @pytest.mark.parametrize("N,D,B,R,k,metric", [(20_000, 128, 16, 100, 10, 0), (20_000, 128, 8, 100, 10, 1),
                                                (20_000, 96, 8, 64, 64, 2), (300_000, 768, 4, 100, 10, 0),
@@ -282,3 +295,14 @@ def test_sharded_candidates_merge_equals_single_device(g, oracle_mod):
     ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R, kind=0)
     assert (mi.cpu().numpy().view(np.uint64) == ri[:, :k]).all()
     assert same_f32(ms.cpu().numpy(), rs[:, :k])
+
+
+def test_reference_unit_tests_through_cpp_mirror(g):
+    """The reference's own unit tests (quantization.rs:361-400, query.rs:428-483)
+    re-run through the C++ host mirror grape-vector-db_amd/host/gvdb.hpp."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(g.lib()._name), "build", "reference_tests")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
