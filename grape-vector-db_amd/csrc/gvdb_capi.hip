@@ -269,7 +269,6 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     gvdb_status pst = prepare_stage1(ws, s1, B, v.D, R, v.N, s);
     if (pst != GVDB_OK) return pst;
     uint32_t* d_flags = s1.any_fail;  // [0] any stage-1 failure, [1] NaN
-    HIP_TRY(launch_row_norms(a.d_q, B, (uint32_t)a.qlen, ws.qnorm.as<float>(), s), "qnorm");
 
     std::vector<uint32_t> slow_q;
     bool fast_ran = false;
@@ -311,7 +310,6 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         rr.norms = v.norms;
         rr.q = a.d_q + (uint64_t)q0 * a.qlen;
         rr.qlen = a.qlen;
-        rr.qnorm = ws.qnorm.as<float>() + q0;
         rr.s1_rows = ws.s1_rows.as<uint32_t>() + (uint64_t)q0 * R;
         rr.B = nq;
         rr.R = R;

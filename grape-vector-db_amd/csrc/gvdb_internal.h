@@ -94,9 +94,8 @@ struct RerankArgs {
     const float* rows;       // [*][clen]
     uint64_t clen;
     const float* norms;      // [*]
-    const float* q;          // [B][qlen]
+    const float* q;          // [B][qlen]   (query norms are folded in-kernel)
     uint64_t qlen;
-    const float* qnorm;      // [B]
     const uint32_t* s1_rows; // [B][R]
     uint32_t B, R;
     int kind;                // ScoreKind

@@ -300,22 +300,47 @@ __global__ __launch_bounds__(256) void k_sample_hist(const uint4* __restrict__ c
     }
 }
 
-// T[q] = smallest t with (sample count of d <= t) >= target; D if never.
-// Also emits T into counts' companion (thr) and resets nothing else.
-__global__ void k_threshold(const uint32_t* __restrict__ hist, uint32_t B, uint32_t D, uint32_t target,
-                            uint32_t* __restrict__ thr) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= B) return;
-    const uint32_t* h = hist + (uint64_t)q * (D + 1u);
-    uint32_t cum = 0, t = D;
-    for (uint32_t i = 0; i <= D; ++i) {
-        cum += h[i];
-        if (cum >= target) {
-            t = i;
-            break;
+// Smallest t in [0, nb) with sum(h[0..t]) >= target (nb-1 if never), by one
+// full wave: each lane sums a contiguous segment, a shuffle scan finds the
+// segment that crosses the target, that lane walks its segment.
+__device__ uint32_t wave_find_cum(const uint32_t* h, uint32_t nb, uint32_t target) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t seg = (nb + 63u) / 64u;
+    const uint32_t b0 = lane * seg;
+    const uint32_t b1 = min(b0 + seg, nb);
+    uint32_t s = 0;
+    for (uint32_t i = b0; i < b1; ++i) s += h[i];
+    uint32_t incl = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off);
+        if ((int)lane >= off) incl += v;
+    }
+    const uint64_t m = __ballot(incl >= target);
+    if (m == 0) return nb - 1;
+    const uint32_t first = __ffsll((long long)m) - 1;
+    uint32_t t = nb - 1;
+    if (lane == first) {
+        uint32_t cum = incl - s;
+        for (uint32_t i = b0; i < b1; ++i) {
+            cum += h[i];
+            if (cum >= target) {
+                t = i;
+                break;
+            }
         }
     }
-    thr[q] = t;
+    return __shfl(t, first);
+}
+
+// T[q] = smallest t with (sample count of d <= t) >= target; D if never.
+// One wave per query.
+__global__ __launch_bounds__(256) void k_threshold(const uint32_t* __restrict__ hist, uint32_t B, uint32_t D,
+                                                   uint32_t target, uint32_t* __restrict__ thr) {
+    const uint32_t q = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (q >= B) return;
+    const uint32_t t = wave_find_cum(hist + (uint64_t)q * (D + 1u), D + 1u, target);
+    if ((threadIdx.x & 63u) == 0) thr[q] = t;
 }
 
 // The hot loop.  Each lane holds CPL rows' codes in VGPRs (coalesced 16-B
@@ -484,16 +509,9 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += 256) atomicAdd(&hist[(uint32_t)(b[i] >> 32)], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t cum = 0, t = D;
-        for (uint32_t i = 0; i <= D; ++i) {
-            cum += hist[i];
-            if (cum >= R) {
-                t = i;
-                break;
-            }
-        }
-        s_T = t;
+    if (threadIdx.x < 64) {
+        const uint32_t t = wave_find_cum(hist, D + 1u, R);
+        if (threadIdx.x == 0) s_T = t;
     }
     __syncthreads();
     const uint32_t T = s_T;
@@ -570,7 +588,7 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
                                a.N, a.D, W4, a.sample_stride, a.qcodes, a.B, a.hist);
     }
     GVDB_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_threshold, dim3((a.B + 255) / 256), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
+    hipLaunchKernelGGL(k_threshold, dim3((a.B + 3) / 4), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
     switch (W4) {
@@ -662,62 +680,125 @@ hipError_t launch_iota_rows(uint32_t* rows, uint32_t B, uint32_t R, hipStream_t 
 }
 
 // ============================================================================
-// K3: exact rerank.  Block = 4 waves of one query; lane = one stage-1
-// candidate; the lane folds q . x (or sum (q-x)^2) over the dims in order.
+// K3: exact rerank.  A block of 512 threads owns 64 stage-1 candidates of one
+// query.  All 8 waves stream the candidates' rows through a double-buffered
+// LDS tile ([64 rows][256 dims], 16-B loads, one 1-KiB row segment per
+// wave-instruction; the next chunk's loads are in flight while the current
+// one is folded); wave 0 folds: lane r owns candidate r and accumulates
+// q_j*x_j (or (q_j-x_j)^2) left to right, and every lane also folds q_j*q_j
+// for the query norm -- the reference's exact sequential order, so cosine /
+// L2 are bit-identical to cosine_similarity_manual / VectorPoint::distance.
+// Row stride 260 floats: conflict-free ds_read_b128 (16-lane groups) and
+// ds_write_b128 (8-lane groups).
 // ============================================================================
-__global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ rows, uint64_t clen,
-                                                const float* __restrict__ norms, const float* __restrict__ q,
-                                                uint64_t qlen, const float* __restrict__ qnorm,
-                                                const uint32_t* __restrict__ s1_rows, uint32_t R, int kind,
-                                                float* __restrict__ scores) {
-    __shared__ __attribute__((aligned(16))) float tiles[4][64 * kTileLd];
-    __shared__ __attribute__((aligned(16))) float qs[kCh];
-    __shared__ uint64_t bases[4][64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+constexpr int kRrRows = 64;
+constexpr int kRrCh = 256;
+constexpr int kRrLd = kRrCh + 4;
+constexpr int kRrThreads = 512;
+constexpr int kRrPer = kRrRows * (kRrCh / 4) / kRrThreads;  // float4 per thread per chunk (8)
+
+__device__ __forceinline__ float4 load4_guarded(const float* __restrict__ src, uint64_t base, uint64_t j, uint64_t len,
+                                               bool vec4) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (base == ~0ull) return v;
+    if (vec4 && j + 3 < len) return *(const float4*)(src + base + j);
+    if (j + 0 < len) v.x = src[base + j + 0];
+    if (j + 1 < len) v.y = src[base + j + 1];
+    if (j + 2 < len) v.z = src[base + j + 2];
+    if (j + 3 < len) v.w = src[base + j + 3];
+    return v;
+}
+
+__global__ __launch_bounds__(kRrThreads) void k_rerank(const float* __restrict__ rows, uint64_t clen,
+                                                       const float* __restrict__ norms, const float* __restrict__ q,
+                                                       uint64_t qlen, const uint32_t* __restrict__ s1_rows, uint32_t R,
+                                                       int kind, float* __restrict__ scores) {
+    __shared__ __attribute__((aligned(16))) float tiles[2][kRrRows * kRrLd];
+    __shared__ __attribute__((aligned(16))) float qs[2][kRrCh];
+    __shared__ uint64_t bases[kRrRows];
+    const uint32_t tid = threadIdx.x;
     const uint32_t qi = blockIdx.y;
-    const uint32_t r = blockIdx.x * 256u + threadIdx.x;
-    const bool valid = r < R;
-    const uint32_t row = valid ? s1_rows[(uint64_t)qi * R + r] : 0u;
-    bases[wv][lane] = valid ? (uint64_t)row * clen : ~0ull;
-    const float* qv = q + (uint64_t)qi * qlen;
-    float* tile = tiles[wv];
-    // dot: zip(query, cand) truncates to min(qlen, clen); L2 uses the same length.
-    const uint64_t len = qlen < clen ? qlen : clen;
-    const bool vec4 = (clen & 3u) == 0;
-    float acc = -0.0f;
+    const uint32_t r0 = blockIdx.x * kRrRows;
+    if (tid < kRrRows) {
+        const uint32_t r = r0 + tid;
+        bases[tid] = r < R ? (uint64_t)s1_rows[(uint64_t)qi * R + r] * clen : ~0ull;
+    }
     __syncthreads();
-    for (uint64_t c0 = 0; c0 < len; c0 += kCh) {
-        stage_tile(tile, rows, bases[wv], c0, len, vec4, lane);
-        if (threadIdx.x < kCh) qs[threadIdx.x] = (c0 + threadIdx.x < len) ? qv[c0 + threadIdx.x] : 0.0f;
-        __syncthreads();
-        const uint32_t m = (uint32_t)((len - c0) < (uint64_t)kCh ? (len - c0) : kCh);
-        const float* tr = tile + lane * kTileLd;
-        if (kind == kScoreL2) {
-            for (uint32_t j = 0; j < m; ++j) {
-                const float d = qs[j] - tr[j];
-                acc = acc + d * d;
-            }
-        } else if (m == kCh) {
+    const float* qv = q + (uint64_t)qi * qlen;
+    const uint64_t len = qlen < clen ? qlen : clen;  // zip() truncates
+    const bool vec4 = (clen & 3u) == 0;
+    const bool qvec4 = (qlen & 3u) == 0 && (((uintptr_t)qv) & 15u) == 0;
+    const uint32_t nch = (uint32_t)((len + kRrCh - 1) / kRrCh);
+    float4 rg[kRrPer];
+    float4 qg = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load = [&](uint32_t c) {
 #pragma unroll
-            for (int j = 0; j < kCh; j += 4) {
-                const float4 v = *(const float4*)(tr + j);
-                const float4 w = *(const float4*)(qs + j);
-                acc = acc + w.x * v.x;
-                acc = acc + w.y * v.y;
-                acc = acc + w.z * v.z;
-                acc = acc + w.w * v.w;
-            }
-        } else {
-            for (uint32_t j = 0; j < m; ++j) acc = acc + qs[j] * tr[j];
+        for (int it = 0; it < kRrPer; ++it) {
+            const uint32_t idx = it * kRrThreads + tid;
+            rg[it] = load4_guarded(rows, bases[idx >> 6], (uint64_t)c * kRrCh + 4u * (idx & 63u), len, vec4);
         }
+        if (tid < kRrCh / 4) qg = load4_guarded(qv, 0, (uint64_t)c * kRrCh + 4u * tid, len, qvec4);
+    };
+    auto store = [&](uint32_t c) {
+        float* t = tiles[c & 1];
+#pragma unroll
+        for (int it = 0; it < kRrPer; ++it) {
+            const uint32_t idx = it * kRrThreads + tid;
+            *(float4*)(t + (idx >> 6) * kRrLd + 4u * (idx & 63u)) = rg[it];
+        }
+        if (tid < kRrCh / 4) *(float4*)(qs[c & 1] + 4u * tid) = qg;
+    };
+    float acc = -0.0f, qq = -0.0f;
+    if (nch) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (uint32_t c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load(c + 1);
+        if (tid < 64) {
+            const float* tr = tiles[c & 1] + tid * kRrLd;
+            const float* qc = qs[c & 1];
+            const uint32_t m = (uint32_t)min((uint64_t)kRrCh, len - (uint64_t)c * kRrCh);
+            if (kind == kScoreL2) {
+                for (uint32_t j = 0; j < m; ++j) {
+                    const float d = qc[j] - tr[j];
+                    acc = acc + d * d;
+                }
+            } else if (m == kRrCh) {
+#pragma unroll 8
+                for (int j = 0; j < kRrCh; j += 4) {
+                    const float4 x = *(const float4*)(tr + j);
+                    const float4 w = *(const float4*)(qc + j);
+                    acc = acc + w.x * x.x;
+                    acc = acc + w.y * x.y;
+                    acc = acc + w.z * x.z;
+                    acc = acc + w.w * x.w;
+                    qq = qq + w.x * w.x;
+                    qq = qq + w.y * w.y;
+                    qq = qq + w.z * w.z;
+                    qq = qq + w.w * w.w;
+                }
+            } else {
+                for (uint32_t j = 0; j < m; ++j) {
+                    acc = acc + qc[j] * tr[j];
+                    qq = qq + qc[j] * qc[j];
+                }
+            }
+        }
+        if (c + 1 < nch) store(c + 1);
         __syncthreads();
     }
-    if (!valid) return;
+    if (tid >= 64) return;
+    const uint32_t r = r0 + tid;
+    if (r >= R) return;
     float score;
     if (kind == kScoreL2) {
         score = sqrtf(acc);
     } else {
-        const float na = qnorm[qi], nb = norms[row];
+        for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+        const float na = sqrtf(qq);
+        const float nb = norms[s1_rows[(uint64_t)qi * R + r]];
         if (kind == kScoreCosine) {
             score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
         } else {
@@ -729,8 +810,8 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ rows, 
 
 hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
     if (a.B == 0 || a.R == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rerank, dim3((a.R + 255) / 256, a.B), dim3(256), 0, s, a.rows, a.clen, a.norms, a.q, a.qlen,
-                       a.qnorm, a.s1_rows, a.R, a.kind, a.scores);
+    hipLaunchKernelGGL(k_rerank, dim3((a.R + kRrRows - 1) / kRrRows, a.B), dim3(kRrThreads), 0, s, a.rows, a.clen,
+                       a.norms, a.q, a.qlen, a.s1_rows, a.R, a.kind, a.scores);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
