@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -214,6 +215,9 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t& chunks, uint32_t& stride, u
 gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D, uint32_t R, uint32_t N,
                            hipStream_t s) {
     plan_sampling(N, R, s1.sample_chunks, s1.sample_stride, s1.target, s1.bufcap);
+    // GVDB_SCAN=valu forces the popcount scan for every batch size (A/B runs)
+    const char* scan = getenv("GVDB_SCAN");
+    s1.use_mfma = !(scan && strcmp(scan, "valu") == 0);
     const size_t nb = (size_t)D + 1u;
     const size_t words = 4 + 2 * (size_t)B + (size_t)B * nb;
     HIP_TRY(ws.zero.ensure(words * 4 + 16), "alloc stage-1 state");

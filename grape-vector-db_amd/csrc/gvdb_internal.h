@@ -76,7 +76,9 @@ struct Stage1Args {
     uint32_t* s1_rows;       // [B][R]
     uint32_t* s1_dist;       // [B][R]
     hipEvent_t* ev;          // optional [4]: before hist, before scan, after scan, after select
+    int use_mfma;            // allow the i8-MFMA scan for large batches
 };
+constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 // hist/counts/fail must be zeroed by the caller on stream s.
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s);
 // Exact slow path for ONE query: all N distances + stable radix sort.

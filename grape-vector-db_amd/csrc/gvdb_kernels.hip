@@ -545,6 +545,176 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
     }
 }
 
+// ----------------------------------------------------------------------------
+// k_scan_mfma — the same stage-1 filter for LARGE batches on the matrix cores.
+//
+// Hamming as a +/-1 dot product: with s(b) = 1 - 2b per bit,
+//   sum_k s(q_k) s(c_k) = Kpad - 2 * hamming(q, c)
+// (pad bits are 0 in both codes and cancel), so one 32-bit code word is one
+// K=32 step of v_mfma_i32_32x32x32_i8 and the distances stay exact integers.
+// Which k-slot a lane's 16 bytes occupy never matters: A (queries) and B
+// (candidates) are fed with the same bit->slot map, and the dot product sums
+// over all slots.
+//
+// Block = 8 waves, one CU.  Wave w keeps the +/-1 fragments of query tile w
+// (32 queries x all KS k-steps, KS = 4*W4) in VGPRs for the whole launch.
+// The block walks candidate tiles of 64 rows (persistent grid): all 512
+// threads expand the tile's codes (coalesced SoA 16-B loads) into a
+// double-buffered LDS image laid out so every B fragment is one contiguous
+// ds_read_b128 per wave; each wave then runs KS x 2 MFMAs (2 sub-tiles of 32
+// candidates) and compares its 2 x 16 i32 results with its queries'
+// thresholds.  Per pair: 768/1024 of an i8 MFMA slot at D=768, instead of
+// 48 VALU ops on the popcount path.
+// ----------------------------------------------------------------------------
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v16i_t __attribute__((ext_vector_type(16)));
+
+// 4 code bits -> 4 bytes of +/-1 (bit 0 -> 0x01, bit 1 -> 0xFF): spread the
+// bits to bit 0 of each byte with one 24-bit multiply, then byte*255 | 1.
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pm1_x4(uint32_t nib) {
+    const uint32_t t = __umul24(nib, 0x00204081u) & 0x01010101u;
+    // byte*255 per 16-bit half (v_pk_mul_lo_u16: full rate; a 32-bit t*255
+    // would become a quarter-rate v_mul_lo_u32)
+    const u16x2_t m = __builtin_bit_cast(u16x2_t, t) * (u16x2_t){255, 255};
+    return __builtin_bit_cast(uint32_t, m) | 0x01010101u;
+}
+__device__ __forceinline__ v4i_t pm1_x16(uint32_t h16) {
+    v4i_t r;
+    r.x = (int)pm1_x4(h16 & 15u);
+    r.y = (int)pm1_x4((h16 >> 4) & 15u);
+    r.z = (int)pm1_x4((h16 >> 8) & 15u);
+    r.w = (int)pm1_x4((h16 >> 12) & 15u);
+    return r;
+}
+
+constexpr int kMfThreads = 512;
+constexpr int kMfCand = 64;  // candidates per tile (2 MFMA sub-tiles of 32)
+
+template <int W4>
+__global__ __launch_bounds__(kMfThreads, 2) void k_scan_mfma(const uint4* __restrict__ codes, uint64_t cap,
+                                                            uint32_t N, const uint32_t* __restrict__ qwords,
+                                                            const uint32_t* __restrict__ thr, uint32_t B,
+                                                            uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                            uint32_t bufcap) {
+    constexpr int KS = 4 * W4;              // k-steps = 32-bit code words
+    constexpr int kTileBytes = 2 * KS * 64 * 16;  // [sub-tile][k-step][lane][16 B]
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2][kTileBytes];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t q0 = wv * 32u;
+    const bool active = q0 < B;
+    // query fragments (A operand): lane holds query (q0 + lane&31), half (lane>>5)
+    v4i_t qa[KS];
+    int32_t T[16];  // per accumulator row: threshold of that query, -1 = padding row (never emits)
+    {
+        const uint32_t qr = min(q0 + (lane & 31u), B - 1u);
+        const uint32_t* qw = qwords + (uint64_t)qr * (4u * W4);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) qa[s] = pm1_x16(qw[s] >> (16u * (lane >> 5)));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            T[r] = qi < B ? (int32_t)thr[qi] : -1;
+        }
+    }
+    constexpr uint32_t kPad = 32u * KS;
+    const uint32_t ntiles = (N + kMfCand - 1) / kMfCand;
+    // expansion work: (candidate c in tile, plane w4) items; each produces 4 words x 2 halves
+    constexpr int kItems = kMfCand * W4;
+    uint4 cw[(kItems + kMfThreads - 1) / kMfThreads];
+    auto load = [&](uint32_t t) {
+#pragma unroll
+        for (int i = 0; i < (kItems + kMfThreads - 1) / kMfThreads; ++i) {
+            const uint32_t it = i * kMfThreads + tid;
+            if (it < (uint32_t)kItems) {
+                const uint32_t c = it % kMfCand, w4 = it / kMfCand;
+                const uint32_t n = min(t * kMfCand + c, N - 1u);
+                cw[i] = codes[(uint64_t)w4 * cap + n];
+            }
+        }
+    };
+    auto expand = [&](int b) {
+#pragma unroll
+        for (int i = 0; i < (kItems + kMfThreads - 1) / kMfThreads; ++i) {
+            const uint32_t it = i * kMfThreads + tid;
+            if (it < (uint32_t)kItems) {
+                const uint32_t c = it % kMfCand, w4 = it / kMfCand;
+                const uint32_t st = c >> 5, col = c & 31u;
+                const uint32_t words[4] = {cw[i].x, cw[i].y, cw[i].z, cw[i].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t s = 4u * w4 + j;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t off = ((st * KS + s) * 64u + h * 32u + col) * 16u;
+                        *(v4i_t*)(&lds[b][off]) = pm1_x16(words[j] >> (16 * h));
+                    }
+                }
+            }
+        }
+    };
+    uint32_t t = blockIdx.x;
+    if (t < ntiles) {
+        load(t);
+        expand(0);
+    }
+    __syncthreads();
+    for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+        const int b = it & 1;
+        const uint32_t tn = t + gridDim.x;
+        if (tn < ntiles) load(tn);
+        if (active) {
+            v16i_t acc0 = {0}, acc1 = {0};
+            const v4i_t* bf = (const v4i_t*)lds[b];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], bf[(0 * KS + s) * 64 + lane], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], bf[(1 * KS + s) * 64 + lane], acc1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                const v16i_t& acc = st ? acc1 : acc0;
+                const uint32_t n = t * kMfCand + st * 32u + (lane & 31u);
+                bool any = false;
+                uint32_t d[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    d[r] = (kPad - (uint32_t)acc[r]) >> 1;
+                    any |= (int32_t)d[r] <= T[r];
+                }
+                if (any && n < N) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        if ((int32_t)d[r] <= T[r]) {
+                            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            const uint32_t pos = atomicAdd(&counts[qi], 1u);
+                            if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = ((uint64_t)d[r] << 32) | n;
+                        }
+                    }
+                }
+            }
+        }
+        if (tn < ntiles) expand(b ^ 1);
+        __syncthreads();
+    }
+}
+
+template <int W4>
+static void launch_scan_mfma_t(const Stage1Args& a, hipStream_t s) {
+    const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t grid = min(ntiles, (uint32_t)cus);
+    // 256 queries per launch (8 waves x 32); larger batches loop over query groups
+    for (uint32_t g = 0; g < a.B; g += 256) {
+        const uint32_t bg = min(256u, a.B - g);
+        hipLaunchKernelGGL((k_scan_mfma<W4>), dim3(grid), dim3(kMfThreads), 0, s, a.codes, a.cap, a.N,
+                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
+                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+    }
+}
+
 template <int W4, int CPL>
 static void launch_scan_t(const Stage1Args& a, hipStream_t s) {
     const uint64_t per_block = 256ull * CPL;
@@ -591,7 +761,16 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_threshold, dim3((a.B + 3) / 4), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
-    switch (W4) {
+    const bool mfma = a.use_mfma && a.B >= kMfmaMinB && (W4 == 2 || W4 == 3 || W4 == 4 || W4 == 6 || W4 == 8);
+    if (mfma) {
+        switch (W4) {
+            case 2: launch_scan_mfma_t<2>(a, s); break;
+            case 3: launch_scan_mfma_t<3>(a, s); break;
+            case 4: launch_scan_mfma_t<4>(a, s); break;
+            case 6: launch_scan_mfma_t<6>(a, s); break;
+            default: launch_scan_mfma_t<8>(a, s); break;
+        }
+    } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \
     case w:                           \
         launch_scan_t<w, cpl>(a, s);  \

@@ -130,6 +130,29 @@ def test_stage1_topr_matches_oracle(g, oracle_mod, N, D, B, R, dup):
     assert (gi == ri).all()
 
 
+@pytest.mark.parametrize("N,D,B,R", [(200_000, 768, 160, 100), (100_000, 256, 96, 64), (120_000, 384, 128, 200),
+                                     (90_000, 512, 300, 50), (80_000, 1024, 100, 100), (70_000, 768, 256, 1000)])
+def test_stage1_mfma_batches_match_oracle(g, oracle_mod, N, D, B, R):
+    """Large batches take the i8-MFMA scan (B >= 96, W4 in {2,3,4,6,8});
+    distances must equal the popcount path and the oracle bit for bit."""
+    import os
+
+    x = rng_rows(N + 3 * D, N, D, dup=200)
+    Q = rng_rows(D + 77, B, D)
+    Q[3] = x[11]
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    gi, gd = topr(g, ix, Q, R)
+    os.environ["GVDB_SCAN"] = "valu"
+    try:
+        vi, vd = topr(g, ix, Q, R)
+    finally:
+        del os.environ["GVDB_SCAN"]
+    assert (gi == vi).all() and (gd == vd).all()
+    ri, rd = oracle_mod.bq_topr_batch(oracle_mod.quantize(Q), oracle_mod.quantize(x), D, R)
+    assert (gd == rd).all() and (gi == ri).all()
+
+
 def test_stage1_massive_ties_fallback(g, oracle_mod):
     # 12k identical nearest rows > the 8192-key LDS select: exact slow path
     N, D, R = 30_000, 64, 500
