@@ -38,6 +38,7 @@ SEED = 0x6772617065  # "grape"
 CHUNK = 1 << 20      # rows per generated chunk (global chunking: shard-independent data)
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8 TB/s
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 ops
+PEAK_I8_TOPS = 5000.0  # dense i8 MFMA = 2x the 2.5 PF dense bf16 peak (MI355X_MICROARCH.md, Matrix cores)
 
 
 def log(*a):
@@ -243,24 +244,40 @@ def main():
             },
         }
 
-    # ---------------- roofline of the dominant kernel (k_scan at batch B)
+    # ---------------- roofline of the dominant kernel (stage-1 scan at batch B)
     scan_avg = scan_ms / max(scan_n, 1)
-    words = (D + 31) // 32
-    ops = float(n_local) * B * words * 2  # v_xor_b32 + v_bcnt_u32_b32 per 32-bit code word per pair
-    achieved = ops / (scan_avg * 1e-3) / 1e12
-    roof = {
-        "kernel": "k_scan (stage-1 BQ Hamming filter, popcount on VALU)",
-        "bound": "valu",
-        "achieved": achieved,
-        "peak": PEAK_VALU_TOPS,
-        "unit": "Tops/s (int32 lane-ops)",
-        "frac": achieved / PEAK_VALU_TOPS,
+    words = 4 * gvdb_code_w4(D)          # 32-bit code words per row (padded)
+    mfma = B >= 96 and gvdb_code_w4(D) in (2, 3, 4, 6, 8) and os.environ.get("GVDB_SCAN") != "valu"
+    if mfma:
+        bpad = ((B + 31) // 32) * 32
+        ops = float(n_local) * bpad * words * 32 * 2  # i8 MACs x 2 (one +/-1 product per code bit)
+        peak = PEAK_I8_TOPS
+        roof = {
+            "kernel": "k_scan_mfma (stage-1 BQ Hamming as +/-1 i8 dot, v_mfma_i32_32x32x32_i8)",
+            "bound": "mfma",
+            "achieved": ops / (scan_avg * 1e-3) / 1e12,
+            "peak": peak,
+            "unit": "TFLOP/s (i8 MAC = 2 ops)",
+        }
+    else:
+        ops = float(n_local) * B * words * 2  # v_xor_b32 + v_bcnt_u32_b32 per 32-bit word per pair
+        peak = PEAK_VALU_TOPS
+        roof = {
+            "kernel": "k_scan (stage-1 BQ Hamming, xor+popcount on VALU)",
+            "bound": "valu",
+            "achieved": ops / (scan_avg * 1e-3) / 1e12,
+            "peak": peak,
+            "unit": "Tops/s (int32 lane-ops)",
+        }
+    roof.update({
+        "frac": roof["achieved"] / peak,
         "traffic": None,
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
-        "note": "batch-256 is integer-VALU bound (48 ops/pair vs 96 B/row read once per batch); "
-                "batch-1 HBM roofline in batch1.roofline",
-    }
+        "hbm_bytes_per_launch": n_local * gvdb_code_w4(D) * 16,
+        "note": "batch-256 stage 1 is compute-bound (96 B of codes per row read once per batch); "
+                "the HBM-bound batch-1 scan is in batch1.roofline",
+    })
 
     # ---------------- CPU baseline (oracle = reference algorithm restated), bounded sample
     cpu = None
