@@ -39,6 +39,7 @@ CHUNK = 1 << 20      # rows per generated chunk (global chunking: shard-independ
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8 TB/s
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 ops
 PEAK_I8_TOPS = 5000.0  # dense i8 MFMA = 2x the 2.5 PF dense bf16 peak (MI355X_MICROARCH.md, Matrix cores)
+PEAK_FP4_TFLOPS = 10000.0  # dense MX-FP4 MFMA = 4x dense bf16 (MI355X_MICROARCH.md: ~10 PF dense)
 
 
 def log(*a):
@@ -247,17 +248,21 @@ def main():
     # ---------------- roofline of the dominant kernel (stage-1 scan at batch B)
     scan_avg = scan_ms / max(scan_n, 1)
     words = 4 * gvdb_code_w4(D)          # 32-bit code words per row (padded)
-    mfma = B >= 96 and gvdb_code_w4(D) in (2, 3, 4, 6, 8) and os.environ.get("GVDB_SCAN") != "valu"
+    variant = os.environ.get("GVDB_SCAN", "fp4")
+    mfma = B >= 96 and gvdb_code_w4(D) in (2, 3, 4, 6) and variant != "valu"
     if mfma:
         bpad = ((B + 31) // 32) * 32
-        ops = float(n_local) * bpad * words * 32 * 2  # i8 MACs x 2 (one +/-1 product per code bit)
-        peak = PEAK_I8_TOPS
+        ops = float(n_local) * bpad * words * 32 * 2  # MACs x 2: one +/-1 product per code bit
+        if variant == "i8":
+            peak, kname = PEAK_I8_TOPS, "k_scan_mfma (+/-1 i8 dot, v_mfma_i32_32x32x32_i8)"
+        else:
+            peak, kname = PEAK_FP4_TFLOPS, "k_scan_mx (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4)"
         roof = {
-            "kernel": "k_scan_mfma (stage-1 BQ Hamming as +/-1 i8 dot, v_mfma_i32_32x32x32_i8)",
+            "kernel": "stage-1 BQ Hamming filter: " + kname,
             "bound": "mfma",
             "achieved": ops / (scan_avg * 1e-3) / 1e12,
             "peak": peak,
-            "unit": "TFLOP/s (i8 MAC = 2 ops)",
+            "unit": "TFLOP/s (MAC = 2 ops)",
         }
     else:
         ops = float(n_local) * B * words * 2  # v_xor_b32 + v_bcnt_u32_b32 per 32-bit word per pair

@@ -192,7 +192,10 @@ struct ShardView {
 constexpr uint32_t kExactN = 262144;  // below this the "sample" is the whole shard
 
 // Stage-1 sampling plan: S rows in 4096-row chunks spread over the shard.
-void plan_sampling(uint32_t N, uint32_t R, uint32_t& chunks, uint32_t& stride, uint32_t& target, uint32_t& bufcap) {
+// sample_div: the sample is ~N/sample_div rows (32; 64 for large batches,
+// where the VALU sample pass would otherwise cost ~10% of the MFMA scan).
+void plan_sampling(uint32_t N, uint32_t R, uint32_t sample_div, uint32_t& chunks, uint32_t& stride, uint32_t& target,
+                   uint32_t& bufcap) {
     if (N <= kExactN) {
         chunks = (N + 4095u) / 4096u;
         stride = 4096u;
@@ -200,7 +203,7 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t& chunks, uint32_t& stride, u
         bufcap = std::min<uint64_t>(N, 8ull * R + 2048ull);
         return;
     }
-    uint64_t S = std::max<uint64_t>(kExactN, N / 32u);
+    uint64_t S = std::max<uint64_t>(kExactN / 2, N / sample_div);
     chunks = (uint32_t)(S / 4096u);
     stride = N / chunks;  // >= 4096: chunks never overlap
     S = (uint64_t)chunks * 4096u;
@@ -214,10 +217,13 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t& chunks, uint32_t& stride, u
 // sit contiguously in ws.zero (flags[0] = any stage-1 failure, flags[1] = NaN).
 gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D, uint32_t R, uint32_t N,
                            hipStream_t s) {
-    plan_sampling(N, R, s1.sample_chunks, s1.sample_stride, s1.target, s1.bufcap);
-    // GVDB_SCAN=valu forces the popcount scan for every batch size (A/B runs)
+    // GVDB_SCAN=valu forces the popcount scan for every batch size, =i8 the
+    // i8-MFMA scan instead of the FP4 one (A/B runs); default: FP4 MFMA for
+    // large batches
     const char* scan = getenv("GVDB_SCAN");
-    s1.use_mfma = !(scan && strcmp(scan, "valu") == 0);
+    s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0 : (scan && strcmp(scan, "i8") == 0) ? 2 : 1;
+    plan_sampling(N, R, (s1.use_mfma && B >= kMfmaMinB) ? 64u : 32u, s1.sample_chunks, s1.sample_stride, s1.target,
+                  s1.bufcap);
     const size_t nb = (size_t)D + 1u;
     const size_t words = 4 + 2 * (size_t)B + (size_t)B * nb;
     HIP_TRY(ws.zero.ensure(words * 4 + 16), "alloc stage-1 state");

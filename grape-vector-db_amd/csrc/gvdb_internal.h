@@ -76,9 +76,12 @@ struct Stage1Args {
     uint32_t* s1_rows;       // [B][R]
     uint32_t* s1_dist;       // [B][R]
     hipEvent_t* ev;          // optional [4]: before hist, before scan, after scan, after select
-    int use_mfma;            // allow the i8-MFMA scan for large batches
+    int use_mfma;            // large batches: 0 popcount only, 1 FP4 MFMA scan, 2 i8 MFMA scan
 };
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
+// code widths with an MFMA scan instantiation (D <= 768; wider codes would
+// not fit the query fragments + prefetch in 256 VGPRs at 2 waves/SIMD)
+__host__ __device__ inline bool mfma_scan_supported(uint32_t W4) { return W4 == 2 || W4 == 3 || W4 == 4 || W4 == 6; }
 // hist/counts/fail must be zeroed by the caller on stream s.
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s);
 // Exact slow path for ONE query: all N distances + stable radix sort.

@@ -597,12 +597,14 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mfma(const uint4* __rest
                                                             const uint32_t* __restrict__ thr, uint32_t B,
                                                             uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
                                                             uint32_t bufcap) {
-    constexpr int KS = 4 * W4;              // k-steps = 32-bit code words
-    constexpr int kTileBytes = 2 * KS * 64 * 16;  // [sub-tile][k-step][lane][16 B]
+    constexpr int KS = 4 * W4;                    // k-steps = 32-bit code words
+    constexpr int kTileBytes = 2 * KS * 64 * 16;  // [sub-tile][k-step][half][col][16 B]
+    constexpr int U = KS / 4;                     // expansion units per thread per tile (= W4)
     __shared__ __attribute__((aligned(16))) uint8_t lds[2][kTileBytes];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
     const uint32_t q0 = wv * 32u;
-    const bool active = q0 < B;
+    const bool active = q0 < B;  // scalar branch: whole waves compute or only expand
     // query fragments (A operand): lane holds query (q0 + lane&31), half (lane>>5)
     v4i_t qa[KS];
     int32_t T[16];  // per accumulator row: threshold of that query, -1 = padding row (never emits)
@@ -619,57 +621,57 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mfma(const uint4* __rest
     }
     constexpr uint32_t kPad = 32u * KS;
     const uint32_t ntiles = (N + kMfCand - 1) / kMfCand;
-    // expansion work: (candidate c in tile, plane w4) items; each produces 4 words x 2 halves
-    constexpr int kItems = kMfCand * W4;
-    uint4 cw[(kItems + kMfThreads - 1) / kMfThreads];
-    auto load = [&](uint32_t t) {
+    // Expansion unit g = u*512 + tid  <->  (sub-tile st, word s, half h, col):
+    //   g = ((st*KS + s)*2 + h)*32 + col, LDS byte offset g*16 (one wave writes 1 KiB contiguously).
+    // Codes are prefetched TWO tiles ahead (nw: tile t+1, expanded during tile
+    // t's MFMAs; nw2: tile t+2, in flight), so no expansion waits on HBM.
+    uint32_t nw[U], nw2[U];
+    auto load = [&](uint32_t t, uint32_t (&dst)[U]) {
 #pragma unroll
-        for (int i = 0; i < (kItems + kMfThreads - 1) / kMfThreads; ++i) {
-            const uint32_t it = i * kMfThreads + tid;
-            if (it < (uint32_t)kItems) {
-                const uint32_t c = it % kMfCand, w4 = it / kMfCand;
-                const uint32_t n = min(t * kMfCand + c, N - 1u);
-                cw[i] = codes[(uint64_t)w4 * cap + n];
-            }
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = u * kMfThreads + tid;
+            const uint32_t col = g & 31u, s = (g >> 6) % KS, st = (g >> 6) / KS;
+            const uint32_t n = min(t * kMfCand + st * 32u + col, N - 1u);
+            dst[u] = ((const uint32_t*)codes)[(((uint64_t)(s >> 2) * cap) + n) * 4u + (s & 3u)];
         }
     };
-    auto expand = [&](int b) {
-#pragma unroll
-        for (int i = 0; i < (kItems + kMfThreads - 1) / kMfThreads; ++i) {
-            const uint32_t it = i * kMfThreads + tid;
-            if (it < (uint32_t)kItems) {
-                const uint32_t c = it % kMfCand, w4 = it / kMfCand;
-                const uint32_t st = c >> 5, col = c & 31u;
-                const uint32_t words[4] = {cw[i].x, cw[i].y, cw[i].z, cw[i].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t s = 4u * w4 + j;
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t off = ((st * KS + s) * 64u + h * 32u + col) * 16u;
-                        *(v4i_t*)(&lds[b][off]) = pm1_x16(words[j] >> (16 * h));
-                    }
-                }
-            }
-        }
+    auto expand_unit = [&](int u, int b) {
+        const uint32_t g = u * kMfThreads + tid;
+        const uint32_t h = (g >> 5) & 1u;
+        *(v4i_t*)(&lds[b][g * 16u]) = pm1_x16(nw[u] >> (16u * h));
     };
     uint32_t t = blockIdx.x;
     if (t < ntiles) {
-        load(t);
-        expand(0);
+        load(t, nw);
+#pragma unroll
+        for (int u = 0; u < U; ++u) expand_unit(u, 0);
+        if (t + gridDim.x < ntiles) load(t + gridDim.x, nw);
     }
     __syncthreads();
     for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
         const int b = it & 1;
         const uint32_t tn = t + gridDim.x;
-        if (tn < ntiles) load(tn);
+        const bool more = tn < ntiles;
+        const bool more2 = tn + gridDim.x < ntiles;
+        if (more2) load(tn + gridDim.x, nw2);
         if (active) {
-            v16i_t acc0 = {0}, acc1 = {0};
+            // B fragments are read one k-step ahead of the MFMAs that use them;
+            // the next tile's expansion (other buffer) rides in the MFMA gaps.
             const v4i_t* bf = (const v4i_t*)lds[b];
+            v16i_t acc0 = {0}, acc1 = {0};
+            v4i_t b0 = bf[(0 * KS) * 64 + lane], b1 = bf[(1 * KS) * 64 + lane];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], bf[(0 * KS + s) * 64 + lane], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], bf[(1 * KS + s) * 64 + lane], acc1, 0, 0, 0);
+                v4i_t n0 = b0, n1 = b1;
+                if (s + 1 < KS) {
+                    n0 = bf[(0 * KS + s + 1) * 64 + lane];
+                    n1 = bf[(1 * KS + s + 1) * 64 + lane];
+                }
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], b1, acc1, 0, 0, 0);
+                if ((s & 3) == 3 && more) expand_unit(s >> 2, b ^ 1);
+                b0 = n0;
+                b1 = n1;
             }
 #pragma unroll
             for (int st = 0; st < 2; ++st) {
@@ -693,9 +695,170 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mfma(const uint4* __rest
                     }
                 }
             }
+        } else if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) expand_unit(u, b ^ 1);
         }
-        if (tn < ntiles) expand(b ^ 1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) nw[u] = nw2[u];
         __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------------------------
+// k_scan_mx — the large-batch stage-1 filter on block-scaled FP4 MFMA.
+// Same +/-1 identity as k_scan_mfma, with each code bit an e2m1 value
+// (+1.0 = 0b0010, -1.0 = 0b1010) and unit E8M0 scales (0x7f):
+// v_mfma_scale_f32_32x32x64_f8f6f4 runs K=64 per instruction at twice the
+// i8 rate, sums exactly in f32 (|dot| <= D < 2^24), and its operands are
+// half the LDS bytes.  One k-step = two 32-bit code words; lane half h of a
+// fragment carries word (2s + h) as 32 nibbles (verified exact on gfx950 by
+// tools/mx_fp4_probe.hip).
+// ----------------------------------------------------------------------------
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float v16f_t __attribute__((ext_vector_type(16)));
+
+// 8 code bits -> 8 e2m1 nibbles: spread bit i to bit 4i, then (b<<3) | 0x2.
+__device__ __forceinline__ uint32_t fp4_x8(uint32_t byte) {
+    uint32_t x = byte & 0xFFu;
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    return (x << 3) | 0x22222222u;
+}
+__device__ __forceinline__ v4i_t fp4_x32(uint32_t w) {
+    v4i_t r;
+    r.x = (int)fp4_x8(w);
+    r.y = (int)fp4_x8(w >> 8);
+    r.z = (int)fp4_x8(w >> 16);
+    r.w = (int)fp4_x8(w >> 24);
+    return r;
+}
+__device__ __forceinline__ v16f_t mfma_fp4(const v4i_t& a, const v4i_t& b, const v16f_t& c) {
+    const v8i_t a8 = {a.x, a.y, a.z, a.w, 0, 0, 0, 0};
+    const v8i_t b8 = {b.x, b.y, b.z, b.w, 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+}
+
+template <int W4>
+__global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                          const uint32_t* __restrict__ qwords,
+                                                          const uint32_t* __restrict__ thr, uint32_t B,
+                                                          uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                          uint32_t bufcap) {
+    constexpr int KW = 4 * W4;                 // 32-bit code words per row
+    constexpr int KS = KW / 2;                 // K=64 steps (two words each)
+    constexpr int kUnits = kMfCand * KW;       // (candidate, word) expansion units per tile
+    constexpr int U = (kUnits + kMfThreads - 1) / kMfThreads;
+    constexpr int kTileBytes = kUnits * 16;    // [sub-tile][k-step][half][col][16 B]
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2][kTileBytes];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t q0 = wv * 32u;
+    const bool active = q0 < B;
+    v4i_t qa[KS];
+    int32_t T[16];
+    {
+        const uint32_t qr = min(q0 + (lane & 31u), B - 1u);
+        const uint32_t* qw = qwords + (uint64_t)qr * KW;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) qa[s] = fp4_x32(qw[2 * s + (lane >> 5)]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            T[r] = qi < B ? (int32_t)thr[qi] : -1;
+        }
+    }
+    constexpr int32_t kPad = 32 * KW;
+    const uint32_t ntiles = (N + kMfCand - 1) / kMfCand;
+    // unit g = ((st*KS + s)*2 + h)*32 + col  <->  word (2s+h) of candidate st*32+col
+    uint32_t nw[U];
+    auto load = [&](uint32_t t) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = u * kMfThreads + tid;
+            if (g < (uint32_t)kUnits) {
+                const uint32_t col = g & 31u, h = (g >> 5) & 1u, s = (g >> 6) % KS, st = (g >> 6) / KS;
+                const uint32_t w = 2u * s + h;
+                const uint32_t n = min(t * kMfCand + st * 32u + col, N - 1u);
+                nw[u] = ((const uint32_t*)codes)[(((uint64_t)(w >> 2) * cap) + n) * 4u + (w & 3u)];
+            }
+        }
+    };
+    auto expand = [&](int b) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = u * kMfThreads + tid;
+            if (g < (uint32_t)kUnits) *(v4i_t*)(&lds[b][g * 16u]) = fp4_x32(nw[u]);
+        }
+    };
+    uint32_t t = blockIdx.x;
+    if (t < ntiles) {
+        load(t);
+        expand(0);
+    }
+    __syncthreads();
+    for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+        const int b = it & 1;
+        const uint32_t tn = t + gridDim.x;
+        const bool more = tn < ntiles;
+        if (more) load(tn);  // lands during this tile's MFMAs
+        if (active) {
+            const v4i_t* bf = (const v4i_t*)lds[b];
+            v16f_t acc0 = {0}, acc1 = {0};
+            v4i_t b0 = bf[(0 * KS) * 64 + lane], b1 = bf[(1 * KS) * 64 + lane];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                v4i_t n0 = b0, n1 = b1;
+                if (s + 1 < KS) {
+                    n0 = bf[(0 * KS + s + 1) * 64 + lane];
+                    n1 = bf[(1 * KS + s + 1) * 64 + lane];
+                }
+                acc0 = mfma_fp4(qa[s], b0, acc0);
+                acc1 = mfma_fp4(qa[s], b1, acc1);
+                b0 = n0;
+                b1 = n1;
+            }
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                const v16f_t& acc = st ? acc1 : acc0;
+                const uint32_t n = t * kMfCand + st * 32u + (lane & 31u);
+                bool any = false;
+                int32_t d[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    d[r] = (kPad - (int32_t)acc[r]) >> 1;
+                    any |= d[r] <= T[r];
+                }
+                if (any && n < N) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        if (d[r] <= T[r]) {
+                            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            const uint32_t pos = atomicAdd(&counts[qi], 1u);
+                            if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = ((uint64_t)(uint32_t)d[r] << 32) | n;
+                        }
+                    }
+                }
+            }
+        }
+        if (more) expand(b ^ 1);
+        __syncthreads();
+    }
+}
+
+template <int W4>
+static void launch_scan_mx_t(const Stage1Args& a, hipStream_t s) {
+    const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t grid = min(ntiles, (uint32_t)cus);
+    for (uint32_t g = 0; g < a.B; g += 256) {
+        const uint32_t bg = min(256u, a.B - g);
+        hipLaunchKernelGGL((k_scan_mx<W4>), dim3(grid), dim3(kMfThreads), 0, s, a.codes, a.cap, a.N,
+                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
+                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
 }
 
@@ -761,14 +924,20 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_threshold, dim3((a.B + 3) / 4), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
-    const bool mfma = a.use_mfma && a.B >= kMfmaMinB && (W4 == 2 || W4 == 3 || W4 == 4 || W4 == 6 || W4 == 8);
-    if (mfma) {
+    const bool mfma = a.use_mfma && a.B >= kMfmaMinB && mfma_scan_supported(W4);
+    if (mfma && a.use_mfma == 2) {  // i8 MFMA variant (A/B comparison)
         switch (W4) {
             case 2: launch_scan_mfma_t<2>(a, s); break;
             case 3: launch_scan_mfma_t<3>(a, s); break;
             case 4: launch_scan_mfma_t<4>(a, s); break;
-            case 6: launch_scan_mfma_t<6>(a, s); break;
-            default: launch_scan_mfma_t<8>(a, s); break;
+            default: launch_scan_mfma_t<6>(a, s); break;
+        }
+    } else if (mfma) {  // FP4 block-scaled MFMA (default for large batches)
+        switch (W4) {
+            case 2: launch_scan_mx_t<2>(a, s); break;
+            case 3: launch_scan_mx_t<3>(a, s); break;
+            case 4: launch_scan_mx_t<4>(a, s); break;
+            default: launch_scan_mx_t<6>(a, s); break;
         }
     } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \

@@ -143,12 +143,13 @@ def test_stage1_mfma_batches_match_oracle(g, oracle_mod, N, D, B, R):
     ix = g.GpuVectorIndex(dimension=D)
     ix.add_batch(np.arange(N, dtype=np.uint64), x)
     gi, gd = topr(g, ix, Q, R)
-    os.environ["GVDB_SCAN"] = "valu"
-    try:
-        vi, vd = topr(g, ix, Q, R)
-    finally:
-        del os.environ["GVDB_SCAN"]
-    assert (gi == vi).all() and (gd == vd).all()
+    for variant in ("valu", "i8"):
+        os.environ["GVDB_SCAN"] = variant
+        try:
+            vi, vd = topr(g, ix, Q, R)
+        finally:
+            del os.environ["GVDB_SCAN"]
+        assert (gi == vi).all() and (gd == vd).all(), variant
     ri, rd = oracle_mod.bq_topr_batch(oracle_mod.quantize(Q), oracle_mod.quantize(x), D, R)
     assert (gd == rd).all() and (gi == ri).all()
 
