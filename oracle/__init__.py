@@ -42,6 +42,9 @@ _SIG = {
     "orc_row_norms": (None, [P, u64, u64, P]),
     "orc_bq_shard_merge": (None, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P]),
     "orc_multi_stage_search_batch_r": (None, [P, u32, P, u64, P, P, u64, u64, C.c_int, P, P, C.c_int]),
+    "hnsw_build": (C.c_void_p, [P, u64, u32, u32, u32, u64, C.c_int]),
+    "hnsw_free": (None, [C.c_void_p]),
+    "hnsw_search": (C.c_int, [C.c_void_p, P, u64, u32, u32, C.c_int, P, P, P]),
 }
 
 
@@ -250,3 +253,32 @@ def multi_stage_search_batch_r(q_bits, c_bits, q, cands, R, kind=0, threads=0):
     lib().orc_multi_stage_search_batch_r(_p(q_bits), D, _p(c_bits), N, _p(q), _p(cands), B, R, kind, _p(oi), _p(os_),
                                          threads)
     return oi[:, :r], os_[:, :r]
+
+
+class Hnsw:
+    """instant-distance 0.6.1 restatement (oracle/hnsw_oracle.cpp): the CPU-HNSW
+    baseline of HnswVectorIndex (index.rs:140-154, 212-231).  Distances are L2
+    (index.rs:64-79).  Recall-only parity; the rows array must stay alive."""
+
+    def __init__(self, rows, M=32, ef_construction=100, seed=0x6772617065, threads=0):
+        self.rows = _f32(rows)
+        n, d = self.rows.shape
+        self.d = d
+        self.h = lib().hnsw_build(_p(self.rows), n, d, M, ef_construction, seed, threads)
+        if not self.h:
+            raise ValueError("hnsw_build failed")
+
+    def search(self, q, k=10, ef_search=100, threads=0):
+        q = _f32(q).reshape(-1, self.d)
+        B = q.shape[0]
+        ids = np.zeros((B, k), dtype=np.uint64)
+        dist = np.zeros((B, k), dtype=np.float32)
+        n = np.zeros(B, dtype=np.uint32)
+        if lib().hnsw_search(self.h, _p(q), B, k, ef_search, threads, _p(ids), _p(dist), _p(n)) != 0:
+            raise ValueError("hnsw_search failed")
+        return ids, dist, n
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().hnsw_free(self.h)
+            self.h = None
