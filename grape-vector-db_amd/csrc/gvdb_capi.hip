@@ -221,7 +221,12 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     // i8-MFMA scan instead of the FP4 one (A/B runs); default: FP4 MFMA for
     // large batches
     const char* scan = getenv("GVDB_SCAN");
-    s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0 : (scan && strcmp(scan, "i8") == 0) ? 2 : 1;
+    s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0
+                  : (scan && strcmp(scan, "i8") == 0)  ? 2
+                  : (scan && strcmp(scan, "fp4u") == 0) ? 3
+                                                        : 1;
+    const char* dbg = getenv("GVDB_SCAN_DBG");  // ablation timing only (results invalid when set)
+    s1.dbg = dbg ? atoi(dbg) : 0;
     plan_sampling(N, R, (s1.use_mfma && B >= kMfmaMinB) ? 64u : 32u, s1.sample_chunks, s1.sample_stride, s1.target,
                   s1.bufcap);
     const size_t nb = (size_t)D + 1u;

@@ -77,6 +77,7 @@ struct Stage1Args {
     uint32_t* s1_dist;       // [B][R]
     hipEvent_t* ev;          // optional [4]: before hist, before scan, after scan, after select
     int use_mfma;            // large batches: 0 popcount only, 1 FP4 MFMA scan, 2 i8 MFMA scan
+    int dbg;                 // ablation switches for timing studies (GVDB_SCAN_DBG); 0 in production
 };
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 // code widths with an MFMA scan instantiation (D <= 768; wider codes would

@@ -19,6 +19,8 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "gvdb_internal.h"
 
 namespace gvdb {
@@ -589,6 +591,10 @@ __device__ __forceinline__ v4i_t pm1_x16(uint32_t h16) {
 }
 
 constexpr int kMfThreads = 512;
+constexpr int kMxDepth = 4;
+constexpr int kMxLdsDepth = 3;  // k-steps of B-fragment LDS prefetch in k_scan_mx2
+constexpr uint32_t kStampTiles = 64;
+__device__ unsigned long long g_stamps[2][kStampTiles][8];   // register tile-ring depth of k_scan_mx2
 constexpr int kMfCand = 64;  // candidates per tile (2 MFMA sub-tiles of 32)
 
 template <int W4>
@@ -719,19 +725,16 @@ typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef float v16f_t __attribute__((ext_vector_type(16)));
 
 // 8 code bits -> 8 e2m1 nibbles: spread bit i to bit 4i, then (b<<3) | 0x2.
-__device__ __forceinline__ uint32_t fp4_x8(uint32_t byte) {
-    uint32_t x = byte & 0xFFu;
-    x = (x | (x << 12)) & 0x000F000Fu;
-    x = (x | (x << 6)) & 0x03030303u;
-    x = (x | (x << 3)) & 0x11111111u;
-    return (x << 3) | 0x22222222u;
-}
+// 32 code bits -> 32 e2m1 nibbles: bit 1 -> -1.0 (0b1010), bit 0 -> +1.0 (0b0010).
+// Nibble i of output dword j takes bit 4i+j of w: a fixed permutation of the
+// bits, applied identically to query and candidate words, so the dot product
+// (and the Hamming distance it encodes) is unchanged; 2 VALU ops per dword.
 __device__ __forceinline__ v4i_t fp4_x32(uint32_t w) {
     v4i_t r;
-    r.x = (int)fp4_x8(w);
-    r.y = (int)fp4_x8(w >> 8);
-    r.z = (int)fp4_x8(w >> 16);
-    r.w = (int)fp4_x8(w >> 24);
+    r.x = (int)(((w << 3) & 0x88888888u) | 0x22222222u);
+    r.y = (int)(((w << 2) & 0x88888888u) | 0x22222222u);
+    r.z = (int)(((w << 1) & 0x88888888u) | 0x22222222u);
+    r.w = (int)((w & 0x88888888u) | 0x22222222u);
     return r;
 }
 __device__ __forceinline__ v16f_t mfma_fp4(const v4i_t& a, const v4i_t& b, const v16f_t& c) {
@@ -739,6 +742,26 @@ __device__ __forceinline__ v16f_t mfma_fp4(const v4i_t& a, const v4i_t& b, const
     const v8i_t b8 = {b.x, b.y, b.z, b.w, 0, 0, 0, 0};
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
 }
+
+// The same instruction as inline asm with 4-VGPR fp4 operands.  Through the
+// builtin, hipcc hoists the (v4i, 0,0,0,0) -> v8i operand construction out of
+// the k-loop and keeps 8-register tuples live per query fragment, which
+// spills the two-tile consumer waves.  Hazards handled here (hipcc pads
+// nothing inside asm): the chain's first MFMA takes C = literal 0 (no VALU
+// write -> srcC hazard), later ones take the previous D whole as C (no wait
+// states), and mfma_fp4_drain() puts 32 wait states after a chain's last
+// MFMA before any VALU reads D.
+__device__ __forceinline__ void mfma_fp4_first(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "=&v"(d)
+                 : "v"(a), "v"(b), "v"(scale));
+}
+__device__ __forceinline__ void mfma_fp4_acc(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "+v"(d)
+                 : "v"(a), "v"(b), "v"(scale));
+}
+__device__ __forceinline__ void mfma_fp4_drain() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); }
 
 template <int W4>
 __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
@@ -847,6 +870,261 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restri
     }
 }
 
+// k_scan_mx2: the FP4 scan with staggered wave halves.  8 waves per CU, one
+// 32-query tile each; waves w and w+4 share a SIMD.  Every tile both halves
+// run the same work in opposite order:
+//   waves 0-3:  issue loads(t+1) -> MFMAs(t) -> threshold test -> expand(t+1, half)
+//   waves 4-7:  expand(t+1, half, from registers loaded one tile earlier)
+//               -> issue loads(t+2) -> MFMAs(t) -> threshold test
+// so on each SIMD one wave's expansion VALU runs beside the other wave's
+// MFMAs instead of all waves alternating between the two phases together.
+// Each half keeps ONE register set for its codes (expanded, then reloaded:
+// no register moves, which would wait on the loads).  One barrier per tile.
+template <int W4>
+__global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restrict__ codes, uint64_t cap,
+                                                           uint32_t N, const uint32_t* __restrict__ qwords,
+                                                           const uint32_t* __restrict__ thr, uint32_t B,
+                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                           uint32_t bufcap, int dbg) {
+    constexpr int KW = 4 * W4;
+    constexpr int KS = KW / 2;
+    constexpr int kUnits = kMfCand * KW;       // (candidate, word) units per tile
+    constexpr int kHalf = kUnits / 2;          // per wave half
+    constexpr int U = (kHalf + 255) / 256;     // units per thread
+    constexpr int kTileBytes = kUnits * 16;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2][kTileBytes];
+    __shared__ __attribute__((aligned(16))) float tf_lds[256];
+    // Candidate staging: a returning global atomic per emit would stall the
+    // emitting wave ~2 us and, through the per-tile barrier, the whole block.
+    // Emits append to LDS (LDS atomic) and are flushed to the per-query global
+    // buffers once, after the last tile; overflow falls back to direct emits.
+    constexpr uint32_t kStage = 2048;
+    __shared__ uint64_t st_key[kStage];
+    __shared__ uint8_t st_q[kStage];
+    __shared__ uint32_t st_n;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool late = wv >= 4;                 // second half: expand first, then MFMA
+    const uint32_t q0 = wv * 32u;
+    const bool active = q0 < B;
+    const uint32_t ntiles = (N + kMfCand - 1) / kMfCand;
+    const uint32_t G = gridDim.x;
+    constexpr float kPadF = (float)(32 * KW);
+    const int scale1 = 0x7f7f7f7f;
+    if (tid < 256) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
+    if (tid == 0) st_n = 0;
+
+    // expansion units of this thread: g = (late ? kHalf : 0) + u*256 + (tid & 255)
+    // unit g = ((st*KS + s)*2 + h)*32 + col  <->  word (2s+h) of candidate st*32+col
+    uint64_t woff[U];   // u32-element offset of the unit's word in row 0
+    uint32_t rofs[U];   // unit's row within a tile
+    bool uok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t g = (late ? kHalf : 0) + u * 256u + (tid & 255u);
+        uok[u] = u * 256u + (tid & 255u) < (uint32_t)kHalf;
+        const uint32_t col = g & 31u, h = (g >> 5) & 1u, s = (g >> 6) % KS, st = (g >> 6) / KS;
+        const uint32_t w = 2u * s + h;
+        woff[u] = uok[u] ? ((uint64_t)(w >> 2) * cap) * 4u + (w & 3u) : 0;
+        rofs[u] = uok[u] ? st * 32u + col : 0;
+    }
+    const uint32_t* cw = (const uint32_t*)codes;
+    // D register sets of raw code words: tile j of this block lives in set j % D,
+    // so every load is issued D-1..D tiles (>= the HBM latency) before its expand.
+    // Loads are unconditional and branch-free (rows clamped to N-1, also past the
+    // last tile): a conditional load makes the compiler merge register sets with
+    // copies that wait for the load, serialising the ring.
+    constexpr int D = kMxDepth;
+    uint32_t nw[D][U];
+    auto load = [&](uint32_t t, uint32_t (&w)[U]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t n = min(t * kMfCand + rofs[u], N - 1u);
+            w[u] = cw[woff[u] + (uint64_t)n * 4u];
+        }
+    };
+    auto expand = [&](int b, const uint32_t (&w)[U]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = (late ? kHalf : 0) + u * 256u + (tid & 255u);
+            if (uok[u]) *(v4i_t*)(&lds[b][g * 16u]) = fp4_x32(w[u]);
+        }
+    };
+    v4i_t qa[KS];
+    if (active) {
+        const uint32_t qr = min(q0 + (lane & 31u), B - 1u);
+        const uint32_t* qw = qwords + (uint64_t)qr * KW;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) qa[s] = fp4_x32(qw[2 * s + (lane >> 5)]);
+    }
+    // dbg & 16: shader-clock stamps of waves 0 and 4 of block 0 (dev aid)
+    const bool stamp = (dbg & 16) && blockIdx.x == 0 && (wv & 3u) == 0 && lane == 0;
+    auto mark = [&](uint32_t j, int p) __attribute__((always_inline)) {
+        if (stamp && j < kStampTiles) g_stamps[wv >> 2][j][p] = __builtin_amdgcn_s_memtime();
+    };
+    // Early half (waves 0-3): MFMA, then expand tile j+1, then refill its set.
+    // Late half (waves 4-7): expand first, so the halves' VALU and MFMA phases
+    // interleave on each SIMD.  Separate loops keep the register ring static.
+    auto consume = [&](uint32_t t, int b) __attribute__((always_inline)) {
+        const v4i_t* bf = (const v4i_t*)lds[b];
+        v16f_t acc0, acc1;
+        // B fragments ride a PF-deep register ring: the LDS read for k-step s is
+        // issued PF steps (2*PF MFMAs) before its use, covering LDS latency
+        constexpr int PF = kMxLdsDepth < KS ? kMxLdsDepth : KS;
+        v4i_t r0[PF], r1[PF];
+#pragma unroll
+        for (int s = 0; s < PF; ++s) {
+            r0[s] = bf[(0 * KS + s) * 64 + lane];
+            r1[s] = bf[(1 * KS + s) * 64 + lane];
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const v4i_t b0 = r0[s % PF], b1 = r1[s % PF];
+            if (s == 0) {
+                mfma_fp4_first(acc0, qa[s], b0, scale1);
+                mfma_fp4_first(acc1, qa[s], b1, scale1);
+            } else {
+                mfma_fp4_acc(acc0, qa[s], b0, scale1);
+                mfma_fp4_acc(acc1, qa[s], b1, scale1);
+            }
+            if (s + PF < KS) {
+                r0[s % PF] = bf[(0 * KS + s + PF) * 64 + lane];
+                r1[s % PF] = bf[(1 * KS + s + PF) * 64 + lane];
+            }
+        }
+        mfma_fp4_drain();
+        mark((t - blockIdx.x) / gridDim.x, 5);
+        if (dbg & 4) return;
+        float Tf[16];
+        const float* tq = tf_lds + q0 + 4u * (lane >> 5);
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const float4 v = *(const float4*)(tq + 8 * g4);
+            Tf[4 * g4 + 0] = v.x;
+            Tf[4 * g4 + 1] = v.y;
+            Tf[4 * g4 + 2] = v.z;
+            Tf[4 * g4 + 3] = v.w;
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const v16f_t& acc = st ? acc1 : acc0;
+            const uint32_t n = t * kMfCand + st * 32u + (lane & 31u);
+            bool hit[16];
+            bool any = false;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                hit[r] = acc[r] >= Tf[r] && n < N;
+                any |= hit[r];
+            }
+            // wave-level compaction: one LDS atomic reserves the wave's staging
+            // slots, per-row ballots + mbcnt place each lane's hits
+            if (__ballot(any)) {
+                uint32_t total = 0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) total += __popcll(__ballot(hit[r]));
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&st_n, total);
+                uint32_t run = __builtin_amdgcn_readlane(base, 0);
+                uint32_t rb = q0 + 4u * (lane >> 5);
+                asm volatile("" : "+v"(rb));  // keep row addresses out of the tile loop
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint64_t m = __ballot(hit[r]);
+                    if (m) {
+                        if (hit[r]) {
+                            const uint32_t sp = run + __builtin_amdgcn_mbcnt_hi(
+                                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
+                            const uint32_t d = (uint32_t)(kPadF - acc[r]) >> 1;
+                            const uint64_t key = ((uint64_t)d << 32) | n;
+                            if (sp < kStage) {
+                                st_key[sp] = key;
+                                st_q[sp] = (uint8_t)qi;
+                            } else {
+                                const uint32_t pos = atomicAdd(&counts[qi], 1u);
+                                if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = key;
+                            }
+                        }
+                        run += __popcll(m);
+                    }
+                }
+            }
+        }
+    };
+    // block-local tile j is global tile blockIdx.x + j*G
+    const uint32_t nt = blockIdx.x < ntiles ? (ntiles - blockIdx.x + G - 1) / G : 0;
+    auto tile = [&](uint32_t j) { return blockIdx.x + j * G; };
+#pragma unroll
+    for (int s = 0; s < D; ++s) load(tile(s), nw[s]);
+    if (nt) expand(0, nw[0]);
+    load(tile(D), nw[0]);
+    __syncthreads();
+    // iteration j: consume tile j (lds[j&1]); expand tile j+1 (set (j+1)%D) into
+    // lds[(j+1)&1]; refill that set with tile j+1+D.  Early half: MFMA first; late
+    // half: expand first, so the two halves' VALU and MFMA phases interleave.
+    auto step = [&](uint32_t j, auto S, auto LATE) __attribute__((always_inline)) {
+        constexpr int s1 = (decltype(S)::value + 1) % D;
+        constexpr int b = decltype(S)::value & 1;
+        const bool more = j + 1 < nt;
+        mark(j, 0);
+        if constexpr (!decltype(LATE)::value) {
+            if (active && !(dbg & 1)) consume(tile(j), b);
+            mark(j, 1);
+            if (more && !(dbg & 2)) expand(b ^ 1, nw[s1]);
+            mark(j, 2);
+            load(tile(j + 1 + D), nw[s1]);
+        } else {
+            if (more && !(dbg & 2)) expand(b ^ 1, nw[s1]);
+            mark(j, 1);
+            load(tile(j + 1 + D), nw[s1]);
+            mark(j, 2);
+            if (active && !(dbg & 1)) consume(tile(j), b);
+        }
+        mark(j, 3);
+        __syncthreads();
+        mark(j, 4);
+    };
+    static_assert(D == 4, "the unrolled ring below has four steps");
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    auto run = [&](auto LATE) __attribute__((always_inline)) {
+        for (uint32_t j = 0; j < nt; j += D) {
+            step(j, I0{}, LATE);
+            if (j + 1 < nt) step(j + 1, I1{}, LATE);
+            if (j + 2 < nt) step(j + 2, I2{}, LATE);
+            if (j + 3 < nt) step(j + 3, I3{}, LATE);
+        }
+    };
+    if (late)
+        run(std::true_type{});
+    else
+        run(std::false_type{});
+    // flush the staged candidates: all global atomics of the block in flight at once
+    const uint32_t ns = min(st_n, kStage);
+    for (uint32_t e = tid; e < ns; e += kMfThreads) {
+        const uint32_t qi = st_q[e];
+        const uint32_t pos = atomicAdd(&counts[qi], 1u);
+        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[e];
+    }
+}
+
+template <int W4>
+static void launch_scan_mx2_t(const Stage1Args& a, hipStream_t s) {
+    const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t grid = min(ntiles, (uint32_t)cus);
+    for (uint32_t g = 0; g < a.B; g += 256) {
+        const uint32_t bg = min(256u, a.B - g);
+        hipLaunchKernelGGL((k_scan_mx2<W4>), dim3(grid), dim3(kMfThreads), 0, s, a.codes, a.cap, a.N,
+                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
+                           a.buf + (uint64_t)g * a.bufcap, a.bufcap, a.dbg);
+    }
+}
+
 template <int W4>
 static void launch_scan_mx_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
@@ -932,12 +1210,19 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 4: launch_scan_mfma_t<4>(a, s); break;
             default: launch_scan_mfma_t<6>(a, s); break;
         }
-    } else if (mfma) {  // FP4 block-scaled MFMA (default for large batches)
+    } else if (mfma && a.use_mfma == 3) {  // FP4, uniform waves (A/B comparison)
         switch (W4) {
             case 2: launch_scan_mx_t<2>(a, s); break;
             case 3: launch_scan_mx_t<3>(a, s); break;
             case 4: launch_scan_mx_t<4>(a, s); break;
             default: launch_scan_mx_t<6>(a, s); break;
+        }
+    } else if (mfma) {  // FP4 block-scaled MFMA, producer/consumer waves (default for large batches)
+        switch (W4) {
+            case 2: launch_scan_mx2_t<2>(a, s); break;
+            case 3: launch_scan_mx2_t<3>(a, s); break;
+            case 4: launch_scan_mx2_t<4>(a, s); break;
+            default: launch_scan_mx2_t<6>(a, s); break;
         }
     } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \
@@ -1670,3 +1955,7 @@ hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, ui
 }
 
 }  // namespace gvdb
+
+extern "C" int gvdb_debug_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(gvdb::g_stamps), sizeof(gvdb::g_stamps));
+}
