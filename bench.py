@@ -256,7 +256,7 @@ def main():
         if variant == "i8":
             peak, kname = PEAK_I8_TOPS, "k_scan_mfma (+/-1 i8 dot, v_mfma_i32_32x32x32_i8)"
         else:
-            peak, kname = PEAK_FP4_TFLOPS, "k_scan_mx (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4)"
+            peak, kname = PEAK_FP4_TFLOPS, "k_scan_mx2 (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4)"
         roof = {
             "kernel": "stage-1 BQ Hamming filter: " + kname,
             "bound": "mfma",

@@ -896,12 +896,13 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
     __shared__ __attribute__((aligned(16))) float tf_lds[256];
     // Candidate staging: a returning global atomic per emit would stall the
     // emitting wave ~2 us and, through the per-tile barrier, the whole block.
-    // Emits append to LDS (LDS atomic) and are flushed to the per-query global
-    // buffers once, after the last tile; overflow falls back to direct emits.
-    constexpr uint32_t kStage = 2048;
-    __shared__ uint64_t st_key[kStage];
-    __shared__ uint8_t st_q[kStage];
-    __shared__ uint32_t st_n;
+    // Each wave appends its emits to a private LDS slice (its fill count is a
+    // wave-uniform scalar: no atomics) and the slices are flushed to the
+    // per-query global buffers once, after the last tile; a full slice falls
+    // back to direct global emits.
+    constexpr uint32_t kWaveStage = 512;
+    __shared__ uint64_t st_key[kMfThreads / 64][kWaveStage];
+    __shared__ uint8_t st_q[kMfThreads / 64][kWaveStage];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool late = wv >= 4;                 // second half: expand first, then MFMA
@@ -912,7 +913,6 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
     constexpr float kPadF = (float)(32 * KW);
     const int scale1 = 0x7f7f7f7f;
     if (tid < 256) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
-    if (tid == 0) st_n = 0;
 
     // expansion units of this thread: g = (late ? kHalf : 0) + u*256 + (tid & 255)
     // unit g = ((st*KS + s)*2 + h)*32 + col  <->  word (2s+h) of candidate st*32+col
@@ -957,19 +957,22 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
 #pragma unroll
         for (int s = 0; s < KS; ++s) qa[s] = fp4_x32(qw[2 * s + (lane >> 5)]);
     }
-    // dbg & 16: shader-clock stamps of waves 0 and 4 of block 0 (dev aid)
-    const bool stamp = (dbg & 16) && blockIdx.x == 0 && (wv & 3u) == 0 && lane == 0;
+    // dbg & 16 in a -DGVDB_SCAN_STAMPS build: shader-clock stamps of waves 0 and
+    // 4 of block 0 (dev aid; compiled out by default)
     auto mark = [&](uint32_t j, int p) __attribute__((always_inline)) {
-        if (stamp && j < kStampTiles) g_stamps[wv >> 2][j][p] = __builtin_amdgcn_s_memtime();
+#ifdef GVDB_SCAN_STAMPS
+        if ((dbg & 16) && blockIdx.x == 0 && (wv & 3u) == 0 && lane == 0 && j < kStampTiles)
+            g_stamps[wv >> 2][j][p] = __builtin_amdgcn_s_memtime();
+#else
+        (void)j;
+        (void)p;
+#endif
     };
-    // Early half (waves 0-3): MFMA, then expand tile j+1, then refill its set.
-    // Late half (waves 4-7): expand first, so the halves' VALU and MFMA phases
-    // interleave on each SIMD.  Separate loops keep the register ring static.
-    auto consume = [&](uint32_t t, int b) __attribute__((always_inline)) {
+    // MFMA phase of a tile: 2 x KS block-scaled FP4 MFMAs into one accumulator pair.
+    // B fragments ride a PF-deep register ring: the LDS read for k-step s is
+    // issued PF steps (2*PF MFMAs) before its use, covering LDS latency.
+    auto mma = [&](int b, v16f_t& acc0, v16f_t& acc1) __attribute__((always_inline)) {
         const v4i_t* bf = (const v4i_t*)lds[b];
-        v16f_t acc0, acc1;
-        // B fragments ride a PF-deep register ring: the LDS read for k-step s is
-        // issued PF steps (2*PF MFMAs) before its use, covering LDS latency
         constexpr int PF = kMxLdsDepth < KS ? kMxLdsDepth : KS;
         v4i_t r0[PF], r1[PF];
 #pragma unroll
@@ -992,8 +995,11 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
                 r1[s % PF] = bf[(1 * KS + s + PF) * 64 + lane];
             }
         }
-        mfma_fp4_drain();
-        mark((t - blockIdx.x) / gridDim.x, 5);
+    };
+    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
+    // Threshold epilogue of a tile whose MFMAs were issued one step earlier (its
+    // results are complete by then: the wave does not wait on the MFMA pipe).
+    auto epi = [&](uint32_t t, const v16f_t& acc0, const v16f_t& acc1) __attribute__((always_inline)) {
         if (dbg & 4) return;
         float Tf[16];
         const float* tq = tf_lds + q0 + 4u * (lane >> 5);
@@ -1008,45 +1014,34 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
             const v16f_t& acc = st ? acc1 : acc0;
+            // fast reject: one max-reduction per lane, one ballot per wave
+            float mx = acc[0] - Tf[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r] - Tf[r]);
+            if (!__ballot(mx >= 0.0f) || (dbg & 8)) continue;
             const uint32_t n = t * kMfCand + st * 32u + (lane & 31u);
-            bool hit[16];
-            bool any = false;
+            uint32_t rb = q0 + 4u * (lane >> 5);
+            asm volatile("" : "+v"(rb));  // keep row addresses out of the tile loop
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                hit[r] = acc[r] >= Tf[r] && n < N;
-                any |= hit[r];
-            }
-            // wave-level compaction: one LDS atomic reserves the wave's staging
-            // slots, per-row ballots + mbcnt place each lane's hits
-            if (__ballot(any)) {
-                uint32_t total = 0;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) total += __popcll(__ballot(hit[r]));
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&st_n, total);
-                uint32_t run = __builtin_amdgcn_readlane(base, 0);
-                uint32_t rb = q0 + 4u * (lane >> 5);
-                asm volatile("" : "+v"(rb));  // keep row addresses out of the tile loop
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const uint64_t m = __ballot(hit[r]);
-                    if (m) {
-                        if (hit[r]) {
-                            const uint32_t sp = run + __builtin_amdgcn_mbcnt_hi(
-                                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
-                            const uint32_t d = (uint32_t)(kPadF - acc[r]) >> 1;
-                            const uint64_t key = ((uint64_t)d << 32) | n;
-                            if (sp < kStage) {
-                                st_key[sp] = key;
-                                st_q[sp] = (uint8_t)qi;
-                            } else {
-                                const uint32_t pos = atomicAdd(&counts[qi], 1u);
-                                if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = key;
-                            }
+                const bool hit = acc[r] >= Tf[r] && n < N;
+                const uint64_t m = __ballot(hit);
+                if (m) {
+                    if (hit) {
+                        const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
+                        const uint32_t d = (uint32_t)(kPadF - acc[r]) >> 1;
+                        const uint64_t key = ((uint64_t)d << 32) | n;
+                        if (sp < kWaveStage) {
+                            st_key[wv][sp] = key;
+                            st_q[wv][sp] = (uint8_t)qi;
+                        } else {
+                            const uint32_t pos = atomicAdd(&counts[qi], 1u);
+                            if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = key;
                         }
-                        run += __popcll(m);
                     }
+                    wcnt += (uint32_t)__popcll(m);
                 }
             }
         }
@@ -1059,26 +1054,38 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
     if (nt) expand(0, nw[0]);
     load(tile(D), nw[0]);
     __syncthreads();
-    // iteration j: consume tile j (lds[j&1]); expand tile j+1 (set (j+1)%D) into
-    // lds[(j+1)&1]; refill that set with tile j+1+D.  Early half: MFMA first; late
-    // half: expand first, so the two halves' VALU and MFMA phases interleave.
+    // Step j: MFMAs of tile j (lds[j&1]) into accumulator pair j&1; threshold
+    // epilogue of tile j-1 from the other pair (software-pipelined, so no wave
+    // waits on its own MFMA results); expand tile j+1 (set (j+1)%D) into
+    // lds[(j+1)&1] and refill that set with tile j+1+D.  The early half (waves
+    // 0-3) issues its MFMAs first, the late half (waves 4-7) expands first, so
+    // the halves' VALU and MFMA phases interleave on each SIMD.  Separate loops
+    // per half keep the register ring static.
+    v16f_t accA0, accA1, accB0, accB1;
     auto step = [&](uint32_t j, auto S, auto LATE) __attribute__((always_inline)) {
         constexpr int s1 = (decltype(S)::value + 1) % D;
         constexpr int b = decltype(S)::value & 1;
+        v16f_t& c0 = b ? accB0 : accA0;
+        v16f_t& c1 = b ? accB1 : accA1;
+        const v16f_t& p0 = b ? accA0 : accB0;
+        const v16f_t& p1 = b ? accA1 : accB1;
         const bool more = j + 1 < nt;
+        const bool work = active && !(dbg & 1);
         mark(j, 0);
         if constexpr (!decltype(LATE)::value) {
-            if (active && !(dbg & 1)) consume(tile(j), b);
+            if (work) mma(b, c0, c1);
             mark(j, 1);
-            if (more && !(dbg & 2)) expand(b ^ 1, nw[s1]);
+            if (work && j > 0) epi(tile(j - 1), p0, p1);
             mark(j, 2);
+            if (more && !(dbg & 2)) expand(b ^ 1, nw[s1]);
             load(tile(j + 1 + D), nw[s1]);
         } else {
             if (more && !(dbg & 2)) expand(b ^ 1, nw[s1]);
-            mark(j, 1);
             load(tile(j + 1 + D), nw[s1]);
+            mark(j, 1);
+            if (work) mma(b, c0, c1);
             mark(j, 2);
-            if (active && !(dbg & 1)) consume(tile(j), b);
+            if (work && j > 0) epi(tile(j - 1), p0, p1);
         }
         mark(j, 3);
         __syncthreads();
@@ -1101,12 +1108,21 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
         run(std::true_type{});
     else
         run(std::false_type{});
-    // flush the staged candidates: all global atomics of the block in flight at once
-    const uint32_t ns = min(st_n, kStage);
-    for (uint32_t e = tid; e < ns; e += kMfThreads) {
-        const uint32_t qi = st_q[e];
+    // epilogue of the block's last tile
+    if (nt && active && !(dbg & 1)) {
+        mfma_fp4_drain();
+        if ((nt - 1) & 1)
+            epi(tile(nt - 1), accB0, accB1);
+        else
+            epi(tile(nt - 1), accA0, accA1);
+    }
+    __syncthreads();
+    // flush the staged candidates: all global atomics of the wave in flight at once
+    const uint32_t ns = min(wcnt, kWaveStage);
+    for (uint32_t e = lane; e < ns; e += 64u) {
+        const uint32_t qi = st_q[wv][e];
         const uint32_t pos = atomicAdd(&counts[qi], 1u);
-        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[e];
+        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
     }
 }
 

@@ -46,7 +46,9 @@ for cfg in configs:
         L.gvdb_debug_stamps(C.c_void_p(st.ctypes.data))
         d = np.diff(st[:, 4:60, :5].astype(np.int64), axis=2)
         mf = (st[:, 4:60, 5].astype(np.int64) - st[:, 4:60, 0].astype(np.int64))
+        e6 = (st[:, 4:60, 6].astype(np.int64) - st[:, 4:60, 0].astype(np.int64))
+        e7 = (st[:, 4:60, 7].astype(np.int64) - st[:, 4:60, 0].astype(np.int64))
         per = np.diff(st[:, 4:60, 0].astype(np.int64), axis=1)
         for h, name in enumerate(("early", "late")):
             print(f"  {name}: phase cycles (mean) {d[h].mean(0).round(0).tolist()} tile {per[h].mean():.0f}"
-                  f"  consume-MFMA end at {mf[h].mean():.0f}  samples {d[h][:6].tolist()}", flush=True)
+                  f"  consume-MFMA end at {mf[h].mean():.0f} cmp0 {e6[h].mean():.0f} emit0 {e7[h].mean():.0f}  samples {d[h][:6].tolist()}", flush=True)
