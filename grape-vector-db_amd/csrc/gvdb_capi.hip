@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -53,6 +54,14 @@ gvdb_status dim_mismatch(uint64_t expected, uint64_t actual) {
         if (e_ != hipSuccess) return dev_fail(e_, where); \
     } while (0)
 
+// GVDB_DEBUG_SYNC=1: synchronize and check after each launch of the flat
+// MFMA path (fault attribution while developing; off in production)
+#define DBG_SYNC(s, where)                                                     \
+    do {                                                                       \
+        static const bool on_ = getenv("GVDB_DEBUG_SYNC") != nullptr;          \
+        if (on_) HIP_TRY(hipStreamSynchronize(s), where);                      \
+    } while (0)
+
 // Rust `f32 as usize` (saturating; NaN -> 0).
 uint64_t rust_f32_as_usize(float v) {
     if (!(v == v) || v <= 0.0f) return 0;
@@ -64,7 +73,18 @@ uint64_t rust_f32_as_usize(float v) {
 // Kernel timing (HIP events around the launches, read after the batch's
 // stream sync; enabled by gvdb_timing_enable, used by bench.py)
 // ============================================================================
-enum { kTimSampleHist = 0, kTimScan = 1, kTimSelect = 2, kTimRerank = 3, kTimFinal = 4, kTimN = 5 };
+bool getenv_flag(const char* name) {
+    const char* v = getenv(name);
+    return v && *v && strcmp(v, "0") != 0;
+}
+// flat searches whose MFMA candidate pass could not be certified (exact rescan)
+std::atomic<uint64_t>& flat_fallbacks() {
+    static std::atomic<uint64_t> n{0};
+    return n;
+}
+
+enum { kTimSampleHist = 0, kTimScan = 1, kTimSelect = 2, kTimRerank = 3, kTimFinal = 4, kTimFlatEmit = 5, kTimFlat = 6,
+       kTimN = 7 };
 struct Timing {
     std::mutex mu;
     bool on = false;
@@ -120,12 +140,13 @@ struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
-        rows, norms, codes, misc;
+        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     ~Workspace() {
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
-                        &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc})
+                        &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_cand,
+                        &fx_scores})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -425,14 +446,24 @@ struct gvdb_index {
     std::unordered_map<uint64_t, uint64_t> id_row;    // live id -> row
     hipStream_t stream = nullptr;                     // mutations
     uint64_t capacity_hint = 0;
+    // bf16 k-chunk-major mirror of the rows for the MFMA flat search, built
+    // lazily by the first flat search after a mutation (version counter)
+    uint64_t version = 0;
+    mutable std::mutex rowsb_mu;
+    mutable uint16_t* rowsb = nullptr;
+    mutable uint64_t rowsb_cap = 0, rowsb_version = ~0ull;
+    mutable bool rows_have_nan = false;
 
     uint32_t w4() const { return code_w4(dim); }
     size_t device_bytes() const {
         return cap * ((size_t)dim * 4 + (size_t)w4() * 16 + 4 + 8);
     }
     void free_all() {
-        for (void* p : {(void*)rows, (void*)codes, (void*)norms, (void*)ids})
+        for (void* p : {(void*)rows, (void*)codes, (void*)norms, (void*)ids, (void*)rowsb})
             if (p) (void)hipFree(p);
+        rowsb = nullptr;
+        rowsb_cap = 0;
+        ++version;
         rows = nullptr;
         codes = nullptr;
         norms = nullptr;
@@ -512,6 +543,7 @@ std::vector<uint64_t> register_ids(gvdb_index* ix, const uint64_t* h_new_ids, ui
 
 gvdb_status finish_add(gvdb_index* ix, uint64_t n, const std::vector<uint64_t>& orphaned) {
     const uint64_t r0 = ix->n;
+    ++ix->version;
     HIP_TRY(launch_pack(ix->rows + r0 * ix->dim, n, ix->dim, ix->thr, ix->codes, kPackSoA, ix->cap, r0, ix->stream),
             "pack rows");
     HIP_TRY(launch_row_norms(ix->rows + r0 * ix->dim, n, ix->dim, ix->norms + r0, ix->stream), "row norms");
@@ -647,6 +679,137 @@ gvdb_status gvdb_index_build(gvdb_index* ix) {
 
 gvdb_status gvdb_index_optimize(gvdb_index* ix) { return gvdb_index_build(ix); }
 
+// Lazily (re)build the bf16 mirror of the rows for the MFMA flat search.
+static gvdb_status ensure_rowsb(const gvdb_index* ix, Workspace& ws, hipStream_t s) {
+    std::lock_guard<std::mutex> g(ix->rowsb_mu);
+    if (ix->rowsb && ix->rowsb_version == ix->version) return GVDB_OK;
+    const uint32_t KC = fx_kc(ix->dim);
+    if (!ix->rowsb || ix->rowsb_cap != ix->cap) {
+        if (ix->rowsb) (void)hipFree(ix->rowsb);
+        ix->rowsb = nullptr;
+        HIP_TRY(hipMalloc((void**)&ix->rowsb, (size_t)KC * ix->cap * 64 * 2), "alloc bf16 rows");
+        ix->rowsb_cap = ix->cap;
+    }
+    HIP_TRY(ws.flags.ensure(16), "alloc flags");
+    uint32_t* d_nan = ws.flags.as<uint32_t>() + 3;
+    HIP_TRY(hipMemsetAsync(d_nan, 0, 4, s), "memset nan flag");
+    HIP_TRY(launch_rows_to_bf16(ix->rows, ix->n, ix->dim, ix->rowsb, ix->cap, d_nan, s), "rows to bf16");
+        DBG_SYNC(s, "dbg: rows to bf16");
+    HIP_TRY(hipMemcpyAsync(ws.h_flags + 3, d_nan, 4, hipMemcpyDeviceToHost, s), "nan flag");
+    HIP_TRY(hipStreamSynchronize(s), "sync bf16 rows");
+    ix->rows_have_nan = ws.h_flags[3] != 0;
+    ix->rowsb_version = ix->version;
+    return GVDB_OK;
+}
+
+// K4 on MFMA: certified candidate pass + exact rerank (gvdb_flat.hip).  Sets
+// *certified = false when any query's list could not be proven exact (the
+// caller then runs the exact full scan); results are then meaningless.
+static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32_t B, uint32_t dim, uint32_t k, int kind,
+                           int descending, uint64_t* d_ids, float* d_scores, uint32_t* d_n, Workspace& ws,
+                           hipStream_t s, bool* certified) {
+    *certified = false;
+    gvdb_status st = ensure_rowsb(ix, ws, s);
+    if (st != GVDB_OK) return st;
+    if (ix->rows_have_nan) return GVDB_OK;  // the exact scan reproduces the reference's NaN behaviour
+    const uint32_t N = (uint32_t)ix->n, KC = fx_kc(dim);
+    const uint32_t ntiles = (N + kFxRows - 1) / kFxRows;
+    const uint32_t sampled = (ntiles + kFxSampleEvery - 1) / kFxSampleEvery;
+    const uint32_t S = sampled * kFxRows;
+    const double target = std::max(384.0, 4.0 * k);  // expected candidates per query
+    const uint32_t m = (uint32_t)std::ceil(target * (double)S / (double)N);
+    if (m < 1 || m > 16 || m > S) return GVDB_OK;
+    const uint32_t cc = kFxCandCap;
+    HIP_TRY(ws.qnorm.ensure(kFxQ * 4), "alloc qnorm");
+    HIP_TRY(ws.fx_qb.ensure((size_t)KC * kFxQ * 64 * 2 + kFxQ * 4), "alloc bf16 queries");
+    HIP_TRY(ws.fx_smp.ensure((size_t)kFxQ * S * 4), "alloc sample scores");
+    HIP_TRY(ws.fx_cand.ensure((size_t)kFxQ * cc * 4), "alloc candidates");
+    HIP_TRY(ws.fx_scores.ensure((size_t)kFxQ * cc * 4), "alloc candidate scores");
+    HIP_TRY(ws.thr.ensure(kFxQ * 4), "alloc thresholds");
+    HIP_TRY(ws.zero.ensure((kFxQ + 4) * 4), "alloc counts");
+    uint16_t* qb = ws.fx_qb.as<uint16_t>();
+    float* qinv = (float*)(qb + (size_t)KC * kFxQ * 64);
+    uint32_t* fail = ws.zero.as<uint32_t>();
+    uint32_t* counts = fail + 4;
+    const float eps = flat_eps(dim);
+    bool timed;
+    {
+        std::lock_guard<std::mutex> g(timing().mu);
+        timed = timing().on;
+    }
+    if (timed && !ws.ev.ok) ws.ev.create();
+    timed = timed && ws.ev.ok;
+    HIP_TRY(hipMemsetAsync(fail, 0, 16, s), "memset fail");
+    for (uint32_t g0 = 0; g0 < B; g0 += kFxQ) {
+        if (timed) HIP_TRY(hipEventRecord(ws.ev.e[0], s), "event");
+        const uint32_t Bg = std::min<uint32_t>(kFxQ, B - g0);
+        const float* q = d_q + (size_t)g0 * dim;
+        HIP_TRY(hipMemsetAsync(counts, 0, kFxQ * 4, s), "memset counts");
+        HIP_TRY(launch_row_norms(q, Bg, dim, ws.qnorm.as<float>(), s), "qnorm");
+        HIP_TRY(launch_queries_to_bf16(q, Bg, dim, ws.qnorm.as<float>(), qb, qinv, s), "queries to bf16");
+        DBG_SYNC(s, "dbg: queries to bf16");
+        FlatMxArgs a{};
+        a.rowsb = ix->rowsb;
+        a.cap = ix->cap;
+        a.N = N;
+        a.KC = KC;
+        a.qb = qb;
+        a.qinv = qinv;
+        a.rnorm = ix->norms;
+        a.B = Bg;
+        a.every = kFxSampleEvery;
+        a.smp = ws.fx_smp.as<float>();
+        a.S = S;
+        a.thr = ws.thr.as<float>();
+        a.counts = counts;
+        a.cand = ws.fx_cand.as<uint32_t>();
+        a.candcap = cc;
+        a.overflow = fail;
+        HIP_TRY(launch_flat_mx_sample(a, s), "flat sample pass");
+        DBG_SYNC(s, "dbg: flat sample pass");
+        HIP_TRY(launch_flat_threshold(a.smp, Bg, S, m, ws.thr.as<float>(), s), "flat thresholds");
+        DBG_SYNC(s, "dbg: flat thresholds");
+        if (timed) HIP_TRY(hipEventRecord(ws.ev.e[1], s), "event");
+        HIP_TRY(launch_flat_mx_emit(a, s), "flat candidate pass");
+        if (timed) HIP_TRY(hipEventRecord(ws.ev.e[2], s), "event");
+        DBG_SYNC(s, "dbg: flat candidate pass");
+        RerankArgs rr{};
+        rr.rows = ix->rows;
+        rr.clen = dim;
+        rr.norms = ix->norms;
+        rr.q = q;
+        rr.qlen = dim;
+        rr.s1_rows = a.cand;
+        rr.B = Bg;
+        rr.R = cc;
+        rr.kind = kind;
+        rr.scores = ws.fx_scores.as<float>();
+        rr.counts = counts;
+        HIP_TRY(launch_rerank(rr, s), "flat rerank");
+        DBG_SYNC(s, "dbg: flat rerank");
+        HIP_TRY(launch_flat_final(counts, a.cand, cc, rr.scores, ws.thr.as<float>(), eps, Bg, k, descending, ix->ids,
+                                  d_ids + (size_t)g0 * k, d_scores + (size_t)g0 * k, d_n ? d_n + g0 : nullptr, fail, s),
+                "flat final");
+        DBG_SYNC(s, "dbg: flat final");
+        if (timed) {  // timing mode only: per-group sync to read the events
+            HIP_TRY(hipEventRecord(ws.ev.e[3], s), "event");
+            HIP_TRY(hipEventSynchronize(ws.ev.e[3]), "event sync");
+            float te = 0, tt = 0;
+            (void)hipEventElapsedTime(&te, ws.ev.e[1], ws.ev.e[2]);
+            (void)hipEventElapsedTime(&tt, ws.ev.e[0], ws.ev.e[3]);
+            std::lock_guard<std::mutex> g(timing().mu);
+            timing().ms[kTimFlatEmit] += te;
+            timing().n[kTimFlatEmit] += 1;
+            timing().ms[kTimFlat] += tt;
+            timing().n[kTimFlat] += 1;
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(ws.h_flags, fail, 4, hipMemcpyDeviceToHost, s), "fail flag");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    *certified = ws.h_flags[0] == 0;
+    return GVDB_OK;
+}
+
 static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                      const gvdb_search_params* sp_in, uint64_t* d_ids, float* d_scores, uint32_t* d_n,
                                      Workspace& ws, hipStream_t s) {
@@ -659,6 +822,14 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
                      : sp.metric == GVDB_METRIC_COSINE_DISTANCE ? kScoreCosineDistance
                                                                  : kScoreCosine;
     const int descending = kind == kScoreCosine;
+    if (sp.mode == GVDB_SEARCH_FLAT && kind != kScoreL2 && ix->n >= kFxMinN && k >= 1 && k <= 256 &&
+        !getenv_flag("GVDB_FLAT_EXACT_ONLY")) {
+        bool certified = false;
+        gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
+                                        d_n, ws, s, &certified);
+        if (st != GVDB_OK || certified) return st;
+        flat_fallbacks().fetch_add(1);
+    }
     if (sp.mode == GVDB_SEARCH_FLAT) {
         HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
         HIP_TRY(ws.scores.ensure(B * ix->n * 4), "alloc flat scores");
@@ -1204,4 +1375,7 @@ gvdb_status gvdb_topk_merge_device(const uint64_t* d_ids, const float* d_scores,
     return GVDB_OK;
 }
 
+uint64_t gvdb_flat_fallback_count(void) { return flat_fallbacks().load(); }
+
 }  // extern "C"
+

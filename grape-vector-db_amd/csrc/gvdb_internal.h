@@ -106,6 +106,7 @@ struct RerankArgs {
     uint32_t B, R;
     int kind;                // ScoreKind
     float* scores;           // [B][R]
+    const uint32_t* counts;  // optional [B]: only the first counts[q] entries are valid
 };
 hipError_t launch_rerank(const RerankArgs& a, hipStream_t s);
 
@@ -139,6 +140,47 @@ hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint3
                               int has_threshold, float threshold, const uint64_t* ids, uint64_t* out_idx,
                               float* out_scores, uint32_t* out_n, void* tmp, size_t tmp_bytes, uint32_t* nan_flag,
                               hipStream_t s);
+
+// ---- K4 flat exact search on bf16 MFMA (gvdb_flat.hip) ---------------------------
+// Candidate pass on bf16 MFMA + exact rerank + per-query certificate; see
+// gvdb_flat.hip.  rowsb: bf16 [KC][cap][64], KC = fx_kc(D).
+constexpr uint32_t kFxRows = 256;      // rows per tile
+constexpr uint32_t kFxQ = 256;         // query slots per launch group
+constexpr uint32_t kFxCandCap = 4096;  // candidates per query (LDS sort capacity)
+constexpr uint32_t kFxMinN = 65536;    // smaller shards use the exact full scan
+constexpr uint32_t kFxSampleEvery = 64;  // sample pass: every 64th row tile
+__host__ __device__ inline uint32_t fx_kc(uint32_t D) { return (D + 63u) / 64u; }
+struct FlatMxArgs {
+    const uint16_t* rowsb;   // [KC][cap][64] bf16
+    uint64_t cap;
+    uint32_t N, KC;
+    const uint16_t* qb;      // [KC][kFxQ][64] bf16
+    const float* qinv;       // [kFxQ]
+    const float* rnorm;      // [N] exact row norms
+    uint32_t B;              // live query slots (<= kFxQ)
+    uint32_t every;          // sample pass: tile stride
+    float* smp;              // sample pass: [B][S] approx scores
+    uint32_t S;              // sample pass: sampled rows (= sampled tiles * kFxRows)
+    const float* thr;        // emit pass: [B]
+    uint32_t* counts;        // emit pass: [B] (zeroed by the caller)
+    uint32_t* cand;          // emit pass: [B][candcap] candidate rows
+    uint32_t candcap;
+    uint32_t* overflow;      // emit pass: set to 1 if a wave's LDS staging slice overflowed
+};
+float flat_eps(uint32_t D);
+hipError_t launch_rows_to_bf16(const float* rows, uint64_t n, uint32_t D, uint16_t* rowsb, uint64_t cap,
+                               uint32_t* nan_flag, hipStream_t s);
+hipError_t launch_queries_to_bf16(const float* q, uint32_t B, uint32_t D, const float* qnorm, uint16_t* qb,
+                                  float* qinv, hipStream_t s);
+hipError_t launch_flat_mx_sample(const FlatMxArgs& a, hipStream_t s);
+hipError_t launch_flat_mx_emit(const FlatMxArgs& a, hipStream_t s);
+// thr[q] = m-th largest sampled score (m <= 16)
+hipError_t launch_flat_threshold(const float* smp, uint32_t B, uint32_t S, uint32_t m, float* thr, hipStream_t s);
+// sort reranked candidates by (exact score, row), emit first k live rows,
+// OR 1 into *fail for a query whose list is not certified exact
+hipError_t launch_flat_final(const uint32_t* counts, const uint32_t* cand, uint32_t candcap, const float* scores,
+                             const float* thr, float eps, uint32_t B, uint32_t k, int descending, const uint64_t* ids,
+                             uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s);
 
 // ---- shard merge (shard.rs:776-784) --------------------------------------------
 hipError_t launch_topk_merge(const uint64_t* ids, const float* scores, const uint32_t* counts, uint32_t n_shards,

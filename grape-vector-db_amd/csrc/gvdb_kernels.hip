@@ -21,15 +21,11 @@
 
 #include <type_traits>
 
+#include "gvdb_device.h"
 #include "gvdb_internal.h"
 
 namespace gvdb {
 
-#define GVDB_LAUNCH_CHECK() \
-    do {                    \
-        hipError_t e__ = hipGetLastError(); \
-        if (e__ != hipSuccess) return e__;  \
-    } while (0)
 
 // ============================================================================
 // K1: sign/threshold packing
@@ -454,32 +450,6 @@ __global__ void k_sample_hist_generic(const uint4* __restrict__ codes, uint64_t 
     }
 }
 
-// In-LDS bitonic sort (ascending) of P = power-of-two u64 keys by a whole
-// workgroup.
-__device__ void bitonic_sort_lds(uint64_t* s, uint32_t P) {
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t a = s[i], b = s[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        s[i] = b;
-                        s[ixj] = a;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
-    uint32_t p = 1;
-    while (p < x) p <<= 1;
-    return p;
-}
 
 // Exact top-R from the candidate buffer: histogram -> T_R (R-th smallest d),
 // gather every key with d <= T_R, sort (d, row) ascending, keep R.  Any
@@ -1361,16 +1331,19 @@ __device__ __forceinline__ float4 load4_guarded(const float* __restrict__ src, u
 __global__ __launch_bounds__(kRrThreads) void k_rerank(const float* __restrict__ rows, uint64_t clen,
                                                        const float* __restrict__ norms, const float* __restrict__ q,
                                                        uint64_t qlen, const uint32_t* __restrict__ s1_rows, uint32_t R,
-                                                       int kind, float* __restrict__ scores) {
+                                                       const uint32_t* __restrict__ counts, int kind,
+                                                       float* __restrict__ scores) {
     __shared__ __attribute__((aligned(16))) float tiles[2][kRrRows * kRrLd];
     __shared__ __attribute__((aligned(16))) float qs[2][kRrCh];
     __shared__ uint64_t bases[kRrRows];
     const uint32_t tid = threadIdx.x;
     const uint32_t qi = blockIdx.y;
     const uint32_t r0 = blockIdx.x * kRrRows;
+    const uint32_t Rq = counts ? min(counts[qi], R) : R;  // valid entries of this query's list
+    if (r0 >= Rq) return;
     if (tid < kRrRows) {
         const uint32_t r = r0 + tid;
-        bases[tid] = r < R ? (uint64_t)s1_rows[(uint64_t)qi * R + r] * clen : ~0ull;
+        bases[tid] = r < Rq ? (uint64_t)s1_rows[(uint64_t)qi * R + r] * clen : ~0ull;
     }
     __syncthreads();
     const float* qv = q + (uint64_t)qi * qlen;
@@ -1440,7 +1413,7 @@ __global__ __launch_bounds__(kRrThreads) void k_rerank(const float* __restrict__
     }
     if (tid >= 64) return;
     const uint32_t r = r0 + tid;
-    if (r >= R) return;
+    if (r >= Rq) return;
     float score;
     if (kind == kScoreL2) {
         score = sqrtf(acc);
@@ -1460,17 +1433,11 @@ __global__ __launch_bounds__(kRrThreads) void k_rerank(const float* __restrict__
 hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
     if (a.B == 0 || a.R == 0) return hipSuccess;
     hipLaunchKernelGGL(k_rerank, dim3((a.R + kRrRows - 1) / kRrRows, a.B), dim3(kRrThreads), 0, s, a.rows, a.clen,
-                       a.norms, a.q, a.qlen, a.s1_rows, a.R, a.kind, a.scores);
+                       a.norms, a.q, a.qlen, a.s1_rows, a.R, a.counts, a.kind, a.scores);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-// Total order key for f32 scores: -0.0 == +0.0 (Rust partial_cmp), ascending.
-__device__ __forceinline__ uint32_t f32_order(float f) {
-    uint32_t u = __float_as_uint(f);
-    if (u == 0x80000000u) u = 0u;
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
 
 __global__ __launch_bounds__(256) void k_final_sort(const float* __restrict__ scores,
                                                     const uint32_t* __restrict__ s1_rows, uint32_t R, uint32_t kout,
@@ -1712,7 +1679,7 @@ __global__ void k_emit_flat(const uint32_t* __restrict__ ranks, const float* __r
         }
         o += __popcll(m);
     }
-    if (threadIdx.x == 0) *out_n = o < limit ? o : limit;
+    if (threadIdx.x == 0 && out_n) *out_n = o < limit ? o : limit;
 }
 
 hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint32_t limit, int descending,
@@ -1735,7 +1702,8 @@ hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint3
         hipError_t e = hipcub::DeviceRadixSort::SortPairs(ctmp, cbytes, kb, vb, (int)N, 0, 32, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_emit_flat, dim3(1), dim3(64), 0, s, vb.Current(), sc, N, limit, has_threshold, threshold,
-                           ids, out_idx + (uint64_t)q * limit, out_scores + (uint64_t)q * limit, out_n + q);
+                           ids, out_idx + (uint64_t)q * limit, out_scores + (uint64_t)q * limit,
+                           out_n ? out_n + q : nullptr);
         GVDB_LAUNCH_CHECK();
     }
     return hipSuccess;
@@ -1779,7 +1747,7 @@ __global__ __launch_bounds__(256) void k_topk_merge(const uint64_t* __restrict__
         out_ids[(uint64_t)q * limit + i] = ids[((uint64_t)sh * B + q) * stride + j];
         out_scores[(uint64_t)q * limit + i] = scores[((uint64_t)sh * B + q) * stride + j];
     }
-    if (threadIdx.x == 0) out_n[q] = take;
+    if (threadIdx.x == 0 && out_n) out_n[q] = take;
 }
 
 hipError_t launch_topk_merge(const uint64_t* ids, const float* scores, const uint32_t* counts, uint32_t n_shards,

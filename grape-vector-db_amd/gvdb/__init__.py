@@ -353,6 +353,12 @@ class GpuVectorIndex:
         check(self._lib.gvdb_index_remove(self._h, u, C.byref(r)))
         return bool(r.value)
 
+    def remove_vector_id(self, u: int) -> bool:
+        """remove_vector by the u64 id of add_batch."""
+        r = C.c_int32()
+        check(self._lib.gvdb_index_remove(self._h, int(u), C.byref(r)))
+        return bool(r.value)
+
     def len(self) -> int:
         return int(self._lib.gvdb_index_len(self._h))
 

@@ -241,6 +241,95 @@ def test_index_flat_mode_matches_oracle(g, oracle_mod):
         assert list(ids[b, :n[b]]) == list(ri) and same_f32(sc[b, :n[b]], rs)
 
 
+@pytest.mark.parametrize("N,D,B,k,metric", [(200_000, 768, 48, 10, 0), (150_000, 100, 300, 25, 0),
+                                             (100_000, 200, 17, 100, 2), (70_000, 64, 1, 1, 0)])
+def test_flat_mfma_certified_matches_oracle(g, oracle_mod, N, D, B, k, metric):
+    """K4 on bf16 MFMA (gvdb_flat.hip): candidates from the MFMA pass, exact
+    rerank, certificate.  Ids equal and scores bit-identical to the oracle's
+    storage.rs / index.rs flat search, with NO exact-rescan fallback taken."""
+    x = rng_rows(N + D, N, D, dup=40)
+    x[5] = 0.0  # zero-norm row scores 0 (cosine) / +inf (distance)
+    Q = rng_rows(D + 11, B, D)
+    r = np.random.default_rng(B)
+    planted = r.integers(0, N, size=B)
+    Q[: B // 2] = x[planted[: B // 2]] + 0.05 * Q[: B // 2]  # true near neighbours for half the batch
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    before = g.lib().gvdb_flat_fallback_count()
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=metric))
+    assert g.lib().gvdb_flat_fallback_count() == before, "MFMA candidate pass was not certified"
+    for b in range(B):
+        if metric == 0:
+            ri, rs = oracle_mod.storage_vector_search(Q[b], x, k)
+        else:
+            ri, rs = oracle_mod.flat_cosine_distance_search(Q[b], x, k)
+        assert n[b] == len(ri)
+        assert list(ids[b, : n[b]]) == list(ri), b
+        assert same_f32(sc[b, : n[b]], rs)
+
+
+def test_flat_mfma_uncertifiable_falls_back_exactly(g, oracle_mod):
+    """A zero query ties every row at 0.0: no certificate is possible, the exact
+    full scan answers (storage.rs order: first k rows)."""
+    N, D = 70_000, 64
+    x = rng_rows(3, N, D)
+    Q = np.zeros((2, D), np.float32)
+    Q[1] = x[123]
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    before = g.lib().gvdb_flat_fallback_count()
+    ids, sc, n = ix.search_batch(Q, 10, g.SearchParams(mode=1, metric=0))
+    assert g.lib().gvdb_flat_fallback_count() == before + 1
+    for b in range(2):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], x, 10)
+        assert list(ids[b, : n[b]]) == list(ri) and same_f32(sc[b, : n[b]], rs)
+
+
+def test_flat_device_api_without_out_n(g, oracle_mod):
+    """gvdb_index_search_device with out_n = NULL (optional) on the MFMA flat path
+    and, for a batch over 256 queries, across launch groups."""
+    import torch
+
+    N, D, B, k = 70_000, 64, 300, 5
+    x = rng_rows(31, N, D)
+    Q = rng_rows(32, B, D)
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    q = torch.from_numpy(Q).cuda()
+    oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+    osc = torch.zeros((B, k), device="cuda")
+    ix.search_device(q, k, oi, osc, None, g.SearchParams(mode=1, metric=0))
+    torch.cuda.synchronize()
+    ids, sc = oi.cpu().numpy(), osc.cpu().numpy()
+    for b in (0, 255, 256, 299):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], x, k)
+        assert list(ids[b]) == list(ri) and same_f32(sc[b], rs)
+
+
+def test_flat_mfma_after_mutations(g, oracle_mod):
+    """The bf16 mirror is rebuilt after add / remove (version counter)."""
+    N, D = 80_000, 96
+    x = rng_rows(21, N, D)
+    Q = x[[10, 20_000, 79_999]] + 0.01
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    p = g.SearchParams(mode=1, metric=0)
+    ids, _, _ = ix.search_batch(Q, 5, p)
+    assert list(ids[:, 0]) == [10, 20_000, 79_999]
+    extra = rng_rows(22, 1000, D)
+    extra[7] = Q[1]  # exact match appended
+    ix.add_batch(np.arange(N, N + 1000, dtype=np.uint64), extra)
+    ids, _, _ = ix.search_batch(Q, 5, p)
+    assert ids[1, 0] == N + 7
+    assert ix.remove_vector_id(N + 7)
+    ids, sc, n = ix.search_batch(Q, 5, p)
+    allx = np.concatenate([x, np.delete(extra, 7, axis=0)])
+    for b in range(3):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], allx, 5)
+        live = np.concatenate([np.arange(N), np.delete(np.arange(N, N + 1000), 7)])
+        assert list(ids[b, : n[b]]) == list(live[ri]) and same_f32(sc[b, : n[b]], rs)
+
+
 def test_flat_search_threshold(g, oracle_mod):
     N, D = 2000, 32
     x = rng_rows(11, N, D)
