@@ -12,6 +12,6 @@ step() {  # step <name> <timeout> <cmd...>
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
     return 0
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q -rf
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_1m 600 python bench.py --n 1000000 --steps 5 --warmup 2 --no-cpu-baseline --b1-queries 50

@@ -13,7 +13,7 @@ step() {
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
     return 0
 }
-if [ -z "$SKIP_TESTS" ]; then step pytest_gpu 900 python -m pytest tests -m gpu -q -rf; fi
+if [ -z "$SKIP_TESTS" ]; then step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread; fi
 step bench_full 900 python bench.py
 step prof_full 900 rocprofv3 --kernel-trace --stats --output-format csv -T -d gpurun_out/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 2
 # keep only the summaries (the per-dispatch trace is large)

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r01}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
-ARGS="--no-cpu-baseline --steps 10 --warmup 2 --b1-queries ${B1Q:-50}"
+ARGS="--no-cpu-baseline --no-points --steps 10 --warmup 2 --b1-queries ${B1Q:-50}"
 i=0
 for set in "SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES" \
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY" \
