@@ -77,14 +77,19 @@ bool getenv_flag(const char* name) {
     const char* v = getenv(name);
     return v && *v && strcmp(v, "0") != 0;
 }
-// flat searches whose MFMA candidate pass could not be certified (exact rescan)
+// flat searches whose bf16-MFMA candidate pass could not be certified (exact rescan)
 std::atomic<uint64_t>& flat_fallbacks() {
+    static std::atomic<uint64_t> n{0};
+    return n;
+}
+// flat searches whose i8-MFMA candidate pass could not be certified (bf16 retry)
+std::atomic<uint64_t>& flat_fallbacks_i8() {
     static std::atomic<uint64_t> n{0};
     return n;
 }
 
 enum { kTimSampleHist = 0, kTimScan = 1, kTimSelect = 2, kTimRerank = 3, kTimFinal = 4, kTimFlatEmit = 5, kTimFlat = 6,
-       kTimN = 7 };
+       kTimFlatEmitI8 = 7, kTimFlatI8 = 8, kTimN = 9 };
 struct Timing {
     std::mutex mu;
     bool on = false;
@@ -140,12 +145,12 @@ struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
-        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores;
+        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     ~Workspace() {
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
-                        &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_cand,
+                        &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
                         &fx_scores})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
@@ -453,16 +458,26 @@ struct gvdb_index {
     mutable uint16_t* rowsb = nullptr;
     mutable uint64_t rowsb_cap = 0, rowsb_version = ~0ull;
     mutable bool rows_have_nan = false;
+    // int8 mirror (k-chunk-major, [KC_i8][cap][128]) + per-row s_x/|x|
+    // (rowsq_aux[0, cap)) and relative quantisation error (rowsq_aux[cap, 2cap))
+    mutable int8_t* rowsq = nullptr;
+    mutable float* rowsq_aux = nullptr;
+    mutable uint64_t rowsq_cap = 0, rowsq_version = ~0ull;
+    mutable bool rows_nonfinite = false;
 
     uint32_t w4() const { return code_w4(dim); }
     size_t device_bytes() const {
         return cap * ((size_t)dim * 4 + (size_t)w4() * 16 + 4 + 8);
     }
     void free_all() {
-        for (void* p : {(void*)rows, (void*)codes, (void*)norms, (void*)ids, (void*)rowsb})
+        for (void* p : {(void*)rows, (void*)codes, (void*)norms, (void*)ids, (void*)rowsb, (void*)rowsq,
+                        (void*)rowsq_aux})
             if (p) (void)hipFree(p);
         rowsb = nullptr;
         rowsb_cap = 0;
+        rowsq = nullptr;
+        rowsq_aux = nullptr;
+        rowsq_cap = 0;
         ++version;
         rows = nullptr;
         codes = nullptr;
@@ -687,7 +702,7 @@ static gvdb_status ensure_rowsb(const gvdb_index* ix, Workspace& ws, hipStream_t
     if (!ix->rowsb || ix->rowsb_cap != ix->cap) {
         if (ix->rowsb) (void)hipFree(ix->rowsb);
         ix->rowsb = nullptr;
-        HIP_TRY(hipMalloc((void**)&ix->rowsb, (size_t)KC * ix->cap * 64 * 2), "alloc bf16 rows");
+        HIP_TRY(hipMalloc((void**)&ix->rowsb, fx_mirror_bytes(ix->cap, KC)), "alloc bf16 rows");
         ix->rowsb_cap = ix->cap;
     }
     HIP_TRY(ws.flags.ensure(16), "alloc flags");
@@ -702,36 +717,83 @@ static gvdb_status ensure_rowsb(const gvdb_index* ix, Workspace& ws, hipStream_t
     return GVDB_OK;
 }
 
+// Lazily (re)build the int8 mirror of the rows for the i8-MFMA flat search.
+static gvdb_status ensure_rowsq(const gvdb_index* ix, Workspace& ws, hipStream_t s) {
+    std::lock_guard<std::mutex> g(ix->rowsb_mu);
+    if (ix->rowsq && ix->rowsq_version == ix->version) return GVDB_OK;
+    const uint32_t KC = fx_kc_i8(ix->dim);
+    if (!ix->rowsq || ix->rowsq_cap != ix->cap) {
+        if (ix->rowsq) (void)hipFree(ix->rowsq);
+        if (ix->rowsq_aux) (void)hipFree(ix->rowsq_aux);
+        ix->rowsq = nullptr;
+        ix->rowsq_aux = nullptr;
+        HIP_TRY(hipMalloc((void**)&ix->rowsq, fx_mirror_bytes(ix->cap, KC)), "alloc i8 rows");
+        HIP_TRY(hipMalloc((void**)&ix->rowsq_aux, (size_t)ix->cap * 8), "alloc i8 row scales");
+        ix->rowsq_cap = ix->cap;
+    }
+    HIP_TRY(ws.flags.ensure(16), "alloc flags");
+    uint32_t* d_bad = ws.flags.as<uint32_t>() + 3;
+    HIP_TRY(hipMemsetAsync(d_bad, 0, 4, s), "memset flag");
+    HIP_TRY(launch_rows_to_i8(ix->rows, ix->norms, ix->n, ix->dim, ix->rowsq, ix->cap, ix->rowsq_aux,
+                              ix->rowsq_aux + ix->cap, d_bad, s),
+            "rows to i8");
+    DBG_SYNC(s, "dbg: rows to i8");
+    HIP_TRY(hipMemcpyAsync(ws.h_flags + 3, d_bad, 4, hipMemcpyDeviceToHost, s), "flag");
+    HIP_TRY(hipStreamSynchronize(s), "sync i8 rows");
+    ix->rows_nonfinite = ws.h_flags[3] != 0;
+    ix->rowsq_version = ix->version;
+    return GVDB_OK;
+}
+
 // K4 on MFMA: certified candidate pass + exact rerank (gvdb_flat.hip).  Sets
 // *certified = false when any query's list could not be proven exact (the
 // caller then runs the exact full scan); results are then meaningless.
 static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32_t B, uint32_t dim, uint32_t k, int kind,
                            int descending, uint64_t* d_ids, float* d_scores, uint32_t* d_n, Workspace& ws,
-                           hipStream_t s, bool* certified) {
+                           hipStream_t s, bool i8, bool* certified) {
     *certified = false;
-    gvdb_status st = ensure_rowsb(ix, ws, s);
+    gvdb_status st = i8 ? ensure_rowsq(ix, ws, s) : ensure_rowsb(ix, ws, s);
     if (st != GVDB_OK) return st;
-    if (ix->rows_have_nan) return GVDB_OK;  // the exact scan reproduces the reference's NaN behaviour
-    const uint32_t N = (uint32_t)ix->n, KC = fx_kc(dim);
+    // the exact scan reproduces the reference's NaN behaviour
+    if (i8 ? ix->rows_nonfinite : ix->rows_have_nan) return GVDB_OK;
+    const uint32_t N = (uint32_t)ix->n, KC = i8 ? fx_kc_i8(dim) : fx_kc(dim);
     const uint32_t ntiles = (N + kFxRows - 1) / kFxRows;
     const uint32_t sampled = (ntiles + kFxSampleEvery - 1) / kFxSampleEvery;
     const uint32_t S = sampled * kFxRows;
-    const double target = std::max(384.0, 4.0 * k);  // expected candidates per query
-    const uint32_t m = (uint32_t)std::ceil(target * (double)S / (double)N);
-    if (m < 1 || m > 16 || m > S) return GVDB_OK;
+
+    // mk: the sample rank whose score (minus eps) bounds the threshold.  The
+    // sample holds ~Poisson(lambda = k*S/N) of the true top-k rows; mk is the
+    // smallest rank with P(X >= mk) <= 1e-6, so T + eps stays below the k-th
+    // score unless the sample over-represents the top k that much.
+    const double lambda = (double)k * (double)S / (double)N;
+    uint32_t mk = 1;
+    {
+        double p = std::exp(-lambda), cdf = p;  // P(X = 0), P(X <= 0)
+        while (mk < 16 && 1.0 - cdf > 1e-6) {
+            p *= lambda / (double)mk;
+            cdf += p;
+            ++mk;
+        }
+    }
+    if (mk > S) return GVDB_OK;
     const uint32_t cc = kFxCandCap;
     HIP_TRY(ws.qnorm.ensure(kFxQ * 4), "alloc qnorm");
-    HIP_TRY(ws.fx_qb.ensure((size_t)KC * kFxQ * 64 * 2 + kFxQ * 4), "alloc bf16 queries");
+    HIP_TRY(ws.fx_qb.ensure((size_t)KC * kFxQ * 128 + kFxQ * 12), "alloc converted queries");
     HIP_TRY(ws.fx_smp.ensure((size_t)kFxQ * S * 4), "alloc sample scores");
+    HIP_TRY(ws.fx_probe.ensure((size_t)kFxQ * 33 * 4), "alloc probes");
+    uint32_t* probes = ws.fx_probe.as<uint32_t>();
+    float* pscores = (float*)(probes + kFxQ * 16);
+    uint32_t* pcount = probes + kFxQ * 32;
     HIP_TRY(ws.fx_cand.ensure((size_t)kFxQ * cc * 4), "alloc candidates");
     HIP_TRY(ws.fx_scores.ensure((size_t)kFxQ * cc * 4), "alloc candidate scores");
     HIP_TRY(ws.thr.ensure(kFxQ * 4), "alloc thresholds");
     HIP_TRY(ws.zero.ensure((kFxQ + 4) * 4), "alloc counts");
-    uint16_t* qb = ws.fx_qb.as<uint16_t>();
-    float* qinv = (float*)(qb + (size_t)KC * kFxQ * 64);
+    char* qx = ws.fx_qb.as<char>();
+    float* qinv = (float*)(qx + (size_t)KC * kFxQ * 128);
+    float* qa = qinv + kFxQ;
+    float* qd = qa + kFxQ;
     uint32_t* fail = ws.zero.as<uint32_t>();
     uint32_t* counts = fail + 4;
-    const float eps = flat_eps(dim);
     bool timed;
     {
         std::lock_guard<std::mutex> g(timing().mu);
@@ -746,16 +808,26 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         const float* q = d_q + (size_t)g0 * dim;
         HIP_TRY(hipMemsetAsync(counts, 0, kFxQ * 4, s), "memset counts");
         HIP_TRY(launch_row_norms(q, Bg, dim, ws.qnorm.as<float>(), s), "qnorm");
-        HIP_TRY(launch_queries_to_bf16(q, Bg, dim, ws.qnorm.as<float>(), qb, qinv, s), "queries to bf16");
-        DBG_SYNC(s, "dbg: queries to bf16");
+        if (i8)
+            HIP_TRY(launch_queries_to_i8(q, Bg, dim, ws.qnorm.as<float>(), (int8_t*)qx, qinv, qa, qd, s),
+                    "queries to i8");
+        else
+            HIP_TRY(launch_queries_to_bf16(q, Bg, dim, ws.qnorm.as<float>(), (uint16_t*)qx, qinv, qd, s),
+                    "queries to bf16");
+        DBG_SYNC(s, "dbg: queries converted");
         FlatMxArgs a{};
-        a.rowsb = ix->rowsb;
+        a.i8 = i8 ? 1 : 0;
+        a.rowsx = i8 ? (const void*)ix->rowsq : (const void*)ix->rowsb;
         a.cap = ix->cap;
         a.N = N;
         a.KC = KC;
-        a.qb = qb;
+        a.qx = qx;
         a.qinv = qinv;
         a.rnorm = ix->norms;
+        a.rscale = ix->rowsq_aux;
+        a.rrho = ix->rowsq_aux ? ix->rowsq_aux + ix->cap : nullptr;
+        a.qa = qa;
+        a.qd = qd;
         a.B = Bg;
         a.every = kFxSampleEvery;
         a.smp = ws.fx_smp.as<float>();
@@ -765,9 +837,33 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         a.cand = ws.fx_cand.as<uint32_t>();
         a.candcap = cc;
         a.overflow = fail;
+        {
+            const char* d = getenv("GVDB_FLAT_DBG");  // ablation timing only (results invalid when set)
+            a.dbg = d ? atoi(d) : 0;
+        }
         HIP_TRY(launch_flat_mx_sample(a, s), "flat sample pass");
         DBG_SYNC(s, "dbg: flat sample pass");
-        HIP_TRY(launch_flat_threshold(a.smp, Bg, S, m, ws.thr.as<float>(), s), "flat thresholds");
+        // tau from exactly re-scored probes (the 16 best sampled rows per query)
+        HIP_TRY(launch_flat_probes(a.smp, Bg, S, kFxSampleEvery, N, probes, pcount, s), "flat probes");
+        {
+            RerankArgs pr{};
+            pr.rows = ix->rows;
+            pr.clen = dim;
+            pr.norms = ix->norms;
+            pr.q = q;
+            pr.qlen = dim;
+            pr.s1_rows = probes;
+            pr.B = Bg;
+            pr.R = 16;
+            pr.kind = kind;
+            pr.scores = pscores;
+            pr.counts = pcount;
+            HIP_TRY(launch_rerank(pr, s), "flat probe rerank");
+        }
+        const bool dbg_noemit = getenv_flag("GVDB_FLAT_DBG_NOEMIT");  // ablation timing only (results invalid)
+        HIP_TRY(launch_flat_tau(pscores, pcount, dbg_noemit ? 0 : Bg, mk, kind == kScoreCosineDistance, qd,
+                                ws.thr.as<float>(), s),
+                "flat thresholds");
         DBG_SYNC(s, "dbg: flat thresholds");
         if (timed) HIP_TRY(hipEventRecord(ws.ev.e[1], s), "event");
         HIP_TRY(launch_flat_mx_emit(a, s), "flat candidate pass");
@@ -787,7 +883,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         rr.counts = counts;
         HIP_TRY(launch_rerank(rr, s), "flat rerank");
         DBG_SYNC(s, "dbg: flat rerank");
-        HIP_TRY(launch_flat_final(counts, a.cand, cc, rr.scores, ws.thr.as<float>(), eps, Bg, k, descending, ix->ids,
+        HIP_TRY(launch_flat_final(counts, a.cand, cc, rr.scores, ws.thr.as<float>(), qd, Bg, k, descending, ix->ids,
                                   d_ids + (size_t)g0 * k, d_scores + (size_t)g0 * k, d_n ? d_n + g0 : nullptr, fail, s),
                 "flat final");
         DBG_SYNC(s, "dbg: flat final");
@@ -798,10 +894,11 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
             (void)hipEventElapsedTime(&te, ws.ev.e[1], ws.ev.e[2]);
             (void)hipEventElapsedTime(&tt, ws.ev.e[0], ws.ev.e[3]);
             std::lock_guard<std::mutex> g(timing().mu);
-            timing().ms[kTimFlatEmit] += te;
-            timing().n[kTimFlatEmit] += 1;
-            timing().ms[kTimFlat] += tt;
-            timing().n[kTimFlat] += 1;
+            const int se = i8 ? kTimFlatEmitI8 : kTimFlatEmit, sg = i8 ? kTimFlatI8 : kTimFlat;
+            timing().ms[se] += te;
+            timing().n[se] += 1;
+            timing().ms[sg] += tt;
+            timing().n[sg] += 1;
         }
     }
     HIP_TRY(hipMemcpyAsync(ws.h_flags, fail, 4, hipMemcpyDeviceToHost, s), "fail flag");
@@ -824,9 +921,22 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
     const int descending = kind == kScoreCosine;
     if (sp.mode == GVDB_SEARCH_FLAT && kind != kScoreL2 && ix->n >= kFxMinN && k >= 1 && k <= 256 &&
         !getenv_flag("GVDB_FLAT_EXACT_ONLY")) {
+        // bf16 candidates (2^-8 margin) by default.  GVDB_FLAT=i8 tries the i8
+        // tier first (half the bytes, twice the MFMA rate, but a ~4x wider
+        // certified margin: on high-entropy data such as i.i.d. 768-d vectors at
+        // 10M rows its candidate set overflows); a batch a tier cannot certify
+        // is retried on the next one (i8 -> bf16 -> exact scan).
+        const char* fk = getenv("GVDB_FLAT");
+        const bool try_i8 = fk && strcmp(fk, "i8") == 0;
         bool certified = false;
+        if (try_i8) {
+            gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
+                                            d_n, ws, s, true, &certified);
+            if (st != GVDB_OK || certified) return st;
+            flat_fallbacks_i8().fetch_add(1);
+        }
         gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
-                                        d_n, ws, s, &certified);
+                                        d_n, ws, s, false, &certified);
         if (st != GVDB_OK || certified) return st;
         flat_fallbacks().fetch_add(1);
     }
@@ -1376,6 +1486,7 @@ gvdb_status gvdb_topk_merge_device(const uint64_t* d_ids, const float* d_scores,
 }
 
 uint64_t gvdb_flat_fallback_count(void) { return flat_fallbacks().load(); }
+uint64_t gvdb_flat_i8_fallback_count(void) { return flat_fallbacks_i8().load(); }
 
 }  // extern "C"
 

@@ -149,38 +149,64 @@ constexpr uint32_t kFxQ = 256;         // query slots per launch group
 constexpr uint32_t kFxCandCap = 4096;  // candidates per query (LDS sort capacity)
 constexpr uint32_t kFxMinN = 65536;    // smaller shards use the exact full scan
 constexpr uint32_t kFxSampleEvery = 64;  // sample pass: every 64th row tile
-__host__ __device__ inline uint32_t fx_kc(uint32_t D) { return (D + 63u) / 64u; }
+__host__ __device__ inline uint32_t fx_kc(uint32_t D) { return (D + 63u) / 64u; }        // bf16 chunks
+__host__ __device__ inline uint32_t fx_kc_i8(uint32_t D) { return (D + 127u) / 128u; }  // i8 chunks
+// byte offset of (row, chunk c) in a tile-major flat mirror [ceil(cap/256)][KC][256][128 B]
+__host__ __device__ inline uint64_t fx_off(uint64_t row, uint32_t c, uint32_t KC) {
+    return ((((row >> 8) * KC + c) << 8) | (row & 255u)) * 128u;
+}
+__host__ __device__ inline uint64_t fx_mirror_bytes(uint64_t cap, uint32_t KC) {
+    return ((cap + 255u) >> 8) * KC * 256u * 128u;
+}
 struct FlatMxArgs {
-    const uint16_t* rowsb;   // [KC][cap][64] bf16
+    int i8;                  // element kind: 1 = int8 (k_flat_mx<., true>), 0 = bf16
+    const void* rowsx;       // tile-major [tiles][KC][256][128 B] (fx_off): bf16 x64 or int8 x128 per chunk row
     uint64_t cap;
     uint32_t N, KC;
-    const uint16_t* qb;      // [KC][kFxQ][64] bf16
-    const float* qinv;       // [kFxQ]
-    const float* rnorm;      // [N] exact row norms
+    const void* qx;          // [KC][kFxQ][128 B]
+    const float* qinv;       // [kFxQ]  bf16: 1/|q|; i8: s_q/|q|
+    const float* rnorm;      // [N] exact row norms (bf16)
+    const float* rscale;     // [N] s_x/|x| (i8)
+    const float* rrho;       // [N] relative quantisation error rho_x (i8)
+    const float* qa;         // [kFxQ] pair-bound terms (see k_flat_mx's epilogue)
+    const float* qd;         // [kFxQ]
     uint32_t B;              // live query slots (<= kFxQ)
     uint32_t every;          // sample pass: tile stride
-    float* smp;              // sample pass: [B][S] approx scores
+    float* smp;              // sample pass: [B][S] MFMA scores of the sampled rows
     uint32_t S;              // sample pass: sampled rows (= sampled tiles * kFxRows)
     const float* thr;        // emit pass: [B]
     uint32_t* counts;        // emit pass: [B] (zeroed by the caller)
     uint32_t* cand;          // emit pass: [B][candcap] candidate rows
     uint32_t candcap;
     uint32_t* overflow;      // emit pass: set to 1 if a wave's LDS staging slice overflowed
+    int dbg;                 // ablation timing only (GVDB_FLAT_DBG): 1 skip query loads, 2 skip row loads, 4 skip MFMA
 };
 float flat_eps(uint32_t D);
 hipError_t launch_rows_to_bf16(const float* rows, uint64_t n, uint32_t D, uint16_t* rowsb, uint64_t cap,
                                uint32_t* nan_flag, hipStream_t s);
 hipError_t launch_queries_to_bf16(const float* q, uint32_t B, uint32_t D, const float* qnorm, uint16_t* qb,
-                                  float* qinv, hipStream_t s);
+                                  float* qinv, float* qd, hipStream_t s);
+// rows -> int8 [KC_i8][cap][128], rscale = s_x/|x|, rrho = relative
+// quantisation error, *bad = non-finite rows
+hipError_t launch_rows_to_i8(const float* rows, const float* norms, uint64_t n, uint32_t D, int8_t* rowsq, uint64_t cap,
+                             float* rscale, float* rrho, uint32_t* bad_flag, hipStream_t s);
+hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const float* qnorm, int8_t* qq, float* qinv,
+                                float* qa, float* qd, hipStream_t s);
 hipError_t launch_flat_mx_sample(const FlatMxArgs& a, hipStream_t s);
 hipError_t launch_flat_mx_emit(const FlatMxArgs& a, hipStream_t s);
-// thr[q] = m-th largest sampled score (m <= 16)
-hipError_t launch_flat_threshold(const float* smp, uint32_t B, uint32_t S, uint32_t m, float* thr, hipStream_t s);
+// probes[q][16] = rows of the 16 largest sampled MFMA scores, pcount[q] valid
+hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, uint32_t* probes,
+                              uint32_t* pcount, hipStream_t s);
+// thr[q] = (mk-th largest exact probe score) - qd[q] (mk <= 16); +inf for q >= B.
+// distance: pscores hold 1 - cos (the index metric's rerank output).
+hipError_t launch_flat_tau(const float* pscores, const uint32_t* pcount, uint32_t B, uint32_t mk, int distance,
+                           const float* qd, float* thr, hipStream_t s);
 // sort reranked candidates by (exact score, row), emit first k live rows,
 // OR 1 into *fail for a query whose list is not certified exact
 hipError_t launch_flat_final(const uint32_t* counts, const uint32_t* cand, uint32_t candcap, const float* scores,
-                             const float* thr, float eps, uint32_t B, uint32_t k, int descending, const uint64_t* ids,
-                             uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s);
+                             const float* thr, const float* qd, uint32_t B, uint32_t k, int descending,
+                             const uint64_t* ids, uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail,
+                             hipStream_t s);
 
 // ---- shard merge (shard.rs:776-784) --------------------------------------------
 hipError_t launch_topk_merge(const uint64_t* ids, const float* scores, const uint32_t* counts, uint32_t n_shards,

@@ -1299,22 +1299,25 @@ hipError_t launch_iota_rows(uint32_t* rows, uint32_t B, uint32_t R, hipStream_t 
 }
 
 // ============================================================================
-// K3: exact rerank.  A block of 512 threads owns 64 stage-1 candidates of one
-// query.  All 8 waves stream the candidates' rows through a double-buffered
-// LDS tile ([64 rows][256 dims], 16-B loads, one 1-KiB row segment per
-// wave-instruction; the next chunk's loads are in flight while the current
-// one is folded); wave 0 folds: lane r owns candidate r and accumulates
-// q_j*x_j (or (q_j-x_j)^2) left to right, and every lane also folds q_j*q_j
-// for the query norm -- the reference's exact sequential order, so cosine /
-// L2 are bit-identical to cosine_similarity_manual / VectorPoint::distance.
-// Row stride 260 floats: conflict-free ds_read_b128 (16-lane groups) and
-// ds_write_b128 (8-lane groups).
+// K3: exact rerank.  A work item = 64 consecutive candidates of one query; a
+// block of 512 threads takes items from a compact list (grid-stride over the
+// prefix sum of the per-query counts, so no block is launched for an empty
+// slot).  All 8 waves stream the item's rows through a double-buffered LDS
+// tile ([64 rows][128 dims], 16-B loads, one 512-B row segment per 32 lanes;
+// the next chunk's loads are in flight while the current one is folded); wave
+// 0 folds: lane r owns candidate r and accumulates q_j*x_j (or (q_j-x_j)^2)
+// left to right, and every lane also folds q_j*q_j for the query norm -- the
+// reference's exact sequential order, so cosine / L2 are bit-identical to
+// cosine_similarity_manual / VectorPoint::distance.  Row stride 132 floats:
+// conflict-free ds_read_b128 / ds_write_b128.  67 KiB of LDS: two blocks per
+// CU.
 // ============================================================================
 constexpr int kRrRows = 64;
-constexpr int kRrCh = 256;
+constexpr int kRrCh = 128;
 constexpr int kRrLd = kRrCh + 4;
 constexpr int kRrThreads = 512;
-constexpr int kRrPer = kRrRows * (kRrCh / 4) / kRrThreads;  // float4 per thread per chunk (8)
+constexpr int kRrPer = kRrRows * (kRrCh / 4) / kRrThreads;  // float4 per thread per chunk (4)
+constexpr uint32_t kRrMaxB = 1024;                            // queries per launch (prefix in LDS)
 
 __device__ __forceinline__ float4 load4_guarded(const float* __restrict__ src, uint64_t base, uint64_t j, uint64_t len,
                                                bool vec4) {
@@ -1328,113 +1331,164 @@ __device__ __forceinline__ float4 load4_guarded(const float* __restrict__ src, u
     return v;
 }
 
-__global__ __launch_bounds__(kRrThreads) void k_rerank(const float* __restrict__ rows, uint64_t clen,
-                                                       const float* __restrict__ norms, const float* __restrict__ q,
-                                                       uint64_t qlen, const uint32_t* __restrict__ s1_rows, uint32_t R,
-                                                       const uint32_t* __restrict__ counts, int kind,
-                                                       float* __restrict__ scores) {
+__global__ __launch_bounds__(kRrThreads, 2) void k_rerank(const float* __restrict__ rows, uint64_t clen,
+                                                          const float* __restrict__ norms, const float* __restrict__ q,
+                                                          uint64_t qlen, const uint32_t* __restrict__ s1_rows,
+                                                          uint32_t B, uint32_t R, const uint32_t* __restrict__ counts,
+                                                          int kind, float* __restrict__ scores) {
     __shared__ __attribute__((aligned(16))) float tiles[2][kRrRows * kRrLd];
     __shared__ __attribute__((aligned(16))) float qs[2][kRrCh];
     __shared__ uint64_t bases[kRrRows];
+    __shared__ uint32_t pre[kRrMaxB + 1];  // items before query i
     const uint32_t tid = threadIdx.x;
-    const uint32_t qi = blockIdx.y;
-    const uint32_t r0 = blockIdx.x * kRrRows;
-    const uint32_t Rq = counts ? min(counts[qi], R) : R;  // valid entries of this query's list
-    if (r0 >= Rq) return;
-    if (tid < kRrRows) {
-        const uint32_t r = r0 + tid;
-        bases[tid] = r < Rq ? (uint64_t)s1_rows[(uint64_t)qi * R + r] * clen : ~0ull;
-    }
-    __syncthreads();
-    const float* qv = q + (uint64_t)qi * qlen;
-    const uint64_t len = qlen < clen ? qlen : clen;  // zip() truncates
-    const bool vec4 = (clen & 3u) == 0;
-    const bool qvec4 = (qlen & 3u) == 0 && (((uintptr_t)qv) & 15u) == 0;
-    const uint32_t nch = (uint32_t)((len + kRrCh - 1) / kRrCh);
-    float4 rg[kRrPer];
-    float4 qg = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto load = [&](uint32_t c) {
-#pragma unroll
-        for (int it = 0; it < kRrPer; ++it) {
-            const uint32_t idx = it * kRrThreads + tid;
-            rg[it] = load4_guarded(rows, bases[idx >> 6], (uint64_t)c * kRrCh + 4u * (idx & 63u), len, vec4);
+    // exclusive prefix of per-query item counts (B <= kRrMaxB), block-wide
+    {
+        const uint32_t per = (B + kRrThreads - 1) / kRrThreads;
+        const uint32_t b0 = tid * per;
+        uint32_t loc = 0;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) {
+            const uint32_t c = counts ? min(counts[b0 + i], R) : R;
+            loc += (c + kRrRows - 1) / kRrRows;
         }
-        if (tid < kRrCh / 4) qg = load4_guarded(qv, 0, (uint64_t)c * kRrCh + 4u * tid, len, qvec4);
-    };
-    auto store = [&](uint32_t c) {
-        float* t = tiles[c & 1];
-#pragma unroll
-        for (int it = 0; it < kRrPer; ++it) {
-            const uint32_t idx = it * kRrThreads + tid;
-            *(float4*)(t + (idx >> 6) * kRrLd + 4u * (idx & 63u)) = rg[it];
+        // inclusive scan of the per-thread sums through LDS (Hillis-Steele)
+        __shared__ uint32_t part[kRrThreads];
+        part[tid] = loc;
+        __syncthreads();
+        for (uint32_t o = 1; o < kRrThreads; o <<= 1) {
+            const uint32_t v = tid >= o ? part[tid - o] : 0u;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
         }
-        if (tid < kRrCh / 4) *(float4*)(qs[c & 1] + 4u * tid) = qg;
-    };
-    float acc = -0.0f, qq = -0.0f;
-    if (nch) {
-        load(0);
-        store(0);
-    }
-    __syncthreads();
-    for (uint32_t c = 0; c < nch; ++c) {
-        if (c + 1 < nch) load(c + 1);
-        if (tid < 64) {
-            const float* tr = tiles[c & 1] + tid * kRrLd;
-            const float* qc = qs[c & 1];
-            const uint32_t m = (uint32_t)min((uint64_t)kRrCh, len - (uint64_t)c * kRrCh);
-            if (kind == kScoreL2) {
-                for (uint32_t j = 0; j < m; ++j) {
-                    const float d = qc[j] - tr[j];
-                    acc = acc + d * d;
-                }
-            } else if (m == kRrCh) {
-#pragma unroll 8
-                for (int j = 0; j < kRrCh; j += 4) {
-                    const float4 x = *(const float4*)(tr + j);
-                    const float4 w = *(const float4*)(qc + j);
-                    acc = acc + w.x * x.x;
-                    acc = acc + w.y * x.y;
-                    acc = acc + w.z * x.z;
-                    acc = acc + w.w * x.w;
-                    qq = qq + w.x * w.x;
-                    qq = qq + w.y * w.y;
-                    qq = qq + w.z * w.z;
-                    qq = qq + w.w * w.w;
-                }
-            } else {
-                for (uint32_t j = 0; j < m; ++j) {
-                    acc = acc + qc[j] * tr[j];
-                    qq = qq + qc[j] * qc[j];
-                }
-            }
+        uint32_t run = part[tid] - loc;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) {
+            pre[b0 + i] = run;
+            const uint32_t c = counts ? min(counts[b0 + i], R) : R;
+            run += (c + kRrRows - 1) / kRrRows;
         }
-        if (c + 1 < nch) store(c + 1);
+        if (tid == kRrThreads - 1) pre[B] = part[tid];
         __syncthreads();
     }
-    if (tid >= 64) return;
-    const uint32_t r = r0 + tid;
-    if (r >= Rq) return;
-    float score;
-    if (kind == kScoreL2) {
-        score = sqrtf(acc);
-    } else {
-        for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
-        const float na = sqrtf(qq);
-        const float nb = norms[s1_rows[(uint64_t)qi * R + r]];
-        if (kind == kScoreCosine) {
-            score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
-        } else {
-            score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+    const uint32_t items = pre[B];
+    const uint64_t len = qlen < clen ? qlen : clen;  // zip() truncates
+    const bool vec4 = (clen & 3u) == 0;
+    const uint32_t nch = (uint32_t)((len + kRrCh - 1) / kRrCh);
+    for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
+        // item -> (query qi, first candidate r0): last qi with pre[qi] <= item
+        uint32_t lo = 0, hi = B;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= item) lo = mid; else hi = mid;
         }
+        const uint32_t qi = lo;
+        const uint32_t r0 = (item - pre[qi]) * kRrRows;
+        const uint32_t Rq = counts ? min(counts[qi], R) : R;  // valid entries of this query's list
+        if (tid < kRrRows) {
+            const uint32_t r = r0 + tid;
+            bases[tid] = r < Rq ? (uint64_t)s1_rows[(uint64_t)qi * R + r] * clen : ~0ull;
+        }
+        __syncthreads();
+        const float* qv = q + (uint64_t)qi * qlen;
+        const bool qvec4 = (qlen & 3u) == 0 && (((uintptr_t)qv) & 15u) == 0;
+        float4 rg[kRrPer];
+        float4 qg = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto load = [&](uint32_t c) {
+#pragma unroll
+            for (int it = 0; it < kRrPer; ++it) {
+                const uint32_t idx = it * kRrThreads + tid;
+                rg[it] = load4_guarded(rows, bases[idx >> 5], (uint64_t)c * kRrCh + 4u * (idx & 31u), len, vec4);
+            }
+            if (tid < kRrCh / 4) qg = load4_guarded(qv, 0, (uint64_t)c * kRrCh + 4u * tid, len, qvec4);
+        };
+        auto store = [&](uint32_t c) {
+            float* t = tiles[c & 1];
+#pragma unroll
+            for (int it = 0; it < kRrPer; ++it) {
+                const uint32_t idx = it * kRrThreads + tid;
+                *(float4*)(t + (idx >> 5) * kRrLd + 4u * (idx & 31u)) = rg[it];
+            }
+            if (tid < kRrCh / 4) *(float4*)(qs[c & 1] + 4u * tid) = qg;
+        };
+        float acc = -0.0f, qq = -0.0f;
+        if (nch) {
+            load(0);
+            store(0);
+        }
+        __syncthreads();
+        for (uint32_t c = 0; c < nch; ++c) {
+            if (c + 1 < nch) load(c + 1);
+            if (tid < 64) {
+                const float* tr = tiles[c & 1] + tid * kRrLd;
+                const float* qc = qs[c & 1];
+                const uint32_t m = (uint32_t)min((uint64_t)kRrCh, len - (uint64_t)c * kRrCh);
+                if (kind == kScoreL2) {
+                    for (uint32_t j = 0; j < m; ++j) {
+                        const float d = qc[j] - tr[j];
+                        acc = acc + d * d;
+                    }
+                } else if (m == kRrCh) {
+#pragma unroll 8
+                    for (int j = 0; j < kRrCh; j += 4) {
+                        const float4 x = *(const float4*)(tr + j);
+                        const float4 w = *(const float4*)(qc + j);
+                        acc = acc + w.x * x.x;
+                        acc = acc + w.y * x.y;
+                        acc = acc + w.z * x.z;
+                        acc = acc + w.w * x.w;
+                        qq = qq + w.x * w.x;
+                        qq = qq + w.y * w.y;
+                        qq = qq + w.z * w.z;
+                        qq = qq + w.w * w.w;
+                    }
+                } else {
+                    for (uint32_t j = 0; j < m; ++j) {
+                        acc = acc + qc[j] * tr[j];
+                        qq = qq + qc[j] * qc[j];
+                    }
+                }
+            }
+            if (c + 1 < nch) store(c + 1);
+            __syncthreads();
+        }
+        if (tid < 64) {
+            const uint32_t r = r0 + tid;
+            if (r < Rq) {
+                float score;
+                if (kind == kScoreL2) {
+                    score = sqrtf(acc);
+                } else {
+                    for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+                    const float na = sqrtf(qq);
+                    const float nb = norms[s1_rows[(uint64_t)qi * R + r]];
+                    if (kind == kScoreCosine) {
+                        score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+                    } else {
+                        score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+                    }
+                }
+                scores[(uint64_t)qi * R + r] = score;
+            }
+        }
+        __syncthreads();  // bases / tiles are rewritten by the next item
     }
-    scores[(uint64_t)qi * R + r] = score;
 }
 
 hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
     if (a.B == 0 || a.R == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rerank, dim3((a.R + kRrRows - 1) / kRrRows, a.B), dim3(kRrThreads), 0, s, a.rows, a.clen,
-                       a.norms, a.q, a.qlen, a.s1_rows, a.R, a.counts, a.kind, a.scores);
-    GVDB_LAUNCH_CHECK();
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    for (uint32_t b0 = 0; b0 < a.B; b0 += kRrMaxB) {
+        const uint32_t nb = std::min<uint32_t>(kRrMaxB, a.B - b0);
+        // upper bound of the work items (counts are on the device): every item
+        // slot up to 2 resident blocks per CU, the loop takes the rest
+        const uint64_t max_items = (uint64_t)nb * ((a.R + kRrRows - 1) / kRrRows);
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(max_items, 2ull * cus);
+        hipLaunchKernelGGL(k_rerank, dim3(grid), dim3(kRrThreads), 0, s, a.rows, a.clen, a.norms,
+                           a.q + (uint64_t)b0 * a.qlen, a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
+                           a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R);
+        GVDB_LAUNCH_CHECK();
+    }
     return hipSuccess;
 }
 

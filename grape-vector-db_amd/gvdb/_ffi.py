@@ -75,6 +75,7 @@ SIGNATURES = {
     "gvdb_timing_reset": (None, []),
     "gvdb_timing_read": (C.c_int, [u32, C.POINTER(C.c_double), PU64]),
     "gvdb_flat_fallback_count": (C.c_uint64, []),
+    "gvdb_flat_i8_fallback_count": (C.c_uint64, []),
     "gvdb_index_create": (C.c_int, [C.POINTER(gvdb_params), C.POINTER(P)]),
     "gvdb_index_destroy": (None, [P]),
     "gvdb_index_add": (C.c_int, [P, P, u64, u32, P]),

@@ -108,14 +108,17 @@ int32_t gvdb_device_count(void);
  * they run on (read after each batch's own stream sync).  Slots:
  * 0 = stage-1 sample histogram + threshold, 1 = k_scan (the BQ Hamming hot
  * loop), 2 = stage-1 select, 3 = stage 2 (rerank + final sort), 5 = flat
- * search bf16-MFMA candidate pass (k_flat_mx), 6 = whole flat MFMA search per
- * 256-query group. */
+ * search bf16-MFMA candidate pass (k_flat_mx), 6 = whole bf16 flat MFMA search
+ * per 256-query group, 7 / 8 = the same for the i8-MFMA tier. */
 void gvdb_timing_enable(int32_t on);
 void gvdb_timing_reset(void);
 gvdb_status gvdb_timing_read(uint32_t which, double* total_ms, uint64_t* launches);
 /* Diagnostics: flat searches (GVDB_SEARCH_FLAT) whose bf16-MFMA candidate pass
- * could not be certified exact and were answered by the exact full scan. */
+ * could not be certified exact and were answered by the exact full scan, and
+ * those whose i8-MFMA candidate pass (the first tier) could not be certified
+ * and were retried on bf16. */
 uint64_t gvdb_flat_fallback_count(void);
+uint64_t gvdb_flat_i8_fallback_count(void);
 
 /* ---- VectorIndex (index.rs:35-62) --------------------------------------- */
 /* HnswVectorIndex::new / with_config (index.rs:100-117) */

@@ -241,12 +241,17 @@ def test_index_flat_mode_matches_oracle(g, oracle_mod):
         assert list(ids[b, :n[b]]) == list(ri) and same_f32(sc[b, :n[b]], rs)
 
 
+@pytest.mark.parametrize("kind", ["i8", "bf16"])
 @pytest.mark.parametrize("N,D,B,k,metric", [(200_000, 768, 48, 10, 0), (150_000, 100, 300, 25, 0),
-                                             (100_000, 200, 17, 100, 2), (70_000, 64, 1, 1, 0)])
-def test_flat_mfma_certified_matches_oracle(g, oracle_mod, N, D, B, k, metric):
-    """K4 on bf16 MFMA (gvdb_flat.hip): candidates from the MFMA pass, exact
-    rerank, certificate.  Ids equal and scores bit-identical to the oracle's
-    storage.rs / index.rs flat search, with NO exact-rescan fallback taken."""
+                                             (100_000, 200, 17, 100, 2), (70_000, 64, 1, 1, 0),
+                                             (66_000, 1100, 9, 10, 0)])
+def test_flat_mfma_certified_matches_oracle(g, oracle_mod, monkeypatch, kind, N, D, B, k, metric):
+    """K4 on i8 / bf16 MFMA (gvdb_flat.hip): candidates from the MFMA pass,
+    exact rerank, certificate.  Ids equal and scores bit-identical to the
+    oracle's storage.rs / index.rs flat search, with NO fallback taken (i8:
+    neither the bf16 retry nor the exact rescan).  D=1100 covers the i8
+    quantiser's second 1024-element pass and a ragged last chunk."""
+    monkeypatch.setenv("GVDB_FLAT", kind)
     x = rng_rows(N + D, N, D, dup=40)
     x[5] = 0.0  # zero-norm row scores 0 (cosine) / +inf (distance)
     Q = rng_rows(D + 11, B, D)
@@ -256,8 +261,10 @@ def test_flat_mfma_certified_matches_oracle(g, oracle_mod, N, D, B, k, metric):
     ix = g.GpuVectorIndex(dimension=D)
     ix.add_batch(np.arange(N, dtype=np.uint64), x)
     before = g.lib().gvdb_flat_fallback_count()
+    before_i8 = g.lib().gvdb_flat_i8_fallback_count()
     ids, sc, n = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=metric))
     assert g.lib().gvdb_flat_fallback_count() == before, "MFMA candidate pass was not certified"
+    assert g.lib().gvdb_flat_i8_fallback_count() == before_i8, "i8 candidate pass was not certified"
     for b in range(B):
         if metric == 0:
             ri, rs = oracle_mod.storage_vector_search(Q[b], x, k)
@@ -266,6 +273,56 @@ def test_flat_mfma_certified_matches_oracle(g, oracle_mod, N, D, B, k, metric):
         assert n[b] == len(ri)
         assert list(ids[b, : n[b]]) == list(ri), b
         assert same_f32(sc[b, : n[b]], rs)
+
+
+def test_flat_i8_margin_too_wide_retries_on_bf16(g, oracle_mod, monkeypatch):
+    """6000 rows at cosine 0.900..0.910 to the query e_0: with the i8 margin (the
+    rows' ~1.6 % quantisation error) every one of them is a candidate, over the
+    4096-candidate capacity; bf16's 2^-8 margin nominates ~40 % of them: the
+    batch is retried on bf16, certified there, and the result is still exactly
+    the oracle's."""
+    N, D, k = 70_000, 64, 10
+    r = np.random.default_rng(77)
+    x = r.standard_normal((N, D)).astype(np.float32) * np.float32(0.05)
+    x[:, 0] = 0.0
+    special = r.choice(N, 6000, replace=False)
+    c = np.linspace(0.90, 0.91, 6000, dtype=np.float64)
+    u = r.standard_normal((6000, D))
+    u[:, 0] = 0.0
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    x[special] = (c[:, None] * np.eye(D)[0] + np.sqrt(1 - c[:, None] ** 2) * u).astype(np.float32)
+    Q = np.zeros((1, D), np.float32)
+    Q[0, 0] = 1.0
+    monkeypatch.setenv("GVDB_FLAT", "i8")
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    before = g.lib().gvdb_flat_fallback_count()
+    before_i8 = g.lib().gvdb_flat_i8_fallback_count()
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=0))
+    assert g.lib().gvdb_flat_i8_fallback_count() == before_i8 + 1
+    assert g.lib().gvdb_flat_fallback_count() == before
+    ri, rs = oracle_mod.storage_vector_search(Q[0], x, k)
+    assert list(ids[0, : n[0]]) == list(ri) and same_f32(sc[0, : n[0]], rs)
+
+
+def test_flat_nonfinite_row_takes_exact_scan(g, oracle_mod):
+    """An +inf element makes a row's cosine NaN in the reference fold; the MFMA
+    tiers refuse such a shard and the exact scan reproduces the reference."""
+    N, D = 70_000, 64
+    x = rng_rows(41, N, D)
+    x[777, 3] = np.inf
+    Q = rng_rows(42, 2, D)
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    before = g.lib().gvdb_flat_fallback_count()
+    try:
+        ids, sc, n = ix.search_batch(Q, 10, g.SearchParams(mode=1, metric=2))
+    except g.QuantizationError:
+        return  # the NaN score is reported as the reference's sort would panic
+    assert g.lib().gvdb_flat_fallback_count() == before + 1
+    for b in range(2):
+        ri, rs = oracle_mod.flat_cosine_distance_search(Q[b], x, 10)
+        assert list(ids[b, : n[b]]) == list(ri) and same_f32(sc[b, : n[b]], rs)
 
 
 def test_flat_mfma_uncertifiable_falls_back_exactly(g, oracle_mod):
