@@ -1490,3 +1490,6 @@ uint64_t gvdb_flat_i8_fallback_count(void) { return flat_fallbacks_i8().load(); 
 
 }  // extern "C"
 
+
+// Shared error reporting for the other translation units (gvdb_sparse.hip).
+gvdb_status gvdb::report_status(gvdb_status s, const std::string& msg) { return fail(s, msg); }

@@ -12,6 +12,8 @@
 //   norms : float [cap]               sqrt(sequential sum x*x) per row
 //   ids   : uint64 [cap]              caller ids; GVDB_ORPHAN = shadowed row
 #pragma once
+#include "../../include/gvdb.h"
+#include <string>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -230,5 +232,9 @@ hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, con
 hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, uint4* ncodes, const float* norms,
                          float* nnorms, const uint64_t* ids, uint64_t* nids, const uint64_t* map, uint64_t m,
                          uint64_t cap, uint32_t D, hipStream_t s);
+
+// ---- error reporting shared by the C-ABI translation units ---------------------
+// sets the thread-local gvdb_last_error() text and returns s
+gvdb_status report_status(gvdb_status s, const std::string& msg);
 
 }  // namespace gvdb

@@ -60,6 +60,20 @@ class gvdb_index_stats(C.Structure):
     ]
 
 
+class gvdb_bm25_params(C.Structure):
+    _fields_ = [("k1", C.c_float), ("b", C.c_float), ("device", C.c_int32), ("reserved", C.c_uint32)]
+
+
+class gvdb_bm25_stats(C.Structure):
+    _fields_ = [
+        ("total_documents", C.c_uint64),
+        ("average_document_length", C.c_float),
+        ("reserved", C.c_uint32),
+        ("vocabulary_size", C.c_uint64),
+        ("total_entries", C.c_uint64),
+    ]
+
+
 P = C.c_void_p
 u32, u64, i32, f32 = C.c_uint32, C.c_uint64, C.c_int32, C.c_float
 PU64, PU32, PF32 = C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_float)
@@ -101,6 +115,16 @@ SIGNATURES = {
     "gvdb_topk_merge_device": (C.c_int, [P, P, P, u64, u64, u64, u64, i32, P, P, P, P]),
     "gvdb_bq_shard_merge": (C.c_int, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P]),
     "gvdb_bq_shard_merge_device": (C.c_int, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P, P]),
+    "gvdb_sparse_create": (C.c_int, [C.POINTER(gvdb_bm25_params), C.POINTER(P)]),
+    "gvdb_sparse_destroy": (None, [P]),
+    "gvdb_sparse_add_document": (C.c_int, [P, u64, P, P, u64, f32]),
+    "gvdb_sparse_add_documents": (C.c_int, [P, P, P, P, P, P, u64]),
+    "gvdb_sparse_remove_document": (C.c_int, [P, u64, C.POINTER(i32)]),
+    "gvdb_sparse_get_stats": (C.c_int, [P, C.POINTER(gvdb_bm25_stats)]),
+    "gvdb_sparse_clear": (None, [P]),
+    "gvdb_sparse_search_bm25": (C.c_int, [P, P, P, P, u64, u64, P, P, P]),
+    "gvdb_rrf_fuse": (C.c_int, [P, P, P, u32, P, P, P, u32, P, P, P, u32, u64, f32, u64, P, P, P, P]),
+    "gvdb_rrf_fuse_device": (C.c_int, [P, P, P, u32, P, P, P, u32, P, P, P, u32, u64, f32, u64, P, P, P, P, P]),
 }
 
 _lib = None

@@ -226,6 +226,73 @@ gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d
                                        uint64_t R, uint64_t k, uint64_t* d_out_ids, float* d_out_scores,
                                        uint32_t* d_out_n, void* stream);
 
+/* ---- BM25 sparse index (src/sparse.rs:29-222) ---------------------------- */
+/* SparseIndex: an HBM forward index over document slots; documents are
+ * (term id, term frequency) lists with a document_length, exactly what
+ * DocumentSparseRepresentation carries (types.rs:93-102). */
+typedef struct gvdb_bm25_params {  /* BM25Parameters, sparse.rs:42-53 */
+    float k1;                       /* default 1.2 */
+    float b;                        /* default 0.75 */
+    int32_t device;                 /* HIP device ordinal */
+    uint32_t reserved;
+} gvdb_bm25_params;
+
+typedef struct gvdb_bm25_stats {   /* BM25Stats, types.rs:104-115 */
+    uint64_t total_documents;
+    float average_document_length;  /* sum of EVERY posting entry's length / N (sparse.rs:96-104) */
+    uint32_t reserved;
+    uint64_t vocabulary_size;       /* terms with a document frequency */
+    uint64_t total_entries;         /* posting entries held */
+} gvdb_bm25_stats;
+
+typedef struct gvdb_sparse gvdb_sparse;
+
+/* SparseIndex::new (sparse.rs:57-69); params NULL = defaults */
+gvdb_status gvdb_sparse_create(const gvdb_bm25_params* params, gvdb_sparse** out);
+void gvdb_sparse_destroy(gvdb_sparse* index);
+/* add_document (sparse.rs:71-107): n distinct terms with their tf; a second
+ * add of the same id adds a second entry per term (as the reference's
+ * posting lists do).  Duplicate terms in one call: GVDB_ERR_INVALID_ARGUMENT. */
+gvdb_status gvdb_sparse_add_document(gvdb_sparse* index, uint64_t doc_id, const uint32_t* terms, const float* tfs,
+                                     uint64_t n, float document_length);
+/* Bulk add: document d's terms are terms[doc_ptr[d] .. doc_ptr[d+1]). */
+gvdb_status gvdb_sparse_add_documents(gvdb_sparse* index, const uint64_t* doc_ids, const uint64_t* doc_ptr,
+                                      const uint32_t* terms, const float* tfs, const float* document_lengths,
+                                      uint64_t n_docs);
+/* remove_document (sparse.rs:109-149): *removed = 1 if any entry went. */
+gvdb_status gvdb_sparse_remove_document(gvdb_sparse* index, uint64_t doc_id, int32_t* removed);
+gvdb_status gvdb_sparse_get_stats(const gvdb_sparse* index, gvdb_bm25_stats* out);
+void gvdb_sparse_clear(gvdb_sparse* index);
+/* search_bm25 (sparse.rs:151-198) for B queries given as CSR: query q's
+ * SparseVector indices / values are q_terms / q_values[q_ptr[q] ..
+ * q_ptr[q+1]).  Per query up to `limit` (id, score) pairs, score descending,
+ * out_ids[q*limit + i], count out_n[q].  Equal scores: ascending document slot
+ * (first add); the reference leaves them in HashMap order. */
+gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* index, const uint64_t* q_ptr, const uint32_t* q_terms,
+                                    const float* q_values, uint64_t B, uint64_t limit, uint64_t* out_ids,
+                                    float* out_scores, uint32_t* out_n);
+
+/* ---- reciprocal-rank fusion (HybridSearchEngine::rrf_fusion, hybrid.rs:422-488) */
+/* Per query three ranked id lists (dense, sparse, text; NULL counts = empty
+ * list), list l of query q at ids_l[q*stride_l + r], r < n_l[q], with its raw
+ * score.  Fused score = sum of 1/(k + rank+1) (a repeated dense id replaces,
+ * sparse / text repeats add), descending, ties by first appearance; the first
+ * `limit` per query go to out_ids / out_scores [q*limit + i] and, when
+ * out_breakdown is non-NULL, the raw dense / sparse / text score of each
+ * result to out_breakdown[(q*limit + i)*3 + l] (NaN = absent, ScoreBreakdown).
+ * At most 1024 items per query.  The _device form takes device pointers. */
+gvdb_status gvdb_rrf_fuse(const uint64_t* dense_ids, const float* dense_scores, const uint32_t* dense_n,
+                          uint32_t dense_stride, const uint64_t* sparse_ids, const float* sparse_scores,
+                          const uint32_t* sparse_n, uint32_t sparse_stride, const uint64_t* text_ids,
+                          const float* text_scores, const uint32_t* text_n, uint32_t text_stride, uint64_t B, float k,
+                          uint64_t limit, uint64_t* out_ids, float* out_scores, float* out_breakdown, uint32_t* out_n);
+gvdb_status gvdb_rrf_fuse_device(const uint64_t* d_dense_ids, const float* d_dense_scores, const uint32_t* d_dense_n,
+                                 uint32_t dense_stride, const uint64_t* d_sparse_ids, const float* d_sparse_scores,
+                                 const uint32_t* d_sparse_n, uint32_t sparse_stride, const uint64_t* d_text_ids,
+                                 const float* d_text_scores, const uint32_t* d_text_n, uint32_t text_stride, uint64_t B,
+                                 float k, uint64_t limit, uint64_t* d_out_ids, float* d_out_scores,
+                                 float* d_out_breakdown, uint32_t* d_out_n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,13 @@ _SIG = {
     "orc_bq_shard_merge": (None, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P]),
     "orc_multi_stage_search_batch_r": (None, [P, u32, P, u64, P, P, u64, u64, C.c_int, P, P, C.c_int]),
     "hnsw_build": (C.c_void_p, [P, u64, u32, u32, u32, u64, C.c_int]),
+    "bm25o_create": (C.c_void_p, [f32, f32]),
+    "bm25o_free": (None, [C.c_void_p]),
+    "bm25o_add": (None, [C.c_void_p, u64, P, P, u64, f32]),
+    "bm25o_remove": (C.c_int, [C.c_void_p, u64]),
+    "bm25o_stats": (None, [C.c_void_p, P, P, P]),
+    "bm25o_search": (u64, [C.c_void_p, P, P, u64, u64, P, P]),
+    "bm25o_rrf": (u64, [P, P, u64, P, P, u64, P, P, u64, f32, P, P, P, P, P]),
     "hnsw_free": (None, [C.c_void_p]),
     "hnsw_search": (C.c_int, [C.c_void_p, P, u64, u32, u32, C.c_int, P, P, P]),
 }
@@ -282,3 +289,55 @@ class Hnsw:
         if getattr(self, "h", None):
             lib().hnsw_free(self.h)
             self.h = None
+
+
+class Bm25:
+    """SparseIndex restatement (oracle/bm25_oracle.cpp; sparse.rs:71-222): the
+    checker for the GPU BM25 path.  Ties by document slot, avgdl folded in slot
+    order (the reference leaves both to HashMap order)."""
+
+    def __init__(self, k1=1.2, b=0.75):
+        self.h = lib().bm25o_create(float(k1), float(b))
+
+    def add_document(self, doc_id, terms, tfs, doc_length):
+        t = np.ascontiguousarray(np.asarray(terms, dtype=np.uint32))
+        v = _f32(tfs)
+        lib().bm25o_add(self.h, int(doc_id), _p(t), _p(v), t.size, float(np.float32(doc_length)))
+
+    def remove_document(self, doc_id) -> bool:
+        return bool(lib().bm25o_remove(self.h, int(doc_id)))
+
+    def stats(self):
+        n, v = np.zeros(1, np.uint64), np.zeros(1, np.uint64)
+        a = np.zeros(1, np.float32)
+        lib().bm25o_stats(self.h, _p(n), _p(a), _p(v))
+        return int(n[0]), a[0], int(v[0])
+
+    def search(self, terms, values, limit):
+        t = np.ascontiguousarray(np.asarray(terms, dtype=np.uint32))
+        v = _f32(values)
+        ids = np.zeros(max(limit, 1), np.uint64)
+        sc = np.zeros(max(limit, 1), np.float32)
+        n = lib().bm25o_search(self.h, _p(t), _p(v), t.size, limit, _p(ids), _p(sc))
+        return ids[:n], sc[:n]
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().bm25o_free(self.h)
+            self.h = None
+
+
+def rrf_fusion(dense, sparse, text, k=60.0):
+    """hybrid.rs:422-488 restated: lists of (id, raw score) -> [(id, rrf score,
+    dense, sparse, text)] sorted by score desc (ties: first appearance)."""
+    def arr(lst):
+        ids = np.ascontiguousarray(np.array([int(i) for i, _ in lst], dtype=np.uint64))
+        sc = _f32([s for _, s in lst]) if lst else np.zeros(0, np.float32)
+        return ids, sc
+    (di, ds), (si, ss), (ti, ts) = arr(dense), arr(sparse), arr(text)
+    n = len(dense) + len(sparse) + len(text)
+    oi = np.zeros(max(n, 1), np.uint64)
+    os_, od, osp, ot = (np.zeros(max(n, 1), np.float32) for _ in range(4))
+    m = lib().bm25o_rrf(_p(di), _p(ds), di.size, _p(si), _p(ss), si.size, _p(ti), _p(ts), ti.size, float(k),
+                        _p(oi), _p(os_), _p(od), _p(osp), _p(ot))
+    return [(int(oi[i]), os_[i], od[i], osp[i], ot[i]) for i in range(m)]
