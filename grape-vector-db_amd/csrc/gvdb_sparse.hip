@@ -51,9 +51,10 @@ using namespace gvdb;
 namespace {
 
 constexpr uint32_t kSpTile = 64;        // documents per tile (one per lane of a wave)
-constexpr uint32_t kSpThreads = 256;    // 4 query groups x 64 documents
-constexpr uint32_t kSpEnt = 8192;       // staged term entries per tile (else read from HBM)
-constexpr uint32_t kSpQT = 4096;        // query terms per launch group (LDS)
+constexpr uint32_t kSpThreads = 512;    // 8 query groups x 64 documents: 16 waves per CU at 2 blocks (the loop is latency-bound)
+constexpr uint32_t kSpEnt = 4096;       // staged term entries per tile (else read from HBM)
+constexpr uint32_t kSpQT = 1024;        // query terms per launch group (LDS)
+constexpr uint32_t kSpU = 512;          // distinct terms per launch group (LDS match map)
 constexpr uint32_t kSpMaxB = 256;       // queries per launch group
 constexpr uint32_t kSpCand = 4096;      // candidates per query (LDS sort)
 constexpr uint32_t kSpTopLocal = 8;     // per-thread keys kept by the tau pass
@@ -77,8 +78,10 @@ struct SpArgs {
     const float* tf;
     const float* dl;
     uint32_t N;            // slots
-    const uint32_t* qp;    // [B+1] offsets into qt/qv/qidf
-    const uint32_t* qt;
+    const uint32_t* qp;    // [B+1] offsets into qb/qv/qidf
+    const uint16_t* qb;    // index of each query term in ut
+    const uint32_t* ut;    // the group's distinct live terms, ascending
+    uint32_t nu;
     const float* qv;
     const float* qidf;
     uint32_t B;
@@ -95,20 +98,30 @@ struct SpArgs {
 
 // MODE 0: sample (every `every`-th tile -> smp), 1: emit (key >= tau ->
 // cand), 2: dense keys of one query.
+// Per 64-document tile: the documents' term lists are staged in LDS, then a
+// (document x batch-term) match map is built -- each entry looks its term up
+// once among the batch's distinct terms `ut` (sorted, <= kSpU) and records its
+// position (first entry of a run; 255 = "search", for documents past 254
+// entries).  Scoring a (document, query) pair is then one LDS byte per query
+// term instead of a binary search.
 template <int MODE>
-__global__ __launch_bounds__(kSpThreads) void k_bm25(SpArgs a) {
+__global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
     __shared__ uint32_t s_qp[kSpMaxB + 1];
-    __shared__ uint32_t s_qt[kSpQT];
+    __shared__ uint16_t s_qb[kSpQT];
     __shared__ float s_qv[kSpQT], s_qidf[kSpQT];
+    __shared__ uint32_t s_ut[kSpU];
     __shared__ uint32_t s_ent[kSpEnt];
+    __shared__ float s_tfc[kSpEnt];  // tf_component of each staged entry (query-independent)
     __shared__ uint32_t s_dp[kSpTile + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_map[kSpTile * kSpU];
     const uint32_t tid = threadIdx.x, doc = tid & (kSpTile - 1), qg = tid / kSpTile;
-    const uint32_t B = a.B;
+    const uint32_t B = a.B, nu = a.nu;
     for (uint32_t i = tid; i <= B; i += kSpThreads) s_qp[i] = a.qp[i];
+    for (uint32_t i = tid; i < nu; i += kSpThreads) s_ut[i] = a.ut[i];
     __syncthreads();
     const uint32_t nqt = s_qp[B];
     for (uint32_t i = tid; i < nqt; i += kSpThreads) {
-        s_qt[i] = a.qt[i];
+        s_qb[i] = a.qb[i];
         s_qv[i] = a.qv[i];
         s_qidf[i] = a.qidf[i];
     }
@@ -117,46 +130,107 @@ __global__ __launch_bounds__(kSpThreads) void k_bm25(SpArgs a) {
     const uint32_t ntiles_all = (a.N + kSpTile - 1) / kSpTile;
     const uint32_t every = MODE == 0 ? a.every : 1u;
     const uint32_t ntiles = (ntiles_all + every - 1) / every;
+    const uint32_t map_words = (kSpTile * nu + 3) / 4;
     for (uint32_t j = blockIdx.x; j < ntiles; j += gridDim.x) {
         const uint32_t d0 = j * every * kSpTile;
         const uint32_t nd = min(kSpTile, a.N - d0);
         __syncthreads();  // previous tile's LDS readers are done
         if (tid <= nd) s_dp[tid] = (uint32_t)(a.ptr[d0 + tid] - a.ptr[d0]);
+        for (uint32_t i = tid; i < map_words; i += kSpThreads) ((uint32_t*)s_map)[i] = 0u;
         __syncthreads();
         const uint64_t base = a.ptr[d0];
         const uint32_t E = s_dp[nd];
         const bool staged = E <= kSpEnt;
-        if (staged)
-            for (uint32_t i = tid; i < E; i += kSpThreads) s_ent[i] = a.term[base + i];
+        // calculate_bm25_score's tf_component (sparse.rs:215-218) depends on the
+        // entry only: evaluated once per staged entry
+        auto tfc_of = [&](uint64_t g) {
+            const float tfv = a.tf[g], dlv = a.dl[g];
+            return (tfv * k1p1) / (tfv + k1 * (omb + b * (dlv / avgdl)));
+        };
+        if (staged) {
+            // all loads first (up to kSpEnt / kSpThreads per thread in flight),
+            // then the arithmetic: a load-compute-store loop would serialise
+            // one HBM latency per entry
+            constexpr uint32_t kPer = kSpEnt / kSpThreads;
+            uint32_t tv[kPer];
+            float fv[kPer], dv[kPer];
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint32_t i = tid + k * kSpThreads;
+                if (i < E) {
+                    tv[k] = a.term[base + i];
+                    fv[k] = a.tf[base + i];
+                    dv[k] = a.dl[base + i];
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint32_t i = tid + k * kSpThreads;
+                if (i < E) {
+                    s_ent[i] = tv[k];
+                    s_tfc[i] = (fv[k] * k1p1) / (fv[k] + k1 * (omb + b * (dv[k] / avgdl)));
+                }
+            }
+        }
         __syncthreads();
-        const uint32_t* ent = staged ? s_ent : a.term + base;  // generic pointer: LDS or HBM
+        auto term_at = [&](uint32_t e) { return staged ? s_ent[e] : a.term[base + e]; };
         const bool live = doc < nd;
         const uint32_t lo0 = live ? s_dp[doc] : 0u, hi0 = live ? s_dp[doc + 1] : 0u;
+        // match map: 4 threads per document walk its entries
+        for (uint32_t e = lo0 + qg; e < hi0; e += kSpThreads / kSpTile) {
+            const uint32_t t = term_at(e);
+            if (e > lo0 && term_at(e - 1) == t) continue;  // not the first of a run (re-added id)
+            uint32_t lo = 0, hi = nu;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_ut[mid] < t) lo = mid + 1; else hi = mid;
+            }
+            if (lo < nu && s_ut[lo] == t) s_map[lo * kSpTile + doc] = (uint8_t)min(e - lo0 + 1u, 255u);
+        }
+        __syncthreads();
         const uint32_t slot = d0 + doc;
         const uint32_t qbeg = MODE == 2 ? a.dense_q : qg, qstep = MODE == 2 ? B + 1 : kSpThreads / kSpTile;
         for (uint32_t q = qbeg; q < B; q += qstep) {
             if (MODE == 2 && qg != 0) break;
             float acc = 0.0f;
             bool hit = false;
-            for (uint32_t p = s_qp[q]; p < s_qp[q + 1]; ++p) {
-                const uint32_t t = s_qt[p];
-                uint32_t lo = lo0, hi = hi0;  // lower_bound(t) in [lo0, hi0)
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (ent[mid] < t) lo = mid + 1; else hi = mid;
+            const uint32_t p0 = s_qp[q], p1 = s_qp[q + 1];
+            for (uint32_t pc = p0; pc < p1; pc += 8) {
+                // 8 map lookups in flight, then the contributions in query-term order
+                uint32_t vv[8];
+#pragma unroll
+                for (uint32_t i = 0; i < 8; ++i) {
+                    const bool in = pc + i < p1;
+                    const uint32_t ub = in ? s_qb[pc + i] : 0u;
+                    vv[i] = in && live ? ((uint32_t)s_map[ub * kSpTile + doc] | (ub << 8)) : 0u;
                 }
-                for (uint32_t e = lo; e < hi0 && ent[e] == t; ++e) {
-                    const float tfv = a.tf[base + e], dlv = a.dl[base + e];
-                    // calculate_bm25_score (sparse.rs:206-222), query_tf * tf_component * idf
-                    const float tfc = (tfv * k1p1) / (tfv + k1 * (omb + b * (dlv / avgdl)));
-                    const float s = s_qv[p] * tfc * s_qidf[p];
-                    acc = hit ? acc + s : 0.0f + s;  // or_insert(0.0) += s
-                    hit = true;
+#pragma unroll
+                for (uint32_t i = 0; i < 8; ++i) {
+                    const uint32_t v = vv[i] & 255u;
+                    if (v == 0) continue;
+                    const uint32_t p = pc + i;
+                    const uint32_t t = s_ut[vv[i] >> 8];
+                    uint32_t e = lo0 + v - 1;
+                    if (v == 255) {  // long document: lower_bound(t)
+                        uint32_t lo = lo0, hi = hi0;
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (term_at(mid) < t) lo = mid + 1; else hi = mid;
+                        }
+                        e = lo;
+                    }
+                    for (; e < hi0 && term_at(e) == t; ++e) {
+                        const float tfc = staged ? s_tfc[e] : tfc_of(base + e);
+                        // calculate_bm25_score (sparse.rs:206-222): query_tf * tf_component * idf
+                        const float sc = s_qv[p] * tfc * s_qidf[p];
+                        acc = hit ? acc + sc : 0.0f + sc;  // or_insert(0.0) += s
+                        hit = true;
+                    }
                 }
             }
             const uint64_t key = hit && live ? sp_key(acc, slot) : 0ull;
             if (MODE == 0) {
-                if (live || doc < kSpTile) a.smp[(uint64_t)q * a.S + (uint64_t)j * kSpTile + doc] = key;
+                a.smp[(uint64_t)q * a.S + (uint64_t)j * kSpTile + doc] = key;
             } else if (MODE == 1) {
                 if (key != 0 && key >= a.tau[q]) {
                     const uint32_t pos = atomicAdd(&a.counts[q], 1u);
@@ -365,6 +439,7 @@ struct gvdb_sparse {
     void* scratch = nullptr;
     size_t scratch_n = 0;
     uint32_t* h_fail = nullptr;
+    uint64_t dense_fallbacks = 0;
 
     // avgdl's fold order: storage order = slot order, each slot's entries by
     // (term, add order); a new slot appends, so adds of new ids fold
@@ -535,6 +610,66 @@ gvdb_status gvdb_sparse_add_documents(gvdb_sparse* sp, const uint64_t* doc_ids, 
                                       uint64_t n_docs) {
     if (!sp || (n_docs && (!doc_ids || !doc_ptr || !doc_lengths)))
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    {
+        // fast path: every id new and distinct -> append whole documents to the
+        // CSR in one pass (same state as n_docs single adds)
+        std::lock_guard<std::mutex> g(sp->mu);
+        bool fresh = true;
+        std::unordered_map<uint64_t, uint32_t> batch;
+        batch.reserve(n_docs);
+        for (uint64_t d = 0; d < n_docs && fresh; ++d)
+            fresh = sp->slot_of.find(doc_ids[d]) == sp->slot_of.end() && batch.emplace(doc_ids[d], 0).second;
+        if (fresh) {
+            const uint64_t E0 = sp->term.size();
+            const uint64_t add = doc_ptr[n_docs] - doc_ptr[0];
+            sp->term.reserve(E0 + add);
+            sp->tf.reserve(E0 + add);
+            sp->dl.reserve(E0 + add);
+            sp->ptr.reserve(sp->ptr.size() + n_docs);
+            sp->slot_id.reserve(sp->slot_id.size() + n_docs);
+            std::vector<std::pair<uint32_t, float>> e;
+            for (uint64_t d = 0; d < n_docs; ++d) {
+                const uint64_t a = doc_ptr[d], b = doc_ptr[d + 1];
+                e.resize(b - a);
+                bool sorted = true;
+                for (uint64_t i = a; i < b; ++i) {
+                    e[i - a] = {terms[i], tfs[i]};
+                    if (i > a && terms[i] <= terms[i - 1]) sorted = false;
+                }
+                if (!sorted) {
+                    std::stable_sort(e.begin(), e.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+                    for (size_t i = 1; i < e.size(); ++i)
+                        if (e[i].first == e[i - 1].first) {
+                            // roll back this batch: nothing of it was committed to the maps yet
+                            sp->term.resize(E0);
+                            sp->tf.resize(E0);
+                            sp->dl.resize(E0);
+                            sp->ptr.resize(sp->slot_id.size() + 1);
+                            return report_status(GVDB_ERR_INVALID_ARGUMENT,
+                                                 "duplicate term in one document (term_frequencies is a map)");
+                        }
+                }
+                for (const auto& x : e) {
+                    sp->term.push_back(x.first);
+                    sp->tf.push_back(x.second);
+                    sp->dl.push_back(doc_lengths[d]);
+                }
+                sp->ptr.push_back(sp->term.size());
+            }
+            for (uint64_t d = 0; d < n_docs; ++d) {
+                sp->slot_of[doc_ids[d]] = (uint32_t)sp->slot_id.size();
+                sp->slot_id.push_back(doc_ids[d]);
+            }
+            for (uint64_t i = E0; i < sp->term.size(); ++i) {
+                sp->df[sp->term[i]] += 1;
+                sp->plen[sp->term[i]] += 1;
+                sp->total_length = sp->total_length + sp->dl[i];  // slot order: appended slots fold last
+            }
+            sp->total_documents += n_docs;
+            if (sp->total_documents) sp->avgdl = sp->total_length / (float)sp->total_documents;
+            return GVDB_OK;
+        }
+    }
     for (uint64_t d = 0; d < n_docs; ++d) {
         const uint64_t a = doc_ptr[d], b = doc_ptr[d + 1];
         gvdb_status st = gvdb_sparse_add_document(sp, doc_ids[d], terms + a, tfs + a, b - a, doc_lengths[d]);
@@ -593,6 +728,7 @@ gvdb_status gvdb_sparse_get_stats(const gvdb_sparse* sp, gvdb_bm25_stats* out) {
     out->average_document_length = sp->avgdl;
     out->vocabulary_size = sp->df.size();
     out->total_entries = sp->term.size();
+    out->dense_fallbacks = sp->dense_fallbacks;
     return GVDB_OK;
 }
 
@@ -645,6 +781,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         h_qt.clear();
         h_qv.clear();
         h_qidf.clear();
+        std::vector<uint32_t> group_terms;  // distinct live terms of the group
         uint64_t q1 = q0;
         while (q1 < B && q1 - q0 < kSpMaxB) {
             std::vector<uint32_t> t;
@@ -661,8 +798,20 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
                 v.push_back(q_values[p]);
                 idf.push_back(std::log(x));
             }
-            if (t.size() > kSpQT) return report_status(GVDB_ERR_INVALID_ARGUMENT, "query has more than 4096 terms");
+            if (t.size() > kSpQT) return report_status(GVDB_ERR_INVALID_ARGUMENT, "query has more than 1024 terms");
             if (h_qt.size() + t.size() > kSpQT) break;
+            {
+                std::vector<uint32_t> u(group_terms);
+                u.insert(u.end(), t.begin(), t.end());
+                std::sort(u.begin(), u.end());
+                u.erase(std::unique(u.begin(), u.end()), u.end());
+                if (u.size() > kSpU) {
+                    if (q1 == q0)
+                        return report_status(GVDB_ERR_INVALID_ARGUMENT, "query has more than 512 distinct terms");
+                    break;
+                }
+                group_terms.swap(u);
+            }
             h_qt.insert(h_qt.end(), t.begin(), t.end());
             h_qv.insert(h_qv.end(), v.begin(), v.end());
             h_qidf.insert(h_qidf.end(), idf.begin(), idf.end());
@@ -671,9 +820,13 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         }
         const uint32_t Bg = (uint32_t)(q1 - q0);
         const uint32_t nqt = (uint32_t)h_qt.size();
+        const uint32_t nu = (uint32_t)group_terms.size();
+        std::vector<uint16_t> h_qb(nqt);
+        for (uint32_t i = 0; i < nqt; ++i)
+            h_qb[i] = (uint16_t)(std::lower_bound(group_terms.begin(), group_terms.end(), h_qt[i]) - group_terms.begin());
         // scratch: qp | qt | qv | qidf | tau | counts | fail | out_n | smp | cand | out ids | out scores
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-        const size_t o_qp = 0, o_qt = o_qp + al((Bg + 1) * 4), o_qv = o_qt + al(nqt * 4 + 4),
+        const size_t o_qp = 0, o_ut = o_qp + al((Bg + 1) * 4), o_qt = o_ut + al(nu * 4 + 4), o_qv = o_qt + al(nqt * 4 + 4),
                      o_qidf = o_qv + al(nqt * 4 + 4), o_tau = o_qidf + al(nqt * 4 + 4), o_cnt = o_tau + al(Bg * 8),
                      o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_smp = o_n + al(Bg * 4),
                      o_cand = o_smp + al((size_t)Bg * S * 8), o_oi = o_cand + al((size_t)Bg * kSpCand * 8),
@@ -688,7 +841,8 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         char* base = (char*)sp->scratch;
         SP_TRY(hipMemcpyAsync(base + o_qp, h_qp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
         if (nqt) {
-            SP_TRY(hipMemcpyAsync(base + o_qt, h_qt.data(), nqt * 4, hipMemcpyHostToDevice, s), "qt");
+            SP_TRY(hipMemcpyAsync(base + o_qt, h_qb.data(), nqt * 2, hipMemcpyHostToDevice, s), "qb");
+            SP_TRY(hipMemcpyAsync(base + o_ut, group_terms.data(), nu * 4, hipMemcpyHostToDevice, s), "ut");
             SP_TRY(hipMemcpyAsync(base + o_qv, h_qv.data(), nqt * 4, hipMemcpyHostToDevice, s), "qv");
             SP_TRY(hipMemcpyAsync(base + o_qidf, h_qidf.data(), nqt * 4, hipMemcpyHostToDevice, s), "qidf");
         }
@@ -700,7 +854,9 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         a.dl = sp->d_dl;
         a.N = N;
         a.qp = (const uint32_t*)(base + o_qp);
-        a.qt = (const uint32_t*)(base + o_qt);
+        a.qb = (const uint16_t*)(base + o_qt);
+        a.ut = (const uint32_t*)(base + o_ut);
+        a.nu = nu;
         a.qv = (const float*)(base + o_qv);
         a.qidf = (const float*)(base + o_qidf);
         a.B = Bg;
@@ -732,6 +888,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         // exact fallback for overflowing queries: dense keys + radix sort
         for (uint32_t q = 0; q < Bg; ++q) {
             if (!sp->h_fail[q]) continue;
+            ++sp->dense_fallbacks;
             size_t cub_bytes = 0;
             hipcub::DoubleBuffer<uint64_t> kb(nullptr, nullptr);
             SP_TRY(hipcub::DeviceRadixSort::SortKeysDescending(nullptr, cub_bytes, kb, (int)N, 0, 64, s), "cub size");

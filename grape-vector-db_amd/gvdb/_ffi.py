@@ -71,6 +71,7 @@ class gvdb_bm25_stats(C.Structure):
         ("reserved", C.c_uint32),
         ("vocabulary_size", C.c_uint64),
         ("total_entries", C.c_uint64),
+        ("dense_fallbacks", C.c_uint64),
     ]
 
 

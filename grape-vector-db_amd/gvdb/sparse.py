@@ -103,6 +103,7 @@ class BM25Stats:
     average_document_length: float
     vocabulary_size: int
     total_entries: int = 0
+    dense_fallbacks: int = 0
 
 
 class SparseIndex:
@@ -199,7 +200,7 @@ class SparseIndex:
         s = _ffi.gvdb_bm25_stats()
         _check(self._lib.gvdb_sparse_get_stats(self._h, C.byref(s)))
         return BM25Stats(int(s.total_documents), float(s.average_document_length), int(s.vocabulary_size),
-                         int(s.total_entries))
+                         int(s.total_entries), int(s.dense_fallbacks))
 
     def clear(self) -> None:
         self._lib.gvdb_sparse_clear(self._h)

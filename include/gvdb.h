@@ -243,6 +243,7 @@ typedef struct gvdb_bm25_stats {   /* BM25Stats, types.rs:104-115 */
     uint32_t reserved;
     uint64_t vocabulary_size;       /* terms with a document frequency */
     uint64_t total_entries;         /* posting entries held */
+    uint64_t dense_fallbacks;       /* diagnostics: queries answered by the dense-key fallback */
 } gvdb_bm25_stats;
 
 typedef struct gvdb_sparse gvdb_sparse;

@@ -50,6 +50,8 @@ _SIG = {
     "bm25o_stats": (None, [C.c_void_p, P, P, P]),
     "bm25o_search": (u64, [C.c_void_p, P, P, u64, u64, P, P]),
     "bm25o_rrf": (u64, [P, P, u64, P, P, u64, P, P, u64, f32, P, P, P, P, P]),
+    "bm25o_search_batch": (None, [C.c_void_p, P, P, P, u64, u64, P, P, P, C.c_int]),
+    "bm25o_add_csr": (None, [C.c_void_p, P, P, P, P, P, u64]),
     "hnsw_free": (None, [C.c_void_p]),
     "hnsw_search": (C.c_int, [C.c_void_p, P, u64, u32, u32, C.c_int, P, P, P]),
 }
@@ -304,6 +306,13 @@ class Bm25:
         v = _f32(tfs)
         lib().bm25o_add(self.h, int(doc_id), _p(t), _p(v), t.size, float(np.float32(doc_length)))
 
+    def add_documents_csr(self, ids, doc_ptr, terms, tfs, doc_lengths):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        dp = np.ascontiguousarray(doc_ptr, dtype=np.uint64)
+        t = np.ascontiguousarray(terms, dtype=np.uint32)
+        v, dl = _f32(tfs), _f32(doc_lengths)
+        lib().bm25o_add_csr(self.h, _p(ids), _p(dp), _p(t), _p(v), _p(dl), ids.size)
+
     def remove_document(self, doc_id) -> bool:
         return bool(lib().bm25o_remove(self.h, int(doc_id)))
 
@@ -320,6 +329,17 @@ class Bm25:
         sc = np.zeros(max(limit, 1), np.float32)
         n = lib().bm25o_search(self.h, _p(t), _p(v), t.size, limit, _p(ids), _p(sc))
         return ids[:n], sc[:n]
+
+    def search_batch(self, q_ptr, q_terms, q_values, limit, threads=0):
+        qp = np.ascontiguousarray(q_ptr, dtype=np.uint64)
+        qt = np.ascontiguousarray(q_terms, dtype=np.uint32)
+        qv = _f32(q_values)
+        B = qp.size - 1
+        ids = np.zeros((B, max(limit, 1)), np.uint64)
+        sc = np.zeros((B, max(limit, 1)), np.float32)
+        n = np.zeros(B, np.uint64)
+        lib().bm25o_search_batch(self.h, _p(qp), _p(qt), _p(qv), B, limit, _p(ids), _p(sc), _p(n), threads)
+        return ids[:, :limit], sc[:, :limit], n
 
     def __del__(self):
         if getattr(self, "h", None):

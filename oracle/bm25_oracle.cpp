@@ -35,11 +35,19 @@
 #include <unordered_map>
 #include <vector>
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
 namespace {
 
 struct Entry {
     uint32_t term;
     float tf, dl;
+};
+struct Posting {
+    uint32_t slot;
+    float tf, dl;  // InvertedIndexEntry {term_frequency, document_length} (sparse.rs:19-27)
 };
 
 struct Bm25Oracle {
@@ -47,7 +55,7 @@ struct Bm25Oracle {
     std::unordered_map<uint64_t, uint32_t> slot_of;
     std::vector<uint64_t> slot_id;
     std::vector<std::vector<Entry>> slot_entries;       // per slot, add order
-    std::map<uint32_t, std::vector<uint32_t>> postings;  // term -> slots, posting order
+    std::map<uint32_t, std::vector<Posting>> postings;   // term -> entries, posting order
     std::unordered_map<uint32_t, uint64_t> df;
     uint64_t total_documents = 0;
     float total_length = 0.0f;
@@ -98,7 +106,7 @@ void bm25o_add(void* h, uint64_t id, const uint32_t* terms, const float* tfs, ui
     }
     for (uint64_t i = 0; i < n; ++i) {
         o->slot_entries[slot].push_back({terms[i], tfs[i], dl});
-        o->postings[terms[i]].push_back(slot);
+        o->postings[terms[i]].push_back({slot, tfs[i], dl});
         o->df[terms[i]] += 1;
     }
     o->total_documents += 1;
@@ -108,6 +116,14 @@ void bm25o_add(void* h, uint64_t id, const uint32_t* terms, const float* tfs, ui
         o->recompute_length();
     }
     o->refresh_avgdl();
+}
+
+// n_docs add_document calls in one (CSR: document d = terms[doc_ptr[d] ..
+// doc_ptr[d+1])), for building large baselines without per-call overhead.
+void bm25o_add_csr(void* h, const uint64_t* ids, const uint64_t* doc_ptr, const uint32_t* terms, const float* tfs,
+                   const float* dls, uint64_t n_docs) {
+    for (uint64_t d = 0; d < n_docs; ++d)
+        bm25o_add(h, ids[d], terms + doc_ptr[d], tfs + doc_ptr[d], doc_ptr[d + 1] - doc_ptr[d], dls[d]);
 }
 
 // remove_document (sparse.rs:109-149): the FIRST entry of the id in every
@@ -120,7 +136,7 @@ int bm25o_remove(void* h, uint64_t id) {
     bool removed = false;
     for (auto& kv : o->postings) {
         auto& v = kv.second;
-        auto p = std::find(v.begin(), v.end(), slot);
+        auto p = std::find_if(v.begin(), v.end(), [&](const Posting& x) { return x.slot == slot; });
         if (p == v.end()) continue;
         v.erase(p);
         removed = true;
@@ -168,20 +184,10 @@ uint64_t bm25o_search(void* h, const uint32_t* q_terms, const float* q_vals, uin
         const uint64_t dfv = d == o->df.end() ? 1 : d->second;
         // calculate_idf (sparse.rs:200-203)
         const float idf = std::log(((float)o->total_documents - (float)dfv + 0.5f) / ((float)dfv + 0.5f));
-        // the posting list is walked in order; an entry's tf/dl are those of the
-        // slot's k-th entry of this term when it is the list's k-th occurrence
-        std::unordered_map<uint32_t, uint32_t> seen;
-        for (uint32_t slot : pl->second) {
-            const uint32_t kth = seen[slot]++;
-            const Entry* e = nullptr;
-            uint32_t c = 0;
-            for (const Entry& x : o->slot_entries[slot])
-                if (x.term == q_terms[p] && c++ == kth) {
-                    e = &x;
-                    break;
-                }
+        for (const Posting& e : pl->second) {  // posting order
+            const uint32_t slot = e.slot;
             // calculate_bm25_score (sparse.rs:206-222)
-            const float tfc = (e->tf * (k1 + 1.0f)) / (e->tf + k1 * (1.0f - b + b * (e->dl / o->avgdl)));
+            const float tfc = (e.tf * (k1 + 1.0f)) / (e.tf + k1 * (1.0f - b + b * (e.dl / o->avgdl)));
             const float s = q_vals[p] * tfc * idf;
             if (!hit[slot]) {
                 hit[slot] = 1;
@@ -204,6 +210,19 @@ uint64_t bm25o_search(void* h, const uint32_t* q_terms, const float* q_vals, uin
         out_scores[i] = score[order[i]];
     }
     return n;
+}
+
+// B queries in CSR (q_ptr[B+1]), one query per thread: the CPU baseline's
+// throughput leg (concurrent readers, as SparseIndex's RwLock allows).
+void bm25o_search_batch(void* h, const uint64_t* q_ptr, const uint32_t* q_terms, const float* q_vals, uint64_t B,
+                        uint64_t limit, uint64_t* out_ids, float* out_scores, uint64_t* out_n, int threads) {
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int64_t q = 0; q < (int64_t)B; ++q)
+        out_n[q] = bm25o_search(h, q_terms + q_ptr[q], q_vals + q_ptr[q], q_ptr[q + 1] - q_ptr[q], limit,
+                                out_ids + q * limit, out_scores + q * limit);
 }
 
 // rrf_fusion (hybrid.rs:422-488): ranked id lists -> fused (id, score), all of
