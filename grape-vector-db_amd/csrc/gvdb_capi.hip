@@ -250,6 +250,7 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0
                   : (scan && strcmp(scan, "i8") == 0)  ? 2
                   : (scan && strcmp(scan, "fp4u") == 0) ? 3
+                  : (scan && strcmp(scan, "fp4lds") == 0) ? 4
                                                         : 1;
     const char* dbg = getenv("GVDB_SCAN_DBG");  // ablation timing only (results invalid when set)
     s1.dbg = dbg ? atoi(dbg) : 0;

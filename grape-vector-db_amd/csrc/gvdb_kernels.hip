@@ -1096,6 +1096,217 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
     }
 }
 
+// k_scan_mx3: the FP4 scan with the candidates in REGISTERS and the queries
+// resident in LDS.  The whole query batch (<= 256 queries) is expanded to fp4
+// MFMA fragments once per block (96 KiB at 768 bits), then every wave streams
+// its own 32-row sub-tiles of the code planes straight from HBM into VGPRs
+// (two register sets: the next sub-tile's planes are in flight while the
+// current one is consumed), expands one code word per lane per k-step and runs
+// it against all query tiles (one A fragment per MFMA from LDS, a 4-deep
+// register ring hides the LDS latency).  No LDS traffic for candidates and no
+// block barrier in the loop: waves run independently, so one wave's
+// expansion / threshold VALU fills the other wave's MFMA gaps on the SIMD.
+// Semantics are those of k_scan_mx2 (exact +/-1 dot = D_pad - 2 Hamming;
+// emits (d << 32 | row) for d <= thr[q], staged per wave in LDS).
+constexpr int kMx3Rows = 32;  // candidates per wave sub-tile
+// Two shapes: 8 waves per CU (2 per SIMD) with the query tiles in two passes
+// (64 accumulator VGPRs), or 4 waves per CU (1 per SIMD, 512 VGPRs) with all
+// eight query tiles live in one pass and a 3-deep code-plane ring.
+#ifndef GVDB_MX3_WAVES
+#define GVDB_MX3_WAVES 8
+#endif
+constexpr int kMx3Threads = 64 * GVDB_MX3_WAVES;
+constexpr int kMx3Passes = GVDB_MX3_WAVES == 4 ? 1 : 2;
+constexpr int kMx3Ring = GVDB_MX3_WAVES == 4 ? 3 : 2;
+template <int W4>
+__global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                           const uint32_t* __restrict__ qwords,
+                                                           const uint32_t* __restrict__ thr, uint32_t B,
+                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                           uint32_t bufcap) {
+    constexpr int KW = 4 * W4;  // 32-bit code words per row
+    constexpr int KS = KW / 2;  // k-steps of 64 bits
+    constexpr int QT = 8;       // query tiles of 32 (256 queries per launch)
+    constexpr uint32_t kWaveStage = 512;
+    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
+    __shared__ __attribute__((aligned(16))) float tf_lds[QT * 32];
+    __shared__ uint64_t st_key[kMx3Threads / 64][kWaveStage];
+    __shared__ uint8_t st_q[kMx3Threads / 64][kWaveStage];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr float kPadF = (float)(32 * KW);
+    const int scale1 = 0x7f7f7f7f;
+    // query fragments: (tile qt, k-step s, lane l) = query qt*32 + (l & 31), code word 2s + (l >> 5)
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx3Threads) {
+        const uint32_t l = i & 63u, st = i >> 6, qs = st % KS, qt = st / KS;
+        const uint32_t q = qt * 32u + (l & 31u);
+        qfrag[i] = fp4_x32(q < B ? qwords[(uint64_t)q * KW + 2u * qs + (l >> 5)] : 0u);
+    }
+    if (tid < QT * 32) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
+    __syncthreads();
+    // per (query tile, lane half): the smallest threshold among the 16 queries a
+    // lane's accumulator rows hold, so a sub-tile with no hit is rejected with a
+    // max over the accumulator and one compare per query tile
+    __shared__ float tmin_lds[QT * 2];
+    if (tid < QT * 2) {
+        const float* tq = tf_lds + (tid >> 1) * 32 + 4u * (tid & 1u);
+        float m = tq[0];
+        for (int r = 1; r < 16; ++r) m = fminf(m, tq[(r & 3) + 8 * (r >> 2)]);
+        tmin_lds[tid] = m;
+    }
+    __syncthreads();
+    const uint32_t nqt = (B + 31u) / 32u;
+    const uint32_t nsub = (N + kMx3Rows - 1) / kMx3Rows;
+    const uint32_t W = gridDim.x * (kMx3Threads / 64);  // waves in the grid
+    const uint32_t h = lane >> 5;                      // lane half: code word 2s + h
+    // code planes of one sub-tile: lane holds plane p of row (lane & 31) (both halves the same row)
+    uint4 ca[W4], cb[W4];
+    auto load = [&](uint32_t sb, uint4 (&c)[W4]) __attribute__((always_inline)) {
+        const uint32_t n = min(sb * (uint32_t)kMx3Rows + (lane & 31u), N - 1u);  // clamped: branch-free ring
+#pragma unroll
+        for (int p = 0; p < W4; ++p) c[p] = codes[(uint64_t)p * cap + n];
+    };
+    auto word = [&](const uint4 (&c)[W4], int s) __attribute__((always_inline)) {
+        // code word 2s + h = component (2s & 3) + h of plane (2s >> 2)
+        const uint4 v = c[(2 * s) >> 2];
+        return (2 * s) & 3 ? (h ? v.w : v.z) : (h ? v.y : v.x);
+    };
+    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
+    // MX3_PASSES passes of QH query tiles per sub-tile: 1 = every query tile's
+    // accumulator live (128 VGPRs), 2 = half of them (the row fragment is then
+    // re-expanded per pass: 8 VALU per k-step).
+    constexpr int QH = QT / kMx3Passes;
+    v16f_t acc[QH];
+
+    auto process = [&](uint32_t sb, const uint4 (&c)[W4]) __attribute__((always_inline)) {
+        const uint32_t n = sb * (uint32_t)kMx3Rows + (lane & 31u);
+#pragma unroll 1
+        for (int pass = 0; pass < kMx3Passes; ++pass) {
+            if (pass * QH >= (int)nqt) break;
+            // k-loop: one expanded row fragment per k-step, reused by QH query tiles
+            const v4i_t* qf = qfrag + lane;
+            constexpr int PF = 4;  // A-fragment LDS ring depth (in MFMAs)
+            v4i_t ar[PF];
+            auto aidx = [&](int m) { return ((pass * QH + m % QH) * KS + (m / QH)) * 64; };  // MFMA m = s*QH + qt
+#pragma unroll
+            for (int m = 0; m < PF; ++m) ar[m] = qf[aidx(m)];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                // keep the scheduler from hoisting later k-steps' LDS reads and
+                // expansions (their registers would spill)
+                __builtin_amdgcn_sched_barrier(0);
+                const v4i_t b = fp4_x32(word(c, s));
+#pragma unroll
+                for (int qt = 0; qt < QH; ++qt) {
+                    const int m = s * QH + qt;
+                    const v4i_t a = ar[m % PF];
+                    if (m + PF < KS * QH) ar[m % PF] = qf[aidx(m + PF)];
+                    if (s == 0)
+                        mfma_fp4_first(acc[qt], a, b, scale1);
+                    else
+                        mfma_fp4_acc(acc[qt], a, b, scale1);
+                }
+            }
+            mfma_fp4_drain();
+            // threshold epilogue of these QH query tiles
+#pragma unroll
+            for (int qh = 0; qh < QH; ++qh) {
+                const int qt = pass * QH + qh;
+                if (qt >= (int)nqt) break;
+                float amax = acc[qh][0];
+#pragma unroll
+                for (int r = 1; r < 16; ++r) amax = fmaxf(amax, acc[qh][r]);
+                if (!__ballot(amax >= tmin_lds[qt * 2 + h] && n < N)) continue;
+                float Tf[16];
+                const float* tq = tf_lds + qt * 32 + 4u * h;
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const float4 v = *(const float4*)(tq + 8 * g4);
+                    Tf[4 * g4 + 0] = v.x;
+                    Tf[4 * g4 + 1] = v.y;
+                    Tf[4 * g4 + 2] = v.z;
+                    Tf[4 * g4 + 3] = v.w;
+                }
+                float mx = acc[qh][0] - Tf[0];
+#pragma unroll
+                for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[qh][r] - Tf[r]);
+                if (!__ballot(mx >= 0.0f && n < N)) continue;
+                const uint32_t rb = qt * 32u + 4u * h;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const bool hit = acc[qh][r] >= Tf[r] && n < N;
+                    const uint64_t m = __ballot(hit);
+                    if (m) {
+                        if (hit) {
+                            const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
+                                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
+                            const uint32_t d = (uint32_t)(kPadF - acc[qh][r]) >> 1;
+                            const uint64_t key = ((uint64_t)d << 32) | n;
+                            if (sp < kWaveStage) {
+                                st_key[wv][sp] = key;
+                                st_q[wv][sp] = (uint8_t)qi;
+                            } else {
+                                const uint32_t pos = atomicAdd(&counts[qi], 1u);
+                                if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = key;
+                            }
+                        }
+                        wcnt += (uint32_t)__popcll(m);
+                    }
+                }
+            }
+        }
+    };
+    uint32_t sb = blockIdx.x * (kMx3Threads / 64) + wv;
+    if constexpr (kMx3Ring == 2) {
+        load(sb, ca);
+        load(sb + W, cb);
+        for (; sb < nsub; sb += 2 * W) {
+            process(sb, ca);
+            load(sb + 2 * W, ca);
+            if (sb + W < nsub) process(sb + W, cb);
+            load(sb + 3 * W, cb);
+        }
+    } else {
+        uint4 cc[W4];
+        load(sb, ca);
+        load(sb + W, cb);
+        load(sb + 2 * W, cc);
+        for (; sb < nsub; sb += 3 * W) {
+            process(sb, ca);
+            load(sb + 3 * W, ca);
+            if (sb + W < nsub) process(sb + W, cb);
+            load(sb + 4 * W, cb);
+            if (sb + 2 * W < nsub) process(sb + 2 * W, cc);
+            load(sb + 5 * W, cc);
+        }
+    }
+    // drain the clamped prefetches, then flush the staged candidates
+    __syncthreads();
+    const uint32_t ns = min(wcnt, kWaveStage);
+    for (uint32_t e = lane; e < ns; e += 64u) {
+        const uint32_t qi = st_q[wv][e];
+        const uint32_t pos = atomicAdd(&counts[qi], 1u);
+        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
+    }
+}
+
+template <int W4>
+static void launch_scan_mx3_t(const Stage1Args& a, hipStream_t s) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t nsub = (a.N + kMx3Rows - 1) / kMx3Rows;
+    const uint32_t wpb = kMx3Threads / 64;
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus, (nsub + wpb - 1) / wpb));
+    for (uint32_t g = 0; g < a.B; g += 256) {
+        const uint32_t bg = min(256u, a.B - g);
+        hipLaunchKernelGGL((k_scan_mx3<W4>), dim3(grid), dim3(kMx3Threads), 0, s, a.codes, a.cap, a.N,
+                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
+                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+    }
+}
+
 template <int W4>
 static void launch_scan_mx2_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
@@ -1203,7 +1414,21 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 4: launch_scan_mx_t<4>(a, s); break;
             default: launch_scan_mx_t<6>(a, s); break;
         }
-    } else if (mfma) {  // FP4 block-scaled MFMA, producer/consumer waves (default for large batches)
+    } else if (mfma && a.use_mfma == 4) {  // FP4, LDS-shared candidate tiles (the previous default; A/B)
+        switch (W4) {
+            case 2: launch_scan_mx2_t<2>(a, s); break;
+            case 3: launch_scan_mx2_t<3>(a, s); break;
+            case 4: launch_scan_mx2_t<4>(a, s); break;
+            default: launch_scan_mx2_t<6>(a, s); break;
+        }
+    } else if (mfma) {  // FP4 block-scaled MFMA, candidates in registers (default for large batches)
+        switch (W4) {
+            case 2: launch_scan_mx3_t<2>(a, s); break;
+            case 3: launch_scan_mx3_t<3>(a, s); break;
+            case 4: launch_scan_mx3_t<4>(a, s); break;
+            default: launch_scan_mx3_t<6>(a, s); break;
+        }
+    } else if (false) {
         switch (W4) {
             case 2: launch_scan_mx2_t<2>(a, s); break;
             case 3: launch_scan_mx2_t<3>(a, s); break;

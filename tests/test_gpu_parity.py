@@ -143,7 +143,7 @@ def test_stage1_mfma_batches_match_oracle(g, oracle_mod, N, D, B, R):
     ix = g.GpuVectorIndex(dimension=D)
     ix.add_batch(np.arange(N, dtype=np.uint64), x)
     gi, gd = topr(g, ix, Q, R)
-    for variant in ("valu", "i8", "fp4u"):
+    for variant in ("valu", "i8", "fp4u", "fp4lds"):
         os.environ["GVDB_SCAN"] = variant
         try:
             vi, vd = topr(g, ix, Q, R)
