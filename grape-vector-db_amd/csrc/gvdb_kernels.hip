@@ -1109,15 +1109,12 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
 // Semantics are those of k_scan_mx2 (exact +/-1 dot = D_pad - 2 Hamming;
 // emits (d << 32 | row) for d <= thr[q], staged per wave in LDS).
 constexpr int kMx3Rows = 32;  // candidates per wave sub-tile
-// Two shapes: 8 waves per CU (2 per SIMD) with the query tiles in two passes
-// (64 accumulator VGPRs), or 4 waves per CU (1 per SIMD, 512 VGPRs) with all
-// eight query tiles live in one pass and a 3-deep code-plane ring.
-#ifndef GVDB_MX3_WAVES
-#define GVDB_MX3_WAVES 8
-#endif
-constexpr int kMx3Threads = 64 * GVDB_MX3_WAVES;
-constexpr int kMx3Passes = GVDB_MX3_WAVES == 4 ? 1 : 2;
-constexpr int kMx3Ring = GVDB_MX3_WAVES == 4 ? 3 : 2;
+// 8 waves per CU (2 per SIMD), the query tiles in two passes of four (64
+// accumulator VGPRs: all eight at once, or one wave per SIMD with 512
+// registers, spill under hipcc), a 2-deep code-plane ring.
+constexpr int kMx3Threads = 512;
+constexpr int kMx3Passes = 2;
+constexpr int kMx3Ring = 2;
 template <int W4>
 __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const uint32_t* __restrict__ qwords,
