@@ -286,7 +286,7 @@ def main():
         if variant == "i8":
             peak, kname = PEAK_I8_TOPS, "k_scan_mfma (+/-1 i8 dot, v_mfma_i32_32x32x32_i8)"
         else:
-            peak, kname = PEAK_FP4_TFLOPS, "k_scan_mx2 (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4)"
+            peak, kname = PEAK_FP4_TFLOPS, "k_scan_mx3 (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4, rows in VGPRs)"
         roof = {
             "kernel": "stage-1 BQ Hamming filter: " + kname,
             "bound": "mfma",
@@ -306,7 +306,7 @@ def main():
         }
     roof.update({
         "frac": roof["achieved"] / peak,
-        "traffic": pmc_traffic("gvdb::k_scan_mx2<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
+        "traffic": pmc_traffic("gvdb::k_scan_mx3<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
         "hbm_bytes_per_launch": n_local * gvdb_code_w4(D) * 16,
