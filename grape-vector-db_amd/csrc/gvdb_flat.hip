@@ -20,9 +20,9 @@
 //                    not nominated has exact score < T_q + eps <= k-th: exact.
 //
 // Two element kinds share one kernel body (the byte geometry is identical):
-//   bf16: rowsx = bf16 [KC][cap][64],  KC = ceil(D/64),  v_mfma_f32_32x32x16_bf16;
+//   bf16: rowsx = bf16 x64 per chunk row,  KC = ceil(D/64),  v_mfma_f32_32x32x16_bf16;
 //         eps = 2^-8 (+ rounding terms, flat_eps below) for every pair.
-//   i8:   rowsx = int8 [KC][cap][128], KC = ceil(D/128), v_mfma_i32_32x32x32_i8
+//   i8:   rowsx = int8 x128 per chunk row, KC = ceil(D/128), v_mfma_i32_32x32x32_i8
 //         (exact i32 dot of the quantised vectors).  Row x is stored as
 //         xq = rint(x * 127/max|x_i|), s_x = max|x_i|/127, with
 //         rscale = s_x/|x| and rho_x = |x - s_x xq| / |x| (fp64, rounded up);
@@ -30,15 +30,13 @@
 //         cosine units, eps_q = rho_q + (1 + rho_q) max_x rho_x (+ norm and
 //         fold rounding terms): half the HBM bytes of bf16 and twice the
 //         MFMA rate, for a ~4x wider (still certified) candidate margin.
-// Either way a row chunk is 128 B and the mirror is TILE-major,
-// [ceil(cap/256)][KC][256][128 B] (fx_off): one chunk of a 256-row tile is a
-// contiguous 32 KiB block and a tile's KC chunks are adjacent, so a block
-// streams one contiguous KC*32 KiB region per tile (few TLB pages in flight;
-// a chunk-major [KC][cap] layout put each step 1-2 GB from the last).
-// Queries are [KC][256][128 B].
-// Tile = 256 rows x 256 query slots; 8 waves = 2 query halves x 4 row
-// quarters, each wave 128 queries x 64 rows = 4 x 2 32x32 MFMA tiles: per
-// k-step 6 ds_read_b128 feed 8 MFMAs.
+// Either way a row chunk is 128 B and the mirror is tile-major and
+// FRAGMENT-major (fx_frag, gvdb_internal.h): one chunk of a 256-row tile is a
+// contiguous 32 KiB block of eight 4 KiB 32-row groups, each laid out as the
+// MFMA operand fragments of its 4 k-steps, and a tile's KC chunks are
+// adjacent, so a block streams one contiguous KC*32 KiB region per tile and a
+// wave loads its row fragments with lane-linear 16-B loads.  Queries use the
+// same layout (one 256-slot tile).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -65,7 +63,7 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
     return (uint16_t)(u >> 16);
 }
 
-// rows f32 [n][D] (rows row0.. of the index) -> rowsb bf16 [KC][cap][64]; one
+// rows f32 [n][D] (rows row0.. of the index) -> rowsb bf16 mirror (fx_frag); one
 // thread per (row, 8-element group).  Flags NaN elements.
 __global__ __launch_bounds__(256) void k_rows_to_bf16(const float* __restrict__ rows, uint64_t n, uint32_t D,
                                                       uint16_t* __restrict__ rowsb, uint64_t cap,
@@ -91,10 +89,10 @@ __global__ __launch_bounds__(256) void k_rows_to_bf16(const float* __restrict__ 
     o.y = v[2] | ((uint32_t)v[3] << 16);
     o.z = v[4] | ((uint32_t)v[5] << 16);
     o.w = v[6] | ((uint32_t)v[7] << 16);
-    *(uint4*)(rowsb + fx_off(row, c, KC) / 2u + (grp & 7u) * 8u) = o;
+    *(uint4*)(rowsb + fx_frag(row, c, KC, grp & 7u) / 2u) = o;
 }
 
-// queries f32 [B][D] -> qb bf16 [KC][256][64] (slots >= B zero), qinv = 1/|q| (0 for |q| = 0)
+// queries f32 [B][D] -> qb bf16 (fx_frag, slots >= B zero), qinv = 1/|q| (0 for |q| = 0)
 __global__ __launch_bounds__(256) void k_queries_to_bf16(const float* __restrict__ q, uint32_t B, uint32_t D,
                                                          const float* __restrict__ qnorm, uint16_t* __restrict__ qb,
                                                          float* __restrict__ qinv, float* __restrict__ qd, float eps) {
@@ -115,7 +113,7 @@ __global__ __launch_bounds__(256) void k_queries_to_bf16(const float* __restrict
     o.y = v[2] | ((uint32_t)v[3] << 16);
     o.z = v[4] | ((uint32_t)v[5] << 16);
     o.w = v[6] | ((uint32_t)v[7] << 16);
-    *(uint4*)(qb + ((uint64_t)c * kFxQ + slot) * 64u + (grp & 7u) * 8u) = o;
+    *(uint4*)(qb + fx_frag(slot, c, KC, grp & 7u) / 2u) = o;
     if (grp == 0) {
         const float nq = slot < B ? qnorm[slot] : 0.0f;
         qinv[slot] = nq == 0.0f ? 0.0f : 1.0f / nq;
@@ -130,11 +128,11 @@ __host__ __device__ inline float fx_fold_slack(uint32_t D) { return 2.0f * (floa
 
 // Per-vector symmetric int8 quantisation of one D-vector by one wave: in pass
 // p lane l owns elements [1024p + 16l, +16) = 16-B piece (l & 7) of chunk
-// 8p + (l >> 3), written to dst + chunk * cstride + piece * 16 (chunks < KC;
+// 8p + (l >> 3), written at dst + fx_frag(row, chunk, KC, piece) (chunks < KC;
 // padding elements are 0).  Returns s = max|v|/127 and rho = |v - s*vq| / |v|
 // in fp64 (0 for a zero vector) on every lane, and flags non-finite values.
 __device__ inline void fx_quantize_i8_wave(const float* __restrict__ v, uint32_t D, uint32_t lane, bool live,
-                                           int8_t* __restrict__ dst, uint64_t cstride, float& s_out, double& rho_out,
+                                           int8_t* __restrict__ dst, uint64_t row, float& s_out, double& rho_out,
                                            bool& bad) {
     const uint32_t KC = (D + 127u) / 128u, passes = (KC + 7u) / 8u;
     float amax = 0.0f;
@@ -169,7 +167,7 @@ __device__ inline void fx_quantize_i8_wave(const float* __restrict__ v, uint32_t
             n2 += (double)x * (double)x;
             w[i >> 2] |= ((uint32_t)qi & 0xffu) << (8 * (i & 3));
         }
-        if (chunk < KC) *(uint4*)(dst + (uint64_t)chunk * cstride + (lane & 7u) * 16u) = make_uint4(w[0], w[1], w[2], w[3]);
+        if (chunk < KC) *(uint4*)(dst + fx_frag(row, chunk, KC, lane & 7u)) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -182,7 +180,7 @@ __device__ inline void fx_quantize_i8_wave(const float* __restrict__ v, uint32_t
     bad = __ballot(nf) != 0;
 }
 
-// rows f32 [n][D] -> rowsq int8 [KC][cap][128] (KC = ceil(D/128)); one wave per
+// rows f32 [n][D] -> rowsq int8 mirror (fx_frag, KC = ceil(D/128)); one wave per
 // row.  rscale[row] = s_x/|x|_f32 (0 for a zero row), rrho[row] = rho_x
 // rounded up; non-finite rows flag *bad.
 __global__ __launch_bounds__(256) void k_rows_to_i8(const float* __restrict__ rows, const float* __restrict__ norms,
@@ -195,8 +193,7 @@ __global__ __launch_bounds__(256) void k_rows_to_i8(const float* __restrict__ ro
     float sc;
     double rho;
     bool bad;
-    fx_quantize_i8_wave(rows + row * D, D, lane, true, rowsq + fx_off(row, 0, (D + 127u) / 128u),
-                        (uint64_t)kFxRows * 128u, sc, rho, bad);
+    fx_quantize_i8_wave(rows + row * D, D, lane, true, rowsq, row, sc, rho, bad);
     if (bad && lane == 0) atomicOr(bad_flag, 1u);
     if (lane == 0) {
         const float nx = norms[row];
@@ -205,7 +202,7 @@ __global__ __launch_bounds__(256) void k_rows_to_i8(const float* __restrict__ ro
     }
 }
 
-// queries f32 [B][D] -> qq int8 [KC][256][128] (slots >= B zero); qinv = s_q/|q|,
+// queries f32 [B][D] -> qq int8 (fx_frag, slots >= B zero); qinv = s_q/|q|,
 // (qa, qd) = the query's terms of the pair bound (epilogue of k_flat_mx):
 // qa = c (1 + rho_q), qd = c rho_q + fold slack, c = the norm factor.
 __global__ __launch_bounds__(256) void k_queries_to_i8(const float* __restrict__ q, uint32_t B, uint32_t D,
@@ -219,8 +216,7 @@ __global__ __launch_bounds__(256) void k_queries_to_i8(const float* __restrict__
     float sc;
     double rho;
     bool bad;
-    fx_quantize_i8_wave(q + (uint64_t)(live ? slot : 0) * D, D, lane, live, qq + (uint64_t)slot * 128u,
-                        (uint64_t)kFxQ * 128u, sc, rho, bad);
+    fx_quantize_i8_wave(q + (uint64_t)(live ? slot : 0) * D, D, lane, live, qq, slot, sc, rho, bad);
     if (lane == 0) {
         const float nq = live ? qnorm[slot] : 0.0f;
         qinv[slot] = nq == 0.0f ? 0.0f : sc / nq;
@@ -233,32 +229,43 @@ __global__ __launch_bounds__(256) void k_queries_to_i8(const float* __restrict__
 
 // The MFMA pass.  SAMPLE: every `every`-th row tile, approx scores -> smp[q][S].
 // EMIT: every tile, rows with approx >= thr[q] -> cand[q][*] (counts[q]).
-// Staging: global_load_lds (16 B per lane, no VGPRs), 64 k (128 B) per row and
-// chunk; the query chunk (A, L2-resident) is double-buffered, the row chunk (B,
-// from HBM) triple-buffered so its loads are issued two chunks ahead: the wait
-// at the end of step u retires A(u+1) and B(u+1) with a counted vmcnt and leaves
-// B(u+2) in flight across the raw s_barrier.  The 160 KiB of LDS hold only the
-// five chunk buffers; thresholds and inverse norms are read from L1/L2 in the
-// once-per-tile epilogue.  The LDS image is lane-linear, so the bank-conflict
-// swizzle is applied on the global side: 16-B piece j of row r sits at slot
-// j ^ ((r >> 1) & 7) of the row's 128 B (conflict-free ds_read_b128 fragments).
+// Tile = 256 rows x 256 query slots; 8 waves = 2 query halves (wq) x 4 row
+// quarters (wr), each wave 128 queries x 64 rows = 4 x 2 32x32 MFMA tiles.
+// Rows (B operand, from HBM) go straight to VGPRs: the fragment-major mirror
+// (fx_frag) makes each (32-row group, k-step) fragment 1 KiB contiguous, and
+// the fragment consumed at k-step s is reloaded for the next chunk right after
+// its MFMAs (one chunk of prefetch distance, 32 VGPRs).  The query chunk (A,
+// 32 KiB, L2-resident) is loaded to VGPRs one chunk ahead and written to a
+// 2-buffer LDS ring (plain loads, not global_load_lds: an in-flight LDS DMA
+// makes the compiler drain vmcnt to 0 before every ds_read, row loads
+// included).  The LDS image of a chunk is its fragment-major global image, so
+// every ds_read_b128 fragment read is lane-linear (conflict-free).
+// Thresholds and inverse norms are read from L1/L2 in the once-per-tile
+// epilogue.
+// FX_ABL (timing ablation builds only, results invalid): 1 no query loads,
+// 2 no row loads, 4 no epilogue, 8 no MFMA, 16 rows loaded by one wave of
+// each pair only.
+#ifndef FX_ABL
+#define FX_ABL 0
+#endif
 template <bool SAMPLE, bool I8>
 __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
-    // five distinct LDS objects (not one indexed array): with every buffer index
-    // a compile-time constant the waitcnt pass can tell an in-flight
-    // global_load_lds into one buffer from ds_reads of another.  A chunk row is
-    // 128 B (64 bf16 or 128 i8).
-    __shared__ __attribute__((aligned(16))) uint16_t As0[kFxQ * 64], As1[kFxQ * 64];
-    __shared__ __attribute__((aligned(16))) uint16_t Bs0[kFxRows * 64], Bs1[kFxRows * 64], Bs2[kFxRows * 64];
+    // two distinct LDS objects (not one indexed array), each 1 query chunk
+    constexpr uint32_t kChunk = kFxQ * 128u;  // bytes of one query chunk
+    __shared__ __attribute__((aligned(16))) char As0[kChunk], As1[kChunk];
+    // EMIT: the block's nominations, (query << 32) | row, flushed to the
+    // global per-query lists once at the end (an LDS atomic per nomination
+    // instead of a global atomic round trip inside the MFMA loop)
+    constexpr uint32_t kCl = SAMPLE ? 1u : 2048u;
+    __shared__ uint64_t cl[kCl];
+    __shared__ uint32_t cl_n;
+    // per-slot epilogue operands, staged once: qinv, thr - (i8) qa
+    __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[I8 ? kFxQ : 4];
     const char* rowsx = (const char*)a.rowsx;
     const char* qx = (const char*)a.qx;
-    auto abuf = [&](auto I) -> uint16_t* {
-        if constexpr (decltype(I)::value == 0) return As0; else return As1;
-    };
-    auto bbuf = [&](auto I) -> uint16_t* {
-        if constexpr (decltype(I)::value == 0) return Bs0;
-        else if constexpr (decltype(I)::value == 1) return Bs1;
-        else return Bs2;
+    auto abuf = [&](auto I) -> char* {
+        if constexpr (decltype(I)::value == 0) return As0;
+        else return As1;
     };
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -273,42 +280,32 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
     const uint32_t nt = blockIdx.x < ntiles ? (ntiles - blockIdx.x + G - 1) / G : 0;
     const uint32_t nsteps = nt * KC;
     auto tile_of = [&](uint32_t j) { return (blockIdx.x + j * G) * every; };
-
-    // this lane's staging slot: wave wv fills LDS rows [32*wv, 32*wv+32) of each
-    // operand, 8 rows (1 KiB) per instruction; lane -> row L/8, slot L%8
-    const uint32_t srow0 = wv * 32u + (lane >> 3);
     auto step_of = [&](uint32_t u, uint32_t& t, uint32_t& c) __attribute__((always_inline)) {
         const uint32_t uu = u < nsteps ? u : (nsteps ? nsteps - 1 : 0);  // clamp: branch-free
         const uint32_t j = uu / KC;
         c = uu - j * KC;
         t = tile_of(j);
     };
-    auto issueA = [&](uint32_t u, auto BI) __attribute__((always_inline)) {
+    // query chunk of step u: wave wv stages bytes [4 KiB wv, +4 KiB), 1 KiB per load
+    fx_v4i qs[4];
+    auto loadA = [&](uint32_t u) __attribute__((always_inline)) {
         uint32_t t, c;
         step_of(u, t, c);
+        const char* ga = qx + (uint64_t)c * kChunk + wv * 4096u + lane * 16u;
+        if constexpr (FX_ABL & 1) return;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t row = srow0 + i * 8u;
-            const uint32_t piece = (lane & 7u) ^ ((row >> 1) & 7u);
-            const char* ga = qx + ((uint64_t)c * kFxQ + row) * 128u + piece * 16u;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
-                                             (__attribute__((address_space(3))) void*)(abuf(BI) + (wv * 32u + i * 8u) * 64u),
-                                             16, 0, 0);
-        }
+        for (int i = 0; i < 4; ++i) qs[i] = *(const fx_v4i*)(ga + i * 1024);
     };
-    auto issueB = [&](uint32_t u, auto BI) __attribute__((always_inline)) {
+    auto storeA = [&](auto BI) __attribute__((always_inline)) {
+        char* d = abuf(BI) + wv * 4096u + lane * 16u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *(fx_v4i*)(d + i * 1024) = qs[i];
+    };
+    // row fragments of step u: groups 2 wr + r of tile t, chunk c; (r, s) at +4 KiB r + 1 KiB s
+    auto rowbase = [&](uint32_t u) __attribute__((always_inline)) -> const char* {
         uint32_t t, c;
         step_of(u, t, c);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t row = srow0 + i * 8u;
-            const uint32_t piece = (lane & 7u) ^ ((row >> 1) & 7u);
-            const uint32_t grow = min(t * kFxRows + row, N - 1u);
-            const char* gb = rowsx + fx_off(grow, c, KC) + piece * 16u;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gb,
-                                             (__attribute__((address_space(3))) void*)(bbuf(BI) + (wv * 32u + i * 8u) * 64u),
-                                             16, 0, 0);
-        }
+        return rowsx + (((uint64_t)t * KC + c) * 8u + 2u * wr) * 4096u + lane * 16u;
     };
 
     using AccT = std::conditional_t<I8, fx_v16i, fx_v16f>;
@@ -321,27 +318,23 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[i][r][e] = 0;
     };
-    // Fragment reads: rows i*32 + (lane & 31) of a 32-row block all share the
-    // swizzle ((lane & 31) >> 1) & 7, so a fragment address is a per-lane base,
-    // plus one of 4 per-lane piece offsets (k-step s), plus a constant
-    // 4 KiB * block.
-    const uint32_t swz = ((lane & 31u) >> 1) & 7u;
-    uint32_t poff[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) poff[s] = (((uint32_t)(2 * s) + (lane >> 5)) ^ swz) * 16u;
-    const uint32_t abase = (wq * 128u + (lane & 31u)) * 128u;
-    const uint32_t bbase = (wr * 64u + (lane & 31u)) * 128u;
-    // 4 k-steps of 16 over one LDS chunk; fragments of step s+1 are read while
-    // the 8 MFMAs of step s run
-    auto mma = [&](auto AI, auto BI) __attribute__((always_inline)) {
+    // row fragments [ring slot][r][k-step]: bf16 keeps two chunks in flight
+    // (slot = step parity), i8 (half the bytes per step) one
+    constexpr int kRing = I8 ? 1 : 2;
+    fx_v4i rf[kRing][2][4];
+    const uint32_t abase = (wq * 16u * 64u + lane) * 16u;  // query groups 4 wq + i: +4 KiB i, +1 KiB s
+    // 4 k-steps of 16 (i8: 32) over one chunk; the query fragments of k-step
+    // s+1 are read while the 8 MFMAs of k-step s run, and row fragment s is
+    // reloaded for the next chunk as soon as its MFMAs have issued (pinned
+    // there, so every row load has one whole chunk step to land)
+    auto mma = [&](uint32_t u, auto AI) __attribute__((always_inline)) {
+        constexpr int R = decltype(AI)::value % kRing;
         const char* A = (const char*)abuf(AI) + abase;
-        const char* Bt = (const char*)bbuf(BI) + bbase;
-        fx_v4i fa[2][4], fb[2][2];
+        const char* rn = rowbase(u + kRing);
+        fx_v4i fa[2][4];
         auto rd = [&](int s, int slot) __attribute__((always_inline)) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) fa[slot][i] = *(const fx_v4i*)(A + poff[s] + i * 4096);
-#pragma unroll
-            for (int r = 0; r < 2; ++r) fb[slot][r] = *(const fx_v4i*)(Bt + poff[s] + r * 4096);
+            for (int i = 0; i < 4; ++i) fa[slot][i] = *(const fx_v4i*)(A + i * 4096 + s * 1024);
         };
         rd(0, 0);
 #pragma unroll
@@ -351,20 +344,46 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 2; ++r) {
-                    if constexpr (I8)
-                        acc[i][r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s & 1][i], fb[s & 1][r], acc[i][r], 0, 0,
-                                                                          0);
+                    if constexpr (FX_ABL & 8)
+                        acc[i][r][0] += __builtin_bit_cast(float, fa[s & 1][i][0] ^ rf[R][r][s][0]);
+                    else if constexpr (I8)
+                        acc[i][r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s & 1][i], rf[R][r][s], acc[i][r], 0, 0, 0);
                     else
                         acc[i][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(fx_v8bf, fa[s & 1][i]),
-                                                                            __builtin_bit_cast(fx_v8bf, fb[s & 1][r]),
+                                                                            __builtin_bit_cast(fx_v8bf, rf[R][r][s]),
                                                                             acc[i][r], 0, 0, 0);
                 }
+            if constexpr (!(FX_ABL & 2)) {
+                if (!(FX_ABL & 16) || wq == 0) {
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) rf[R][r][s] = *(const fx_v4i*)(rn + r * 4096 + s * 1024);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
     // Epilogue.  Per pair the exact f32 cosine is at most U = approx + qa*rho_x
     // + qd (i8: qa = (1+rho_q)*c, qd = rho_q*c + slack, rho_x per row; bf16:
     // qa = 0, qd = eps).  SAMPLE stores approx; EMIT nominates a row iff
     // U >= tau, as approx + qa*rho_x >= thr with thr = tau - qd.
+    // per-row operands of the epilogue, (re)loaded every step so the
+    // once-per-tile epilogue never waits on a global load: bf16 |x| (rv0),
+    // i8 s_x/|x| (rv0) and rho_x (rv1), for this lane's rows r = 0, 1
+    float rv0[2], rv1[2];
+    auto load_rowops = [&](uint32_t u) __attribute__((always_inline)) {
+        uint32_t t, c;
+        step_of(u, t, c);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t n = min(t * kFxRows + wr * 64u + r * 32u + (lane & 31u), N - 1u);
+            if constexpr (I8) {
+                rv0[r] = a.rscale[n];
+                rv1[r] = a.rrho[n];
+            } else {
+                rv0[r] = a.rnorm[n];
+            }
+        }
+    };
     auto epilogue = [&](uint32_t j) __attribute__((always_inline)) {
         const uint32_t t = tile_of(j);
 #pragma unroll
@@ -372,10 +391,10 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
             const uint32_t n = t * kFxRows + wr * 64u + r * 32u + (lane & 31u);
             float rinv, rho = 0.0f;
             if constexpr (I8) {
-                rinv = n < N ? a.rscale[n] : 0.0f;  // s_x / |x|
-                rho = n < N ? a.rrho[n] : 0.0f;
+                rinv = n < N ? rv0[r] : 0.0f;  // s_x / |x|
+                rho = n < N ? rv1[r] : 0.0f;
             } else {
-                const float nb = n < N ? a.rnorm[n] : 0.0f;
+                const float nb = n < N ? rv0[r] : 0.0f;
                 rinv = nb == 0.0f ? 0.0f : 1.0f / nb;
             }
 #pragma unroll
@@ -386,16 +405,16 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
                 float qs[16], ts[16];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const float4 qv = *(const float4*)(a.qinv + qb0 + 8 * g);
+                    const float4 qv = *(const float4*)(qinv_l + qb0 + 8 * g);
                     qs[4 * g + 0] = qv.x * rinv;
                     qs[4 * g + 1] = qv.y * rinv;
                     qs[4 * g + 2] = qv.z * rinv;
                     qs[4 * g + 3] = qv.w * rinv;
                     // EMIT: ts = thr - qa*rho (the row-dependent part of U); SAMPLE: ts = 0
                     float4 tv = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if constexpr (!SAMPLE) tv = *(const float4*)(a.thr + qb0 + 8 * g);
+                    if constexpr (!SAMPLE) tv = *(const float4*)(thr_l + qb0 + 8 * g);
                     if constexpr (I8 && !SAMPLE) {
-                        const float4 av = *(const float4*)(a.qa + qb0 + 8 * g);
+                        const float4 av = *(const float4*)(qa_l + qb0 + 8 * g);
                         tv.x -= av.x * rho;
                         tv.y -= av.y * rho;
                         tv.z -= av.z * rho;
@@ -425,8 +444,13 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
                     for (int e = 0; e < 16; ++e) {
                         const uint32_t q = qb0 + (e & 3) + 8 * (e >> 2);
                         if (n < N && (float)acc[i][r][e] * qs[e] >= ts[e]) {
-                            const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-                            if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = n;
+                            const uint32_t li = atomicAdd(&cl_n, 1u);
+                            if (li < kCl) {
+                                cl[li] = ((uint64_t)q << 32) | n;
+                            } else {  // block list full: straight to the global list
+                                const uint32_t pos = atomicAdd(&a.counts[q], 1u);
+                                if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = n;
+                            }
                         }
                     }
                 }
@@ -434,45 +458,64 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
         }
     };
 
-    // s_waitcnt encodings (gfx9): vmcnt in [3:0], expcnt [6:4], lgkmcnt [11:8]
-    constexpr int kWaitAll = 0x0000;        // vmcnt(0) expcnt(0) lgkmcnt(0)
-    constexpr int kWaitKeepB = 0x0074;      // vmcnt(4) lgkmcnt(0): the 4 newest (B(u+2)) stay in flight
+    // Per step: the query chunk of step u+1 is loaded to VGPRs at the start,
+    // written to the other LDS buffer after the MFMAs (it was last read in
+    // step u-1, before that step's barrier), then one barrier.  The barrier
+    // waits for LDS only (vmcnt(63) lgkmcnt(0)): the row loads stay in flight.
+    constexpr int kWaitLds = (3 << 14) | 0x0070 | 0xF;  // vmcnt(63) expcnt(7) lgkmcnt(0)
     using C0 = std::integral_constant<int, 0>;
     using C1 = std::integral_constant<int, 1>;
-    using C2 = std::integral_constant<int, 2>;
-    issueA(0, C0{});
-    issueB(0, C0{});
-    issueB(1, C1{});
-    __builtin_amdgcn_s_waitcnt(kWaitAll);
+#pragma unroll
+    for (int k = 0; k < kRing; ++k) {
+        const char* r0 = rowbase(k);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) rf[k][r][s] = *(const fx_v4i*)(r0 + r * 4096 + s * 1024);
+    }
+    loadA(0);
+    storeA(C0{});
+    if (tid == 0) cl_n = 0;
+    if (tid < kFxQ) {
+        qinv_l[tid] = a.qinv[tid];
+        if constexpr (!SAMPLE) thr_l[tid] = a.thr[tid];
+        if constexpr (I8 && !SAMPLE) qa_l[tid] = a.qa[tid];
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitLds);
     __builtin_amdgcn_s_barrier();
     zero();
-    // step u uses A buffer u%2 and B buffer u%3; six steps per loop trip keep
-    // every buffer index static
-    auto step = [&](uint32_t u, auto AI, auto BI) __attribute__((always_inline)) {
+    // step u reads A buffer u%2 (two steps per loop trip keep it static)
+    auto step = [&](uint32_t u, auto AI) __attribute__((always_inline)) {
         using AN = std::integral_constant<int, 1 - decltype(AI)::value>;
-        using BN2 = std::integral_constant<int, (decltype(BI)::value + 2) % 3>;
-        if (!(a.dbg & 1)) issueA(u + 1, AN{});  // buffers of step u-1 were released by its barrier
-        if (!(a.dbg & 2)) issueB(u + 2, BN2{});
-        if (!(a.dbg & 4)) mma(AI, BI);
+        __builtin_amdgcn_sched_barrier(0);
+        loadA(u + 1);
+        load_rowops(u);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(u, AI);
+        storeA(AN{});  // before the epilogue: its staging registers are free there
         const uint32_t j = u / KC;
         if (u - j * KC == KC - 1) {
-            epilogue(j);
+            if constexpr (!(FX_ABL & 4)) epilogue(j);
             zero();
-            __builtin_amdgcn_s_waitcnt(kWaitAll);  // the epilogue's memory ops break the count
-        } else {
-            __builtin_amdgcn_s_waitcnt(kWaitKeepB);
         }
+        __builtin_amdgcn_s_waitcnt(kWaitLds);
         __builtin_amdgcn_s_barrier();
     };
-    for (uint32_t u = 0; u < nsteps; u += 6) {
-        step(u, C0{}, C0{});
-        if (u + 1 < nsteps) step(u + 1, C1{}, C1{});
-        if (u + 2 < nsteps) step(u + 2, C0{}, C2{});
-        if (u + 3 < nsteps) step(u + 3, C1{}, C0{});
-        if (u + 4 < nsteps) step(u + 4, C0{}, C1{});
-        if (u + 5 < nsteps) step(u + 5, C1{}, C2{});
+    for (uint32_t u = 0; u < nsteps; u += 2) {
+        step(u, C0{});
+        if (u + 1 < nsteps) step(u + 1, C1{});
     }
-    __builtin_amdgcn_s_waitcnt(kWaitAll);  // drain the clamped prefetches before exit
+    if constexpr (!SAMPLE) {
+        __syncthreads();
+        const uint32_t m = min(cl_n, kCl);
+        for (uint32_t i = tid; i < m; i += kFxThreads) {
+            const uint64_t v = cl[i];
+            const uint32_t q = (uint32_t)(v >> 32);
+            const uint32_t pos = atomicAdd(&a.counts[q], 1u);
+            if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = (uint32_t)v;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // drain the clamped prefetches before exit
 }
 
 // Probe selection: per query the 16 sampled rows with the largest MFMA scores

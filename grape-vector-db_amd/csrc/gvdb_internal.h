@@ -145,7 +145,7 @@ hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint3
 
 // ---- K4 flat exact search on bf16 MFMA (gvdb_flat.hip) ---------------------------
 // Candidate pass on bf16 MFMA + exact rerank + per-query certificate; see
-// gvdb_flat.hip.  rowsb: bf16 [KC][cap][64], KC = fx_kc(D).
+// gvdb_flat.hip.  rowsb: bf16 fragment-major mirror (fx_frag), KC = fx_kc(D).
 constexpr uint32_t kFxRows = 256;      // rows per tile
 constexpr uint32_t kFxQ = 256;         // query slots per launch group
 constexpr uint32_t kFxCandCap = 4096;  // candidates per query (LDS sort capacity)
@@ -153,19 +153,24 @@ constexpr uint32_t kFxMinN = 65536;    // smaller shards use the exact full scan
 constexpr uint32_t kFxSampleEvery = 64;  // sample pass: every 64th row tile
 __host__ __device__ inline uint32_t fx_kc(uint32_t D) { return (D + 63u) / 64u; }        // bf16 chunks
 __host__ __device__ inline uint32_t fx_kc_i8(uint32_t D) { return (D + 127u) / 128u; }  // i8 chunks
-// byte offset of (row, chunk c) in a tile-major flat mirror [ceil(cap/256)][KC][256][128 B]
-__host__ __device__ inline uint64_t fx_off(uint64_t row, uint32_t c, uint32_t KC) {
-    return ((((row >> 8) * KC + c) << 8) | (row & 255u)) * 128u;
+// Fragment-major flat mirror: per 256-row tile and 128-B chunk, 8 groups of
+// 32 rows, each [k-step s 0..3][lane 0..63][16 B] = 4 KiB, so one wave reads
+// the MFMA operand fragment of its 32 rows for one k-step as 1 KiB contiguous
+// (lane = 32 h + r holds bytes [32 s + 16 h, +16) of row r's chunk).  Byte
+// offset of 16-B piece pc (0..7) of chunk c of `row`; queries use the same
+// layout with the slot as the row (one tile).
+__host__ __device__ inline uint64_t fx_frag(uint64_t row, uint32_t c, uint32_t KC, uint32_t pc) {
+    return (((((row >> 8) * KC + c) * 8 + ((row >> 5) & 7u)) * 4 + (pc >> 1)) * 64 + (pc & 1u) * 32 + (row & 31u)) * 16;
 }
 __host__ __device__ inline uint64_t fx_mirror_bytes(uint64_t cap, uint32_t KC) {
     return ((cap + 255u) >> 8) * KC * 256u * 128u;
 }
 struct FlatMxArgs {
     int i8;                  // element kind: 1 = int8 (k_flat_mx<., true>), 0 = bf16
-    const void* rowsx;       // tile-major [tiles][KC][256][128 B] (fx_off): bf16 x64 or int8 x128 per chunk row
+    const void* rowsx;       // fragment-major mirror (fx_frag): bf16 x64 or int8 x128 per chunk row
     uint64_t cap;
     uint32_t N, KC;
-    const void* qx;          // [KC][kFxQ][128 B]
+    const void* qx;          // fragment-major (fx_frag), one 256-slot tile
     const float* qinv;       // [kFxQ]  bf16: 1/|q|; i8: s_q/|q|
     const float* rnorm;      // [N] exact row norms (bf16)
     const float* rscale;     // [N] s_x/|x| (i8)
@@ -181,7 +186,7 @@ struct FlatMxArgs {
     uint32_t* cand;          // emit pass: [B][candcap] candidate rows
     uint32_t candcap;
     uint32_t* overflow;      // emit pass: set to 1 if a wave's LDS staging slice overflowed
-    int dbg;                 // ablation timing only (GVDB_FLAT_DBG): 1 skip query loads, 2 skip row loads, 4 skip MFMA
+    int dbg;                 // unused (kept for ABI stability of the launch struct)
 };
 float flat_eps(uint32_t D);
 hipError_t launch_rows_to_bf16(const float* rows, uint64_t n, uint32_t D, uint16_t* rowsb, uint64_t cap,

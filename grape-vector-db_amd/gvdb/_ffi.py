@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libgvdb.so")
+# GVDB_LIB_PATH: an alternative build (timing ablations only)
+LIB_PATH = os.environ.get("GVDB_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "libgvdb.so")
 
 # gvdb_status (include/gvdb.h)
 GVDB_OK = 0
