@@ -611,6 +611,7 @@ const char* gvdb_status_string(gvdb_status s) {
         case GVDB_ERR_INVALID_ARGUMENT: return "InvalidArgument";
         case GVDB_ERR_DEVICE: return "DeviceError";
         case GVDB_ERR_OUT_OF_MEMORY: return "OutOfMemory";
+        case GVDB_ERR_STORAGE: return "Storage";
     }
     return "unknown";
 }
@@ -1168,6 +1169,34 @@ gvdb_status gvdb_index_get_stats(const gvdb_index* ix, gvdb_index_stats* out) {
 }
 
 const float* gvdb_index_device_rows(const gvdb_index* ix) { return ix ? ix->rows : nullptr; }
+
+gvdb_status gvdb_index_export(const gvdb_index* ix, float* rows, uint64_t* ids, uint64_t cap, uint64_t* n_out) {
+    if (!ix || !n_out) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    uint64_t live = 0;
+    for (uint64_t r = 0; r < ix->n; ++r) live += ix->h_ids[r] != kOrphan;
+    *n_out = live;
+    if (live == 0) return GVDB_OK;
+    if (cap < live) return fail(GVDB_ERR_INVALID_ARGUMENT, "export capacity below the live row count");
+    if (!rows || !ids) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(hipSetDevice(ix->device), "set device");
+    HIP_TRY(hipStreamSynchronize(ix->stream), "sync mutations");
+    const size_t rb = (size_t)ix->dim * 4;
+    // copy runs of live rows straight into place
+    uint64_t out = 0, r = 0;
+    while (r < ix->n) {
+        if (ix->h_ids[r] == kOrphan) {
+            ++r;
+            continue;
+        }
+        uint64_t e = r;
+        while (e < ix->n && ix->h_ids[e] != kOrphan) ids[out + (e - r)] = ix->h_ids[e], ++e;
+        HIP_TRY(hipMemcpy(rows + out * ix->dim, ix->rows + r * ix->dim, (e - r) * rb, hipMemcpyDeviceToHost),
+                "export rows");
+        out += e - r;
+        r = e;
+    }
+    return GVDB_OK;
+}
 
 // ---- kernel timing -------------------------------------------------------------------
 void gvdb_timing_enable(int32_t on) {

@@ -248,11 +248,19 @@ __global__ __launch_bounds__(256) void k_queries_to_i8(const float* __restrict__
 #ifndef FX_ABL
 #define FX_ABL 0
 #endif
+// FX_AMODE: how query chunks reach LDS.  1 (default): LDS DMA issued from
+// inline asm two steps ahead (no staging registers; asm so that the waitcnt
+// pass, which cannot tell a DMA into one buffer from ds_reads of another,
+// does not drain vmcnt before every fragment read) with a counted vmcnt
+// before the barrier.  0: VGPR staging + ds_write one step ahead.
+#ifndef FX_AMODE
+#define FX_AMODE 1
+#endif
 template <bool SAMPLE, bool I8>
 __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
-    // two distinct LDS objects (not one indexed array), each 1 query chunk
+    // three distinct LDS objects (not one indexed array), each 1 query chunk
     constexpr uint32_t kChunk = kFxQ * 128u;  // bytes of one query chunk
-    __shared__ __attribute__((aligned(16))) char As0[kChunk], As1[kChunk];
+    __shared__ __attribute__((aligned(16))) char As0[kChunk], As1[kChunk], As2[kChunk];
     // EMIT: the block's nominations, (query << 32) | row, flushed to the
     // global per-query lists once at the end (an LDS atomic per nomination
     // instead of a global atomic round trip inside the MFMA loop)
@@ -265,7 +273,8 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
     const char* qx = (const char*)a.qx;
     auto abuf = [&](auto I) -> char* {
         if constexpr (decltype(I)::value == 0) return As0;
-        else return As1;
+        else if constexpr (decltype(I)::value == 1) return As1;
+        else return As2;
     };
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -287,7 +296,30 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
         t = tile_of(j);
     };
     // query chunk of step u: wave wv stages bytes [4 KiB wv, +4 KiB), 1 KiB per load
-    fx_v4i qs[4];
+    constexpr bool kDma = FX_AMODE == 1;
+    // kDma: every vector-memory op of the step loop is inline asm with its
+    // waits placed by hand (counts below), so the compiler's waitcnt pass
+    // neither drains on the DMA nor miscounts around it
+    auto gload4 = [&](fx_v4i& d, const char* p) __attribute__((always_inline)) {
+        if constexpr (kDma) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+        else d = *(const fx_v4i*)p;
+    };
+    auto gload1 = [&](float& d, const float* p) __attribute__((always_inline)) {
+        if constexpr (kDma) asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+        else d = *p;
+    };
+    // DMA form: wave wv copies bytes [4 KiB wv, +4 KiB) of chunk u, 1 KiB per op
+    auto issueA = [&](uint32_t u, auto BI) __attribute__((always_inline)) {
+        uint32_t t, c;
+        step_of(u, t, c);
+        const char* ga = qx + (uint64_t)c * kChunk + wv * 4096u + lane * 16u;
+        const uint32_t l0 = (uint32_t)(uintptr_t)(abuf(BI) + wv * 4096u);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(ga + i * 1024), "s"(l0 + i * 1024u)
+                         : "memory");
+    };
+    fx_v4i qs[kDma ? 1 : 4];
     auto loadA = [&](uint32_t u) __attribute__((always_inline)) {
         uint32_t t, c;
         step_of(u, t, c);
@@ -318,34 +350,50 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[i][r][e] = 0;
     };
-    // row fragments [ring slot][r][k-step]: bf16 keeps two chunks in flight
-    // (slot = step parity), i8 (half the bytes per step) one
+    // row fragments [ring slot][r][k-step]: bf16 keeps kRing = 2 chunks in
+    // flight (slot = step parity); i8 has no registers to spare for a second
     constexpr int kRing = I8 ? 1 : 2;
     fx_v4i rf[kRing][2][4];
     const uint32_t abase = (wq * 16u * 64u + lane) * 16u;  // query groups 4 wq + i: +4 KiB i, +1 KiB s
+    // query fragments, double-buffered across k-steps AND across steps: the
+    // last k-step of step u reads k-step 0 of chunk u+1 (complete since the
+    // barrier of step u-1), so no LDS latency follows the barrier
+    fx_v4i fa[2][4];
+    auto rd = [&](const char* A, int s, int slot) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[slot][i] = *(const fx_v4i*)(A + abase + i * 4096 + s * 1024);
+    };
     // 4 k-steps of 16 (i8: 32) over one chunk; the query fragments of k-step
     // s+1 are read while the 8 MFMAs of k-step s run, and row fragment s is
     // reloaded for the next chunk as soon as its MFMAs have issued (pinned
     // there, so every row load has one whole chunk step to land)
-    auto mma = [&](uint32_t u, auto AI) __attribute__((always_inline)) {
-        constexpr int R = decltype(AI)::value % kRing;
-        const char* A = (const char*)abuf(AI) + abase;
+    auto mma = [&](uint32_t u, auto AI, auto RI) __attribute__((always_inline)) {
+        using A1 = std::integral_constant<int, (decltype(AI)::value + 1) % 3>;
+        constexpr int R = decltype(RI)::value;
+        const char* A = (const char*)abuf(AI);
         const char* rn = rowbase(u + kRing);
-        fx_v4i fa[2][4];
-        auto rd = [&](int s, int slot) __attribute__((always_inline)) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) fa[slot][i] = *(const fx_v4i*)(A + i * 4096 + s * 1024);
-        };
-        rd(0, 0);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            if (s + 1 < 4) rd(s + 1, (s + 1) & 1);
+            if (s + 1 < 4) rd(A, s + 1, (s + 1) & 1);
+            else if constexpr (!kDma) rd((const char*)abuf(A1{}), 0, 0);
+            __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this k-step's MFMAs
+            if constexpr (kDma) {
+                // rows k-step s of this chunk were loaded kRing steps ago after
+                // that step's k-step s; younger: 2 (3 - s) rows there, 4 DMA +
+                // 8 rows per step in between, then 4 DMA + 2 s rows here =
+                // 10 + 12 (kRing - 1), not counting the operand loads of
+                // tile-end steps (extra younger ops only make a wait stricter)
+                asm volatile("s_waitcnt vmcnt(%2)"
+                             : "+v"(rf[R][0][s]), "+v"(rf[R][1][s])
+                             : "n"(10 + 12 * (kRing - 1)));
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 2; ++r) {
                     if constexpr (FX_ABL & 8)
-                        acc[i][r][0] += __builtin_bit_cast(float, fa[s & 1][i][0] ^ rf[R][r][s][0]);
+                        acc[i][r][0] += __builtin_bit_cast(float, fa[s & 1][i][0] ^ rf[R][r][s][0] ^ rf[R][r][s][1] ^
+                                                                      rf[R][r][s][2] ^ rf[R][r][s][3]);
                     else if constexpr (I8)
                         acc[i][r] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s & 1][i], rf[R][r][s], acc[i][r], 0, 0, 0);
                     else
@@ -356,7 +404,9 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
             if constexpr (!(FX_ABL & 2)) {
                 if (!(FX_ABL & 16) || wq == 0) {
 #pragma unroll
-                    for (int r = 0; r < 2; ++r) rf[R][r][s] = *(const fx_v4i*)(rn + r * 4096 + s * 1024);
+                    for (int r = 0; r < 2; ++r) {
+                        gload4(rf[R][r][s], rn + r * 4096 + s * 1024);
+                    }
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -369,7 +419,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
     // per-row operands of the epilogue, (re)loaded every step so the
     // once-per-tile epilogue never waits on a global load: bf16 |x| (rv0),
     // i8 s_x/|x| (rv0) and rho_x (rv1), for this lane's rows r = 0, 1
-    float rv0[2], rv1[2];
+    float rv0[2] = {0.0f, 0.0f}, rv1[2] = {0.0f, 0.0f};
     auto load_rowops = [&](uint32_t u) __attribute__((always_inline)) {
         uint32_t t, c;
         step_of(u, t, c);
@@ -377,10 +427,10 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
         for (int r = 0; r < 2; ++r) {
             const uint32_t n = min(t * kFxRows + wr * 64u + r * 32u + (lane & 31u), N - 1u);
             if constexpr (I8) {
-                rv0[r] = a.rscale[n];
-                rv1[r] = a.rrho[n];
+                gload1(rv0[r], a.rscale + n);
+                gload1(rv1[r], a.rrho + n);
             } else {
-                rv0[r] = a.rnorm[n];
+                gload1(rv0[r], a.rnorm + n);
             }
         }
     };
@@ -458,23 +508,33 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
         }
     };
 
-    // Per step: the query chunk of step u+1 is loaded to VGPRs at the start,
-    // written to the other LDS buffer after the MFMAs (it was last read in
-    // step u-1, before that step's barrier), then one barrier.  The barrier
-    // waits for LDS only (vmcnt(63) lgkmcnt(0)): the row loads stay in flight.
+    // Per step u: the query chunk of step u+2 is loaded to VGPRs at the start
+    // and written to LDS buffer (u+2)%3 after the MFMAs (that buffer was last
+    // read in step u-1 and by step u-2's tail, both before the barrier of
+    // step u-1), then one barrier.  The barrier waits for LDS only (vmcnt(63)
+    // lgkmcnt(0)): the row loads stay in flight.
     constexpr int kWaitLds = (3 << 14) | 0x0070 | 0xF;  // vmcnt(63) expcnt(7) lgkmcnt(0)
     using C0 = std::integral_constant<int, 0>;
     using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
 #pragma unroll
     for (int k = 0; k < kRing; ++k) {
         const char* r0 = rowbase(k);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int r = 0; r < 2; ++r) rf[k][r][s] = *(const fx_v4i*)(r0 + r * 4096 + s * 1024);
+            for (int r = 0; r < 2; ++r) gload4(rf[k][r][s], r0 + r * 4096 + s * 1024);
     }
-    loadA(0);
-    storeA(C0{});
+    if constexpr (kDma) {
+        issueA(0, C0{});
+        issueA(1, C1{});
+        __builtin_amdgcn_s_waitcnt(0);
+    } else {
+        loadA(0);
+        storeA(C0{});
+        loadA(1);
+        storeA(C1{});
+    }
     if (tid == 0) cl_n = 0;
     if (tid < kFxQ) {
         qinv_l[tid] = a.qinv[tid];
@@ -484,26 +544,53 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
     __builtin_amdgcn_s_waitcnt(kWaitLds);
     __builtin_amdgcn_s_barrier();
     zero();
-    // step u reads A buffer u%2 (two steps per loop trip keep it static)
-    auto step = [&](uint32_t u, auto AI) __attribute__((always_inline)) {
-        using AN = std::integral_constant<int, 1 - decltype(AI)::value>;
-        __builtin_amdgcn_sched_barrier(0);
-        loadA(u + 1);
-        load_rowops(u);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(u, AI);
-        storeA(AN{});  // before the epilogue: its staging registers are free there
+    if constexpr (!kDma) rd((const char*)As0, 0, 0);
+    // step u reads A buffer u%3 (three steps per loop trip keep it static)
+    auto step = [&](uint32_t u, auto AI, auto RI) __attribute__((always_inline)) {
+        using AN = std::integral_constant<int, (decltype(AI)::value + 2) % 3>;
         const uint32_t j = u / KC;
-        if (u - j * KC == KC - 1) {
+        const bool tile_end = u - j * KC == KC - 1;
+        __builtin_amdgcn_sched_barrier(0);
+        if (tile_end) load_rowops(u);  // before the DMA: waiting for these does not wait for it
+        if constexpr (kDma) issueA(u + 2, AN{});
+        else loadA(u + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kDma) rd((const char*)abuf(AI), 0, 0);
+        mma(u, AI, RI);
+        if constexpr (!kDma) storeA(AN{});  // before the epilogue: its staging registers are free there
+        if (tile_end) {
+            if constexpr (kDma) {  // the operand loads: 4 DMA + 8 rows younger
+#pragma unroll
+                for (int r = 0; r < 2; ++r) asm volatile("s_waitcnt vmcnt(12)" : "+v"(rv0[r]), "+v"(rv1[r]));
+            }
             if constexpr (!(FX_ABL & 4)) epilogue(j);
             zero();
         }
-        __builtin_amdgcn_s_waitcnt(kWaitLds);
+        // DMA: chunk u+1 (issued at the start of step u-1) has at least
+        // 8 (step u-1) + 4 + 8 (step u) = 20 younger vector-memory ops (more
+        // only make the wait stricter): vmcnt(20) retires it and leaves the
+        // row loads in flight
+        if constexpr (kDma) asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
+        else __builtin_amdgcn_s_waitcnt(kWaitLds);
         __builtin_amdgcn_s_barrier();
     };
-    for (uint32_t u = 0; u < nsteps; u += 2) {
-        step(u, C0{});
-        if (u + 1 < nsteps) step(u + 1, C1{});
+    // six steps per trip keep the A buffer (u%3) and the row slot (u%kRing) static
+    using R1 = std::integral_constant<int, 1 % kRing>;
+    for (uint32_t u = 0; u < nsteps; u += 6) {
+        step(u, C0{}, C0{});
+        if (u + 1 < nsteps) step(u + 1, C1{}, R1{});
+        if (u + 2 < nsteps) step(u + 2, C2{}, C0{});
+        if (u + 3 < nsteps) step(u + 3, C0{}, R1{});
+        if (u + 4 < nsteps) step(u + 4, C1{}, C0{});
+        if (u + 5 < nsteps) step(u + 5, C2{}, R1{});
+    }
+    // the clamped prefetches of the last steps land before any register is reused
+    if constexpr (kDma) {
+#pragma unroll
+        for (int k = 0; k < kRing; ++k)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(rf[k][0][s]), "+v"(rf[k][1][s]) : : "memory");
     }
     if constexpr (!SAMPLE) {
         __syncthreads();
@@ -534,27 +621,37 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
     // costs one compare + ballot unless a lane beats the current 16th key
     uint64_t mine = 0, t16 = 0;
     const float* src = smp + (uint64_t)q * S;
-    for (uint32_t i0 = wv * 64u; i0 < S; i0 += 1024u * 4u) {
-        uint64_t k4[4];
+    // 8 values per lane per batch, the next batch loaded while this one is
+    // merged (the scan is latency-bound otherwise: one block per query)
+    constexpr int kU = 8;
+    auto load = [&](uint32_t i0, float (&v)[kU]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {  // 16 waves x 4 loads in flight per lane
+        for (int u = 0; u < kU; ++u) {
             const uint32_t i = i0 + u * 1024u + lane;
-            const float v = i < S ? src[i] : -__builtin_inff();
-            k4[u] = v > -__builtin_inff() ? (((uint64_t)f32_order(v) << 32) | i) : 0ull;  // NaN / padding -> empty
+            v[u] = i < S ? src[i] : -__builtin_inff();
         }
+    };
+    float vc[kU], vn[kU];
+    load(wv * 64u, vn);
+    for (uint32_t i0 = wv * 64u; i0 < S; i0 += 1024u * kU) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            uint64_t m = __ballot(k4[u] > t16);
+        for (int u = 0; u < kU; ++u) vc[u] = vn[u];
+        load(i0 + 1024u * kU, vn);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t i = i0 + u * 1024u + lane;
+            const uint64_t key = vc[u] > -__builtin_inff() ? (((uint64_t)f32_order(vc[u]) << 32) | i) : 0ull;  // NaN / padding -> empty
+            uint64_t m = __ballot(key > t16);
             while (m) {
                 const uint32_t l = __builtin_ctzll(m);
                 m &= m - 1;
-                const uint64_t key = __shfl(k4[u], l);
-                if (key <= t16) continue;
+                const uint64_t kk = __shfl(key, l);
+                if (kk <= t16) continue;
                 // insert into lanes 0..15: lanes holding a smaller key shift down
                 const uint64_t up = __shfl_up(mine, 1);
-                const bool below = lane < 16 && key > mine;
-                const bool first = below && (lane == 0 || up >= key);
-                mine = first ? key : (below ? up : mine);
+                const bool below = lane < 16 && kk > mine;
+                const bool first = below && (lane == 0 || up >= kk);
+                mine = first ? kk : (below ? up : mine);
                 t16 = __shfl(mine, 15);
             }
         }

@@ -78,8 +78,13 @@ class OutOfMemory(DeviceError):
     code = _ffi.GVDB_ERR_OUT_OF_MEMORY
 
 
+class StorageError(VectorDbError):
+    """VectorDbError::Storage(String): index file IO / format errors."""
+    code = _ffi.GVDB_ERR_STORAGE
+
+
 _ERRORS = {c.code: c for c in (IndexNotBuilt, DimensionMismatch, InvalidVectorDimension, QuantizationError,
-                               IndexError_, InvalidArgument, DeviceError, OutOfMemory)}
+                               IndexError_, InvalidArgument, DeviceError, OutOfMemory, StorageError)}
 
 
 def check(status: int) -> None:
@@ -382,6 +387,125 @@ class GpuVectorIndex:
         check(self._lib.gvdb_index_get_stats(self._h, C.byref(s)))
         return IndexStats(int(s.vector_count), int(s.dimension), self.index_type, int(s.memory_usage),
                           int(s.device_bytes))
+
+
+    # -- persistence (QueryEngine::save_index / load_index, query.rs:282-409) --
+    def get_all_vectors(self) -> List[Tuple[str, np.ndarray]]:
+        """index.rs:120-135: every live (id, vector), sorted by id."""
+        ids, rows = self._export()
+        out = [(self._str_of[int(u)], rows[i]) for i, u in enumerate(ids)]
+        out.sort(key=lambda t: t[0])
+        return out
+
+    def _export(self):
+        """(u64 ids, rows) of the live rows, device -> host."""
+        cap = self.len()
+        D = self.get_stats().dimension
+        rows = np.empty((cap, D), np.float32)
+        ids = np.empty(cap, np.uint64)
+        n = C.c_uint64()
+        if cap:
+            check(self._lib.gvdb_index_export(self._h, ptr(rows), ptr(ids), cap, C.byref(n)))
+        return ids[: n.value], rows[: n.value]
+
+    def save_index(self, path: str, config: Optional["HnswConfig"] = None, created_at: Optional[str] = None,
+                   level: int = -1, batch: int = 1 << 16) -> None:
+        """Write the reference's index file (gzip(postcard(IndexPersistenceData)),
+        query.rs:16-28, 282-330): metadata {dimension, total_points, created_at,
+        HnswConfig} then every live (id, vector) sorted by id."""
+        import os
+
+        cfg = config or HnswConfig()
+        ids, rows = self._export()
+        names = [self._str_of[int(u)] for u in ids]
+        order = sorted(range(len(names)), key=names.__getitem__)
+        D = rows.shape[1] if rows.ndim == 2 else 0
+        m = _ffi.gvdb_persist_meta(D or self.get_stats().dimension, len(order), cfg.m, cfg.ef_construction,
+                                   cfg.ef_search, cfg.max_layers, (created_at or utc_now_rfc3339()).encode())
+        parent = os.path.dirname(os.path.abspath(path))
+        os.makedirs(parent, exist_ok=True)  # query.rs:286-290 creates the directory
+        w = C.c_void_p()
+        check(self._lib.gvdb_persist_create(path.encode(), C.byref(m), len(order), level, C.byref(w)))
+        try:
+            for b0 in range(0, len(order), batch):
+                sel = order[b0:b0 + batch]
+                enc = [names[i].encode() for i in sel]
+                offs = np.zeros(len(enc) + 1, np.uint64)
+                offs[1:] = np.cumsum([len(e) for e in enc])
+                blob = b"".join(enc) or b"\0"
+                r = np.ascontiguousarray(rows[sel])
+                check(self._lib.gvdb_persist_append(w, ptr(r), len(sel), D, blob, ptr(offs)))
+        except BaseException:
+            self._lib.gvdb_persist_close(w)
+            raise
+        check(self._lib.gvdb_persist_close(w))
+
+    def load_index(self, path: str, batch: int = 1 << 16) -> "PersistMetadata":
+        """query.rs:335-409: read the file, check its dimension against this
+        index's (DimensionMismatch), then replace the contents with its
+        vectors in file order.  Returns the stored metadata."""
+        m = _ffi.gvdb_persist_meta()
+        cnt = C.c_uint64()
+        r = C.c_void_p()
+        check(self._lib.gvdb_persist_open(path.encode(), C.byref(m), C.byref(cnt), C.byref(r)))
+        try:
+            D = int(m.dimension)
+            mine = self.get_stats().dimension
+            if mine and mine != D:
+                raise DimensionMismatch(f"Dimension mismatch: expected {mine}, actual {D}", mine, D)
+            self.clear()
+            self._id_of, self._str_of = {}, []
+            rows = np.empty((batch, D), np.float32)
+            offs = np.empty(batch + 1, np.uint64)
+            cap = batch * 64
+            blob = C.create_string_buffer(cap)
+            got = C.c_uint64()
+            while True:
+                check(self._lib.gvdb_persist_next(r, ptr(rows), D, batch, blob, cap, ptr(offs), C.byref(got)))
+                n = got.value
+                if n == 0:
+                    break
+                raw = blob.raw
+                names = [raw[int(offs[i]):int(offs[i + 1])].decode() for i in range(n)]
+                self.add_batch(np.array([self._u64(x) for x in names], np.uint64), rows[:n])
+        finally:
+            self._lib.gvdb_persist_free(r)
+        return PersistMetadata(int(m.dimension), int(m.total_points), m.created_at.decode(),
+                               HnswConfig(int(m.m), int(m.ef_construction), int(m.ef_search), int(m.max_layers)))
+
+
+@dataclass
+class HnswConfig:
+    """config.rs:196-209 (defaults config.rs:413-422)."""
+    m: int = 16
+    ef_construction: int = 200
+    ef_search: int = 100
+    max_layers: int = 16
+
+
+@dataclass
+class PersistMetadata:
+    """IndexMetadata (query.rs:23-28)."""
+    dimension: int
+    total_points: int
+    created_at: str
+    config: HnswConfig
+
+
+def utc_now_rfc3339() -> str:
+    """chrono's serde form of Utc::now() (RFC 3339, SecondsFormat::AutoSi, 'Z')."""
+    import time
+
+    ns = time.time_ns()
+    sec, frac = divmod(ns, 1_000_000_000)
+    base = time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(sec))
+    if frac == 0:
+        return base + "Z"
+    if frac % 1_000_000 == 0:
+        return f"{base}.{frac // 1_000_000:03d}Z"
+    if frac % 1000 == 0:
+        return f"{base}.{frac // 1000:06d}Z"
+    return f"{base}.{frac:09d}Z"
 
 
 HnswVectorIndex = GpuVectorIndex

@@ -24,6 +24,7 @@ GVDB_ERR_INDEX = 5
 GVDB_ERR_INVALID_ARGUMENT = 6
 GVDB_ERR_DEVICE = 7
 GVDB_ERR_OUT_OF_MEMORY = 8
+GVDB_ERR_STORAGE = 9
 
 GVDB_METRIC_COSINE = 0
 GVDB_METRIC_L2 = 1
@@ -76,6 +77,18 @@ class gvdb_bm25_stats(C.Structure):
     ]
 
 
+class gvdb_persist_meta(C.Structure):
+    _fields_ = [
+        ("dimension", C.c_uint64),
+        ("total_points", C.c_uint64),
+        ("m", C.c_uint64),
+        ("ef_construction", C.c_uint64),
+        ("ef_search", C.c_uint64),
+        ("max_layers", C.c_uint64),
+        ("created_at", C.c_char * 64),
+    ]
+
+
 P = C.c_void_p
 u32, u64, i32, f32 = C.c_uint32, C.c_uint64, C.c_int32, C.c_float
 PU64, PU32, PF32 = C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_float)
@@ -108,6 +121,13 @@ SIGNATURES = {
     "gvdb_index_clear": (None, [P]),
     "gvdb_index_get_stats": (C.c_int, [P, C.POINTER(gvdb_index_stats)]),
     "gvdb_index_device_rows": (P, [P]),
+    "gvdb_index_export": (C.c_int, [P, P, P, u64, PU64]),
+    "gvdb_persist_create": (C.c_int, [C.c_char_p, C.POINTER(gvdb_persist_meta), u64, i32, C.POINTER(P)]),
+    "gvdb_persist_append": (C.c_int, [P, P, u64, u32, P, P]),
+    "gvdb_persist_close": (C.c_int, [P]),
+    "gvdb_persist_open": (C.c_int, [C.c_char_p, C.POINTER(gvdb_persist_meta), PU64, C.POINTER(P)]),
+    "gvdb_persist_next": (C.c_int, [P, P, u32, u64, P, u64, P, PU64]),
+    "gvdb_persist_free": (None, [P]),
     "gvdb_bq_quantize": (C.c_int, [P, u64, u32, f32, P]),
     "gvdb_bq_quantize_device": (C.c_int, [P, u64, u32, f32, P, P]),
     "gvdb_bq_hamming": (C.c_int, [P, P, u64, u32, P]),

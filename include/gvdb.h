@@ -48,7 +48,8 @@ typedef enum gvdb_status {
     GVDB_ERR_INDEX = 5,                    /* VectorDbError::IndexError(String)          */
     GVDB_ERR_INVALID_ARGUMENT = 6,         /* null pointer / bad size at the ABI          */
     GVDB_ERR_DEVICE = 7,                   /* HIP runtime / kernel failure                */
-    GVDB_ERR_OUT_OF_MEMORY = 8             /* device allocation failed                    */
+    GVDB_ERR_OUT_OF_MEMORY = 8,            /* device allocation failed                    */
+    GVDB_ERR_STORAGE = 9                   /* VectorDbError::Storage(String): index file IO */
 } gvdb_status;
 
 /* Scores reported by gvdb_index_search*. */
@@ -120,6 +121,37 @@ gvdb_status gvdb_timing_read(uint32_t which, double* total_ms, uint64_t* launche
 uint64_t gvdb_flat_fallback_count(void);
 uint64_t gvdb_flat_i8_fallback_count(void);
 
+/* ---- persistence: QueryEngine::save_index / load_index (query.rs:282-409) --
+ * File = gzip(postcard(IndexPersistenceData)) exactly as the reference writes
+ * it (query.rs:16-28): IndexMetadata {dimension, total_points, created_at
+ * (RFC 3339 string), HnswConfig {m, ef_construction, ef_search, max_layers}}
+ * then Vec<(String id, Vec<f32>)>.  Streaming: create declares the vector
+ * count, append adds batches (ids as a byte blob + n+1 offsets), close checks
+ * the count; open returns the metadata and count, next returns batches.
+ * Host-only (no device work): rows come from gvdb_index_export and go back
+ * through gvdb_index_add.  IO / format errors are GVDB_ERR_STORAGE. */
+typedef struct gvdb_persist_meta {
+    uint64_t dimension;
+    uint64_t total_points;
+    uint64_t m, ef_construction, ef_search, max_layers; /* HnswConfig (config.rs:196-209) */
+    char created_at[64];                                 /* NUL-terminated RFC 3339 */
+} gvdb_persist_meta;
+typedef struct gvdb_persist_writer gvdb_persist_writer;
+typedef struct gvdb_persist_reader gvdb_persist_reader;
+/* level: gzip level 0-9, < 0 = flate2's Compression::default() (6) */
+gvdb_status gvdb_persist_create(const char* path, const gvdb_persist_meta* meta, uint64_t n_vectors, int32_t level,
+                                gvdb_persist_writer** out);
+gvdb_status gvdb_persist_append(gvdb_persist_writer* w, const float* rows, uint64_t n, uint32_t dim,
+                                const char* id_blob, const uint64_t* id_offs);
+gvdb_status gvdb_persist_close(gvdb_persist_writer* w);
+gvdb_status gvdb_persist_open(const char* path, gvdb_persist_meta* meta, uint64_t* n_vectors,
+                              gvdb_persist_reader** out);
+/* Up to max_n entries whose ids fit in blob_cap bytes; a stored vector whose
+ * length differs from dim is GVDB_ERR_DIMENSION_MISMATCH (index.rs:187-210). */
+gvdb_status gvdb_persist_next(gvdb_persist_reader* r, float* rows, uint32_t dim, uint64_t max_n, char* id_blob,
+                              uint64_t blob_cap, uint64_t* id_offs, uint64_t* n_out);
+void gvdb_persist_free(gvdb_persist_reader* r);
+
 /* ---- VectorIndex (index.rs:35-62) --------------------------------------- */
 /* HnswVectorIndex::new / with_config (index.rs:100-117) */
 gvdb_status gvdb_index_create(const gvdb_params* params, gvdb_index** out);
@@ -171,6 +203,10 @@ void gvdb_index_clear(gvdb_index* index);
 gvdb_status gvdb_index_get_stats(const gvdb_index* index, gvdb_index_stats* out);
 /* Device pointers of the resident corpus, for sharded drivers and tests. */
 const float* gvdb_index_device_rows(const gvdb_index* index);
+/* Live rows and their u64 ids, device -> host, in row order (the source of
+ * HnswVectorIndex::get_all_vectors, index.rs:120-135).  cap < live count:
+ * GVDB_ERR_INVALID_ARGUMENT with *n_out = the live count. */
+gvdb_status gvdb_index_export(const gvdb_index* index, float* rows, uint64_t* ids, uint64_t cap, uint64_t* n_out);
 
 /* ---- BinaryQuantizer (quantization.rs:67-216) --------------------------- */
 /* quantize / quantize_batch (86-127): n rows of D f32 -> n rows of
