@@ -145,13 +145,13 @@ struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
-        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe;
+        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     ~Workspace() {
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
                         &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
-                        &fx_scores})
+                        &fx_scores, &flt_rows, &flt_ids})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -949,7 +949,7 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
         HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
         HIP_TRY(launch_row_norms(d_q, B, dim, ws.qnorm.as<float>(), s), "qnorm");
         HIP_TRY(launch_flat_scores(d_q, (uint32_t)B, ws.qnorm.as<float>(), ix->rows, (uint32_t)ix->n, dim, ix->norms,
-                                   kind, ws.scores.as<float>(), s),
+                                   kind, nullptr, ws.scores.as<float>(), s),
                 "flat scores");
         const size_t need = flat_select_bytes((uint32_t)ix->n);
         HIP_TRY(ws.sort_tmp.ensure(need), "alloc sort tmp");
@@ -1010,6 +1010,75 @@ gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64
     st = index_search_impl(ix, ws.q.as<float>(), B, dim, k, sp, ws.out_ids.as<uint64_t>(), ws.out_scores.as<float>(),
                            ws.out_n.as<uint32_t>(), ws, s);
     if (st != GVDB_OK) return st;
+    HIP_TRY(hipMemcpyAsync(out_ids, ws.out_ids.p, B * k * 8, hipMemcpyDeviceToHost, s), "download ids");
+    HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
+    HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download n");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    return GVDB_OK;
+}
+
+// Filtered search (§8(f) rank 4): the pre-mask of FilterEngine::execute_filter
+// (filtering.rs:374) -> exact scan of the allowed rows only.  The allowed ids
+// are mapped to live rows on the host (unknown ids are ignored, repeats count
+// once), sorted by row so ties keep the unfiltered scan's row order, and the
+// exact flat kernels run over that row list.
+gvdb_status gvdb_index_search_filtered(const gvdb_index* ix, const float* queries, uint64_t B, uint32_t dim, uint64_t k,
+                                       const gvdb_search_params* sp_in, const uint64_t* allowed, uint64_t n_allowed,
+                                       uint64_t* out_ids, float* out_scores, uint32_t* out_n) {
+    gvdb_status st = check_search(ix, dim, B, k);
+    if (st != GVDB_OK) return st;
+    if (B == 0) return GVDB_OK;
+    if (!queries || !out_n || (k && (!out_ids || !out_scores)) || (n_allowed && !allowed))
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    std::vector<uint32_t> rows;
+    rows.reserve((size_t)std::min<uint64_t>(n_allowed, ix->n));
+    for (uint64_t i = 0; i < n_allowed; ++i) {
+        auto it = ix->id_row.find(allowed[i]);
+        if (it != ix->id_row.end()) rows.push_back((uint32_t)it->second);
+    }
+    std::sort(rows.begin(), rows.end());
+    rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+    const uint64_t M = rows.size();
+    if (k == 0 || M == 0) {
+        memset(out_n, 0, B * 4);
+        return GVDB_OK;
+    }
+    std::vector<uint64_t> sub_ids(M);
+    for (uint64_t j = 0; j < M; ++j) sub_ids[j] = ix->h_ids[rows[j]];
+    gvdb_search_params sp{};
+    sp.metric = GVDB_METRIC_COSINE;
+    if (sp_in) sp = *sp_in;
+    const int kind = sp.metric == GVDB_METRIC_L2 ? kScoreL2
+                     : sp.metric == GVDB_METRIC_COSINE_DISTANCE ? kScoreCosineDistance
+                                                                 : kScoreCosine;
+    if ((st = set_device(ix->device)) != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    hipStream_t s = ws.stream;
+    HIP_TRY(hipStreamSynchronize(ix->stream), "sync mutations");
+    HIP_TRY(ws.q.ensure(B * dim * 4), "alloc queries");
+    HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
+    HIP_TRY(ws.flt_rows.ensure(M * 4), "alloc filter rows");
+    HIP_TRY(ws.flt_ids.ensure(M * 8), "alloc filter ids");
+    HIP_TRY(ws.scores.ensure(B * M * 4), "alloc filtered scores");
+    HIP_TRY(ws.flags.ensure(16), "alloc flags");
+    HIP_TRY(ws.sort_tmp.ensure(flat_select_bytes((uint32_t)M)), "alloc sort tmp");
+    HIP_TRY(ws.out_ids.ensure(B * k * 8), "alloc out");
+    HIP_TRY(ws.out_scores.ensure(B * k * 4), "alloc out");
+    HIP_TRY(ws.out_n.ensure(B * 4), "alloc out");
+    HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
+    HIP_TRY(hipMemcpyAsync(ws.q.p, queries, B * dim * 4, hipMemcpyHostToDevice, s), "upload queries");
+    HIP_TRY(hipMemcpyAsync(ws.flt_rows.p, rows.data(), M * 4, hipMemcpyHostToDevice, s), "upload filter rows");
+    HIP_TRY(hipMemcpyAsync(ws.flt_ids.p, sub_ids.data(), M * 8, hipMemcpyHostToDevice, s), "upload filter ids");
+    HIP_TRY(launch_row_norms(ws.q.as<float>(), B, dim, ws.qnorm.as<float>(), s), "qnorm");
+    HIP_TRY(launch_flat_scores(ws.q.as<float>(), (uint32_t)B, ws.qnorm.as<float>(), ix->rows, (uint32_t)M, dim,
+                               ix->norms, kind, ws.flt_rows.as<uint32_t>(), ws.scores.as<float>(), s),
+            "filtered scores");
+    HIP_TRY(launch_flat_select(ws.scores.as<float>(), (uint32_t)B, (uint32_t)M, (uint32_t)k, kind == kScoreCosine, 0,
+                               0.0f, ws.flt_ids.as<uint64_t>(), ws.out_ids.as<uint64_t>(), ws.out_scores.as<float>(),
+                               ws.out_n.as<uint32_t>(), ws.sort_tmp.p, ws.sort_tmp.n, ws.flags.as<uint32_t>() + 1, s),
+            "filtered select");
     HIP_TRY(hipMemcpyAsync(out_ids, ws.out_ids.p, B * k * 8, hipMemcpyDeviceToHost, s), "download ids");
     HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
     HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download n");
@@ -1364,7 +1433,7 @@ gvdb_status gvdb_flat_search(const float* queries, uint64_t B, const float* rows
     HIP_TRY(launch_row_norms(ws.rows.as<float>(), N, D, ws.norms.as<float>(), s), "norms");
     HIP_TRY(launch_row_norms(ws.q.as<float>(), B, D, ws.qnorm.as<float>(), s), "qnorm");
     HIP_TRY(launch_flat_scores(ws.q.as<float>(), (uint32_t)B, ws.qnorm.as<float>(), ws.rows.as<float>(), (uint32_t)N, D,
-                               ws.norms.as<float>(), kind, ws.scores.as<float>(), s),
+                               ws.norms.as<float>(), kind, nullptr, ws.scores.as<float>(), s),
             "flat scores");
     HIP_TRY(launch_flat_select(ws.scores.as<float>(), (uint32_t)B, (uint32_t)N, (uint32_t)limit, kind == kScoreCosine,
                                has_threshold && kind == kScoreCosine, threshold, nullptr, ws.out_ids.as<uint64_t>(),

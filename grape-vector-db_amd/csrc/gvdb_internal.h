@@ -132,8 +132,11 @@ size_t final_sort_global_bytes(uint32_t R);
 hipError_t launch_final_sort_global(const FinalArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s);
 
 // ---- flat exact scan (storage.rs:296-339, index.rs:620-640) --------------------
+// list (optional, [N]): scan the shard rows list[0..N) instead of rows 0..N-1
+// (filtered search); scores stay indexed by scan position.
 hipError_t launch_flat_scores(const float* q, uint32_t B, const float* qnorm, const float* rows, uint32_t N,
-                              uint32_t D, const float* norms, int kind, float* scores /*[B][N]*/, hipStream_t s);
+                              uint32_t D, const float* norms, int kind, const uint32_t* list,
+                              float* scores /*[B][N]*/, hipStream_t s);
 size_t flat_select_bytes(uint32_t N);
 // per query: keep score >= threshold when has_threshold (cosine), stable sort,
 // first `limit`.

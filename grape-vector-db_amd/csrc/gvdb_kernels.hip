@@ -1858,15 +1858,18 @@ constexpr int kFlatQT = 16;
 __global__ __launch_bounds__(256) void k_flat_scores(const float* __restrict__ q, uint32_t B,
                                                      const float* __restrict__ qnorm, const float* __restrict__ rows,
                                                      uint32_t N, uint32_t D, const float* __restrict__ norms, int kind,
-                                                     float* __restrict__ scores) {
+                                                     const uint32_t* __restrict__ list, float* __restrict__ scores) {
     __shared__ __attribute__((aligned(16))) float tiles[4][64 * kTileLd];
     __shared__ __attribute__((aligned(16))) float qs[kFlatQT][kCh];
     __shared__ uint64_t bases[4][64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    // row: position in the scan (scores column); src: the shard row it reads
+    // (list[row] for a filtered scan, else row itself)
     const uint64_t row = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t src = row < N ? (list ? (uint64_t)list[row] : row) : 0;
     const uint32_t q0 = blockIdx.y * kFlatQT;
     const uint32_t qn = (B - q0) < (uint32_t)kFlatQT ? (B - q0) : (uint32_t)kFlatQT;
-    bases[wv][lane] = row < N ? row * D : ~0ull;
+    bases[wv][lane] = row < N ? src * D : ~0ull;
     float* tile = tiles[wv];
     const bool vec4 = (D & 3u) == 0;
     float acc[kFlatQT];
@@ -1898,7 +1901,7 @@ __global__ __launch_bounds__(256) void k_flat_scores(const float* __restrict__ q
         __syncthreads();
     }
     if (row >= N) return;
-    const float nb = norms ? norms[row] : 0.0f;
+    const float nb = norms ? norms[src] : 0.0f;
 #pragma unroll
     for (int i = 0; i < kFlatQT; ++i) {
         if ((uint32_t)i >= qn) break;
@@ -1917,10 +1920,10 @@ __global__ __launch_bounds__(256) void k_flat_scores(const float* __restrict__ q
 }
 
 hipError_t launch_flat_scores(const float* q, uint32_t B, const float* qnorm, const float* rows, uint32_t N, uint32_t D,
-                              const float* norms, int kind, float* scores, hipStream_t s) {
+                              const float* norms, int kind, const uint32_t* list, float* scores, hipStream_t s) {
     if (B == 0 || N == 0) return hipSuccess;
     hipLaunchKernelGGL(k_flat_scores, dim3((N + 255) / 256, (B + kFlatQT - 1) / kFlatQT), dim3(256), 0, s, q, B, qnorm,
-                       rows, N, D, norms, kind, scores);
+                       rows, N, D, norms, kind, list, scores);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

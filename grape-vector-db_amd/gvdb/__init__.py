@@ -339,6 +339,29 @@ class GpuVectorIndex:
         check(self._lib.gvdb_index_search(self._h, ptr(q), B, D, k, C.byref(sp), ptr(ids), ptr(sc), ptr(n)))
         return ids[:, :k], sc[:, :k], n
 
+    def search_batch_filtered(self, queries: np.ndarray, k: int, allowed: Iterable[str],
+                              params: Optional[SearchParams] = None):
+        """Vector search restricted to the ids a FilterEngine::execute_filter
+        (filtering.rs:374) returned: exact scan of those rows (metric of
+        ``params``); ids the index does not hold are ignored."""
+        q = _f32(queries)
+        if q.ndim == 1:
+            q = q.reshape(1, -1)
+        B, D = q.shape
+        sp = (params or self.params).to_c()
+        al = np.array([self._id_of[s] for s in allowed if s in self._id_of], np.uint64)
+        ids = np.zeros((B, max(k, 1)), np.uint64)
+        sc = np.zeros((B, max(k, 1)), np.float32)
+        n = np.zeros(B, np.uint32)
+        check(self._lib.gvdb_index_search_filtered(self._h, ptr(q), B, D, k, C.byref(sp), ptr(al) if al.size else None,
+                                                   al.size, ptr(ids), ptr(sc), ptr(n)))
+        return ids[:, :k], sc[:, :k], n
+
+    def search_filtered(self, query: Sequence[float], k: int, allowed: Iterable[str],
+                        params: Optional[SearchParams] = None) -> List[Tuple[str, float]]:
+        ids, sc, n = self.search_batch_filtered(_f32(query).reshape(1, -1), k, allowed, params)
+        return [(self._str_of[int(ids[0, i])], float(sc[0, i])) for i in range(int(n[0]))]
+
     def search_device(self, queries, k: int, out_ids, out_scores, out_n=None, params: Optional[SearchParams] = None,
                       stream: Optional[int] = None) -> None:
         sp = (params or self.params).to_c()

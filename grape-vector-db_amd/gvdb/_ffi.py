@@ -114,6 +114,7 @@ SIGNATURES = {
     "gvdb_index_search_device": (C.c_int, [P, P, u64, u32, u64, C.POINTER(gvdb_search_params), P, P, P, P]),
     "gvdb_index_bq_topr_device": (C.c_int, [P, P, u64, u32, u64, P, P, P]),
     "gvdb_index_bq_candidates_device": (C.c_int, [P, P, u64, u32, u64, P, P, P, P]),
+    "gvdb_index_search_filtered": (C.c_int, [P, P, u64, u32, u64, C.POINTER(gvdb_search_params), P, u64, P, P, P]),
     "gvdb_index_remove": (C.c_int, [P, u64, C.POINTER(i32)]),
     "gvdb_index_len": (u64, [P]),
     "gvdb_index_is_empty": (i32, [P]),

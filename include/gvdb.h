@@ -195,6 +195,15 @@ gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* index, const float
                                             uint32_t* d_out_dist, float* d_out_scores, void* stream);
 /* remove_vector (index.rs:233-285): order-preserving compaction. *removed=1
  * if the id was present. */
+/* Filtered search: the pre-mask of FilterEngine::execute_filter
+ * (filtering.rs:374, whose Vec<String> result maps to u64 ids through the host
+ * table) applied to the vector search — exact scan (the metric of
+ * sp->metric; sp->mode is ignored) over the live rows whose id is in
+ * allowed[0..n_allowed); unknown ids are ignored, repeats count once, equal
+ * scores keep row order.  Host buffers. */
+gvdb_status gvdb_index_search_filtered(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
+                                       uint64_t k, const gvdb_search_params* sp, const uint64_t* allowed,
+                                       uint64_t n_allowed, uint64_t* out_ids, float* out_scores, uint32_t* out_n);
 gvdb_status gvdb_index_remove(gvdb_index* index, uint64_t id, int32_t* removed);
 uint64_t gvdb_index_len(const gvdb_index* index);
 int32_t gvdb_index_is_empty(const gvdb_index* index);

@@ -476,3 +476,41 @@ def test_reference_unit_tests_through_cpp_mirror(g):
     exe = os.path.join(os.path.dirname(g.lib()._name), "build", "reference_tests")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+# --------------------------------------------------------------------------- filtered search
+@pytest.mark.parametrize("metric", [0, 1, 2])
+def test_search_filtered_matches_oracle_on_subset(g, oracle_mod, metric):
+    """§8(f) rank 4: search restricted to an execute_filter id set = the
+    exact scan (storage.rs:296-339 / index.rs:69-78 / index.rs:686-700) over
+    those rows only."""
+    N, D = 3000, 48
+    x = rng_rows(31, N, D, dup=20)
+    Q = rng_rows(32, 5, D)
+    ix = g.GpuVectorIndex(dimension=D)
+    ids = [f"doc{i}" for i in range(N)]
+    ix.add_vectors(list(zip(ids, x)))
+    ix.remove_vector("doc7")
+    r = np.random.default_rng(33)
+    sub = sorted(set(r.choice(N, 700, replace=False).tolist()) | {7})  # doc7 is gone: ignored
+    allowed = [ids[i] for i in sub] + ["no-such-id"] + [ids[sub[0]]]  # unknown + repeated ids
+    live = [i for i in sub if i != 7]
+    p = g.SearchParams(mode=g._ffi.GVDB_SEARCH_FLAT, metric=metric)
+    oi, osc, on = ix.search_batch_filtered(Q, 25, allowed, p)
+    for b in range(len(Q)):
+        got = [ix._str_of[int(u)] for u in oi[b, :on[b]]]
+        if metric == 0:
+            ri, rs = oracle_mod.storage_vector_search(Q[b], x[live], 25)
+        elif metric == 2:
+            ri, rs = oracle_mod.flat_cosine_distance_search(Q[b], x[live], 25)
+        else:
+            d = np.array([oracle_mod.l2_distance(Q[b], x[i]) for i in live], np.float32)
+            ri = np.argsort(d, kind="stable")[:25]
+            rs = d[ri]
+        assert got == [ids[live[int(j)]] for j in ri]
+        assert same_f32(osc[b, :on[b]], rs)
+    # k larger than the subset; empty subset
+    oi, osc, on = ix.search_batch_filtered(Q[:1], 10, [ids[3], ids[5]], p)
+    assert on[0] == 2
+    oi, osc, on = ix.search_batch_filtered(Q[:1], 10, ["nothing"], p)
+    assert on[0] == 0
