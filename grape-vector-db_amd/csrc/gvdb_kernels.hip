@@ -1108,6 +1108,9 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
 // expansion / threshold VALU fills the other wave's MFMA gaps on the SIMD.
 // Semantics are those of k_scan_mx2 (exact +/-1 dot = D_pad - 2 Hamming;
 // emits (d << 32 | row) for d <= thr[q], staged per wave in LDS).
+#ifndef MX3_PF
+#define MX3_PF 4
+#endif
 constexpr int kMx3Rows = 32;  // candidates per wave sub-tile
 // 8 waves per CU (2 per SIMD), the query tiles in two passes of four (64
 // accumulator VGPRs: all eight at once, or one wave per SIMD with 512
@@ -1182,7 +1185,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
             if (pass * QH >= (int)nqt) break;
             // k-loop: one expanded row fragment per k-step, reused by QH query tiles
             const v4i_t* qf = qfrag + lane;
-            constexpr int PF = 4;  // A-fragment LDS ring depth (in MFMAs)
+            constexpr int PF = MX3_PF;  // A-fragment LDS ring depth (in MFMAs)
             v4i_t ar[PF];
             auto aidx = [&](int m) { return ((pass * QH + m % QH) * KS + (m / QH)) * 64; };  // MFMA m = s*QH + qt
 #pragma unroll
