@@ -297,12 +297,12 @@ def main():
                        "steps": args.steps})
         for r in (1000, 4000):
             run_point(f"bq R={r}", gvdb.SearchParams(rescore_count=r))
-        run_point("exact flat (bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1))
+        run_point("exact flat (i8/bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1))
         if planted:
             ptruth = pi.cpu().numpy()
             for r in (R, 1000):
                 run_point(f"bq R={r}", gvdb.SearchParams(rescore_count=r), qp, ptruth, "planted (x_j + 0.1 n, |n| = 1)")
-            run_point("exact flat (bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1),
+            run_point("exact flat (i8/bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1),
                       qp, ptruth, "planted (x_j + 0.1 n, |n| = 1)")
 
     # ---------------- roofline of the dominant kernel (stage-1 scan at batch B)

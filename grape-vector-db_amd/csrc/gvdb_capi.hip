@@ -465,6 +465,8 @@ struct gvdb_index {
     mutable float* rowsq_aux = nullptr;
     mutable uint64_t rowsq_cap = 0, rowsq_version = ~0ull;
     mutable bool rows_nonfinite = false;
+    // adaptive flat tiers: batches left that skip the i8 tier after it failed
+    mutable std::atomic<uint32_t> i8_skip{0};
 
     uint32_t w4() const { return code_w4(dim); }
     size_t device_bytes() const {
@@ -923,19 +925,31 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
     const int descending = kind == kScoreCosine;
     if (sp.mode == GVDB_SEARCH_FLAT && kind != kScoreL2 && ix->n >= kFxMinN && k >= 1 && k <= 256 &&
         !getenv_flag("GVDB_FLAT_EXACT_ONLY")) {
-        // bf16 candidates (2^-8 margin) by default.  GVDB_FLAT=i8 tries the i8
-        // tier first (half the bytes, twice the MFMA rate, but a ~4x wider
-        // certified margin: on high-entropy data such as i.i.d. 768-d vectors at
-        // 10M rows its candidate set overflows); a batch a tier cannot certify
-        // is retried on the next one (i8 -> bf16 -> exact scan).
+        // Tiers: i8 candidates first (half the bytes of bf16, twice the MFMA
+        // rate, a ~4x wider certified margin: ~2K candidates per query at
+        // 10M x 768 i.i.d.), then bf16 (2^-8 margin), then the exact scan; a
+        // batch a tier cannot certify is retried on the next one.  Default:
+        // adaptive -- after an i8 batch fails to certify, this index skips the
+        // i8 tier for its next 16 batches (bounding the wasted pass on data
+        // whose i8 candidate sets overflow).  GVDB_FLAT=i8 / bf16 forces the
+        // first tier.
         const char* fk = getenv("GVDB_FLAT");
-        const bool try_i8 = fk && strcmp(fk, "i8") == 0;
+        const bool force_i8 = fk && strcmp(fk, "i8") == 0;
+        const bool force_bf16 = fk && strcmp(fk, "bf16") == 0;
+        bool try_i8 = force_i8;
+        if (!force_i8 && !force_bf16) {
+            uint32_t skip = ix->i8_skip.load();
+            while (skip > 0 && !ix->i8_skip.compare_exchange_weak(skip, skip - 1)) {
+            }
+            try_i8 = skip == 0;
+        }
         bool certified = false;
         if (try_i8) {
             gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
                                             d_n, ws, s, true, &certified);
             if (st != GVDB_OK || certified) return st;
             flat_fallbacks_i8().fetch_add(1);
+            if (!force_i8) ix->i8_skip.store(16);
         }
         gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
                                         d_n, ws, s, false, &certified);

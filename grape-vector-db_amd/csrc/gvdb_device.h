@@ -19,19 +19,19 @@ __device__ __forceinline__ uint32_t f32_order(float f) {
 }
 
 // In-LDS bitonic sort (ascending) of P = power-of-two u64 keys by a whole
-// workgroup.
+// workgroup.  Each stage walks the P/2 compare-exchange PAIRS (lo has bit j
+// clear, hi = lo | j), so no thread iteration is spent on the idle half.
 __device__ inline void bitonic_sort_lds(uint64_t* s, uint32_t P) {
     for (uint32_t k = 2; k <= P; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t a = s[i], b = s[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        s[i] = b;
-                        s[ixj] = a;
-                    }
+            for (uint32_t p = threadIdx.x; p < P / 2; p += blockDim.x) {
+                const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                const uint32_t hi = lo | j;
+                const uint64_t a = s[lo], b = s[hi];
+                const bool up = (lo & k) == 0;
+                if ((a > b) == up) {
+                    s[lo] = b;
+                    s[hi] = a;
                 }
             }
             __syncthreads();

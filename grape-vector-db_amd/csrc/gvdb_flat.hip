@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void k_flat_tau(const float* __restrict__ psco
 
 // Per query: sort the reranked candidates (exact score, then row ascending),
 // certify, emit the first k live rows.
-__global__ __launch_bounds__(256) void k_flat_final(const uint32_t* __restrict__ counts,
+__global__ __launch_bounds__(1024) void k_flat_final(const uint32_t* __restrict__ counts,
                                                     const uint32_t* __restrict__ cand, uint32_t candcap,
                                                     const float* __restrict__ scores, const float* __restrict__ thr,
                                                     const float* __restrict__ qd, uint32_t k, int descending,
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(256) void k_flat_final(const uint32_t* __restrict__
         return;
     }
     const uint32_t P = next_pow2(c < 2u ? 2u : c);
-    for (uint32_t i = tid; i < P; i += 256u) {
+    for (uint32_t i = tid; i < P; i += blockDim.x) {
         if (i < c) {
             const float sc = scores[(uint64_t)q * candcap + i];
             const uint32_t o = descending ? ~f32_order(sc) : f32_order(sc);
@@ -842,7 +842,7 @@ hipError_t launch_flat_final(const uint32_t* counts, const uint32_t* cand, uint3
                              const uint64_t* ids, uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail,
                              hipStream_t s) {
     if (B == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_flat_final, dim3(B), dim3(256), 0, s, counts, cand, candcap, scores, thr, qd, k, descending,
+    hipLaunchKernelGGL(k_flat_final, dim3(B), dim3(1024), 0, s, counts, cand, candcap, scores, thr, qd, k, descending,
                        ids, out_ids, out_scores, out_n, fail);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;

@@ -151,7 +151,7 @@ hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint3
 // gvdb_flat.hip.  rowsb: bf16 fragment-major mirror (fx_frag), KC = fx_kc(D).
 constexpr uint32_t kFxRows = 256;      // rows per tile
 constexpr uint32_t kFxQ = 256;         // query slots per launch group
-constexpr uint32_t kFxCandCap = 4096;  // candidates per query (LDS sort capacity)
+constexpr uint32_t kFxCandCap = 8192;  // candidates per query (LDS sort capacity)
 constexpr uint32_t kFxMinN = 65536;    // smaller shards use the exact full scan
 constexpr uint32_t kFxSampleEvery = 64;  // sample pass: every 64th row tile
 __host__ __device__ inline uint32_t fx_kc(uint32_t D) { return (D + 63u) / 64u; }        // bf16 chunks

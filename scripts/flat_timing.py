@@ -44,15 +44,19 @@ for B in [int(b) for b in os.environ.get("BS", "256,64,1").split(",")]:
     L.gvdb_timing_enable(0)
     import ctypes as C
     em, en, tm, tn = C.c_double(), C.c_uint64(), C.c_double(), C.c_uint64()
-    i8 = os.environ.get("GVDB_FLAT", "bf16") == "i8"
-    L.gvdb_timing_read(7 if i8 else 5, C.byref(em), C.byref(en))
-    L.gvdb_timing_read(8 if i8 else 6, C.byref(tm), C.byref(tn))
+    # slots 7/8 = the i8 tier, 5/6 = bf16: report the tier that ran
+    L.gvdb_timing_read(7, C.byref(em), C.byref(en))
+    L.gvdb_timing_read(8, C.byref(tm), C.byref(tn))
+    i8 = en.value > 0
+    if not i8:
+        L.gvdb_timing_read(5, C.byref(em), C.byref(en))
+        L.gvdb_timing_read(6, C.byref(tm), C.byref(tn))
     e_ms = em.value / max(en.value, 1)
-    kpad = (D + 127) // 128 * 128 if os.environ.get("GVDB_FLAT", "bf16") == "i8" else (D + 63) // 64 * 64
+    kpad = (D + 127) // 128 * 128 if i8 else (D + 63) // 64 * 64
     tf = 2.0 * N * kpad * 256 / (e_ms * 1e-3) / 1e12
-    gbs = N * kpad * (1 if kpad % 128 == 0 and os.environ.get("GVDB_FLAT", "bf16") == "i8" else 2) / (e_ms * 1e-3) / 1e9
+    gbs = N * kpad * (1 if i8 else 2) / (e_ms * 1e-3) / 1e9
     print(f"        k_flat_mx emit {e_ms:.3f} ms ({tf:.0f} TOP/s incl. padding slots, {gbs:.0f} GB/s rows), "
           f"group total {tm.value / max(tn.value, 1):.3f} ms", flush=True)
     print(f"B={B:4d}  {ms:8.3f} ms/batch  {B / ms * 1e3:10.0f} QPS  fallbacks {L.gvdb_flat_fallback_count() - f0}"
-          f"  i8->bf16 retries {L.gvdb_flat_i8_fallback_count() - f8}  [{os.environ.get('GVDB_FLAT', 'bf16')}]",
+          f"  i8->bf16 retries {L.gvdb_flat_i8_fallback_count() - f8}  [{'i8' if i8 else 'bf16'} tier timed]",
           flush=True)

@@ -276,18 +276,18 @@ def test_flat_mfma_certified_matches_oracle(g, oracle_mod, monkeypatch, kind, N,
 
 
 def test_flat_i8_margin_too_wide_retries_on_bf16(g, oracle_mod, monkeypatch):
-    """6000 rows at cosine 0.900..0.910 to the query e_0: with the i8 margin (the
+    """12000 rows at cosine 0.900..0.910 to the query e_0: with the i8 margin (the
     rows' ~1.6 % quantisation error) every one of them is a candidate, over the
-    4096-candidate capacity; bf16's 2^-8 margin nominates ~40 % of them: the
+    8192-candidate capacity; bf16's 2^-8 margin nominates ~40 % of them: the
     batch is retried on bf16, certified there, and the result is still exactly
     the oracle's."""
     N, D, k = 70_000, 64, 10
     r = np.random.default_rng(77)
     x = r.standard_normal((N, D)).astype(np.float32) * np.float32(0.05)
     x[:, 0] = 0.0
-    special = r.choice(N, 6000, replace=False)
-    c = np.linspace(0.90, 0.91, 6000, dtype=np.float64)
-    u = r.standard_normal((6000, D))
+    special = r.choice(N, 12000, replace=False)
+    c = np.linspace(0.90, 0.91, 12000, dtype=np.float64)
+    u = r.standard_normal((12000, D))
     u[:, 0] = 0.0
     u /= np.linalg.norm(u, axis=1, keepdims=True)
     x[special] = (c[:, None] * np.eye(D)[0] + np.sqrt(1 - c[:, None] ** 2) * u).astype(np.float32)
