@@ -1698,6 +1698,163 @@ __global__ __launch_bounds__(kRrThreads, 2) void k_rerank(const float* __restric
     }
 }
 
+// k_rerank2: the same exact re-scoring with NO block barrier in the loop.
+// Every wave owns one work item (64 candidates of one query) at a time and a
+// private LDS tile: per 32-dimension chunk it loads the 64 rows' slices with
+// coalesced float4 loads (8 lanes per 128-B row slice) two chunks ahead into
+// registers, writes the current one to its tile, and each lane then folds its
+// own row in order (acc = acc + q_j * x_j, the reference's sequential f32 sum;
+// the query is wave-uniform and comes through scalar loads).  Waves never wait
+// for each other, so 16 waves per CU keep ~256 KiB of gathers in flight (the
+// block-synchronous form above was latency-bound: waves parked 88 % of their
+// cycles).
+constexpr int kRr2Ch = 32;                  // dimensions per chunk
+constexpr int kRr2Ld = kRr2Ch + 4;          // padded row stride (conflict-free b128)
+constexpr int kRr2Threads = 256;            // 4 independent waves
+constexpr int kRr2Per = 64 * kRr2Ch / 4 / 64;  // float4 per lane per chunk (8)
+
+__global__ __launch_bounds__(kRr2Threads, 4) void k_rerank2(const float* __restrict__ rows, uint64_t clen,
+                                                            const float* __restrict__ norms,
+                                                            const float* __restrict__ q, uint64_t qlen,
+                                                            const uint32_t* __restrict__ s1_rows, uint32_t B,
+                                                            uint32_t R, const uint32_t* __restrict__ counts, int kind,
+                                                            float* __restrict__ scores) {
+    __shared__ __attribute__((aligned(16))) float tiles[kRr2Threads / 64][64 * kRr2Ld];
+    __shared__ uint64_t bases[kRr2Threads / 64][64];
+    __shared__ uint32_t pre[kRrMaxB + 1];  // work items before query i
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    {
+        const uint32_t per = (B + kRr2Threads - 1) / kRr2Threads;
+        const uint32_t b0 = tid * per;
+        uint32_t loc = 0;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) {
+            const uint32_t c = counts ? min(counts[b0 + i], R) : R;
+            loc += (c + 63u) / 64u;
+        }
+        __shared__ uint32_t part[kRr2Threads];
+        part[tid] = loc;
+        __syncthreads();
+        for (uint32_t o = 1; o < kRr2Threads; o <<= 1) {
+            const uint32_t v = tid >= o ? part[tid - o] : 0u;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        uint32_t run = part[tid] - loc;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) {
+            pre[b0 + i] = run;
+            const uint32_t c = counts ? min(counts[b0 + i], R) : R;
+            run += (c + 63u) / 64u;
+        }
+        if (tid == kRr2Threads - 1) pre[B] = part[tid];
+        __syncthreads();
+    }
+    const uint32_t items = pre[B];
+    const uint64_t len = qlen < clen ? qlen : clen;  // zip() truncates
+    const bool vec4 = (clen & 3u) == 0;
+    const uint32_t nch = (uint32_t)((len + kRr2Ch - 1) / kRr2Ch);
+    float* tile = tiles[wv];
+    uint64_t* wb = bases[wv];
+    const uint32_t W = gridDim.x * (kRr2Threads / 64);
+    for (uint32_t item = blockIdx.x * (kRr2Threads / 64) + wv; item < items; item += W) {
+        uint32_t lo = 0, hi = B;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= item) lo = mid; else hi = mid;
+        }
+        const uint32_t qi = __builtin_amdgcn_readfirstlane(lo);
+        const uint32_t r0 = (item - pre[qi]) * 64u;
+        const uint32_t Rq = counts ? min(counts[qi], R) : R;
+        const uint32_t r = r0 + lane;
+        const uint32_t row = r < Rq ? s1_rows[(uint64_t)qi * R + r] : 0u;
+        const float nbv = (r < Rq && kind != kScoreL2) ? norms[row] : 0.0f;
+        wb[lane] = r < Rq ? (uint64_t)row * clen : ~0ull;  // read back by other lanes of this wave only
+        __builtin_amdgcn_wave_barrier();
+        const float* qv = q + (uint64_t)qi * qlen;
+        // slice s of a chunk: lane L loads float4 (L & 7) of row 8 s + (L >> 3)
+        float4 rg[2][kRr2Per];
+        auto load = [&](uint32_t c, int sl) __attribute__((always_inline)) {
+#pragma unroll
+            for (int s = 0; s < kRr2Per; ++s) {
+                const uint32_t rr = 8u * s + (lane >> 3);
+                rg[sl][s] = load4_guarded(rows, wb[rr], (uint64_t)c * kRr2Ch + 4u * (lane & 7u), len, vec4);
+            }
+        };
+        auto store = [&](int sl) __attribute__((always_inline)) {
+#pragma unroll
+            for (int s = 0; s < kRr2Per; ++s) {
+                const uint32_t rr = 8u * s + (lane >> 3);
+                *(float4*)(tile + rr * kRr2Ld + 4u * (lane & 7u)) = rg[sl][s];
+            }
+        };
+        float acc = -0.0f, qq = -0.0f;
+        if (nch) load(0, 0);
+        if (nch > 1) load(1, 1);
+        for (uint32_t c = 0; c < nch; ++c) {
+            if (c & 1) store(1); else store(0);
+            __builtin_amdgcn_wave_barrier();
+            if (c + 2 < nch) {
+                if (c & 1) load(c + 2, 1); else load(c + 2, 0);
+            }
+            const float* tr = tile + lane * kRr2Ld;
+            const uint64_t j0 = (uint64_t)c * kRr2Ch;
+            const uint32_t m = (uint32_t)min((uint64_t)kRr2Ch, len - j0);
+            if (kind == kScoreL2) {
+                for (uint32_t j = 0; j < m; ++j) {
+                    const float d = qv[j0 + j] - tr[j];
+                    acc = acc + d * d;
+                }
+            } else if (m == kRr2Ch) {
+#pragma unroll
+                for (int j = 0; j < kRr2Ch; j += 4) {
+                    const float4 x = *(const float4*)(tr + j);
+                    const float w0 = qv[j0 + j], w1 = qv[j0 + j + 1], w2 = qv[j0 + j + 2], w3 = qv[j0 + j + 3];
+                    acc = acc + w0 * x.x;
+                    acc = acc + w1 * x.y;
+                    acc = acc + w2 * x.z;
+                    acc = acc + w3 * x.w;
+                    qq = qq + w0 * w0;
+                    qq = qq + w1 * w1;
+                    qq = qq + w2 * w2;
+                    qq = qq + w3 * w3;
+                }
+            } else {
+                for (uint32_t j = 0; j < m; ++j) {
+                    const float w = qv[j0 + j];
+                    acc = acc + w * tr[j];
+                    qq = qq + w * w;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the tile is rewritten next chunk
+        }
+        if (r < Rq) {
+            float score;
+            if (kind == kScoreL2) {
+                score = sqrtf(acc);
+            } else {
+                for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+                const float na = sqrtf(qq);
+                if (kind == kScoreCosine)
+                    score = (na == 0.0f || nbv == 0.0f) ? 0.0f : acc / (na * nbv);
+                else
+                    score = (na == 0.0f || nbv == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nbv));
+            }
+            scores[(uint64_t)qi * R + r] = score;
+        }
+        __builtin_amdgcn_wave_barrier();  // wb is rewritten by the next item
+    }
+}
+
+// GVDB_RERANK=v1: always the block-synchronous k_rerank (A/B)
+static bool rerank_v2() {
+    static const bool v = [] {
+        const char* e = getenv("GVDB_RERANK");
+        return !(e && strcmp(e, "v1") == 0);
+    }();
+    return v;
+}
+
 hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
     if (a.B == 0 || a.R == 0) return hipSuccess;
     int dev = 0, cus = 256;
@@ -1708,10 +1865,23 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
         // upper bound of the work items (counts are on the device): every item
         // slot up to 2 resident blocks per CU, the loop takes the rest
         const uint64_t max_items = (uint64_t)nb * ((a.R + kRrRows - 1) / kRrRows);
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(max_items, 2ull * cus);
-        hipLaunchKernelGGL(k_rerank, dim3(grid), dim3(kRrThreads), 0, s, a.rows, a.clen, a.norms,
-                           a.q + (uint64_t)b0 * a.qlen, a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
-                           a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R);
+        // k_rerank2 (wave-independent, 32-dim chunks) wins on large gathers
+        // (flat candidate lists: ~13 % on 560K rows); the block-synchronous
+        // k_rerank (128-dim chunks, shorter serial chain per item) on small
+        // ones (batch-1: 34 us vs 60 us)
+        if (rerank_v2() && max_items >= 2048) {
+            // one item per wave; up to 4 resident blocks (16 waves) per CU
+            const uint64_t blocks = (max_items + 3) / 4;
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(blocks, 4ull * cus);
+            hipLaunchKernelGGL(k_rerank2, dim3(grid), dim3(kRr2Threads), 0, s, a.rows, a.clen, a.norms,
+                               a.q + (uint64_t)b0 * a.qlen, a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
+                               a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R);
+        } else {
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(max_items, 2ull * cus);
+            hipLaunchKernelGGL(k_rerank, dim3(grid), dim3(kRrThreads), 0, s, a.rows, a.clen, a.norms,
+                               a.q + (uint64_t)b0 * a.qlen, a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
+                               a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R);
+        }
         GVDB_LAUNCH_CHECK();
     }
     return hipSuccess;

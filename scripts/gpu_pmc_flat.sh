@@ -18,7 +18,7 @@ for set in "${ALL[@]}"; do
     echo "pass $i ($set) rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
     f=$(find $OUT/p$i -name "*counter_collection.csv" | head -1)
-    if [ -n "$f" ]; then head -1 "$f" > $OUT/counters_p$i.csv; grep -E "k_flat" "$f" >> $OUT/counters_p$i.csv; fi
+    if [ -n "$f" ]; then head -1 "$f" > $OUT/counters_p$i.csv; grep -E "k_flat|k_rerank" "$f" >> $OUT/counters_p$i.csv; fi
     rm -rf $OUT/p$i
 done
 ls -la $OUT
