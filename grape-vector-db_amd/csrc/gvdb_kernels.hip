@@ -1117,7 +1117,10 @@ constexpr int kMx3Rows = 32;  // candidates per wave sub-tile
 // registers, spill under hipcc), a 2-deep code-plane ring.
 constexpr int kMx3Threads = 512;
 constexpr int kMx3Passes = 2;
-constexpr int kMx3Ring = 2;
+#ifndef MX3_RING
+#define MX3_RING 2
+#endif
+constexpr int kMx3Ring = MX3_RING;
 template <int W4>
 __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const uint32_t* __restrict__ qwords,
