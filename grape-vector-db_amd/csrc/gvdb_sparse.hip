@@ -176,8 +176,11 @@ __global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
         auto term_at = [&](uint32_t e) { return staged ? s_ent[e] : a.term[base + e]; };
         const bool live = doc < nd;
         const uint32_t lo0 = live ? s_dp[doc] : 0u, hi0 = live ? s_dp[doc + 1] : 0u;
-        // match map: 4 threads per document walk its entries
-        for (uint32_t e = lo0 + qg; e < hi0; e += kSpThreads / kSpTile) {
+        // match map: 8 threads per document walk its entries
+#ifndef BM_ABL
+#define BM_ABL 0
+#endif
+        for (uint32_t e = lo0 + qg; e < hi0 && !(BM_ABL & 1); e += kSpThreads / kSpTile) {
             const uint32_t t = term_at(e);
             if (e > lo0 && term_at(e - 1) == t) continue;  // not the first of a run (re-added id)
             uint32_t lo = 0, hi = nu;
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
         __syncthreads();
         const uint32_t slot = d0 + doc;
         const uint32_t qbeg = MODE == 2 ? a.dense_q : qg, qstep = MODE == 2 ? B + 1 : kSpThreads / kSpTile;
-        for (uint32_t q = qbeg; q < B; q += qstep) {
+        for (uint32_t q = qbeg; q < B && !(BM_ABL & 2); q += qstep) {
             if (MODE == 2 && qg != 0) break;
             float acc = 0.0f;
             bool hit = false;
@@ -204,11 +207,30 @@ __global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
                     const uint32_t ub = in ? s_qb[pc + i] : 0u;
                     vv[i] = in && live ? ((uint32_t)s_map[ub * kSpTile + doc] | (ub << 8)) : 0u;
                 }
+                // fast path, all reads independent: a staged document whose
+                // entry for the term is the whole run (v < 255 and the next
+                // entry holds another term) contributes tf_component[e] once
+                float tf8[8];
+                bool one8[8];
+#pragma unroll
+                for (uint32_t i = 0; i < 8; ++i) {
+                    const uint32_t v = vv[i] & 255u;
+                    const uint32_t e = lo0 + (v ? v - 1 : 0);
+                    const bool cand = staged && v != 0 && v != 255;
+                    tf8[i] = cand ? s_tfc[e] : 0.0f;
+                    one8[i] = cand && (e + 1 >= hi0 || s_ent[e + 1] != s_ut[vv[i] >> 8]);
+                }
 #pragma unroll
                 for (uint32_t i = 0; i < 8; ++i) {
                     const uint32_t v = vv[i] & 255u;
                     if (v == 0) continue;
                     const uint32_t p = pc + i;
+                    if (one8[i]) {
+                        const float sc = s_qv[p] * tf8[i] * s_qidf[p];
+                        acc = hit ? acc + sc : 0.0f + sc;
+                        hit = true;
+                        continue;
+                    }
                     const uint32_t t = s_ut[vv[i] >> 8];
                     uint32_t e = lo0 + v - 1;
                     if (v == 255) {  // long document: lower_bound(t)
