@@ -107,6 +107,7 @@ struct SpArgs {
 template <int MODE>
 __global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
     __shared__ uint32_t s_qp[kSpMaxB + 1];
+    __shared__ uint64_t s_tau[MODE == 1 ? kSpMaxB : 1];  // emit thresholds, staged once
     __shared__ uint16_t s_qb[kSpQT];
     __shared__ float s_qv[kSpQT], s_qidf[kSpQT];
     __shared__ uint32_t s_ut[kSpU];
@@ -117,6 +118,8 @@ __global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
     const uint32_t tid = threadIdx.x, doc = tid & (kSpTile - 1), qg = tid / kSpTile;
     const uint32_t B = a.B, nu = a.nu;
     for (uint32_t i = tid; i <= B; i += kSpThreads) s_qp[i] = a.qp[i];
+    if constexpr (MODE == 1)
+        for (uint32_t i = tid; i < B; i += kSpThreads) s_tau[i] = a.tau[i];
     for (uint32_t i = tid; i < nu; i += kSpThreads) s_ut[i] = a.ut[i];
     __syncthreads();
     const uint32_t nqt = s_qp[B];
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
             if (MODE == 0) {
                 a.smp[(uint64_t)q * a.S + (uint64_t)j * kSpTile + doc] = key;
             } else if (MODE == 1) {
-                if (key != 0 && key >= a.tau[q]) {
+                if (key != 0 && key >= s_tau[q]) {
                     const uint32_t pos = atomicAdd(&a.counts[q], 1u);
                     if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key;
                 }
