@@ -309,12 +309,19 @@ def main():
     scan_avg = scan_ms / max(scan_n, 1)
     words = 4 * gvdb_code_w4(D)          # 32-bit code words per row (padded)
     variant = os.environ.get("GVDB_SCAN", "fp4")
-    mfma = B >= 96 and gvdb_code_w4(D) in (2, 3, 4, 6) and variant != "valu"
+    w4 = gvdb_code_w4(D)
+    wide = w4 in MX4_QT and variant == "fp4"  # k_scan_mx4: ceil(B / 32QT) launches per batch
+    mfma = B >= 96 and (w4 in (2, 3, 4, 6) and variant != "valu" or wide)
+    scan_launches = -(-B // (32 * MX4_QT[w4])) if (mfma and wide) else 1
     if mfma:
         bpad = ((B + 31) // 32) * 32
         ops = float(n_local) * bpad * words * 32 * 2  # MACs x 2: one +/-1 product per code bit
         if variant == "i8":
             peak, kname = PEAK_I8_TOPS, "k_scan_mfma (+/-1 i8 dot, v_mfma_i32_32x32x32_i8)"
+        elif wide:
+            peak, kname = PEAK_FP4_TFLOPS, (f"k_scan_mx4 (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4, rows in "
+                                            f"VGPRs, {32 * MX4_QT[w4]} queries per launch, {scan_launches} launches "
+                                            f"per batch; achieved over the batch's launches)")
         else:
             peak, kname = PEAK_FP4_TFLOPS, "k_scan_mx3 (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4, rows in VGPRs)"
         roof = {
@@ -339,7 +346,7 @@ def main():
         "traffic": pmc_traffic("gvdb::k_scan_mx3<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
-        "hbm_bytes_per_launch": n_local * gvdb_code_w4(D) * 16,
+        "hbm_bytes_per_launch": n_local * w4 * 16 * scan_launches,
         "note": "batch-256 stage 1 is compute-bound (96 B of codes per row read once per batch); "
                 "the HBM-bound batch-1 scan is in batch1.roofline",
     })
@@ -478,6 +485,10 @@ def pmc_traffic(kernel_prefix, n_local, D):
         if name.startswith(kernel_prefix) and "hbm_read_bytes_per_launch" in d:
             return d["hbm_read_bytes_per_launch"]
     return None
+
+
+# query tiles of 32 per k_scan_mx4 launch (LDS-bound), by code planes W4 (gvdb_kernels.hip dispatch)
+MX4_QT = {8: 4, 12: 4, 16: 3, 24: 2, 32: 1}
 
 
 def gvdb_code_w4(D):

@@ -85,6 +85,10 @@ constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replace
 // code widths with an MFMA scan instantiation (D <= 768; wider codes would
 // not fit the query fragments + prefetch in 256 VGPRs at 2 waves/SIMD)
 __host__ __device__ inline bool mfma_scan_supported(uint32_t W4) { return W4 == 2 || W4 == 3 || W4 == 4 || W4 == 6; }
+// k_scan_mx4 (wide codes, D = 1024 / 1536 / 2048 / 3072 / 4096 bits)
+__host__ __device__ inline bool mx4_scan_supported(uint32_t W4) {
+    return W4 == 8 || W4 == 12 || W4 == 16 || W4 == 24 || W4 == 32;
+}
 // hist/counts/fail must be zeroed by the caller on stream s.
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s);
 // Exact slow path for ONE query: all N distances + stable radix sort.

@@ -1310,6 +1310,182 @@ static void launch_scan_mx3_t(const Stage1Args& a, hipStream_t s) {
     }
 }
 
+// k_scan_mx4: k_scan_mx3 for WIDE codes (D > 768, e.g. 3072 bits = 24 planes,
+// SURVEY config 4).  The whole batch's expanded query fragments no longer fit
+// in LDS (8 tiles x 96 k-steps x 1 KiB = 768 KiB at D = 3072), so a launch
+// holds QT query tiles (QT x KS KiB of LDS) and the batch is covered by
+// ceil(B / 32QT) launches, each streaming the code planes once.  A row's W4
+// planes are split into NC chunks of CH planes; the registers hold one whole
+// sub-tile (NC slots of CH planes) and slot c is refilled with chunk c of the
+// wave's NEXT sub-tile as soon as chunk c has been consumed, so NC - 1 chunks
+// of MFMA work cover each chunk's HBM latency.  The QT accumulators live
+// across the chunks; threshold epilogue and emits are those of k_scan_mx3.
+template <int W4, int CH, int QT>
+__global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                           const uint32_t* __restrict__ qwords,
+                                                           const uint32_t* __restrict__ thr, uint32_t B,
+                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                           uint32_t bufcap) {
+    constexpr int KW = 4 * W4;  // 32-bit code words per row
+    constexpr int KS = KW / 2;  // k-steps of 64 bits
+    constexpr int NC = W4 / CH;
+    constexpr int KC = 2 * CH;  // k-steps per chunk
+    static_assert(W4 % CH == 0, "chunks must tile the code planes");
+    constexpr uint32_t kWaveStage = 512;
+    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
+    __shared__ __attribute__((aligned(16))) float tf_lds[QT * 32];
+    __shared__ float tmin_lds[QT * 2];
+    __shared__ uint64_t st_key[kMx3Threads / 64][kWaveStage];
+    __shared__ uint8_t st_q[kMx3Threads / 64][kWaveStage];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr float kPadF = (float)(32 * KW);
+    const int scale1 = 0x7f7f7f7f;
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx3Threads) {
+        const uint32_t l = i & 63u, st = i >> 6, qs = st % KS, qt = st / KS;
+        const uint32_t q = qt * 32u + (l & 31u);
+        qfrag[i] = fp4_x32(q < B ? qwords[(uint64_t)q * KW + 2u * qs + (l >> 5)] : 0u);
+    }
+    if (tid < QT * 32) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
+    __syncthreads();
+    if (tid < QT * 2) {
+        const float* tq = tf_lds + (tid >> 1) * 32 + 4u * (tid & 1u);
+        float m = tq[0];
+        for (int r = 1; r < 16; ++r) m = fminf(m, tq[(r & 3) + 8 * (r >> 2)]);
+        tmin_lds[tid] = m;
+    }
+    __syncthreads();
+    const uint32_t nsub = (N + kMx3Rows - 1) / kMx3Rows;
+    const uint32_t W = gridDim.x * (kMx3Threads / 64);
+    const uint32_t h = lane >> 5;
+    uint4 cr[NC][CH];
+    auto load = [&](uint32_t sb, int c) __attribute__((always_inline)) {
+        const uint32_t n = min(sb * (uint32_t)kMx3Rows + (lane & 31u), N - 1u);  // clamped: branch-free ring
+#pragma unroll
+        for (int p = 0; p < CH; ++p) cr[c][p] = codes[(uint64_t)(c * CH + p) * cap + n];
+    };
+    auto word = [&](int c, int s) __attribute__((always_inline)) {
+        const uint4 v = cr[c][(2 * s) >> 2];
+        return (2 * s) & 3 ? (h ? v.w : v.z) : (h ? v.y : v.x);
+    };
+    uint32_t wcnt = 0;
+    v16f_t acc[QT];
+    auto chunk = [&](int c) __attribute__((always_inline)) {
+        const v4i_t* qf = qfrag + lane;
+        constexpr int PF = MX3_PF;
+        constexpr int M = KC * QT;  // MFMAs of this chunk: m = s*QT + qt
+        v4i_t ar[PF];
+        auto aidx = [&](int m) { return ((m % QT) * KS + c * KC + m / QT) * 64; };
+#pragma unroll
+        for (int m = 0; m < PF; ++m)
+            if (m < M) ar[m] = qf[aidx(m)];
+#pragma unroll
+        for (int s = 0; s < KC; ++s) {
+            __builtin_amdgcn_sched_barrier(0);
+            const v4i_t b = fp4_x32(word(c, s));
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const int m = s * QT + qt;
+                const v4i_t a = ar[m % PF];
+                if (m + PF < M) ar[m % PF] = qf[aidx(m + PF)];
+                if (c == 0 && s == 0)
+                    mfma_fp4_first(acc[qt], a, b, scale1);
+                else
+                    mfma_fp4_acc(acc[qt], a, b, scale1);
+            }
+        }
+    };
+    auto epilogue = [&](uint32_t sb) __attribute__((always_inline)) {
+        const uint32_t n = sb * (uint32_t)kMx3Rows + (lane & 31u);
+        // opaque copies of the emit pointers: otherwise the per-(tile, row)
+        // overflow addresses are hoisted out of the sub-tile loop (64 VGPR pairs)
+        uint32_t* cnt = counts;
+        uint64_t* bf = buf;
+        uint32_t bcap = bufcap;
+        asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            __builtin_amdgcn_sched_barrier(0);
+            float amax = acc[qt][0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) amax = fmaxf(amax, acc[qt][r]);
+            if (!__ballot(amax >= tmin_lds[qt * 2 + h] && n < N)) continue;
+            float Tf[16];
+            const float* tq = tf_lds + qt * 32 + 4u * h;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const float4 v = *(const float4*)(tq + 8 * g4);
+                Tf[4 * g4 + 0] = v.x;
+                Tf[4 * g4 + 1] = v.y;
+                Tf[4 * g4 + 2] = v.z;
+                Tf[4 * g4 + 3] = v.w;
+            }
+            const uint32_t rb = qt * 32u + 4u * h;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const bool hit = acc[qt][r] >= Tf[r] && n < N;
+                const uint64_t m = __ballot(hit);
+                if (m) {
+                    if (hit) {
+                        const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
+                        const uint32_t d = (uint32_t)(kPadF - acc[qt][r]) >> 1;
+                        const uint64_t key = ((uint64_t)d << 32) | n;
+                        if (sp < kWaveStage) {
+                            st_key[wv][sp] = key;
+                            st_q[wv][sp] = (uint8_t)qi;
+                        } else {
+                            const uint32_t pos = atomicAdd(&cnt[qi], 1u);
+                            if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = key;
+                        }
+                    }
+                    wcnt += (uint32_t)__popcll(m);
+                }
+            }
+        }
+    };
+    uint32_t sb = blockIdx.x * (kMx3Threads / 64) + wv;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) load(sb, c);
+    for (; sb < nsub; sb += W) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            __builtin_amdgcn_sched_barrier(0);
+            chunk(c);
+            load(sb + W, c);  // slot c now free: chunk c of the next sub-tile
+        }
+        mfma_fp4_drain();
+        __builtin_amdgcn_sched_barrier(0);
+        epilogue(sb);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    const uint32_t ns = min(wcnt, kWaveStage);
+    for (uint32_t e = lane; e < ns; e += 64u) {
+        const uint32_t qi = st_q[wv][e];
+        const uint32_t pos = atomicAdd(&counts[qi], 1u);
+        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
+    }
+}
+
+template <int W4, int CH, int QT>
+static void launch_scan_mx4_t(const Stage1Args& a, hipStream_t s) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t nsub = (a.N + kMx3Rows - 1) / kMx3Rows;
+    const uint32_t wpb = kMx3Threads / 64;
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus, (nsub + wpb - 1) / wpb));
+    constexpr uint32_t QB = 32u * QT;  // queries per launch
+    for (uint32_t g = 0; g < a.B; g += QB) {
+        const uint32_t bg = min(QB, a.B - g);
+        hipLaunchKernelGGL((k_scan_mx4<W4, CH, QT>), dim3(grid), dim3(kMx3Threads), 0, s, a.codes, a.cap, a.N,
+                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
+                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+    }
+}
+
 template <int W4>
 static void launch_scan_mx2_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
@@ -1403,7 +1579,16 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
     const bool mfma = a.use_mfma && a.B >= kMfmaMinB && mfma_scan_supported(W4);
-    if (mfma && a.use_mfma == 2) {  // i8 MFMA variant (A/B comparison)
+    const bool wide = a.use_mfma == 1 && a.B >= kMfmaMinB && mx4_scan_supported(W4);
+    if (wide) {  // FP4 MFMA for wide codes: query tiles per launch bounded by LDS
+        switch (W4) {
+            case 8: launch_scan_mx4_t<8, 4, 4>(a, s); break;
+            case 12: launch_scan_mx4_t<12, 6, 4>(a, s); break;
+            case 16: launch_scan_mx4_t<16, 8, 3>(a, s); break;
+            case 24: launch_scan_mx4_t<24, 6, 2>(a, s); break;
+            default: launch_scan_mx4_t<32, 8, 1>(a, s); break;
+        }
+    } else if (mfma && a.use_mfma == 2) {  // i8 MFMA variant (A/B comparison)
         switch (W4) {
             case 2: launch_scan_mfma_t<2>(a, s); break;
             case 3: launch_scan_mfma_t<3>(a, s); break;

@@ -131,10 +131,14 @@ def test_stage1_topr_matches_oracle(g, oracle_mod, N, D, B, R, dup):
 
 
 @pytest.mark.parametrize("N,D,B,R", [(200_000, 768, 160, 100), (100_000, 256, 96, 64), (120_000, 384, 128, 200),
-                                     (90_000, 512, 300, 50), (80_000, 1024, 100, 100), (70_000, 768, 256, 1000)])
+                                     (90_000, 512, 300, 50), (80_000, 1024, 100, 100), (70_000, 768, 256, 1000),
+                                     (50_000, 1536, 200, 100), (40_000, 2048, 200, 300), (60_000, 3072, 256, 100),
+                                     (50_000, 3000, 130, 100), (40_000, 4096, 100, 100)])
 def test_stage1_mfma_batches_match_oracle(g, oracle_mod, N, D, B, R):
-    """Large batches take the i8-MFMA scan (B >= 96, W4 in {2,3,4,6,8});
-    distances must equal the popcount path and the oracle bit for bit."""
+    """Large batches (B >= 96) take the FP4-MFMA scan: k_scan_mx3 for W4 in
+    {2,3,4,6}, k_scan_mx4 (query tiles per launch bounded by LDS, partial
+    last launch) for W4 in {8,12,16,24,32}; distances must equal the popcount
+    path (GVDB_SCAN=valu), the A/B variants and the oracle bit for bit."""
     import os
 
     x = rng_rows(N + 3 * D, N, D, dup=200)
