@@ -1096,6 +1096,45 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
     }
 }
 
+// Block-aggregated flush of the per-wave staged emits (k_scan_mx3/mx4): one
+// LDS atomic per entry gives its rank within (block, query), then ONE global
+// atomicAdd per (block, query) reserves the block's slots in the query's
+// candidate buffer.  The per-entry global atomics this replaces all target the
+// same <= 256 counters at the end of the kernel and serialise there (53 us of
+// the 822 us 10M x 768 scan).  Counters still advance by every emit, so an
+// overflow (counts[q] > bufcap) is detected exactly as before.  Call from all
+// threads; qcnt[0..nq) must be zero.
+template <int kWaves, int kStage>
+__device__ __forceinline__ void flush_stage_block(const uint64_t (*st_key)[kStage], const uint8_t (*st_q)[kStage],
+                                                  uint32_t wv, uint32_t lane, uint32_t wcnt, uint32_t nq,
+                                                  uint32_t* qcnt, uint32_t* qbase, uint32_t* __restrict__ counts,
+                                                  uint64_t* __restrict__ buf, uint32_t bufcap) {
+    constexpr int kPer = kStage / 64;
+    const uint32_t ns = min(wcnt, (uint32_t)kStage);
+    uint32_t rk[kPer];
+    __syncthreads();  // every wave's stage complete
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const uint32_t e = lane + 64u * i;
+        if (e < ns) rk[i] = atomicAdd(&qcnt[st_q[wv][e]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nq; q += kWaves * 64) {
+        const uint32_t c = qcnt[q];
+        if (c) qbase[q] = atomicAdd(&counts[q], c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const uint32_t e = lane + 64u * i;
+        if (e < ns) {
+            const uint32_t qi = st_q[wv][e];
+            const uint32_t pos = qbase[qi] + rk[i];
+            if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
+        }
+    }
+}
+
 // k_scan_mx3: the FP4 scan with the candidates in REGISTERS and the queries
 // resident in LDS.  The whole query batch (<= 256 queries) is expanded to fp4
 // MFMA fragments once per block (96 KiB at 768 bits), then every wave streams
@@ -1135,6 +1174,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
     __shared__ __attribute__((aligned(16))) float tf_lds[QT * 32];
     __shared__ uint64_t st_key[kMx3Threads / 64][kWaveStage];
     __shared__ uint8_t st_q[kMx3Threads / 64][kWaveStage];
+    __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr float kPadF = (float)(32 * KW);
@@ -1146,6 +1186,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
         qfrag[i] = fp4_x32(q < B ? qwords[(uint64_t)q * KW + 2u * qs + (l >> 5)] : 0u);
     }
     if (tid < QT * 32) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
+    if (tid < QT * 32) qcnt[tid] = 0u;
     __syncthreads();
     // per (query tile, lane half): the smallest threshold among the 16 queries a
     // lane's accumulator rows hold, so a sub-tile with no hit is rejected with a
@@ -1234,6 +1275,9 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
 #pragma unroll
                 for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[qh][r] - Tf[r]);
                 if (!__ballot(mx >= 0.0f && n < N)) continue;
+#if defined(MX3_ABL) && MX3_ABL == 2  // timing ablation: no emission (results invalid)
+                if (mx < 1e30f) continue;
+#endif
                 const uint32_t rb = qt * 32u + 4u * h;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
@@ -1285,13 +1329,11 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
         }
     }
     // drain the clamped prefetches, then flush the staged candidates
-    __syncthreads();
-    const uint32_t ns = min(wcnt, kWaveStage);
-    for (uint32_t e = lane; e < ns; e += 64u) {
-        const uint32_t qi = st_q[wv][e];
-        const uint32_t pos = atomicAdd(&counts[qi], 1u);
-        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
-    }
+#if defined(MX3_ABL) && MX3_ABL == 1  // timing ablation: no flush (results invalid)
+    wcnt = 0;
+#endif
+    flush_stage_block<kMx3Threads / 64, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt,
+                                                     qbase, counts, buf, bufcap);
 }
 
 template <int W4>
@@ -1337,6 +1379,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
     __shared__ float tmin_lds[QT * 2];
     __shared__ uint64_t st_key[kMx3Threads / 64][kWaveStage];
     __shared__ uint8_t st_q[kMx3Threads / 64][kWaveStage];
+    __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr float kPadF = (float)(32 * KW);
@@ -1347,6 +1390,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
         qfrag[i] = fp4_x32(q < B ? qwords[(uint64_t)q * KW + 2u * qs + (l >> 5)] : 0u);
     }
     if (tid < QT * 32) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
+    if (tid < QT * 32) qcnt[tid] = 0u;
     __syncthreads();
     if (tid < QT * 2) {
         const float* tq = tf_lds + (tid >> 1) * 32 + 4u * (tid & 1u);
@@ -1460,13 +1504,8 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
         epilogue(sb);
         __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
-    const uint32_t ns = min(wcnt, kWaveStage);
-    for (uint32_t e = lane; e < ns; e += 64u) {
-        const uint32_t qi = st_q[wv][e];
-        const uint32_t pos = atomicAdd(&counts[qi], 1u);
-        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
-    }
+    flush_stage_block<kMx3Threads / 64, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt,
+                                                     qbase, counts, buf, bufcap);
 }
 
 template <int W4, int CH, int QT>
