@@ -229,7 +229,15 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t sample_div, uint32_t& chunks
         bufcap = std::min<uint64_t>(N, 8ull * R + 2048ull);
         return;
     }
-    uint64_t S = std::max<uint64_t>(kExactN / 2, N / sample_div);
+    // GVDB_SAMPLE_FLOOR: minimum sample rows (timing experiments).  Default kExactN / 4:
+    // at the 8-GPU shard (1.25M rows) 64K sample rows measured fastest (per-rank step
+    // 0.300 -> 0.282 ms; 131K / 32K / 16K slower: sample pass vs looser threshold)
+    static const uint64_t floor_rows = [] {
+        const char* e = getenv("GVDB_SAMPLE_FLOOR");
+        const long long v = e ? atoll(e) : 0;
+        return v >= 4096 ? (uint64_t)v : (uint64_t)(kExactN / 4);
+    }();
+    uint64_t S = std::max<uint64_t>(floor_rows, N / sample_div);
     chunks = (uint32_t)(S / 4096u);
     stride = N / chunks;  // >= 4096: chunks never overlap
     S = (uint64_t)chunks * 4096u;
@@ -1507,6 +1515,30 @@ gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d
                                   (uint32_t)R, (uint32_t)k, d_out_ids, d_out_scores, d_out_n,
                                   g.w->flags.as<uint32_t>() + 1, s),
             "shard merge");
+    HIP_TRY(hipMemcpyAsync(g.w->h_flags, g.w->flags.p, 8, hipMemcpyDeviceToHost, s), "flags");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    if (g.w->h_flags[1]) return fail(GVDB_ERR_QUANTIZATION, "NaN score in merge");
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_bq_shard_merge_packed_device(const uint32_t* d_gathered, const uint32_t* d_counts, uint64_t G,
+                                              uint64_t B, uint64_t R, uint64_t k, uint64_t* d_out_ids,
+                                              float* d_out_scores, uint32_t* d_out_n, void* stream) {
+    if (B == 0) return GVDB_OK;
+    if (G * R > kSortLdsCap) return fail(GVDB_ERR_INVALID_ARGUMENT, "G*R exceeds 4096");
+    if (!d_gathered || !d_counts || !d_out_ids || !d_out_scores) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if (reinterpret_cast<uintptr_t>(d_gathered) % 8u) return fail(GVDB_ERR_INVALID_ARGUMENT, "gathered buffer not 8-byte aligned");
+    WsGuard g(0);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t BR = B * R;  // rank block: ids (2*BR words) | dist (BR) | cos (BR)
+    HIP_TRY(g.w->flags.ensure(16), "alloc flags");
+    HIP_TRY(hipMemsetAsync(g.w->flags.p, 0, 16, s), "memset flags");
+    HIP_TRY(launch_bq_shard_merge(reinterpret_cast<const uint64_t*>(d_gathered), d_gathered + 2 * BR,
+                                  reinterpret_cast<const float*>(d_gathered + 3 * BR), d_counts, (uint32_t)G,
+                                  (uint32_t)B, (uint32_t)R, (uint32_t)R, (uint32_t)k, d_out_ids, d_out_scores, d_out_n,
+                                  g.w->flags.as<uint32_t>() + 1, s, 2 * BR, 4 * BR),
+            "packed shard merge");
     HIP_TRY(hipMemcpyAsync(g.w->h_flags, g.w->flags.p, 8, hipMemcpyDeviceToHost, s), "flags");
     HIP_TRY(hipStreamSynchronize(s), "sync");
     if (g.w->h_flags[1]) return fail(GVDB_ERR_QUANTIZATION, "NaN score in merge");

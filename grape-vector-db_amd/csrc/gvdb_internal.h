@@ -236,7 +236,8 @@ hipError_t launch_emit_candidates(const uint32_t* s1_rows, const uint32_t* s1_di
 // G*stride <= kSortLdsCap.
 hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cosv, const uint32_t* counts,
                                  uint32_t G, uint32_t B, uint32_t stride, uint32_t R, uint32_t kout, uint64_t* out_ids,
-                                 float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s);
+                                 float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s,
+                                 uint64_t gs_id = 0, uint64_t gs_w = 0);  // rank strides (0 = dense [G][B][stride])
 
 // ---- index maintenance -----------------------------------------------------------
 // Order-preserving gather of rows/codes/norms/ids: new row r <- old row map[r]

@@ -2509,9 +2509,11 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
                                                         const uint32_t* __restrict__ dist,
                                                         const float* __restrict__ cosv,
                                                         const uint32_t* __restrict__ counts, uint32_t G, uint32_t B,
-                                                        uint32_t stride, uint32_t R, uint32_t kout,
-                                                        uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
-                                                        uint32_t* __restrict__ out_n, uint32_t* __restrict__ nan_flag) {
+                                                        uint32_t stride, uint64_t gs_id, uint64_t gs_w, uint32_t R,
+                                                        uint32_t kout, uint64_t* __restrict__ out_ids,
+                                                        float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
+                                                        uint32_t* __restrict__ nan_flag) {
+    // rank g's list for query q starts at gids + g*gs_id + q*stride (dist/cosv: g*gs_w)
     __shared__ uint64_t sk[kSortLdsCap];
     __shared__ uint32_t sv[kSortLdsCap];
     __shared__ uint32_t s_n;
@@ -2521,9 +2523,9 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
     for (uint32_t t = threadIdx.x; t < G * stride; t += 256) {
         const uint32_t g = t / stride, i = t % stride;
         if (i < counts[(uint64_t)g * B + q]) {
-            const uint64_t at = ((uint64_t)g * B + q) * stride + i;
+            const uint64_t at = (uint64_t)q * stride + i;
             const uint32_t pos = atomicAdd(&s_n, 1u);
-            sk[pos] = ((uint64_t)dist[at] << 40) | (gids[at] & ((1ull << 40) - 1));
+            sk[pos] = ((uint64_t)dist[g * gs_w + at] << 40) | (gids[g * gs_id + at] & ((1ull << 40) - 1));
             sv[pos] = t;
         }
     }
@@ -2548,7 +2550,7 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
         if (i < r) {
             const uint32_t t = sv[i];
             const uint32_t g = t / stride, j = t % stride;
-            const float f = cosv[((uint64_t)g * B + q) * stride + j];
+            const float f = cosv[g * gs_w + (uint64_t)q * stride + j];
             if (f != f) s_nan = 1u;
             key = ((uint64_t)(~f32_order(f)) << 32) | i;
             val = t;
@@ -2563,19 +2565,21 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
     for (uint32_t i = threadIdx.x; i < take; i += 256) {
         const uint32_t t = sv[i];
         const uint32_t g = t / stride, j = t % stride;
-        const uint64_t at = ((uint64_t)g * B + q) * stride + j;
-        out_ids[(uint64_t)q * kout + i] = gids[at];
-        out_scores[(uint64_t)q * kout + i] = cosv[at];
+        const uint64_t at = (uint64_t)q * stride + j;
+        out_ids[(uint64_t)q * kout + i] = gids[g * gs_id + at];
+        out_scores[(uint64_t)q * kout + i] = cosv[g * gs_w + at];
     }
     if (threadIdx.x == 0 && out_n) out_n[q] = take;
 }
 
 hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cosv, const uint32_t* counts,
                                  uint32_t G, uint32_t B, uint32_t stride, uint32_t R, uint32_t kout, uint64_t* out_ids,
-                                 float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s) {
+                                 float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s,
+                                 uint64_t gs_id, uint64_t gs_w) {
     if (B == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bq_shard_merge, dim3(B), dim3(256), 0, s, gids, dist, cosv, counts, G, B, stride, R, kout,
-                       out_ids, out_scores, out_n, nan_flag);
+    const uint64_t dense = (uint64_t)B * stride;  // [G][B][stride] when no rank strides are given
+    hipLaunchKernelGGL(k_bq_shard_merge, dim3(B), dim3(256), 0, s, gids, dist, cosv, counts, G, B, stride,
+                       gs_id ? gs_id : dense, gs_w ? gs_w : dense, R, kout, out_ids, out_scores, out_n, nan_flag);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

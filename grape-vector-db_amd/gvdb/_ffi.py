@@ -138,6 +138,7 @@ SIGNATURES = {
     "gvdb_topk_merge_device": (C.c_int, [P, P, P, u64, u64, u64, u64, i32, P, P, P, P]),
     "gvdb_bq_shard_merge": (C.c_int, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P]),
     "gvdb_bq_shard_merge_device": (C.c_int, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P, P]),
+    "gvdb_bq_shard_merge_packed_device": (C.c_int, [P, P, u64, u64, u64, u64, P, P, P, P]),
     "gvdb_sparse_create": (C.c_int, [C.POINTER(gvdb_bm25_params), C.POINTER(P)]),
     "gvdb_sparse_destroy": (None, [P]),
     "gvdb_sparse_add_document": (C.c_int, [P, u64, P, P, u64, f32]),

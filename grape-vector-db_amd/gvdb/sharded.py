@@ -50,8 +50,34 @@ class ShardedBQSearch:
         self.out_ids = torch.zeros((B, k), dtype=torch.int64, device=device)
         self.out_scores = torch.zeros((B, k), dtype=torch.float32, device=device)
         self.out_n = torch.zeros(B, dtype=torch.int32, device=device)
+        # packed fast path (GPU, every shard holds >= R rows): the local
+        # candidates are written straight into this rank's send block
+        # [ids u64 B*R | dist u32 B*R | cos f32 B*R], the all-gather moves the
+        # blocks and the merge reads them in place (no packing copies)
+        self.into = getattr(candidates_fn, "into", None)
+        self.packed = self.on_gpu and self.into is not None and all(r == R for r in self.r_local)
+        if self.packed:
+            self.send = torch.zeros(4 * B * R, dtype=torch.int32, device=device)
+            self.recv = torch.zeros((self.world, 4 * B * R), dtype=torch.int32, device=device)
+
+    def _search_packed(self, q: torch.Tensor):
+        B, R, k = self.B, self.R, self.k
+        p = self.send.data_ptr()
+        self.into(q, R, p, p + 8 * B * R, p + 12 * B * R)
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+            src = self.recv
+        else:
+            src = self.send
+        stream = torch.cuda.current_stream(self.dev).cuda_stream or None
+        check(lib().gvdb_bq_shard_merge_packed_device(src.data_ptr(), self.counts.data_ptr(), self.world, B, R, k,
+                                                      self.out_ids.data_ptr(), self.out_scores.data_ptr(),
+                                                      self.out_n.data_ptr(), stream))
+        return self.out_ids, self.out_scores, self.out_n
 
     def search(self, q: torch.Tensor):
+        if self.packed:
+            return self._search_packed(q)
         B, R, k = self.B, self.R, self.k
         rl = self.r_local[self.rank]
         gids, d, c = self.cand(q, rl)
@@ -96,9 +122,13 @@ def gpu_candidates_fn(index) -> CandidatesFn:
                          torch.zeros((B, r), dtype=torch.int32, device=q.device),
                          torch.zeros((B, r), dtype=torch.float32, device=q.device))
         ids, d, c = bufs[key]
-        stream = torch.cuda.current_stream(q.device).cuda_stream or None
-        check(lib().gvdb_index_bq_candidates_device(index._h, q.data_ptr(), B, q.shape[1], r, ids.data_ptr(),
-                                                     d.data_ptr(), c.data_ptr(), stream))
+        into(q, r, ids.data_ptr(), d.data_ptr(), c.data_ptr())
         return ids, d, c
 
+    def into(q: torch.Tensor, r: int, ids_ptr: int, dist_ptr: int, cos_ptr: int):
+        stream = torch.cuda.current_stream(q.device).cuda_stream or None
+        check(lib().gvdb_index_bq_candidates_device(index._h, q.data_ptr(), q.shape[0], q.shape[1], r, ids_ptr,
+                                                     dist_ptr, cos_ptr, stream))
+
+    fn.into = into
     return fn

@@ -270,6 +270,14 @@ gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d
                                        const uint32_t* d_counts, uint64_t G, uint64_t B, uint64_t stride,
                                        uint64_t R, uint64_t k, uint64_t* d_out_ids, float* d_out_scores,
                                        uint32_t* d_out_n, void* stream);
+/* The same merge over the buffer ONE all-gather produces when every rank
+ * lets gvdb_index_bq_candidates_device write straight into its send block:
+ * rank g's block starts at word g*4*B*R of d_gathered and holds ids (u64
+ * [B][R]), then dist (u32 [B][R]), then cosine (f32 [B][R]).  No packing or
+ * unpacking copies around the collective.  Needs G*R <= 4096. */
+gvdb_status gvdb_bq_shard_merge_packed_device(const uint32_t* d_gathered, const uint32_t* d_counts, uint64_t G,
+                                              uint64_t B, uint64_t R, uint64_t k, uint64_t* d_out_ids,
+                                              float* d_out_scores, uint32_t* d_out_n, void* stream);
 
 /* ---- BM25 sparse index (src/sparse.rs:29-222) ---------------------------- */
 /* SparseIndex: an HBM forward index over document slots; documents are

@@ -469,6 +469,20 @@ def test_sharded_candidates_merge_equals_single_device(g, oracle_mod):
     ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R, kind=0)
     assert (mi.cpu().numpy().view(np.uint64) == ri[:, :k]).all()
     assert same_f32(ms.cpu().numpy(), rs[:, :k])
+    # the packed form: per rank [ids u64 B*R | dist u32 B*R | cos f32 B*R], as one all-gather delivers it
+    packed = np.concatenate([gids.reshape(G, -1).view(np.uint32), dist.reshape(G, -1), cosv.reshape(G, -1).view(np.uint32)],
+                            axis=1)
+    dp = torch.from_numpy(np.ascontiguousarray(packed).view(np.int32)).cuda()
+    pi = torch.zeros_like(mi)
+    ps = torch.zeros_like(ms)
+    pn = torch.zeros_like(mn)
+    st = g.lib().gvdb_bq_shard_merge_packed_device(dp.data_ptr(), dn.data_ptr(), G, B, R, k, pi.data_ptr(),
+                                                   ps.data_ptr(), pn.data_ptr(), None)
+    assert st == 0
+    torch.cuda.synchronize()
+    assert (pi.cpu().numpy().view(np.uint64) == ri[:, :k]).all()
+    assert same_f32(ps.cpu().numpy(), rs[:, :k])
+    assert (pn.cpu().numpy() == k).all()
 
 
 def test_reference_unit_tests_through_cpp_mirror(g):
