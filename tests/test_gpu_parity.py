@@ -532,3 +532,31 @@ def test_search_filtered_matches_oracle_on_subset(g, oracle_mod, metric):
     assert on[0] == 2
     oi, osc, on = ix.search_batch_filtered(Q[:1], 10, ["nothing"], p)
     assert on[0] == 0
+
+
+def test_sharded_packed_world1_equals_single_device(g):
+    """ShardedBQSearch's packed path (candidates written into the all-gather
+    send block, gvdb_bq_shard_merge_packed_device on it) with one rank returns
+    exactly what the single-device search returns; more ranks are covered by
+    the gloo test (host path) and the C-ABI merge test above."""
+    import torch
+
+    from gvdb.sharded import ShardedBQSearch, gpu_candidates_fn
+
+    N, D, B, R, k = 300_000, 768, 128, 100, 10
+    x = rng_rows(91, N, D, dup=50)
+    Q = rng_rows(92, B, D)
+    Q[5] = x[777]
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    q = torch.from_numpy(Q).cuda()
+    sh = ShardedBQSearch(gpu_candidates_fn(ix), [N], B, R, k, torch.device("cuda", 0))
+    assert sh.packed
+    pi, ps, pn = (t.clone() for t in sh.search(q))
+    oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+    osc = torch.zeros((B, k), dtype=torch.float32, device="cuda")
+    on = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ix.search_device(q, k, oi, osc, on, g.SearchParams(rescore_count=R))
+    torch.cuda.synchronize()
+    assert torch.equal(pi, oi) and torch.equal(pn, on)
+    assert same_f32(ps.cpu().numpy(), osc.cpu().numpy())
