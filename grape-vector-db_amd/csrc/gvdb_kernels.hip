@@ -2073,11 +2073,121 @@ __global__ __launch_bounds__(kRr2Threads, 4) void k_rerank2(const float* __restr
     }
 }
 
+// k_rerank_small: the exact re-scoring for SMALL candidate sets (batch-1 and
+// few-query batches, D <= 1024).  The block-synchronous k_rerank walks 128-dim
+// chunks with one chunk of loads in flight, so its time is a chain of gather
+// latencies (34 us for one query's 100 rows at D = 768).  Here a block takes
+// 16 candidates of one query, issues ALL their row loads at once into LDS
+// (16 x D floats, <= 64 KiB) together with the query, and 16 lanes then fold
+// their rows left to right (acc = acc + q_j*x_j, qq = qq + q_j*q_j: the same
+// sequential order as k_rerank / cosine_similarity_manual, so scores are
+// bit-identical).  One block per (query, 16-candidate slot); empty slots exit.
+constexpr int kRsRows = 16;
+constexpr int kRsThreads = 256;
+constexpr uint32_t kRsMaxLen = 1024;
+__global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __restrict__ rows, uint64_t clen,
+                                                            const float* __restrict__ norms,
+                                                            const float* __restrict__ q, uint64_t qlen,
+                                                            const uint32_t* __restrict__ s1_rows, uint32_t B,
+                                                            uint32_t R, const uint32_t* __restrict__ counts, int kind,
+                                                            float* __restrict__ scores) {
+    __shared__ float4 tile4[kRsRows * (kRsMaxLen / 4 + 1)];
+    __shared__ float4 qs4[kRsMaxLen / 4];
+    __shared__ uint64_t bases[kRsRows];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t ipq = (R + kRsRows - 1) / kRsRows;
+    const uint32_t qi = blockIdx.x / ipq;
+    const uint32_t r0 = (blockIdx.x % ipq) * kRsRows;
+    if (qi >= B) return;
+    const uint32_t Rq = counts ? min(counts[qi], R) : R;
+    if (r0 >= Rq) return;  // block-uniform
+    const uint64_t len = qlen < clen ? qlen : clen;  // zip() truncates
+    const uint32_t L4 = (uint32_t)((len + 3) / 4), ld4 = L4 + 1;
+    const bool vec4 = (clen & 3u) == 0;
+    const float* qv = q + (uint64_t)qi * qlen;
+    const bool qvec4 = (qlen & 3u) == 0 && (((uintptr_t)qv) & 15u) == 0;
+    if (tid < kRsRows) bases[tid] = r0 + tid < Rq ? (uint64_t)s1_rows[(uint64_t)qi * R + r0 + tid] * clen : ~0ull;
+    __syncthreads();
+    // every load in flight before the first LDS store (a load -> store loop
+    // would wait one full gather latency per iteration)
+    constexpr int kPer = kRsRows * (kRsMaxLen / 4) / kRsThreads;  // 16 float4 per thread
+    float4 v[kPer];
+    const float4 qv4 = tid < L4 ? load4_guarded(qv, 0, 4ull * tid, len, qvec4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = tid + k * kRsThreads, r = i / L4, c = i - r * L4;
+        v[k] = i < kRsRows * L4 ? load4_guarded(rows, bases[r], 4ull * c, len, vec4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = tid + k * kRsThreads, r = i / L4, c = i - r * L4;
+        if (i < kRsRows * L4) tile4[r * ld4 + c] = v[k];
+    }
+    if (tid < L4) qs4[tid] = qv4;
+    __syncthreads();
+    if (tid >= kRsRows || r0 + tid >= Rq) return;
+    const float4* tr4 = tile4 + tid * ld4;
+    float acc = -0.0f, qq = -0.0f;
+    if (kind == kScoreL2) {
+        const float* tr = (const float*)tr4;
+        const float* qc = (const float*)qs4;
+        for (uint32_t j = 0; j < len; ++j) {
+            const float d = qc[j] - tr[j];
+            acc = acc + d * d;
+        }
+    } else if ((len & 3u) == 0) {
+#pragma unroll 4
+        for (uint32_t c = 0; c < L4; ++c) {
+            const float4 x = tr4[c];
+            const float4 w = qs4[c];
+            acc = acc + w.x * x.x;
+            acc = acc + w.y * x.y;
+            acc = acc + w.z * x.z;
+            acc = acc + w.w * x.w;
+            qq = qq + w.x * w.x;
+            qq = qq + w.y * w.y;
+            qq = qq + w.z * w.z;
+            qq = qq + w.w * w.w;
+        }
+    } else {
+        const float* tr = (const float*)tr4;
+        const float* qc = (const float*)qs4;
+        for (uint32_t j = 0; j < len; ++j) {
+            acc = acc + qc[j] * tr[j];
+            qq = qq + qc[j] * qc[j];
+        }
+    }
+    const uint32_t r = r0 + tid;
+    float score;
+    if (kind == kScoreL2) {
+        score = sqrtf(acc);
+    } else {
+        for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+        const float na = sqrtf(qq);
+        const float nb = norms[s1_rows[(uint64_t)qi * R + r]];
+        if (kind == kScoreCosine) {
+            score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+        } else {
+            score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+        }
+    }
+    scores[(uint64_t)qi * R + r] = score;
+}
+
 // GVDB_RERANK=v1: always the block-synchronous k_rerank (A/B)
 static bool rerank_v2() {
     static const bool v = [] {
         const char* e = getenv("GVDB_RERANK");
         return !(e && strcmp(e, "v1") == 0);
+    }();
+    return v;
+}
+// k_rerank_small slots (query x 16 candidates) up to which it replaces
+// k_rerank; GVDB_RERANK_SMALL=<n> overrides (0 disables; A/B timing)
+static uint64_t rerank_small_max() {
+    static const uint64_t v = [] {
+        const char* e = getenv("GVDB_RERANK_SMALL");
+        return e ? (uint64_t)atoll(e) : (uint64_t)256;
     }();
     return v;
 }
@@ -2087,6 +2197,13 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t small_slots = (uint64_t)a.B * ((a.R + kRsRows - 1) / kRsRows);
+    if (small_slots <= rerank_small_max() && std::min(a.qlen, a.clen) <= kRsMaxLen && small_slots < (1ull << 31)) {
+        hipLaunchKernelGGL(k_rerank_small, dim3((uint32_t)small_slots), dim3(kRsThreads), 0, s, a.rows, a.clen,
+                           a.norms, a.q, a.qlen, a.s1_rows, a.B, a.R, a.counts, a.kind, a.scores);
+        GVDB_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     for (uint32_t b0 = 0; b0 < a.B; b0 += kRrMaxB) {
         const uint32_t nb = std::min<uint32_t>(kRrMaxB, a.B - b0);
         // upper bound of the work items (counts are on the device): every item
