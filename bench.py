@@ -441,8 +441,8 @@ def main():
             "data": f"synthetic: i.i.d. N(0,1) f32 rows and queries, L2-normalised, torch Philox seed {SEED}"
                     + ("; operating_points also on planted queries x_j + 0.1 n, |n| = 1 (SURVEY 8(d))" if planted else ""),
             "config": {
-                "workload": f"{N // 1_000_000}Mx{D} f32 corpus, BQ Hamming prefilter top-{R} + exact cosine rerank, "
-                            f"k={k}, batch-{B} (BASELINE configs[2])",
+                "workload": f"{N / 1e6:g}Mx{D} f32 corpus, BQ Hamming prefilter top-{R} + exact cosine rerank, "
+                            f"k={k}, batch-{B} ({config_label(N, D)})",
                 "n": N, "dim": D, "batch": B, "rescore_R": R, "k": k,
                 "parallelism": f"corpus-shard x{world}" + (" + RCCL all-gather merge" if world > 1 else ""),
             },
@@ -485,6 +485,19 @@ def pmc_traffic(kernel_prefix, n_local, D):
         if name.startswith(kernel_prefix) and "hbm_read_bytes_per_launch" in d:
             return d["hbm_read_bytes_per_launch"]
     return None
+
+
+def config_label(n, d):
+    """Which BASELINE.json config a bench shape is (other shapes are labelled as such)."""
+    if (n, d) == (10_000_000, 768):
+        return "BASELINE configs[2]"
+    if (n, d) == (1_000_000, 768):
+        return "BASELINE configs[1]"
+    if (n, d) == (10_000_000, 3072):
+        return "BASELINE configs[3] corpus"
+    if (n, d) == (1_250_000, 3072):
+        return "one GPU's shard of BASELINE configs[3] (10M x 3072 over 8 GPUs)"
+    return "not a BASELINE config"
 
 
 # query tiles of 32 per k_scan_mx4 launch (LDS-bound), by code planes W4 (gvdb_kernels.hip dispatch)
