@@ -262,8 +262,14 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
                                                         : 1;
     const char* dbg = getenv("GVDB_SCAN_DBG");  // ablation timing only (results invalid when set)
     s1.dbg = dbg ? atoi(dbg) : 0;
-    plan_sampling(N, R, (s1.use_mfma && B >= kMfmaMinB) ? 64u : 32u, s1.sample_chunks, s1.sample_stride, s1.target,
-                  s1.bufcap);
+    // GVDB_SAMPLE_DIV: sample ~N/div rows for large batches (timing experiments; default 64)
+    static const uint32_t big_div = [] {
+        const char* e = getenv("GVDB_SAMPLE_DIV");
+        const int v = e ? atoi(e) : 0;
+        return v >= 8 && v <= 4096 ? (uint32_t)v : 64u;
+    }();
+    plan_sampling(N, R, (s1.use_mfma && B >= kMfmaMinB) ? big_div : 32u, s1.sample_chunks, s1.sample_stride,
+                  s1.target, s1.bufcap);
     const size_t nb = (size_t)D + 1u;
     const size_t words = 4 + 2 * (size_t)B + (size_t)B * nb;
     HIP_TRY(ws.zero.ensure(words * 4 + 16), "alloc stage-1 state");
