@@ -1151,11 +1151,17 @@ __device__ __forceinline__ void flush_stage_block(const uint64_t (*st_key)[kStag
 #define MX3_PF 4
 #endif
 constexpr int kMx3Rows = 32;  // candidates per wave sub-tile
-// 8 waves per CU (2 per SIMD), the query tiles in two passes of four (64
-// accumulator VGPRs: all eight at once, or one wave per SIMD with 512
-// registers, spill under hipcc), a 2-deep code-plane ring.
+// 8 waves per CU (2 per SIMD), all eight query tiles in one pass (MX3_PASSES
+// below), a 2-deep code-plane ring.
 constexpr int kMx3Threads = 512;
-constexpr int kMx3Passes = 2;
+// MX3_PASSES=1 (default): all 8 query tiles' accumulators live (128 VGPRs), each
+// row fragment expanded once per k-step.  It spilled until the emit pointers were
+// made opaque (hipcc hoisted the per-(tile, row) overflow addresses); now 256
+// VGPRs, no spills, 3-4 % faster per batch than two passes (scripts/gpu_p1.sh).
+#ifndef MX3_PASSES
+#define MX3_PASSES 1
+#endif
+constexpr int kMx3Passes = MX3_PASSES;
 #ifndef MX3_RING
 #define MX3_RING 2
 #endif
@@ -1224,6 +1230,12 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
 
     auto process = [&](uint32_t sb, const uint4 (&c)[W4]) __attribute__((always_inline)) {
         const uint32_t n = sb * (uint32_t)kMx3Rows + (lane & 31u);
+        // opaque copies of the emit pointers (see k_scan_mx4): keeps the per-(tile, row)
+        // overflow addresses from being hoisted out of the loop
+        uint32_t* cnt = counts;
+        uint64_t* bf = buf;
+        uint32_t bcap = bufcap;
+        asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
 #pragma unroll 1
         for (int pass = 0; pass < kMx3Passes; ++pass) {
             if (pass * QH >= (int)nqt) break;
@@ -1294,8 +1306,8 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
                                 st_key[wv][sp] = key;
                                 st_q[wv][sp] = (uint8_t)qi;
                             } else {
-                                const uint32_t pos = atomicAdd(&counts[qi], 1u);
-                                if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = key;
+                                const uint32_t pos = atomicAdd(&cnt[qi], 1u);
+                                if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = key;
                             }
                         }
                         wcnt += (uint32_t)__popcll(m);
