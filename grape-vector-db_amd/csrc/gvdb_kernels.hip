@@ -1593,7 +1593,13 @@ static void launch_scan_t(const Stage1Args& a, hipStream_t s) {
 
 template <int W4>
 static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
-    uint32_t QT = 12288u / (a.D + 1u);
+    // GVDB_HIST_LDS_WORDS: LDS histogram words per block (timing knob; default 12288)
+    static const uint32_t words = [] {
+        const char* e = getenv("GVDB_HIST_LDS_WORDS");
+        const long v = e ? atol(e) : 0;
+        return v >= 1024 && v <= 36864 ? (uint32_t)v : 12288u;
+    }();
+    uint32_t QT = words / (a.D + 1u);
     if (QT < 1) QT = 1;
     if (QT > 32) QT = 32;
     if (QT > a.B) QT = a.B;
