@@ -101,10 +101,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    comm_info = None
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+        comm_info = {"world_size": dist.get_world_size(), "torch_backend": dist.get_backend(),
+                     "merge_collective": "ncclAllGather inside libgvdb (gvdb_index_search_sharded_device)"}
+        log(f"[bench] world={dist.get_world_size()} backend={dist.get_backend()} rank={rank} device={local_rank}")
+    elif args.gpus != 1:
+        raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes (WORLD_SIZE=1)")
     L = gvdb.lib()
 
     N, D, B, R, k = args.n, args.dim, args.batch, args.R, args.k
@@ -179,16 +186,13 @@ def main():
         def step():
             ix.search_device(q, k, out_ids, out_sc, out_n, sp)
     else:
-        from gvdb.sharded import ShardedBQSearch, gpu_candidates_fn, shard_bounds
+        # the product path: local candidates -> ncclAllGather -> merge, all in libgvdb
+        from gvdb.sharded import RcclShardedSearch
 
-        b = shard_bounds(N, world)
-        sharded = ShardedBQSearch(gpu_candidates_fn(ix), [b[g + 1] - b[g] for g in range(world)], B, R, k, dev)
+        sharded = RcclShardedSearch(ix, R, k)
 
         def step():
-            ids, sc, n = sharded.search(q)
-            out_ids.copy_(ids)
-            out_sc.copy_(sc)
-            out_n.copy_(n)
+            sharded.search_into(q, out_ids, out_sc, out_n)
 
     def barrier():
         torch.cuda.synchronize()
@@ -293,7 +297,8 @@ def main():
                            **({"flat_fallbacks": int(L.gvdb_flat_fallback_count() - f0)} if params.mode == 1 else {})})
 
         points.append({"search": f"bq R={R}", "queries": "iid", "qps": qps, "ms_per_step": 1e3 * t_max / args.steps,
-                       "recall_at_10": rec, "recall_at_1": float(np.mean(found[:, 0] == truth[:, 0])),
+                       "recall_at_10": rec,
+            "distributed": comm_info, "recall_at_1": float(np.mean(found[:, 0] == truth[:, 0])),
                        "steps": args.steps})
         for r in (1000, 4000):
             run_point(f"bq R={r}", gvdb.SearchParams(rescore_count=r))
@@ -447,6 +452,7 @@ def main():
                 "parallelism": f"corpus-shard x{world}" + (" + RCCL all-gather merge" if world > 1 else ""),
             },
             "recall_at_10": rec,
+            "distributed": comm_info,
             "stage_ms_per_step": {"stage1": s1_ms / max(scan_n, 1), "scan": scan_avg, "stage2": s2_ms / max(scan_n, 1)},
             "roofline": roof,
             "batch1": b1,
@@ -469,6 +475,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        torch.cuda.synchronize()
+        sharded.close()
         dist.destroy_process_group()
 
 

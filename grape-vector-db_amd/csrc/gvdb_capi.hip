@@ -306,6 +306,7 @@ struct BqSearchArgs {
     float* d_out_scores;
     uint32_t* d_out_n;
     uint32_t* d_out_dist;   // candidates mode: stage-1 order, no final sort
+    uint64_t out_stride;    // candidates mode: output row stride (0 = R)
 };
 
 gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
@@ -359,6 +360,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         }
     }
 
+    const uint64_t ostr = a.out_stride ? a.out_stride : R;
     auto run_stage2 = [&](uint32_t q0, uint32_t nq) -> gvdb_status {
         RerankArgs rr{};
         rr.rows = v.rows;
@@ -374,8 +376,8 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         HIP_TRY(launch_rerank(rr, s), "rerank");
         if (a.d_out_dist) {
             HIP_TRY(launch_emit_candidates(rr.s1_rows, ws.s1_dist.as<uint32_t>() + (uint64_t)q0 * R, rr.scores, nq, R,
-                                           v.ids, a.d_out_ids + (uint64_t)q0 * R, a.d_out_dist + (uint64_t)q0 * R,
-                                           a.d_out_scores + (uint64_t)q0 * R, s),
+                                           v.ids, a.d_out_ids + (uint64_t)q0 * ostr, a.d_out_dist + (uint64_t)q0 * ostr,
+                                           a.d_out_scores + (uint64_t)q0 * ostr, s, ostr),
                     "emit candidates");
             return GVDB_OK;
         }
@@ -1644,3 +1646,38 @@ uint64_t gvdb_flat_i8_fallback_count(void) { return flat_fallbacks_i8().load(); 
 
 // Shared error reporting for the other translation units (gvdb_sparse.hip).
 gvdb_status gvdb::report_status(gvdb_status s, const std::string& msg) { return fail(s, msg); }
+
+int gvdb::index_device(const gvdb_index* ix) { return ix->device; }
+
+// Sharded-search building block (gvdb_comm.hip): this shard's stage-1 top-R
+// (R clamped to its row count) with exact cosines, rows of the output at
+// stride `stride`, counts[q] = the clamped R.
+gvdb_status gvdb::shard_candidates(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
+                                   uint64_t stride, uint64_t* ids, uint32_t* dist, float* cosv, uint32_t* counts,
+                                   hipStream_t s) {
+    gvdb_status st = check_search(ix, dim, B, R);
+    if (st != GVDB_OK) return st;
+    const uint64_t Rl = std::min<uint64_t>(R, ix->n);
+    if (B == 0) return GVDB_OK;
+    HIP_TRY(hipMemsetD32Async(counts, (int)Rl, B, s), "candidate counts");
+    if (Rl == 0) return GVDB_OK;
+    if ((st = set_device(ix->device)) != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    BqSearchArgs a{};
+    a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
+    a.d_q = d_q;
+    a.qlen = dim;
+    a.B = (uint32_t)B;
+    a.thr = ix->thr;
+    a.dims_match = true;
+    a.R = (uint32_t)Rl;
+    a.kout = (uint32_t)Rl;
+    a.kind = kScoreCosine;
+    a.descending = 1;
+    a.d_out_ids = ids;
+    a.d_out_scores = cosv;
+    a.d_out_dist = dist;
+    a.out_stride = stride;
+    return bq_search(a, *g.w, s);
+}

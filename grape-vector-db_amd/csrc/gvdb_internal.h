@@ -231,13 +231,15 @@ hipError_t launch_widen(const uint32_t* a, uint64_t* b, uint64_t n, hipStream_t 
 
 hipError_t launch_emit_candidates(const uint32_t* s1_rows, const uint32_t* s1_dist, const float* scores, uint32_t B,
                                   uint32_t R, const uint64_t* ids, uint64_t* out_ids, uint32_t* out_dist,
-                                  float* out_scores, hipStream_t s);
+                                  float* out_scores, hipStream_t s, uint64_t out_stride = 0);  // 0 = R
 // Exact sharded multi-stage merge (one exchange): see gvdb_kernels.hip.
 // G*stride <= kSortLdsCap.
 hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cosv, const uint32_t* counts,
                                  uint32_t G, uint32_t B, uint32_t stride, uint32_t R, uint32_t kout, uint64_t* out_ids,
                                  float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s,
-                                 uint64_t gs_id = 0, uint64_t gs_w = 0);  // rank strides (0 = dense [G][B][stride])
+                                 uint64_t gs_id = 0, uint64_t gs_w = 0,  // rank strides (0 = dense [G][B][stride])
+                                 uint64_t gs_c = 0,                      // count stride per rank (0 = B)
+                                 int mark_nan = 0);                      // poisoned query -> out_n = GVDB_N_POISONED
 
 // ---- index maintenance -----------------------------------------------------------
 // Order-preserving gather of rows/codes/norms/ids: new row r <- old row map[r]
@@ -245,6 +247,14 @@ hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, con
 hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, uint4* ncodes, const float* norms,
                          float* nnorms, const uint64_t* ids, uint64_t* nids, const uint64_t* map, uint64_t m,
                          uint64_t cap, uint32_t D, hipStream_t s);
+
+// ---- sharded search (gvdb_comm.hip) ----------------------------------------------
+int index_device(const gvdb_index* ix);
+// this shard's stage-1 top-min(R, rows) + exact cosines, output rows at `stride`,
+// counts[q] = min(R, rows) (gvdb_capi.hip)
+gvdb_status shard_candidates(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
+                             uint64_t stride, uint64_t* ids, uint32_t* dist, float* cosv, uint32_t* counts,
+                             hipStream_t s);
 
 // ---- error reporting shared by the C-ABI translation units ---------------------
 // sets the thread-local gvdb_last_error() text and returns s

@@ -2587,24 +2587,27 @@ hipError_t launch_widen(const uint32_t* a, uint64_t* b, uint64_t n, hipStream_t 
 }
 
 // Stage-1-ordered candidate list with exact scores (sharded search input).
+// Output row stride out_stride >= R (a shard with fewer rows than the global
+// R fills the first R of each stride-R row of the all-gather send block).
 __global__ void k_emit_candidates(const uint32_t* __restrict__ s1_rows, const uint32_t* __restrict__ s1_dist,
-                                  const float* __restrict__ scores, uint32_t B, uint32_t R,
+                                  const float* __restrict__ scores, uint32_t B, uint32_t R, uint64_t out_stride,
                                   const uint64_t* __restrict__ ids, uint64_t* __restrict__ out_ids,
                                   uint32_t* __restrict__ out_dist, float* __restrict__ out_scores) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (uint64_t)B * R) return;
-    out_ids[t] = ids ? ids[s1_rows[t]] : (uint64_t)s1_rows[t];
-    out_dist[t] = s1_dist[t];
-    out_scores[t] = scores[t];
+    const uint64_t o = (t / R) * out_stride + t % R;
+    out_ids[o] = ids ? ids[s1_rows[t]] : (uint64_t)s1_rows[t];
+    out_dist[o] = s1_dist[t];
+    out_scores[o] = scores[t];
 }
 
 hipError_t launch_emit_candidates(const uint32_t* s1_rows, const uint32_t* s1_dist, const float* scores, uint32_t B,
                                   uint32_t R, const uint64_t* ids, uint64_t* out_ids, uint32_t* out_dist,
-                                  float* out_scores, hipStream_t s) {
+                                  float* out_scores, hipStream_t s, uint64_t out_stride) {
     const uint64_t total = (uint64_t)B * R;
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(k_emit_candidates, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, s1_rows, s1_dist,
-                       scores, B, R, ids, out_ids, out_dist, out_scores);
+                       scores, B, R, out_stride ? out_stride : (uint64_t)R, ids, out_ids, out_dist, out_scores);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2644,11 +2647,13 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
                                                         const uint32_t* __restrict__ dist,
                                                         const float* __restrict__ cosv,
                                                         const uint32_t* __restrict__ counts, uint32_t G, uint32_t B,
-                                                        uint32_t stride, uint64_t gs_id, uint64_t gs_w, uint32_t R,
-                                                        uint32_t kout, uint64_t* __restrict__ out_ids,
+                                                        uint32_t stride, uint64_t gs_id, uint64_t gs_w, uint64_t gs_c,
+                                                        uint32_t R, uint32_t kout, uint64_t* __restrict__ out_ids,
                                                         float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
-                                                        uint32_t* __restrict__ nan_flag) {
-    // rank g's list for query q starts at gids + g*gs_id + q*stride (dist/cosv: g*gs_w)
+                                                        uint32_t* __restrict__ nan_flag, int mark_nan) {
+    // rank g's list for query q starts at gids + g*gs_id + q*stride (dist/cosv: g*gs_w),
+    // its count is counts[g*gs_c + q].  mark_nan: a query whose top-R holds a NaN
+    // cosine (the reference's sort would panic) gets out_n[q] = GVDB_N_POISONED.
     __shared__ uint64_t sk[kSortLdsCap];
     __shared__ uint32_t sv[kSortLdsCap];
     __shared__ uint32_t s_n;
@@ -2657,7 +2662,7 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < G * stride; t += 256) {
         const uint32_t g = t / stride, i = t % stride;
-        if (i < counts[(uint64_t)g * B + q]) {
+        if (i < counts[(uint64_t)g * gs_c + q]) {
             const uint64_t at = (uint64_t)q * stride + i;
             const uint32_t pos = atomicAdd(&s_n, 1u);
             sk[pos] = ((uint64_t)dist[g * gs_w + at] << 40) | (gids[g * gs_id + at] & ((1ull << 40) - 1));
@@ -2694,7 +2699,8 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
         sv[i] = val;
     }
     __syncthreads();
-    if (s_nan && r >= 2 && threadIdx.x == 0) atomicOr(nan_flag, 1u);
+    const bool poisoned = s_nan && r >= 2;
+    if (poisoned && threadIdx.x == 0 && nan_flag) atomicOr(nan_flag, 1u);
     bitonic_sort_pairs_lds(sk, sv, P2);
     const uint32_t take = kout < r ? kout : r;
     for (uint32_t i = threadIdx.x; i < take; i += 256) {
@@ -2704,17 +2710,18 @@ __global__ __launch_bounds__(256) void k_bq_shard_merge(const uint64_t* __restri
         out_ids[(uint64_t)q * kout + i] = gids[g * gs_id + at];
         out_scores[(uint64_t)q * kout + i] = cosv[g * gs_w + at];
     }
-    if (threadIdx.x == 0 && out_n) out_n[q] = take;
+    if (threadIdx.x == 0 && out_n) out_n[q] = (poisoned && mark_nan) ? GVDB_N_POISONED : take;
 }
 
 hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, const float* cosv, const uint32_t* counts,
                                  uint32_t G, uint32_t B, uint32_t stride, uint32_t R, uint32_t kout, uint64_t* out_ids,
                                  float* out_scores, uint32_t* out_n, uint32_t* nan_flag, hipStream_t s,
-                                 uint64_t gs_id, uint64_t gs_w) {
+                                 uint64_t gs_id, uint64_t gs_w, uint64_t gs_c, int mark_nan) {
     if (B == 0) return hipSuccess;
     const uint64_t dense = (uint64_t)B * stride;  // [G][B][stride] when no rank strides are given
     hipLaunchKernelGGL(k_bq_shard_merge, dim3(B), dim3(256), 0, s, gids, dist, cosv, counts, G, B, stride,
-                       gs_id ? gs_id : dense, gs_w ? gs_w : dense, R, kout, out_ids, out_scores, out_n, nan_flag);
+                       gs_id ? gs_id : dense, gs_w ? gs_w : dense, gs_c ? gs_c : (uint64_t)B, R, kout, out_ids,
+                       out_scores, out_n, nan_flag, mark_nan);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

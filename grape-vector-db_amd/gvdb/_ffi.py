@@ -31,6 +31,8 @@ GVDB_METRIC_L2 = 1
 GVDB_METRIC_COSINE_DISTANCE = 2
 GVDB_SEARCH_BQ_RERANK = 0
 GVDB_SEARCH_FLAT = 1
+GVDB_N_POISONED = 0xFFFFFFFF
+GVDB_COMM_ID_BYTES = 128
 
 
 class gvdb_params(C.Structure):
@@ -139,6 +141,12 @@ SIGNATURES = {
     "gvdb_bq_shard_merge": (C.c_int, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P]),
     "gvdb_bq_shard_merge_device": (C.c_int, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P, P]),
     "gvdb_bq_shard_merge_packed_device": (C.c_int, [P, P, u64, u64, u64, u64, P, P, P, P]),
+    "gvdb_comm_get_unique_id": (C.c_int, [P]),
+    "gvdb_comm_create": (C.c_int, [P, i32, i32, i32, C.POINTER(P)]),
+    "gvdb_comm_destroy": (None, [P]),
+    "gvdb_comm_info": (C.c_int, [P, C.POINTER(i32), C.POINTER(i32)]),
+    "gvdb_index_search_sharded_device": (C.c_int, [P, P, P, u64, u32, u64, C.POINTER(gvdb_search_params), P, P, P,
+                                                   P]),
     "gvdb_sparse_create": (C.c_int, [C.POINTER(gvdb_bm25_params), C.POINTER(P)]),
     "gvdb_sparse_destroy": (None, [P]),
     "gvdb_sparse_add_document": (C.c_int, [P, u64, P, P, u64, f32]),

@@ -132,3 +132,50 @@ def gpu_candidates_fn(index) -> CandidatesFn:
 
     fn.into = into
     return fn
+
+
+class RcclShardedSearch:
+    """The same exact sharded search with the collective inside libgvdb
+    (``gvdb_index_search_sharded_device``): local candidates -> ncclAllGather
+    on the caller's stream -> merge, all behind the C ABI, so a host without
+    torch (the Rust FFI of INTEGRATION.md) shards the same way.  torch.distributed
+    is used here only to hand rank 0's RCCL unique id to the other ranks."""
+
+    def __init__(self, index, R: int, k: int, group=None):
+        import ctypes as C
+
+        self.index, self.R, self.k = index, R, k
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        L = lib()
+        uid = (C.c_uint8 * 128)()
+        if self.rank == 0:
+            check(L.gvdb_comm_get_unique_id(uid))
+        if self.world > 1:
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=0, group=group)
+            C.memmove(uid, box[0], 128)
+        h = C.c_void_p()
+        check(L.gvdb_comm_create(uid, self.world, self.rank, index.device, C.byref(h)))
+        self._h = h
+        from . import SearchParams
+
+        self.sp = SearchParams(rescore_count=R).to_c()
+
+    def search_into(self, q: torch.Tensor, out_ids: torch.Tensor, out_scores: torch.Tensor, out_n=None) -> None:
+        import ctypes as C
+
+        stream = torch.cuda.current_stream(q.device).cuda_stream or None
+        check(lib().gvdb_index_search_sharded_device(self.index._h, self._h, q.data_ptr(), q.shape[0], q.shape[1],
+                                                     self.k, C.byref(self.sp), out_ids.data_ptr(),
+                                                     out_scores.data_ptr(),
+                                                     out_n.data_ptr() if out_n is not None else None, stream))
+
+    def close(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib().gvdb_comm_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

@@ -37,7 +37,12 @@
 extern "C" {
 #endif
 
-#define GVDB_ABI_VERSION 1
+#define GVDB_ABI_VERSION 2
+
+/* out_n[q] of a _device search whose query hit a NaN score (the reference's
+ * partial_cmp().unwrap() sort would panic): that query has no results.  The
+ * host-buffer forms return GVDB_ERR_QUANTIZATION instead. */
+#define GVDB_N_POISONED 0xFFFFFFFFu
 
 typedef enum gvdb_status {
     GVDB_OK = 0,
@@ -278,6 +283,36 @@ gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d
 gvdb_status gvdb_bq_shard_merge_packed_device(const uint32_t* d_gathered, const uint32_t* d_counts, uint64_t G,
                                               uint64_t B, uint64_t R, uint64_t k, uint64_t* d_out_ids,
                                               float* d_out_scores, uint32_t* d_out_n, void* stream);
+
+/* ---- sharded search over RCCL (ShardManager::search_vectors, shard.rs:760-786,
+ * inside one node: one process per GPU, corpus split into contiguous row
+ * ranges whose ids are global row numbers) ---------------------------------- */
+#define GVDB_COMM_ID_BYTES 128   /* = sizeof(ncclUniqueId) */
+typedef struct gvdb_comm gvdb_comm;
+/* Rank 0 creates the id and hands it to the other ranks out of band (the
+ * host's own transport: torch.distributed, MPI, a file, ...).  RCCL is loaded
+ * on first use (dlopen "librccl.so.1"); GVDB_ERR_DEVICE when it is absent. */
+gvdb_status gvdb_comm_get_unique_id(uint8_t id[GVDB_COMM_ID_BYTES]);
+/* Collective: every rank of the group calls it (ncclCommInitRank). */
+gvdb_status gvdb_comm_create(const uint8_t id[GVDB_COMM_ID_BYTES], int32_t world, int32_t rank, int32_t device,
+                             gvdb_comm** out);
+void gvdb_comm_destroy(gvdb_comm* comm);
+gvdb_status gvdb_comm_info(const gvdb_comm* comm, int32_t* world, int32_t* rank);
+/* Exact sharded BQ search (collective; every rank passes the same queries and
+ * its own shard).  Per rank: stage 1 local top-R (Hamming asc, id asc) with the
+ * exact cosine of each candidate (quantization.rs:165-187), written straight
+ * into the rank's all-gather block; ONE ncclAllGather on `stream` moves the
+ * blocks over xGMI; every rank merges: union by (Hamming, id) -> first R ->
+ * stable by cosine desc -> first k.  Bit-identical to one multi_stage_search
+ * over the union of the shards.  R = sp->rescore_count (> 0; the global
+ * rescore_ratio form needs the global row count: pass the count), R >= k,
+ * world * R <= 4096.  Results land on every rank, on `stream`; no host sync
+ * (a NaN-poisoned query gets out_n = GVDB_N_POISONED).  Calls on one comm
+ * are serialised. */
+gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm* comm, const float* d_queries,
+                                             uint64_t B, uint32_t dim, uint64_t k, const gvdb_search_params* sp,
+                                             uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
+                                             void* stream);
 
 /* ---- BM25 sparse index (src/sparse.rs:29-222) ---------------------------- */
 /* SparseIndex: an HBM forward index over document slots; documents are

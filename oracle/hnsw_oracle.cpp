@@ -37,6 +37,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <queue>
@@ -52,6 +53,28 @@ float l2(const float* a, const float* b, uint32_t d) {
         s = s + t * t;
     }
     return std::sqrt(s);
+}
+
+// Four independent distances with their folds interleaved: each sum is still
+// the strict left-to-right fold of l2() (bit-identical), but the four
+// dependency chains overlap, so a beam step costs ~1/4 of four l2() calls.
+// (A CPU-side optimisation the reference does not have: it only makes the
+// baseline faster, never different.)
+void l2x4(const float* q, const float* const* r, uint32_t d, float* out) {
+    float s0 = -0.0f, s1 = -0.0f, s2 = -0.0f, s3 = -0.0f;
+    const float *a = r[0], *b = r[1], *c = r[2], *e = r[3];
+    for (uint32_t i = 0; i < d; ++i) {
+        const float x = q[i];
+        const float t0 = x - a[i], t1 = x - b[i], t2 = x - c[i], t3 = x - e[i];
+        s0 = s0 + t0 * t0;
+        s1 = s1 + t1 * t1;
+        s2 = s2 + t2 * t2;
+        s3 = s3 + t3 * t3;
+    }
+    out[0] = std::sqrt(s0);
+    out[1] = std::sqrt(s1);
+    out[2] = std::sqrt(s2);
+    out[3] = std::sqrt(s3);
 }
 
 uint64_t splitmix(uint64_t& s) {
@@ -114,7 +137,8 @@ struct Hnsw {
             res.push(e);
             if (res.size() > ef) res.pop();
         }
-        std::vector<uint32_t> nb;
+        std::vector<uint32_t> nb, todo;
+        std::vector<float> dv4;
         while (!cand.empty()) {
             const Cand c = cand.top();
             if (res.size() >= ef && c.d > res.top().d) break;
@@ -129,10 +153,24 @@ struct Hnsw {
                     nb.assign(l, l + *cnt);
                 }
             }
+            // unseen neighbours in list order, their distances four at a time
+            todo.clear();
             for (uint32_t v : nb) {
                 if (seen[v] == epoch) continue;
                 seen[v] = epoch;
-                const float dv = dist(q, v);
+                todo.push_back(v);
+            }
+            dv4.resize(todo.size() + 3);
+            size_t j = 0;
+            for (; j + 4 <= todo.size(); j += 4) {
+                const float* r4[4];
+                for (int t = 0; t < 4; ++t) r4[t] = rows + (uint64_t)todo[j + t] * d;
+                l2x4(q, r4, d, &dv4[j]);
+            }
+            for (; j < todo.size(); ++j) dv4[j] = dist(q, todo[j]);
+            for (size_t t = 0; t < todo.size(); ++t) {
+                const uint32_t v = todo[t];
+                const float dv = dv4[t];
                 if (res.size() < ef || dv < res.top().d) {
                     cand.push({dv, v});
                     res.push({dv, v});
@@ -154,11 +192,17 @@ struct Hnsw {
         for (const Cand& c : asc) {
             if (keep.size() >= m) break;
             bool good = true;
-            for (const Cand& r : keep)
-                if (l2(rows + (uint64_t)c.id * d, rows + (uint64_t)r.id * d, d) < c.d) {
-                    good = false;
-                    break;
-                }
+            const float* x = rows + (uint64_t)c.id * d;
+            size_t j = 0;
+            for (; good && j + 4 <= keep.size(); j += 4) {  // same test, four distances at a time
+                const float* r4[4];
+                float d4[4];
+                for (int t = 0; t < 4; ++t) r4[t] = rows + (uint64_t)keep[j + t].id * d;
+                l2x4(x, r4, d, d4);
+                for (int t = 0; t < 4; ++t) good = good && !(d4[t] < c.d);
+            }
+            for (; good && j < keep.size(); ++j)
+                if (l2(x, rows + (uint64_t)keep[j].id * d, d) < c.d) good = false;
             (good ? keep : pruned).push_back(c);
         }
         for (size_t i = 0; i < pruned.size() && keep.size() < m; ++i) keep.push_back(pruned[i]);
@@ -265,26 +309,33 @@ void* hnsw_build(const float* rows, uint64_t n, uint32_t d, uint32_t M, uint32_t
     }
     h->locks = std::vector<std::mutex>(n);
     const int T = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
-    // upper-layer points first (sequential, small), then the rest in parallel
-    {
-        std::vector<uint32_t> seen(n, 0);
-        uint32_t epoch = 0;
-        for (uint64_t r = 1; r < std::min<uint64_t>(n, std::max<uint64_t>(nup, 1)); ++r)
-            h->insert(h->order[r], seen, epoch);
+    // layer by layer from the top, each layer's points in parallel (as the
+    // crate does: points of one layer are inserted concurrently once every
+    // higher layer is complete); rank 0 is the entry point
+    std::atomic<uint64_t> done{0};
+    for (int L = (int)h->top; L >= 0; --L) {
+        const uint64_t lo = std::max<uint64_t>(L + 1 < (int)at_least.size() ? at_least[L + 1] : 0, 1);
+        const uint64_t hi = at_least[L];
+        if (lo >= hi) continue;
+        std::atomic<uint64_t> next{lo};
+        std::vector<std::thread> pool;
+        const int TL = (int)std::min<uint64_t>((uint64_t)T, hi - lo);
+        for (int t = 0; t < TL; ++t)
+            pool.emplace_back([&] {
+                std::vector<uint32_t> seen(n, 0);
+                uint32_t epoch = 0;
+                for (;;) {
+                    const uint64_t r = next.fetch_add(1);
+                    if (r >= hi) break;
+                    h->insert(h->order[r], seen, epoch);
+                    // progress for long builds (a silent multi-minute run looks hung to the GPU-box runner)
+                    const uint64_t c = done.fetch_add(1) + 1;
+                    if (n >= 200000 && c % 50000 == 0)
+                        fprintf(stderr, "[hnsw] inserted %llu / %llu\n", (unsigned long long)c, (unsigned long long)n);
+                }
+            });
+        for (auto& th : pool) th.join();
     }
-    std::atomic<uint64_t> next{std::max<uint64_t>(nup, 1)};
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t)
-        pool.emplace_back([&] {
-            std::vector<uint32_t> seen(n, 0);
-            uint32_t epoch = 0;
-            for (;;) {
-                const uint64_t r = next.fetch_add(1);
-                if (r >= n) break;
-                h->insert(h->order[r], seen, epoch);
-            }
-        });
-    for (auto& th : pool) th.join();
     return h;
 }
 
