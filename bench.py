@@ -297,8 +297,7 @@ def main():
                            **({"flat_fallbacks": int(L.gvdb_flat_fallback_count() - f0)} if params.mode == 1 else {})})
 
         points.append({"search": f"bq R={R}", "queries": "iid", "qps": qps, "ms_per_step": 1e3 * t_max / args.steps,
-                       "recall_at_10": rec,
-            "distributed": comm_info, "recall_at_1": float(np.mean(found[:, 0] == truth[:, 0])),
+                       "recall_at_10": rec, "recall_at_1": float(np.mean(found[:, 0] == truth[:, 0])),
                        "steps": args.steps})
         for r in (1000, 4000):
             run_point(f"bq R={r}", gvdb.SearchParams(rescore_count=r))

@@ -90,11 +90,13 @@ std::atomic<uint64_t>& flat_fallbacks_i8() {
 
 enum { kTimSampleHist = 0, kTimScan = 1, kTimSelect = 2, kTimRerank = 3, kTimFinal = 4, kTimFlatEmit = 5, kTimFlat = 6,
        kTimFlatEmitI8 = 7, kTimFlatI8 = 8, kTimN = 9 };
+struct EvSet;
 struct Timing {
     std::mutex mu;
     bool on = false;
     double ms[kTimN] = {0};
     uint64_t n[kTimN] = {0};
+    std::vector<EvSet*> pending, free_sets;  // BQ search events awaiting collection / reusable
 };
 Timing& timing() {
     static Timing t;
@@ -148,7 +150,15 @@ struct Workspace {
         rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
+    // Searches return without a host sync: the workspace goes back to the pool
+    // while its kernels may still run on the caller's stream.  `done` marks the
+    // end of that work; the next user on another stream waits for it on the
+    // device (hipStreamWaitEvent), never on the host.
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+    bool pending = false;
     ~Workspace() {
+        if (done) (void)hipEventDestroy(done);
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
                         &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
                         &fx_scores, &flt_rows, &flt_ids})
@@ -194,9 +204,23 @@ WsPool& global_pool() {
 
 struct WsGuard {
     Workspace* w;
+    hipStream_t s = nullptr;
+    bool begun = false;
     explicit WsGuard(int dev) : w(global_pool().acquire(dev)) {}
+    // order this call's work on stream st after the workspace's previous user
+    void begin(hipStream_t st) {
+        s = st;
+        begun = true;
+        if (w->pending && w->last != st) (void)hipStreamWaitEvent(st, w->done, 0);
+    }
     ~WsGuard() {
-        if (w) global_pool().release(w);
+        if (!w) return;
+        if (begun) {
+            if (!w->done) (void)hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
+            w->pending = w->done && hipEventRecord(w->done, s) == hipSuccess;
+            w->last = s;
+        }
+        global_pool().release(w);
     }
 };
 
@@ -262,6 +286,7 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
                                                         : 1;
     const char* dbg = getenv("GVDB_SCAN_DBG");  // ablation timing only (results invalid when set)
     s1.dbg = dbg ? atoi(dbg) : 0;
+    s1.force_rescan = getenv_flag("GVDB_FORCE_RESCAN") ? 1 : 0;  // tests of the device-side fallback
     // GVDB_SAMPLE_DIV: sample ~N/div rows for large batches (timing experiments; default 64)
     static const uint32_t big_div = [] {
         const char* e = getenv("GVDB_SAMPLE_DIV");
@@ -309,13 +334,61 @@ struct BqSearchArgs {
     uint64_t out_stride;    // candidates mode: output row stride (0 = R)
 };
 
+// Stage-1 + stage-2 timing without a host round trip: events are recorded
+// on the search stream and their elapsed times are collected lazily (at
+// gvdb_timing_read / reset, or when too many are pending).
+EvSet* timing_events() {
+    std::lock_guard<std::mutex> g(timing().mu);
+    auto& fr = timing().free_sets;
+    if (!fr.empty()) {
+        EvSet* e = fr.back();
+        fr.pop_back();
+        return e;
+    }
+    auto* e = new EvSet();
+    e->create();
+    if (!e->ok) {
+        delete e;
+        return nullptr;
+    }
+    return e;
+}
+void timing_drain_locked(size_t n) {
+    auto& pend = timing().pending;
+    n = std::min(n, pend.size());
+    for (size_t i = 0; i < n; ++i) {
+        EvSet* e = pend[i];
+        if (hipEventSynchronize(e->e[5]) == hipSuccess) {
+            float t[4] = {0, 0, 0, 0};
+            (void)hipEventElapsedTime(&t[0], e->e[0], e->e[1]);
+            (void)hipEventElapsedTime(&t[1], e->e[1], e->e[2]);
+            (void)hipEventElapsedTime(&t[2], e->e[2], e->e[3]);
+            (void)hipEventElapsedTime(&t[3], e->e[3], e->e[5]);
+            for (int k = 0; k < 4; ++k) {
+                timing().ms[k] += t[k];
+                timing().n[k] += 1;
+            }
+        }
+        timing().free_sets.push_back(e);
+    }
+    pend.erase(pend.begin(), pend.begin() + n);
+}
+void timing_submit(EvSet* e) {
+    std::lock_guard<std::mutex> g(timing().mu);
+    timing().pending.push_back(e);
+    if (timing().pending.size() > 512) timing_drain_locked(256);
+}
+
+// BQ multi-stage search on one shard view, enqueued on stream s with NO host
+// synchronisation: stage 1 (certified fast path whose rare fallbacks run on
+// the device, k_select), stage 2 (exact rerank), final ordering.  A query whose
+// top-R holds a NaN score gets out_n = GVDB_N_POISONED (the reference panics).
 gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     const ShardView& v = a.v;
     const uint32_t B = a.B, R = a.R;
     if (B == 0) return GVDB_OK;
     if (R == 0) {
         if (a.d_out_n) HIP_TRY(hipMemsetAsync(a.d_out_n, 0, (size_t)B * 4, s), "memset out_n");
-        HIP_TRY(hipStreamSynchronize(s), "sync");
         return GVDB_OK;
     }
     const uint32_t W4 = code_w4(v.D);
@@ -325,17 +398,14 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     Stage1Args s1{};
     gvdb_status pst = prepare_stage1(ws, s1, B, v.D, R, v.N, s);
     if (pst != GVDB_OK) return pst;
-    uint32_t* d_flags = s1.any_fail;  // [0] any stage-1 failure, [1] NaN
+    uint32_t* d_flags = s1.any_fail;  // [0] any stage-1 rescan, [1] NaN seen, [2] per-query NaN scratch
 
-    std::vector<uint32_t> slow_q;
-    bool fast_ran = false;
     bool timed = false;
     {
         std::lock_guard<std::mutex> g(timing().mu);
         timed = timing().on;
     }
-    if (timed && !ws.ev.ok) ws.ev.create();
-    timed = timed && ws.ev.ok;
+    EvSet* ev = nullptr;
     if (!a.dims_match || v.D == 0) {
         HIP_TRY(launch_iota_rows(ws.s1_rows.as<uint32_t>(), B, R, s), "iota");
     } else {
@@ -345,6 +415,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             HIP_TRY(launch_pack(a.d_q, B, v.D, a.thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
         }
         if (R <= kSelectLdsCap) {
+            if (timed) ev = timing_events();
             s1.codes = v.codes;
             s1.cap = v.cap;
             s1.N = v.N;
@@ -352,101 +423,70 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             s1.qcodes = ws.qcodes.as<uint4>();
             s1.B = B;
             s1.R = R;
-            s1.ev = timed ? ws.ev.e : nullptr;
+            s1.ev = ev ? ev->e : nullptr;
             HIP_TRY(launch_stage1_fast(s1, s), "stage1");
-            fast_ran = true;
         } else {
-            for (uint32_t q = 0; q < B; ++q) slow_q.push_back(q);
+            // R beyond the LDS select: every query on the exact all-rows path
+            HIP_TRY(ws.slow.ensure(stage1_slow_bytes(v.N)), "alloc slow path");
+            for (uint32_t q = 0; q < B; ++q)
+                HIP_TRY(launch_stage1_slow(v.codes, v.cap, v.N, v.D, ws.qcodes.as<uint4>() + (uint64_t)q * W4, R,
+                                           ws.s1_rows.as<uint32_t>() + (uint64_t)q * R,
+                                           ws.s1_dist.as<uint32_t>() + (uint64_t)q * R, ws.slow.p, ws.slow.n, s),
+                        "stage1 slow");
         }
     }
 
-    const uint64_t ostr = a.out_stride ? a.out_stride : R;
-    auto run_stage2 = [&](uint32_t q0, uint32_t nq) -> gvdb_status {
-        RerankArgs rr{};
-        rr.rows = v.rows;
-        rr.clen = v.clen;
-        rr.norms = v.norms;
-        rr.q = a.d_q + (uint64_t)q0 * a.qlen;
-        rr.qlen = a.qlen;
-        rr.s1_rows = ws.s1_rows.as<uint32_t>() + (uint64_t)q0 * R;
-        rr.B = nq;
-        rr.R = R;
-        rr.kind = a.kind;
-        rr.scores = ws.scores.as<float>() + (uint64_t)q0 * R;
-        HIP_TRY(launch_rerank(rr, s), "rerank");
-        if (a.d_out_dist) {
-            HIP_TRY(launch_emit_candidates(rr.s1_rows, ws.s1_dist.as<uint32_t>() + (uint64_t)q0 * R, rr.scores, nq, R,
-                                           v.ids, a.d_out_ids + (uint64_t)q0 * ostr, a.d_out_dist + (uint64_t)q0 * ostr,
-                                           a.d_out_scores + (uint64_t)q0 * ostr, s, ostr),
-                    "emit candidates");
-            return GVDB_OK;
-        }
+    RerankArgs rr{};
+    rr.rows = v.rows;
+    rr.clen = v.clen;
+    rr.norms = v.norms;
+    rr.q = a.d_q;
+    rr.qlen = a.qlen;
+    rr.s1_rows = ws.s1_rows.as<uint32_t>();
+    rr.B = B;
+    rr.R = R;
+    rr.kind = a.kind;
+    rr.scores = ws.scores.as<float>();
+    HIP_TRY(launch_rerank(rr, s), "rerank");
+    if (a.d_out_dist) {
+        const uint64_t ostr = a.out_stride ? a.out_stride : R;
+        HIP_TRY(launch_emit_candidates(rr.s1_rows, ws.s1_dist.as<uint32_t>(), rr.scores, B, R, v.ids, a.d_out_ids,
+                                       a.d_out_dist, a.d_out_scores, s, ostr),
+                "emit candidates");
+    } else {
         FinalArgs fa{};
         fa.scores = rr.scores;
         fa.s1_rows = rr.s1_rows;
-        fa.B = nq;
+        fa.B = B;
         fa.R = R;
         fa.kout = a.kout;
         fa.descending = a.descending;
         fa.ids = v.ids;
         fa.row_offset = v.row_offset;
-        fa.out_ids = a.d_out_ids + (uint64_t)q0 * a.kout;
-        fa.out_scores = a.d_out_scores + (uint64_t)q0 * a.kout;
-        fa.out_n = a.d_out_n ? a.d_out_n + q0 : nullptr;
+        fa.out_ids = a.d_out_ids;
+        fa.out_scores = a.d_out_scores;
+        fa.out_n = a.d_out_n;
         fa.nan_flag = d_flags + 1;
         if (R <= kSortLdsCap) {
             HIP_TRY(launch_final_sort(fa, s), "final sort");
         } else {
-            const size_t need = final_sort_global_bytes(R);
-            HIP_TRY(ws.sort_tmp.ensure(need), "alloc sort tmp");
+            HIP_TRY(ws.sort_tmp.ensure(final_sort_global_bytes(R)), "alloc sort tmp");
             HIP_TRY(launch_final_sort_global(fa, ws.sort_tmp.p, ws.sort_tmp.n, s), "final sort (global)");
         }
-        return GVDB_OK;
-    };
+    }
+    if (ev) {
+        HIP_TRY(hipEventRecord(ev->e[5], s), "event");
+        timing_submit(ev);
+    }
+    return GVDB_OK;
+}
 
-    if (slow_q.size() < B) {
-        gvdb_status st = run_stage2(0, B);
-        if (st != GVDB_OK) return st;
-        if (timed) HIP_TRY(hipEventRecord(ws.ev.e[5], s), "event");
-    }
-    // One host sync per batch: flags[0] says whether any query left the
-    // certified fast path, flags[1] whether a NaN score appeared.
-    HIP_TRY(hipMemcpyAsync(ws.h_flags, d_flags, 8, hipMemcpyDeviceToHost, s), "read flags");
-    HIP_TRY(hipStreamSynchronize(s), "sync");
-    if (timed && fast_ran && slow_q.size() < B) {
-        float t[4] = {0, 0, 0, 0};
-        (void)hipEventElapsedTime(&t[0], ws.ev.e[0], ws.ev.e[1]);
-        (void)hipEventElapsedTime(&t[1], ws.ev.e[1], ws.ev.e[2]);
-        (void)hipEventElapsedTime(&t[2], ws.ev.e[2], ws.ev.e[3]);
-        (void)hipEventElapsedTime(&t[3], ws.ev.e[3], ws.ev.e[5]);
-        std::lock_guard<std::mutex> g(timing().mu);
-        for (int i = 0; i < 4; ++i) {
-            timing().ms[i] += t[i];
-            timing().n[i] += 1;
-        }
-    }
-    if (fast_ran && ws.h_flags[0]) {
-        std::vector<uint32_t> fails(B);
-        HIP_TRY(hipMemcpy(fails.data(), s1.fail, (size_t)B * 4, hipMemcpyDeviceToHost), "read fail");
-        for (uint32_t q = 0; q < B; ++q)
-            if (fails[q]) slow_q.push_back(q);
-    }
-    if (!slow_q.empty()) {
-        const size_t need = stage1_slow_bytes(v.N);
-        HIP_TRY(ws.slow.ensure(need), "alloc slow path");
-        for (uint32_t q : slow_q) {
-            HIP_TRY(launch_stage1_slow(v.codes, v.cap, v.N, v.D, ws.qcodes.as<uint4>() + (uint64_t)q * W4, R,
-                                       ws.s1_rows.as<uint32_t>() + (uint64_t)q * R,
-                                       ws.s1_dist.as<uint32_t>() + (uint64_t)q * R, ws.slow.p, ws.slow.n, s),
-                    "stage1 slow");
-            gvdb_status st = run_stage2(q, 1);
-            if (st != GVDB_OK) return st;
-        }
-        HIP_TRY(hipMemcpyAsync(ws.h_flags, d_flags, 8, hipMemcpyDeviceToHost, s), "read flags");
-        HIP_TRY(hipStreamSynchronize(s), "sync");
-    }
-    if (ws.h_flags[1])
-        return fail(GVDB_ERR_QUANTIZATION, "NaN score: the reference's partial_cmp().unwrap() sort would panic");
+// Host-buffer entry points synchronise anyway: map a poisoned query (NaN
+// score, GVDB_N_POISONED) to the reference's failure.
+gvdb_status check_poisoned(const uint32_t* h_n, uint64_t B) {
+    for (uint64_t q = 0; q < B; ++q)
+        if (h_n[q] == GVDB_N_POISONED)
+            return fail(GVDB_ERR_QUANTIZATION, "NaN score: the reference's partial_cmp().unwrap() sort would panic");
     return GVDB_OK;
 }
 
@@ -511,6 +551,17 @@ namespace {
 gvdb_status set_device(int dev) {
     hipError_t e = hipSetDevice(dev);
     if (e != hipSuccess) return dev_fail(e, "hipSetDevice");
+    return GVDB_OK;
+}
+
+// Mutations take the caller's exclusive lock, but searches return before
+// their kernels finish: drain the device before rows / codes / ids change
+// under an in-flight search.
+gvdb_status quiesce(const gvdb_index* ix) {
+    gvdb_status st = set_device(ix->device);
+    if (st != GVDB_OK) return st;
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return dev_fail(e, "drain in-flight searches");
     return GVDB_OK;
 }
 
@@ -667,8 +718,7 @@ gvdb_status gvdb_index_create(const gvdb_params* params, gvdb_index** out) {
 
 void gvdb_index_destroy(gvdb_index* ix) {
     if (!ix) return;
-    (void)hipSetDevice(ix->device);
-    (void)hipStreamSynchronize(ix->stream);
+    (void)quiesce(ix);
     ix->free_all();
     (void)hipStreamDestroy(ix->stream);
     delete ix;
@@ -677,7 +727,7 @@ void gvdb_index_destroy(gvdb_index* ix) {
 gvdb_status gvdb_index_add(gvdb_index* ix, const float* rows, uint64_t n, uint32_t dim, const uint64_t* ids) {
     if (!ix || (n && (!rows || !ids))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (n == 0) return GVDB_OK;
-    gvdb_status st = set_device(ix->device);
+    gvdb_status st = quiesce(ix);
     if (st != GVDB_OK) return st;
     if ((st = check_add_dim(ix, dim)) != GVDB_OK) return st;
     if ((st = ensure_capacity(ix, ix->n + n)) != GVDB_OK) return st;
@@ -691,12 +741,11 @@ gvdb_status gvdb_index_add_device(gvdb_index* ix, const float* d_rows, uint64_t 
                                   void* stream) {
     if (!ix || (n && (!d_rows || !d_ids))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (n == 0) return GVDB_OK;
-    gvdb_status st = set_device(ix->device);
+    gvdb_status st = quiesce(ix);  // also waits for the caller's stream that produced the rows
     if (st != GVDB_OK) return st;
     if ((st = check_add_dim(ix, dim)) != GVDB_OK) return st;
     if ((st = ensure_capacity(ix, ix->n + n)) != GVDB_OK) return st;
-    // the rows were produced on the caller's stream (NULL = default stream): wait for them
-    HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "caller stream");
+    (void)stream;
     HIP_TRY(hipMemcpyAsync(ix->rows + ix->n * dim, d_rows, n * dim * 4, hipMemcpyDeviceToDevice, ix->stream),
             "copy rows");
     HIP_TRY(hipMemcpyAsync(ix->ids + ix->n, d_ids, n * 8, hipMemcpyDeviceToDevice, ix->stream), "copy ids");
@@ -1027,6 +1076,7 @@ gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
     hipStream_t s = ws.stream;
+    g.begin(s);
     const uint64_t kk = k ? k : 1;
     HIP_TRY(ws.q.ensure(B * dim * 4), "alloc queries");
     HIP_TRY(ws.out_ids.ensure(B * kk * 8), "alloc out");
@@ -1044,7 +1094,7 @@ gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64
     HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
     HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download n");
     HIP_TRY(hipStreamSynchronize(s), "sync");
-    return GVDB_OK;
+    return check_poisoned(out_n, B);
 }
 
 // Filtered search (§8(f) rank 4): the pre-mask of FilterEngine::execute_filter
@@ -1086,6 +1136,7 @@ gvdb_status gvdb_index_search_filtered(const gvdb_index* ix, const float* querie
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
     hipStream_t s = ws.stream;
+    g.begin(s);
     HIP_TRY(hipStreamSynchronize(ix->stream), "sync mutations");
     HIP_TRY(ws.q.ensure(B * dim * 4), "alloc queries");
     HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
@@ -1127,6 +1178,7 @@ gvdb_status gvdb_index_search_device(const gvdb_index* ix, const float* d_querie
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
+    g.begin(s);
     return index_search_impl(ix, d_queries, B, dim, k, sp, d_out_ids, d_out_scores, d_out_n, *g.w, s);
 }
 
@@ -1142,6 +1194,7 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream
+    g.begin(s);
     const uint32_t W4 = code_w4(dim);
     const uint32_t RR = (uint32_t)R;
     HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc");
@@ -1149,7 +1202,6 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
     st = prepare_stage1(ws, s1, (uint32_t)B, dim, RR, (uint32_t)ix->n, s);
     if (st != GVDB_OK) return st;
     HIP_TRY(launch_pack(d_queries, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
-    std::vector<uint32_t> fails(B, 1u);
     if (RR <= kSelectLdsCap) {
         s1.codes = ix->codes;
         s1.cap = ix->cap;
@@ -1159,24 +1211,16 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
         s1.B = (uint32_t)B;
         s1.R = RR;
         HIP_TRY(launch_stage1_fast(s1, s), "stage1");
-        HIP_TRY(hipMemcpyAsync(fails.data(), s1.fail, B * 4, hipMemcpyDeviceToHost, s), "read fail");
-        HIP_TRY(hipStreamSynchronize(s), "sync");
-    }
-    bool any_slow = false;
-    for (uint64_t q = 0; q < B; ++q) {
-        if (!fails[q]) continue;
-        if (!any_slow) {
-            HIP_TRY(ws.slow.ensure(stage1_slow_bytes((uint32_t)ix->n)), "alloc slow");
-            any_slow = true;
-        }
-        HIP_TRY(launch_stage1_slow(ix->codes, ix->cap, (uint32_t)ix->n, dim, ws.qcodes.as<uint4>() + q * W4, RR,
-                                   ws.s1_rows.as<uint32_t>() + q * R, ws.s1_dist.as<uint32_t>() + q * R, ws.slow.p,
-                                   ws.slow.n, s),
-                "stage1 slow");
+    } else {
+        HIP_TRY(ws.slow.ensure(stage1_slow_bytes((uint32_t)ix->n)), "alloc slow");
+        for (uint64_t q = 0; q < B; ++q)
+            HIP_TRY(launch_stage1_slow(ix->codes, ix->cap, (uint32_t)ix->n, dim, ws.qcodes.as<uint4>() + q * W4, RR,
+                                       ws.s1_rows.as<uint32_t>() + q * R, ws.s1_dist.as<uint32_t>() + q * R, ws.slow.p,
+                                       ws.slow.n, s),
+                    "stage1 slow");
     }
     HIP_TRY(launch_widen(ws.s1_rows.as<uint32_t>(), d_out_rows, B * R, s), "widen rows");
     HIP_TRY(hipMemcpyAsync(d_out_dist, ws.s1_dist.p, B * R * 4, hipMemcpyDeviceToDevice, s), "dist");
-    HIP_TRY(hipStreamSynchronize(s), "sync");
     return GVDB_OK;
 }
 
@@ -1185,7 +1229,7 @@ gvdb_status gvdb_index_remove(gvdb_index* ix, uint64_t id, int32_t* removed) {
     if (removed) *removed = 0;
     auto it = ix->id_row.find(id);
     if (it == ix->id_row.end()) return GVDB_OK;  // Ok(false) (index.rs:282-284)
-    gvdb_status st = set_device(ix->device);
+    gvdb_status st = quiesce(ix);
     if (st != GVDB_OK) return st;
     const uint64_t gone = it->second;
     ix->id_row.erase(it);
@@ -1250,8 +1294,7 @@ int32_t gvdb_index_is_empty(const gvdb_index* ix) { return gvdb_index_len(ix) ==
 
 void gvdb_index_clear(gvdb_index* ix) {
     if (!ix) return;
-    (void)hipSetDevice(ix->device);
-    (void)hipStreamSynchronize(ix->stream);
+    (void)quiesce(ix);
     ix->free_all();
     ix->dim = 0;  // dimension = None (index.rs:304-309)
     ix->h_ids.clear();
@@ -1305,6 +1348,7 @@ void gvdb_timing_enable(int32_t on) {
 
 void gvdb_timing_reset(void) {
     std::lock_guard<std::mutex> g(timing().mu);
+    timing_drain_locked(timing().pending.size());
     for (int i = 0; i < kTimN; ++i) {
         timing().ms[i] = 0;
         timing().n[i] = 0;
@@ -1314,6 +1358,7 @@ void gvdb_timing_reset(void) {
 gvdb_status gvdb_timing_read(uint32_t which, double* total_ms, uint64_t* launches) {
     if (which >= (uint32_t)kTimN || !total_ms || !launches) return fail(GVDB_ERR_INVALID_ARGUMENT, "bad timing slot");
     std::lock_guard<std::mutex> g(timing().mu);
+    timing_drain_locked(timing().pending.size());
     *total_ms = timing().ms[which];
     *launches = timing().n[which];
     return GVDB_OK;
@@ -1334,6 +1379,7 @@ gvdb_status gvdb_bq_quantize(const float* rows, uint64_t n, uint32_t D, float th
     WsGuard g(0);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
+    g.begin(ws.stream);
     const size_t nb = (D + 7u) / 8u;
     HIP_TRY(ws.rows.ensure(n * D * 4), "alloc");
     HIP_TRY(ws.misc.ensure(n * nb), "alloc");
@@ -1350,6 +1396,7 @@ gvdb_status gvdb_bq_hamming(const uint8_t* a, const uint8_t* b, uint64_t n, uint
     WsGuard g(0);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
+    g.begin(ws.stream);
     const size_t nb = (D + 7u) / 8u;
     HIP_TRY(ws.misc.ensure(2 * n * nb + n * 4 + 512), "alloc");
     uint8_t* da = ws.misc.as<uint8_t>();
@@ -1381,6 +1428,7 @@ gvdb_status gvdb_bq_multi_stage_search(const uint8_t* q_bits, uint32_t qdim, con
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
     hipStream_t s = ws.stream;
+    g.begin(s);
     const uint32_t W4 = code_w4(cdim);
     const size_t nb = (cdim + 7u) / 8u;
     // upload: candidate rows + norms, codes (SoA from Msb0 bytes), query
@@ -1418,12 +1466,17 @@ gvdb_status gvdb_bq_multi_stage_search(const uint8_t* q_bits, uint32_t qdim, con
     a.descending = 1;
     a.d_out_ids = ws.out_ids.as<uint64_t>();
     a.d_out_scores = ws.out_scores.as<float>();
-    a.d_out_n = nullptr;
+    HIP_TRY(ws.out_n.ensure(4), "alloc out");
+    a.d_out_n = ws.out_n.as<uint32_t>();
     gvdb_status st = bq_search(a, ws, s);
     if (st != GVDB_OK) return st;
+    uint32_t got = 0;
     HIP_TRY(hipMemcpyAsync(out_idx, ws.out_ids.p, R * 8, hipMemcpyDeviceToHost, s), "download idx");
     HIP_TRY(hipMemcpyAsync(out_cos, ws.out_scores.p, R * 4, hipMemcpyDeviceToHost, s), "download cos");
+    HIP_TRY(hipMemcpyAsync(ws.h_flags, ws.out_n.p, 4, hipMemcpyDeviceToHost, s), "download n");
     HIP_TRY(hipStreamSynchronize(s), "sync");
+    got = ws.h_flags[0];
+    if ((st = check_poisoned(&got, 1)) != GVDB_OK) return st;
     *out_n = R;
     return GVDB_OK;
 }
@@ -1444,6 +1497,7 @@ gvdb_status gvdb_flat_search(const float* queries, uint64_t B, const float* rows
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
     hipStream_t s = ws.stream;
+    g.begin(s);
     const int kind = metric == GVDB_METRIC_L2 ? kScoreL2
                      : metric == GVDB_METRIC_COSINE_DISTANCE ? kScoreCosineDistance
                                                              : kScoreCosine;
@@ -1489,6 +1543,7 @@ gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* ix, const float* d
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
+    g.begin(s);
     BqSearchArgs a{};
     a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
     a.d_q = d_queries;
@@ -1517,6 +1572,7 @@ gvdb_status gvdb_bq_shard_merge_device(const uint64_t* d_gids, const uint32_t* d
     WsGuard g(0);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
+    g.begin(s);
     HIP_TRY(g.w->flags.ensure(16), "alloc flags");
     HIP_TRY(hipMemsetAsync(g.w->flags.p, 0, 16, s), "memset flags");
     HIP_TRY(launch_bq_shard_merge(d_gids, d_dist, d_cos, d_counts, (uint32_t)G, (uint32_t)B, (uint32_t)stride,
@@ -1539,6 +1595,7 @@ gvdb_status gvdb_bq_shard_merge_packed_device(const uint32_t* d_gathered, const 
     WsGuard g(0);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     hipStream_t s = (hipStream_t)stream;
+    g.begin(s);
     const uint64_t BR = B * R;  // rank block: ids (2*BR words) | dist (BR) | cos (BR)
     HIP_TRY(g.w->flags.ensure(16), "alloc flags");
     HIP_TRY(hipMemsetAsync(g.w->flags.p, 0, 16, s), "memset flags");
@@ -1664,6 +1721,7 @@ gvdb_status gvdb::shard_candidates(const gvdb_index* ix, const float* d_q, uint6
     if ((st = set_device(ix->device)) != GVDB_OK) return st;
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    g.begin(s);
     BqSearchArgs a{};
     a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
     a.d_q = d_q;

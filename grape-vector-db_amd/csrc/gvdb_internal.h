@@ -80,6 +80,7 @@ struct Stage1Args {
     hipEvent_t* ev;          // optional [4]: before hist, before scan, after scan, after select
     int use_mfma;            // large batches: 0 popcount only, 1 FP4 MFMA scan, 2 i8 MFMA scan
     int dbg;                 // ablation switches for timing studies (GVDB_SCAN_DBG); 0 in production
+    int force_rescan;        // tests: every query takes k_select's exact all-rows rescan (GVDB_FORCE_RESCAN)
 };
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 // code widths with an MFMA scan instantiation (D <= 768; wider codes would
@@ -129,7 +130,8 @@ struct FinalArgs {
     uint64_t* out_ids;       // [B][kout]
     float* out_scores;       // [B][kout]
     uint32_t* out_n;         // [B] or nullptr
-    uint32_t* nan_flag;      // set to 1 if a NaN score would make the reference panic
+    uint32_t* nan_flag;      // [0] set to 1 if a NaN score would make the reference panic;
+                             // [1] per-query scratch of the global sort (zero on entry)
 };
 hipError_t launch_final_sort(const FinalArgs& a, hipStream_t s);
 size_t final_sort_global_bytes(uint32_t R);

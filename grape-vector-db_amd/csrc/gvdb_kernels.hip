@@ -451,28 +451,121 @@ __global__ void k_sample_hist_generic(const uint4* __restrict__ codes, uint64_t 
 }
 
 
-// Exact top-R from the candidate buffer: histogram -> T_R (R-th smallest d),
-// gather every key with d <= T_R, sort (d, row) ascending, keep R.  Any
-// uncertainty (too few keys: threshold estimate too tight; buffer overflow;
-// too many ties for LDS) raises fail[q] and the host reruns that query on the
-// exact slow path.
+// Block-wide exclusive prefix of a per-thread flag in thread order (one
+// ballot per wave + the wave totals in LDS).  *total = the block's count.
+__device__ __forceinline__ uint32_t block_prefix_flag(bool f, uint32_t* wcnt, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = (blockDim.x + 63u) >> 6;
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wcnt[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), tot = 0;
+    for (uint32_t i = 0; i < nw; ++i) {
+        const uint32_t c = wcnt[i];
+        if (i < w) pre += c;
+        tot += c;
+    }
+    __syncthreads();  // wcnt is rewritten by the next call
+    *total = tot;
+    return pre;
+}
+
+// Sum of h[0..t) by one full wave.
+__device__ uint32_t wave_sum_below(const uint32_t* h, uint32_t t) {
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x & 63u; i < t; i += 64) s += h[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    return s;
+}
+
+__device__ __forceinline__ uint32_t code_dist(const uint4* __restrict__ codes, uint64_t cap, uint32_t W4,
+                                              const uint4* __restrict__ qc, uint64_t n) {
+    uint32_t d = 0;
+    for (uint32_t w = 0; w < W4; ++w) d = ham4(codes[(uint64_t)w * cap + n], qc[w], d);
+    return d;
+}
+
+// sk[0..n) -> sorted, first R to s1_rows / s1_dist of query q.
+__device__ void select_emit_sorted(uint64_t* sk, uint32_t n, uint32_t R, uint32_t* s1_rows, uint32_t* s1_dist,
+                                   uint32_t q) {
+    const uint32_t P = next_pow2(n);
+    for (uint32_t i = n + threadIdx.x; i < P; i += blockDim.x) sk[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_lds(sk, P);
+    for (uint32_t i = threadIdx.x; i < R; i += blockDim.x) {
+        const uint64_t key = sk[i];
+        s1_rows[(uint64_t)q * R + i] = (uint32_t)key;
+        s1_dist[(uint64_t)q * R + i] = (uint32_t)(key >> 32);
+    }
+}
+
+// Exact stage-1 top-R of ALL rows for one query by this block alone: pass 1
+// histograms every distance -> T_R; pass 2 walks the rows in order keeping
+// d < T_R and the first (R - count(d < T_R)) rows with d == T_R -- the
+// reference's stable sort by (similarity desc, index) restricted to its first
+// R.  The rare fallback of the certified fast path (threshold estimate too
+// tight, candidate buffer overflow); no host round trip.
+__device__ void select_rescan(const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t D, uint32_t W4,
+                              const uint4* __restrict__ qc, uint32_t R, uint64_t* sk, uint32_t* hist,
+                              uint32_t* s1_rows, uint32_t* s1_dist, uint32_t q) {
+    __shared__ uint32_t s_T, s_lt, s_n, s_tie, wcnt[16];
+    for (uint32_t i = threadIdx.x; i <= D; i += blockDim.x) hist[i] = 0u;
+    __syncthreads();
+    for (uint64_t n = threadIdx.x; n < N; n += blockDim.x) atomicAdd(&hist[code_dist(codes, cap, W4, qc, n)], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t t = wave_find_cum(hist, D + 1u, R);
+        const uint32_t lt = wave_sum_below(hist, t);
+        if (threadIdx.x == 0) {
+            s_T = t;
+            s_lt = lt;
+            s_n = 0u;
+            s_tie = 0u;
+        }
+    }
+    __syncthreads();
+    const uint32_t T = s_T, need = R - s_lt;  // R <= N, so count(d <= T) >= R
+    for (uint64_t base = 0; base < N; base += blockDim.x) {
+        const uint64_t n = base + threadIdx.x;
+        const uint32_t d = n < N ? code_dist(codes, cap, W4, qc, n) : ~0u;
+        if (d < T) sk[atomicAdd(&s_n, 1u)] = ((uint64_t)d << 32) | (uint32_t)n;
+        uint32_t tot;
+        const uint32_t rank = s_tie + block_prefix_flag(d == T, wcnt, &tot);
+        if (d == T && rank < need) sk[atomicAdd(&s_n, 1u)] = ((uint64_t)d << 32) | (uint32_t)n;
+        __syncthreads();
+        if (threadIdx.x == 0) s_tie += tot;
+        __syncthreads();
+    }
+    select_emit_sorted(sk, s_n, R, s1_rows, s1_dist, q);
+}
+
+// Exact top-R from the candidate buffer: histogram -> T_R (R-th smallest d);
+// if the keys with d <= T_R fit the LDS sort, gather and sort them; otherwise
+// (many rows tied at T_R) a radix select over the row index picks the first
+// R - count(d < T_R) tied rows in row order, so the sorted list is still the
+// reference's stable order.  A query whose buffer cannot hold its top-R (fewer
+// than R keys passed the estimated threshold, or the buffer overflowed) is
+// answered by select_rescan in the same block: every path is exact and none
+// needs the host.  fail[q] / any_fail record the rescans (diagnostics).
 __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ counts, const uint64_t* __restrict__ buf,
-                                                uint32_t bufcap, uint32_t D, uint32_t R, uint32_t* __restrict__ fail,
-                                                uint32_t* __restrict__ any_fail,
-                                                uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist
+                                                uint32_t bufcap, uint32_t D, uint32_t R,
+                                                const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                uint32_t W4, const uint4* __restrict__ qcodes,
+                                                uint32_t* __restrict__ fail, uint32_t* __restrict__ any_fail,
+                                                uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist,
+                                                int force_rescan) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist, then radix bins
     uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
-    __shared__ uint32_t s_T, s_n;
+    uint32_t* bins = hist + ((D + 4u) & ~3u);
+    __shared__ uint32_t s_T, s_lt, s_n, s_cut;
     const uint32_t q = blockIdx.x;
     const uint32_t cnt = counts[q];
-    if (cnt < R || cnt > bufcap) {
-        // keep the stage-2 launch that still runs over this query in bounds;
-        // the host reruns the query on the exact slow path
-        for (uint32_t i = threadIdx.x; i < R; i += 256) s1_rows[(uint64_t)q * R + i] = 0u;
+    if (cnt < R || cnt > bufcap || force_rescan) {
         if (threadIdx.x == 0) {
             fail[q] = 1u;
             atomicOr(any_fail, 1u);
         }
+        select_rescan(codes, cap, N, D, W4, qcodes + (uint64_t)q * W4, R, sk, hist, s1_rows, s1_dist, q);
         return;
     }
     const uint64_t* b = buf + (uint64_t)q * bufcap;
@@ -483,38 +576,58 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
     __syncthreads();
     if (threadIdx.x < 64) {
         const uint32_t t = wave_find_cum(hist, D + 1u, R);
-        if (threadIdx.x == 0) s_T = t;
+        const uint32_t lt = wave_sum_below(hist, t);
+        if (threadIdx.x == 0) {
+            s_T = t;
+            s_lt = lt;
+        }
     }
     __syncthreads();
     const uint32_t T = s_T;
+    uint32_t cut = ~0u;  // rows tied at T with row <= cut are kept
+    if (s_lt + hist[T] > kSelectLdsCap) {
+        // the need-th smallest row among the keys with d == T: radix select,
+        // 11 + 11 + 10 bits of the row index (rows in the buffer are distinct)
+        uint32_t need = R - s_lt, prefix = 0u, pmask = 0u;
+        for (int pass = 0; pass < 3; ++pass) {
+            const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+            const uint32_t nb = pass == 2 ? 1024u : 2048u, dm = nb - 1u;
+            for (uint32_t i = threadIdx.x; i < nb; i += 256) bins[i] = 0u;
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+                const uint64_t key = b[i];
+                const uint32_t row = (uint32_t)key;
+                if ((uint32_t)(key >> 32) == T && (row & pmask) == prefix) atomicAdd(&bins[(row >> shift) & dm], 1u);
+            }
+            __syncthreads();
+            if (threadIdx.x < 64) {
+                const uint32_t bin = wave_find_cum(bins, nb, need);
+                const uint32_t below = wave_sum_below(bins, bin);
+                if (threadIdx.x == 0) {
+                    s_cut = bin;
+                    s_n = below;
+                }
+            }
+            __syncthreads();
+            need -= s_n;
+            prefix |= s_cut << shift;
+            pmask |= dm << shift;
+            __syncthreads();
+        }
+        cut = prefix;
+        if (threadIdx.x == 0) s_n = 0u;
+        __syncthreads();
+    }
     for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
         const uint64_t key = b[i];
-        if ((uint32_t)(key >> 32) <= T) {
+        const uint32_t d = (uint32_t)(key >> 32);
+        if (d < T || (d == T && (uint32_t)key <= cut)) {
             const uint32_t pos = atomicAdd(&s_n, 1u);
             if (pos < kSelectLdsCap) sk[pos] = key;
         }
     }
     __syncthreads();
-    const uint32_t n = s_n;
-    if (n > kSelectLdsCap) {
-        // keep the stage-2 launch that still runs over this query in bounds;
-        // the host reruns the query on the exact slow path
-        for (uint32_t i = threadIdx.x; i < R; i += 256) s1_rows[(uint64_t)q * R + i] = 0u;
-        if (threadIdx.x == 0) {
-            fail[q] = 1u;
-            atomicOr(any_fail, 1u);
-        }
-        return;
-    }
-    const uint32_t P = next_pow2(n);
-    for (uint32_t i = n + threadIdx.x; i < P; i += 256) sk[i] = ~0ull;
-    __syncthreads();
-    bitonic_sort_lds(sk, P);
-    for (uint32_t i = threadIdx.x; i < R; i += 256) {
-        const uint64_t key = sk[i];
-        s1_rows[(uint64_t)q * R + i] = (uint32_t)key;
-        s1_dist[(uint64_t)q * R + i] = (uint32_t)(key >> 32);
-    }
+    select_emit_sorted(sk, min(s_n, kSelectLdsCap), R, s1_rows, s1_dist, q);
 }
 
 // ----------------------------------------------------------------------------
@@ -1702,9 +1815,9 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     }
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
-    const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)(a.D + 1u) * 4u;
-    hipLaunchKernelGGL(k_select, dim3(a.B), dim3(256), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R, a.fail,
-                       a.any_fail, a.s1_rows, a.s1_dist);
+    const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
+    hipLaunchKernelGGL(k_select, dim3(a.B), dim3(256), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R, a.codes, a.cap,
+                       a.N, W4, a.qcodes, a.fail, a.any_fail, a.s1_rows, a.s1_dist, a.force_rescan);
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[3], s);
     return hipSuccess;
@@ -2302,7 +2415,8 @@ __global__ __launch_bounds__(256) void k_final_sort(const float* __restrict__ sc
             }
             o += __popcll(m);
         }
-        if (threadIdx.x == 0 && out_n) out_n[q] = o;
+        // a NaN score would make the reference's sort panic: the query is poisoned
+        if (threadIdx.x == 0 && out_n) out_n[q] = (s_nan && R >= 2) ? GVDB_N_POISONED : o;
     }
 }
 
@@ -2320,7 +2434,10 @@ __global__ void k_make_keys(const float* __restrict__ sc, uint32_t R, int descen
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
     const float f = sc[i];
-    if (f != f && R >= 2) atomicOr(nan_flag, 1u);
+    if (f != f && R >= 2) {
+        atomicOr(nan_flag, 1u);
+        atomicOr(nan_flag + 1, 1u);  // this query's flag, read and cleared by k_emit_sorted
+    }
     uint32_t o = f32_order(f);
     keys[i] = descending ? ~o : o;
     vals[i] = i;
@@ -2329,7 +2446,7 @@ __global__ void k_make_keys(const float* __restrict__ sc, uint32_t R, int descen
 __global__ void k_emit_sorted(const uint32_t* __restrict__ ranks, const float* __restrict__ sc,
                               const uint32_t* __restrict__ s1_rows, uint32_t take, const uint64_t* __restrict__ ids,
                               uint64_t row_offset, uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
-                              uint32_t* __restrict__ out_n) {
+                              uint32_t* __restrict__ out_n, uint32_t* __restrict__ qnan) {
     // single wave: order-preserving compaction of orphans via ballot prefix.
     uint32_t o = 0;
     for (uint32_t i0 = 0; i0 < take; i0 += 64) {
@@ -2350,7 +2467,10 @@ __global__ void k_emit_sorted(const uint32_t* __restrict__ ranks, const float* _
         }
         o += __popcll(m);
     }
-    if (threadIdx.x == 0 && out_n) *out_n = o;
+    if (threadIdx.x == 0) {
+        if (out_n) *out_n = *qnan ? GVDB_N_POISONED : o;
+        *qnan = 0u;
+    }
 }
 
 static size_t cub_pairs_bytes_u32(uint32_t n) { return cub_pairs_u32_bytes(n); }
@@ -2377,7 +2497,7 @@ hipError_t launch_final_sort_global(const FinalArgs& a, void* tmp, size_t tmp_by
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_emit_sorted, dim3(1), dim3(64), 0, s, vb.Current(), sc, a.s1_rows + (uint64_t)q * a.R,
                            take, a.ids, a.row_offset, a.out_ids + (uint64_t)q * a.kout,
-                           a.out_scores + (uint64_t)q * a.kout, a.out_n ? a.out_n + q : nullptr);
+                           a.out_scores + (uint64_t)q * a.kout, a.out_n ? a.out_n + q : nullptr, a.nan_flag + 1);
         GVDB_LAUNCH_CHECK();
     }
     return hipSuccess;
