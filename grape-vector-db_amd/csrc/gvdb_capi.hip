@@ -157,11 +157,15 @@ struct Workspace {
     hipEvent_t done = nullptr;
     hipStream_t last = nullptr;
     bool pending = false;
+    // batch-1 fast path state (self-cleaning: zero between calls); b1_sig
+    // = the layout it was zeroed for, 0 = must be zeroed
+    DBuf b1;
+    uint64_t b1_sig = 0;
     ~Workspace() {
         if (done) (void)hipEventDestroy(done);
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
                         &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
-                        &fx_scores, &flt_rows, &flt_ids})
+                        &fx_scores, &flt_rows, &flt_ids, &b1})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -379,6 +383,120 @@ void timing_submit(EvSet* e) {
     if (timing().pending.size() > 512) timing_drain_locked(256);
 }
 
+unsigned long long*& debug_b1_clk() {
+    static unsigned long long* p = nullptr;
+    return p;
+}
+
+// GVDB_B1=0 disables the batch-1 fast path (A/B timing; the general path is exact too)
+bool b1_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("GVDB_B1");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
+// Batch-1 fast path (launch_b1_search): sample + threshold, scan, and a tail
+// kernel that selects, re-scores and sorts -- three launches, no memset (the
+// state is left zeroed by the previous call), no host sync.
+gvdb_status bq_search_b1(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
+    const ShardView& v = a.v;
+    const uint32_t R = a.R, D = v.D;
+    B1Args b{};
+    uint32_t chunks, stride, target, bufcap;
+    if (v.N <= kExactN) {
+        chunks = (v.N + kB1ChunkRows - 1) / kB1ChunkRows;
+        stride = kB1ChunkRows;
+        target = R;  // the "sample" is the whole shard: exact threshold
+        bufcap = std::min<uint64_t>(v.N, 8ull * R + 2048ull);
+    } else {
+        // GVDB_B1_SAMPLE_DIV: sample ~N/div rows (timing knob; default 32)
+        static const uint32_t div = [] {
+            const char* e = getenv("GVDB_B1_SAMPLE_DIV");
+            const int d = e ? atoi(e) : 0;
+            return d >= 4 && d <= 4096 ? (uint32_t)d : 32u;
+        }();
+        const uint64_t S = std::max<uint64_t>(kExactN / 4, v.N / div);
+        chunks = (uint32_t)(S / kB1ChunkRows);
+        stride = v.N / chunks;  // >= kB1ChunkRows: chunks never overlap
+        const double Sr = (double)chunks * kB1ChunkRows;
+        const double m = (double)R * Sr / (double)v.N;
+        target = (uint32_t)std::ceil(m + 4.0 * std::sqrt(m) + 4.0);
+        const double expect_full = (double)target * (double)v.N / Sr;
+        bufcap = (uint32_t)std::min<double>((double)v.N, std::max(8.0 * expect_full + 2048.0, 16384.0));
+    }
+    bufcap = std::min<uint32_t>(bufcap, kB1MaxBufcap);
+    const size_t hw = ((size_t)D + 64) & ~(size_t)63;  // hist words (D+1, padded)
+    const size_t off_ctl = hw, off_qw = off_ctl + 16, off_rsc = off_qw + 32;
+    const size_t off_top = (off_rsc + R + 1) & ~(size_t)1;  // u64-aligned
+    const size_t off_sc = off_top + 2 * (size_t)R;
+    const size_t off_buf = (off_sc + bufcap + 1) & ~(size_t)1;
+    const size_t bytes = off_buf * 4 + (size_t)bufcap * 8;
+    const uint64_t sig = ((uint64_t)D << 44) ^ ((uint64_t)R << 24) ^ (uint64_t)bufcap ^ 0x5a5a000000000000ull;
+    if (ws.b1.n < bytes || ws.b1_sig != sig) {
+        HIP_TRY(ws.b1.ensure(bytes), "alloc batch-1 state");
+        HIP_TRY(hipMemsetAsync(ws.b1.p, 0, bytes, s), "zero batch-1 state");
+        ws.b1_sig = sig;
+    }
+    uint32_t* w = ws.b1.as<uint32_t>();
+    b.codes = v.codes;
+    b.cap = v.cap;
+    b.N = v.N;
+    b.D = D;
+    b.R = R;
+    b.kout = a.kout;
+    b.q = a.d_q;
+    b.qlen = a.qlen;
+    b.thr = a.thr;
+    b.rows = v.rows;
+    b.clen = v.clen;
+    b.norms = v.norms;
+    b.ids = v.ids;
+    b.row_offset = v.row_offset;
+    b.kind = a.kind;
+    b.descending = a.descending;
+    b.force_rescan = getenv_flag("GVDB_FORCE_RESCAN") ? 1 : 0;
+    b.sample_chunks = chunks;
+    b.sample_stride = stride;
+    b.target = target;
+    b.bufcap = bufcap;
+    b.hist = w;
+    b.counts = w + off_ctl;
+    b.ticket = w + off_ctl + 4;
+    b.rescans = w + off_ctl + 8;
+    b.qwords = w + off_qw;
+    b.scores = (float*)(w + off_sc);
+    b.rscores = (float*)(w + off_rsc);
+    b.topr = (uint64_t*)(w + off_top);
+    b.buf = (uint64_t*)(w + off_buf);
+    b.out_ids = a.d_out_ids;
+    b.out_scores = a.d_out_scores;
+    b.out_n = a.d_out_n;
+    // GVDB_B1_CLK=1: phase clocks of the tail kernel (timing study; gvdb_debug_b1_clock)
+    static unsigned long long* clk = nullptr;
+    if (getenv_flag("GVDB_B1_CLK") && !clk) (void)hipMalloc((void**)&clk, 16 * 8);
+    b.clk = getenv_flag("GVDB_B1_CLK") ? clk : nullptr;
+    debug_b1_clk() = b.clk;
+    bool timed = false;
+    {
+        std::lock_guard<std::mutex> g(timing().mu);
+        timed = timing().on;
+    }
+    EvSet* ev = timed ? timing_events() : nullptr;
+    b.ev = ev ? ev->e : nullptr;
+    hipError_t e = launch_b1_search(b, s);
+    if (e != hipSuccess) {
+        ws.b1_sig = 0;  // state unknown: zero it again next time
+        return dev_fail(e, "batch-1 search");
+    }
+    if (ev) {
+        HIP_TRY(hipEventRecord(ev->e[5], s), "event");
+        timing_submit(ev);
+    }
+    return GVDB_OK;
+}
+
 // BQ multi-stage search on one shard view, enqueued on stream s with NO host
 // synchronisation: stage 1 (certified fast path whose rare fallbacks run on
 // the device, k_select), stage 2 (exact rerank), final ordering.  A query whose
@@ -392,6 +510,9 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         return GVDB_OK;
     }
     const uint32_t W4 = code_w4(v.D);
+    if (B == 1 && a.dims_match && v.D > 0 && v.D <= kB1MaxD && !a.d_qwords && !a.d_out_dist && R <= kSortLdsCap &&
+        a.qlen == v.clen && v.clen == v.D && b1_enabled())
+        return bq_search_b1(a, ws, s);
     HIP_TRY(ws.qnorm.ensure((size_t)B * 4), "alloc qnorm");
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
     HIP_TRY(ws.scores.ensure((size_t)B * R * 4), "alloc scores");
@@ -1705,6 +1826,12 @@ uint64_t gvdb_flat_i8_fallback_count(void) { return flat_fallbacks_i8().load(); 
 gvdb_status gvdb::report_status(gvdb_status s, const std::string& msg) { return fail(s, msg); }
 
 int gvdb::index_device(const gvdb_index* ix) { return ix->device; }
+
+// timing study: the last k_b1_tail phase clocks (GVDB_B1_CLK=1), 16 words
+extern "C" int gvdb_debug_b1_clock(unsigned long long* out) {
+    if (!debug_b1_clk()) return -1;
+    return (int)hipMemcpy(out, debug_b1_clk(), 16 * 8, hipMemcpyDeviceToHost);
+}
 
 // Sharded-search building block (gvdb_comm.hip): this shard's stage-1 top-R
 // (R clamped to its row count) with exact cosines, rows of the output at

@@ -92,6 +92,45 @@ __host__ __device__ inline bool mx4_scan_supported(uint32_t W4) {
 }
 // hist/counts/fail must be zeroed by the caller on stream s.
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s);
+// Batch-1 fast path (gvdb_kernels.hip: k_b1_sample -> k_b1_scan -> k_b1_tail):
+// sample histogram + threshold, scan, exact select + rerank + final sort, with
+// no host round trip.  D <= 1024, R <= kSortLdsCap.  hist / counts / ticket
+// must be zero before the first call; the path leaves them zero.
+struct B1Args {
+    const uint4* codes;
+    uint64_t cap;
+    uint32_t N, D, R, kout;
+    const float* q;          // [qlen] f32 query (packed in-kernel with thr)
+    uint64_t qlen;
+    float thr;
+    const float* rows;
+    uint64_t clen;
+    const float* norms;
+    const uint64_t* ids;
+    uint64_t row_offset;
+    int kind, descending, force_rescan;
+    uint32_t sample_chunks, sample_stride, target, bufcap;
+    uint32_t* hist;          // [D+1]
+    uint32_t* counts;        // [1]
+    uint32_t* ticket;        // [1]
+    uint32_t* rescans;       // [1] diagnostics
+    uint32_t* qwords;        // [4*W4]
+    float* scores;           // [bufcap] exact scores of the buffered candidates
+    float* rscores;          // [R] exact scores of a rescan's rows
+    uint64_t* topr;          // [R] sorted top-R keys published by the select block
+    uint64_t* buf;           // [bufcap]
+    uint64_t* out_ids;
+    float* out_scores;
+    uint32_t* out_n;         // or nullptr
+    hipEvent_t* ev;          // optional [4]
+    unsigned long long* clk; // timing study only: phase wall clocks of k_b1_tail
+};
+constexpr uint32_t kB1ChunkRows = 1024;  // rows per k_b1_sample chunk
+constexpr uint32_t kB1MaxD = 1024;
+constexpr uint32_t kB1RerankBlocks = 128;  // k_b1_tail blocks re-scoring candidates (16 each per round)
+constexpr uint32_t kB1MaxBufcap = 1u << 20;  // buffer index fits the 21-bit key field
+hipError_t launch_b1_search(const B1Args& b, hipStream_t s);
+
 // Exact slow path for ONE query: all N distances + stable radix sort.
 // tmp buffers sized by stage1_slow_bytes().
 size_t stage1_slow_bytes(uint32_t N);

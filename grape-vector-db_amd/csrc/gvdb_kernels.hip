@@ -485,18 +485,38 @@ __device__ __forceinline__ uint32_t code_dist(const uint4* __restrict__ codes, u
     return d;
 }
 
-// sk[0..n) -> sorted, first R to s1_rows / s1_dist of query q.
-__device__ void select_emit_sorted(uint64_t* sk, uint32_t n, uint32_t R, uint32_t* s1_rows, uint32_t* s1_dist,
-                                   uint32_t q) {
+// sk[0..n) -> sorted ascending (padded to a power of two with ~0).  Keys
+// must be distinct (they carry the row).  Up to kRankSortMax keys: rank
+// counting (key i goes to #{j : key_j < key_i}; no barrier inside, LDS
+// broadcast reads) through `tmp`; larger sets: the LDS bitonic network.
+constexpr uint32_t kRankSortMax = 512;
+__device__ __forceinline__ void select_sort(uint64_t* sk, uint32_t n, uint64_t* tmp) {
+    if (n <= kRankSortMax && tmp) {
+        uint64_t mine[kRankSortMax / 256];
+        uint32_t rank[kRankSortMax / 256];
+#pragma unroll
+        for (int u = 0; u < (int)(kRankSortMax / 256); ++u) {
+            const uint32_t i = threadIdx.x + u * 256u;
+            mine[u] = i < n ? sk[i] : ~0ull;
+            rank[u] = 0u;
+        }
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint64_t kj = sk[j];
+#pragma unroll
+            for (int u = 0; u < (int)(kRankSortMax / 256); ++u) rank[u] += kj < mine[u];
+        }
+#pragma unroll
+        for (int u = 0; u < (int)(kRankSortMax / 256); ++u)
+            if (threadIdx.x + u * 256u < n) tmp[rank[u]] = mine[u];
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) sk[i] = tmp[i];
+        __syncthreads();
+        return;
+    }
     const uint32_t P = next_pow2(n);
     for (uint32_t i = n + threadIdx.x; i < P; i += blockDim.x) sk[i] = ~0ull;
     __syncthreads();
     bitonic_sort_lds(sk, P);
-    for (uint32_t i = threadIdx.x; i < R; i += blockDim.x) {
-        const uint64_t key = sk[i];
-        s1_rows[(uint64_t)q * R + i] = (uint32_t)key;
-        s1_dist[(uint64_t)q * R + i] = (uint32_t)(key >> 32);
-    }
 }
 
 // Exact stage-1 top-R of ALL rows for one query by this block alone: pass 1
@@ -505,9 +525,9 @@ __device__ void select_emit_sorted(uint64_t* sk, uint32_t n, uint32_t R, uint32_
 // reference's stable sort by (similarity desc, index) restricted to its first
 // R.  The rare fallback of the certified fast path (threshold estimate too
 // tight, candidate buffer overflow); no host round trip.
-__device__ void select_rescan(const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t D, uint32_t W4,
-                              const uint4* __restrict__ qc, uint32_t R, uint64_t* sk, uint32_t* hist,
-                              uint32_t* s1_rows, uint32_t* s1_dist, uint32_t q) {
+__device__ __noinline__ void select_rescan(const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t D,
+                                           uint32_t W4, const uint4* __restrict__ qc, uint32_t R, uint64_t* sk,
+                                           uint32_t* hist) {
     __shared__ uint32_t s_T, s_lt, s_n, s_tie, wcnt[16];
     for (uint32_t i = threadIdx.x; i <= D; i += blockDim.x) hist[i] = 0u;
     __syncthreads();
@@ -536,43 +556,64 @@ __device__ void select_rescan(const uint4* __restrict__ codes, uint64_t cap, uin
         if (threadIdx.x == 0) s_tie += tot;
         __syncthreads();
     }
-    select_emit_sorted(sk, s_n, R, s1_rows, s1_dist, q);
+    select_sort(sk, s_n, nullptr);
 }
 
-// Exact top-R from the candidate buffer: histogram -> T_R (R-th smallest d);
-// if the keys with d <= T_R fit the LDS sort, gather and sort them; otherwise
-// (many rows tied at T_R) a radix select over the row index picks the first
+constexpr uint32_t kNoIdx = (1u << 21) - 1u;
+__device__ __forceinline__ uint64_t pack_key_idx(uint64_t key, uint32_t idx) {
+    return ((key >> 32) << 53) | ((key & 0xffffffffull) << 21) | (uint64_t)idx;
+}
+
+// Exact top-R of one query from its candidate buffer, left SORTED in
+// sk[0..R) as (d << 32 | row) keys: histogram -> T_R (R-th smallest d); if the
+// keys with d <= T_R fit the LDS sort, gather and sort them; otherwise (many
+// rows tied at T_R) a radix select over the row index picks the first
 // R - count(d < T_R) tied rows in row order, so the sorted list is still the
 // reference's stable order.  A query whose buffer cannot hold its top-R (fewer
 // than R keys passed the estimated threshold, or the buffer overflowed) is
 // answered by select_rescan in the same block: every path is exact and none
-// needs the host.  fail[q] / any_fail record the rescans (diagnostics).
-__global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ counts, const uint64_t* __restrict__ buf,
-                                                uint32_t bufcap, uint32_t D, uint32_t R,
-                                                const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
-                                                uint32_t W4, const uint4* __restrict__ qcodes,
-                                                uint32_t* __restrict__ fail, uint32_t* __restrict__ any_fail,
-                                                uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist,
-                                                int force_rescan) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist, then radix bins
-    uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
-    uint32_t* bins = hist + ((D + 4u) & ~3u);
+// needs the host.  Returns true when the rescan ran.
+// LDS: sk [kSelectLdsCap] keys, hist [(D+4)&~3], bins [2048].
+__device__ __forceinline__ bool select_topr(uint32_t cnt, const uint64_t* __restrict__ b, uint32_t bufcap,
+                                            uint32_t D, uint32_t R, const uint4* __restrict__ codes, uint64_t cap,
+                                            uint32_t N, uint32_t W4, const uint4* __restrict__ qc, bool force_rescan,
+                                            uint64_t* sk, uint32_t* hist, uint32_t* bins, bool with_idx = false) {
+    // with_idx (batch-1 tail; D <= 2047, bufcap <= 2^21): the sorted keys carry
+    // their buffer index, (d << 53) | (row << 21) | idx -- the same (d, row)
+    // order, plus where the row's exact score was published.  A rescan's keys
+    // carry idx = kNoIdx.
     __shared__ uint32_t s_T, s_lt, s_n, s_cut;
-    const uint32_t q = blockIdx.x;
-    const uint32_t cnt = counts[q];
     if (cnt < R || cnt > bufcap || force_rescan) {
-        if (threadIdx.x == 0) {
-            fail[q] = 1u;
-            atomicOr(any_fail, 1u);
+        select_rescan(codes, cap, N, D, W4, qc, R, sk, hist);
+        if (with_idx) {
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < R; i += blockDim.x) sk[i] = pack_key_idx(sk[i], kNoIdx);
+            __syncthreads();
         }
-        select_rescan(codes, cap, N, D, W4, qcodes + (uint64_t)q * W4, R, sk, hist, s1_rows, s1_dist, q);
-        return;
+        return true;
     }
-    const uint64_t* b = buf + (uint64_t)q * bufcap;
-    for (uint32_t i = threadIdx.x; i <= D; i += 256) hist[i] = 0u;
+    const uint32_t nt = blockDim.x;
+    // small buffers (the common case) stay in registers: one global read
+    constexpr int KPT = 8;
+    const bool inreg = cnt <= KPT * nt;
+    uint64_t kk[KPT];
+    if (inreg) {
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const uint32_t i = threadIdx.x + u * nt;
+            kk[u] = i < cnt ? b[i] : ~0ull;
+        }
+    }
+    for (uint32_t i = threadIdx.x; i <= D; i += nt) hist[i] = 0u;
     if (threadIdx.x == 0) s_n = 0u;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < cnt; i += 256) atomicAdd(&hist[(uint32_t)(b[i] >> 32)], 1u);
+    if (inreg) {
+#pragma unroll
+        for (int u = 0; u < KPT; ++u)
+            if (kk[u] != ~0ull) atomicAdd(&hist[(uint32_t)(kk[u] >> 32)], 1u);
+    } else {
+        for (uint32_t i = threadIdx.x; i < cnt; i += nt) atomicAdd(&hist[(uint32_t)(b[i] >> 32)], 1u);
+    }
     __syncthreads();
     if (threadIdx.x < 64) {
         const uint32_t t = wave_find_cum(hist, D + 1u, R);
@@ -592,9 +633,9 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
         for (int pass = 0; pass < 3; ++pass) {
             const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
             const uint32_t nb = pass == 2 ? 1024u : 2048u, dm = nb - 1u;
-            for (uint32_t i = threadIdx.x; i < nb; i += 256) bins[i] = 0u;
+            for (uint32_t i = threadIdx.x; i < nb; i += nt) bins[i] = 0u;
             __syncthreads();
-            for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
+            for (uint32_t i = threadIdx.x; i < cnt; i += nt) {
                 const uint64_t key = b[i];
                 const uint32_t row = (uint32_t)key;
                 if ((uint32_t)(key >> 32) == T && (row & pmask) == prefix) atomicAdd(&bins[(row >> shift) & dm], 1u);
@@ -618,16 +659,62 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
         if (threadIdx.x == 0) s_n = 0u;
         __syncthreads();
     }
-    for (uint32_t i = threadIdx.x; i < cnt; i += 256) {
-        const uint64_t key = b[i];
-        const uint32_t d = (uint32_t)(key >> 32);
-        if (d < T || (d == T && (uint32_t)key <= cut)) {
-            const uint32_t pos = atomicAdd(&s_n, 1u);
-            if (pos < kSelectLdsCap) sk[pos] = key;
+    if (inreg) {  // wave-aggregated append: one LDS atomic per wave and round
+        const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const uint64_t key = kk[u];
+            const uint32_t d = (uint32_t)(key >> 32);
+            const bool keep = key != ~0ull && (d < T || (d == T && (uint32_t)key <= cut));
+            const uint64_t m = __ballot(keep);
+            if (m == 0) continue;  // wave-uniform
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
+            base = __shfl(base, 0);
+            const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (keep && pos < kSelectLdsCap)
+                sk[pos] = with_idx ? pack_key_idx(key, threadIdx.x + u * nt) : key;
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < cnt; i += nt) {
+            const uint64_t key = b[i];
+            const uint32_t d = (uint32_t)(key >> 32);
+            if (d < T || (d == T && (uint32_t)key <= cut)) {
+                const uint32_t pos = atomicAdd(&s_n, 1u);
+                if (pos < kSelectLdsCap) sk[pos] = with_idx ? pack_key_idx(key, i) : key;
+            }
         }
     }
     __syncthreads();
-    select_emit_sorted(sk, min(s_n, kSelectLdsCap), R, s1_rows, s1_dist, q);
+    // rank-count scratch: the radix bins + whatever follows them (>= 4 KiB)
+    select_sort(sk, min(s_n, kSelectLdsCap), (uint64_t*)bins);
+    return false;
+}
+
+// One block per query: select_topr, then the first R keys -> s1_rows / s1_dist.
+// fail[q] / any_fail record the device-side rescans (diagnostics).
+__global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ counts, const uint64_t* __restrict__ buf,
+                                                uint32_t bufcap, uint32_t D, uint32_t R,
+                                                const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                uint32_t W4, const uint4* __restrict__ qcodes,
+                                                uint32_t* __restrict__ fail, uint32_t* __restrict__ any_fail,
+                                                uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist,
+                                                int force_rescan) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist, then radix bins
+    uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
+    uint32_t* bins = hist + ((D + 4u) & ~3u);
+    const uint32_t q = blockIdx.x;
+    const bool rescanned = select_topr(counts[q], buf + (uint64_t)q * bufcap, bufcap, D, R, codes, cap, N, W4,
+                                       qcodes + (uint64_t)q * W4, force_rescan != 0, sk, hist, bins);
+    if (rescanned && threadIdx.x == 0) {
+        fail[q] = 1u;
+        atomicOr(any_fail, 1u);
+    }
+    for (uint32_t i = threadIdx.x; i < R; i += 256) {
+        const uint64_t key = sk[i];
+        s1_rows[(uint64_t)q * R + i] = (uint32_t)key;
+        s1_dist[(uint64_t)q * R + i] = (uint32_t)(key >> 32);
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -2879,6 +2966,441 @@ hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, ui
     GVDB_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_gather_meta, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, codes, ncodes, norms, nnorms,
                        ids, nids, map, m, cap, code_w4(D));
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ============================================================================
+// Batch-1 fast path: three launches, no host round trip.
+//
+//   k_b1_sample  packs the query (ballots, Msb0 words) in every block and
+//                histograms the Hamming distance of a sample of ~N/32 rows
+//                (1024-row chunks spread over the shard; the whole shard when
+//                N <= kExactN), flushed into one global histogram;
+//   k_b1_scan    the HBM-bound pass over every code: each block derives the
+//                threshold T from that histogram while its code loads are in
+//                flight, rows with d <= T go to the candidate buffer;
+//   k_b1_tail    ceil(R/16) blocks: each one selects the exact top-R from the
+//                buffer (select_topr, with its device-side rescan), re-scores
+//                its 16 rows (sequential f32 fold = cosine_similarity_manual),
+//                publishes the scores, and the last block to arrive sorts all
+//                R scores (stable by stage-1 rank) and writes the top-k.  The
+//                last block also zeroes the histogram and the counter for the
+//                next call (the path is self-cleaning).
+// Hand-off inside k_b1_tail: scores stored `sc1` (agent-scope relaxed atomic
+// stores), the storing waves drain (`s_waitcnt vmcnt(0)`) before one agent
+// atomic add per block, and the block whose add came last reads them with
+// agent-scope atomic loads (MI355X_MICROARCH.md, valid hand-off forms, row 1).
+// ============================================================================
+constexpr uint32_t kB1Chunk = 1024;  // sample rows per k_b1_sample block (4 per thread)
+
+// Query -> 4*W4 Msb0 code words in LDS (pad words zero), by the whole block.
+// 256-thread blocks, D <= 1024: every query load is issued before the first
+// ballot (one memory latency, not one per 64-dim unit).
+template <int W4>
+__device__ __forceinline__ void pack_query_lds(const float* __restrict__ q, uint32_t D, float thr, uint32_t* qw) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t chunks = (D + 63u) / 64u;
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t dim = (wv + 4u * u) * 64u + lane;
+        v[u] = dim < D ? q[dim] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t c = wv + 4u * u;
+        const uint32_t dim = c * 64u + lane;
+        const bool bit = dim < D && v[u] > thr;  // NaN > thr is false (Rust `value > threshold`)
+        const uint64_t m = __ballot(bit);
+        if (c < chunks && lane < 2) {
+            const uint32_t w = 2u * c + lane;
+            if (w < 4u * W4) qw[w] = msb0_word(lane == 0 ? (uint32_t)m : (uint32_t)(m >> 32));
+        }
+    }
+    for (uint32_t w = 2u * chunks + threadIdx.x; w < 4u * W4; w += blockDim.x) qw[w] = 0u;
+}
+
+template <int W4>
+__global__ __launch_bounds__(256) void k_b1_sample(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                   uint32_t D, uint32_t stride, const float* __restrict__ q, float thr,
+                                                   uint32_t* __restrict__ qwords_out, uint32_t* __restrict__ hist) {
+    __shared__ uint4 qc[W4];
+    __shared__ uint32_t lh[kRsMaxLen + 1];  // D <= 1024 on this path
+    const uint32_t tid = threadIdx.x;
+    const uint64_t start = (uint64_t)blockIdx.x * stride;
+    uint4 c[4][W4];
+    bool ok[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {  // loads first: they fly while the query is packed
+        const uint64_t row = start + (uint64_t)it * 256u + tid;
+        ok[it] = row < N;
+        const uint64_t r = ok[it] ? row : 0;
+#pragma unroll
+        for (int w = 0; w < W4; ++w) c[it][w] = codes[(uint64_t)w * cap + r];
+    }
+    pack_query_lds<W4>(q, D, thr, (uint32_t*)qc);
+    for (uint32_t i = tid; i <= D; i += 256) lh[i] = 0u;
+    __syncthreads();
+    if (blockIdx.x == 0 && tid < 4u * W4) qwords_out[tid] = ((const uint32_t*)qc)[tid];
+    uint4 qv[W4];
+#pragma unroll
+    for (int w = 0; w < W4; ++w) qv[w] = qc[w];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        if (!ok[it]) continue;
+        uint32_t d = 0;
+#pragma unroll
+        for (int w = 0; w < W4; ++w) d = ham4(c[it][w], qv[w], d);
+        atomicAdd(&lh[d], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i <= D; i += 256) {
+        const uint32_t v = lh[i];
+        if (v) atomicAdd(&hist[i], v);
+    }
+}
+
+template <int W4, int CPL>
+__global__ __launch_bounds__(256) void k_b1_scan(const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t D,
+                                                 const uint32_t* __restrict__ qwords, const uint32_t* __restrict__ hist,
+                                                 uint32_t target, uint32_t* __restrict__ counts,
+                                                 uint64_t* __restrict__ buf, uint32_t bufcap) {
+    __shared__ uint32_t s_T;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * (256u * CPL);
+    uint4 c[CPL][W4];
+    uint32_t bias[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const uint64_t n = base + (uint64_t)k * 256u + tid;
+        const bool ok = n < N;
+        const uint64_t nc = ok ? n : (uint64_t)(N - 1);
+        bias[k] = ok ? 0u : 0x01000000u;  // out-of-range rows never pass the threshold
+#pragma unroll
+        for (int w = 0; w < W4; ++w) c[k][w] = codes[(uint64_t)w * cap + nc];
+    }
+    // the threshold from the sample histogram, while the code loads fly
+    if (tid < 64) {
+        const uint32_t t = wave_find_cum(hist, D + 1u, target);
+        if (tid == 0) s_T = t;
+    }
+    const uint4* qc = (const uint4*)qwords;
+    uint4 qw[W4];
+#pragma unroll
+    for (int w = 0; w < W4; ++w) qw[w] = qc[w];
+    __syncthreads();
+    const uint32_t T = s_T;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        uint32_t d = bias[k];
+#pragma unroll
+        for (int w = 0; w < W4; ++w) d = ham4(c[k][w], qw[w], d);
+        if (d <= T) {
+            const uint32_t pos = atomicAdd(counts, 1u);
+            if (pos < bufcap) buf[pos] = ((uint64_t)d << 32) | (uint32_t)(base + (uint64_t)k * 256u + tid);
+        }
+    }
+}
+
+// Exact re-score of up to 16 rows (rows[r] for r < nr) by lanes 0..15: every
+// row load in flight at once into LDS, then each lane folds its row left to
+// right (acc = acc + q_j*x_j, qq = qq + q_j*q_j; the reference's order) with
+// the next 8 float4 of its row prefetched from LDS while the current 8 fold.
+__device__ __forceinline__ float rerank16(const float* __restrict__ rows, uint64_t clen, const float* __restrict__ norms,
+                          const float* __restrict__ qv, uint64_t qlen, int kind, const uint32_t* rowid, uint32_t nr,
+                          float4* tile4, float4* qs4, unsigned long long* t_staged = nullptr) {
+    __shared__ uint64_t bases[kRsRows];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t len = qlen < clen ? qlen : clen;
+    const uint32_t L4 = (uint32_t)((len + 3) / 4), ld4 = L4 + 1;
+    const bool vec4 = (clen & 3u) == 0;
+    const bool qvec4 = (qlen & 3u) == 0 && (((uintptr_t)qv) & 15u) == 0;
+    if (tid < kRsRows) bases[tid] = tid < nr ? (uint64_t)rowid[tid] * clen : ~0ull;
+    __syncthreads();
+    constexpr int kPer = kRsRows * (kRsMaxLen / 4) / kRsThreads;
+    float4 v[kPer];
+    const float4 qv4 = tid < L4 ? load4_guarded(qv, 0, 4ull * tid, len, qvec4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = tid + k * kRsThreads, r = i / L4, c = i - r * L4;
+        v[k] = i < kRsRows * L4 ? load4_guarded(rows, bases[r], 4ull * c, len, vec4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = tid + k * kRsThreads, r = i / L4, c = i - r * L4;
+        if (i < kRsRows * L4) tile4[r * ld4 + c] = v[k];
+    }
+    if (tid < L4) qs4[tid] = qv4;
+    __syncthreads();
+    if (t_staged) *t_staged = wall_clock64();
+    if (kind != kScoreL2 && (len & 3u) == 0) {
+        // one chain per lane: lanes 0..15 fold q_j*x_j of their row, lane 16
+        // folds q_j*q_j (the query norm, same for every row); the products of
+        // a float4 go out as packed multiplies, the sums stay sequential
+        if (tid > kRsRows) return 0.0f;
+        typedef float f2_t __attribute__((ext_vector_type(2)));
+        const float4* src = tid < kRsRows ? tile4 + tid * ld4 : qs4;
+        float acc = -0.0f;
+#pragma unroll 8
+        for (uint32_t c = 0; c < L4; ++c) {
+            const float4 x = src[c];
+            const float4 w = qs4[c];
+            const f2_t p01 = (f2_t){w.x, w.y} * (f2_t){x.x, x.y};
+            const f2_t p23 = (f2_t){w.z, w.w} * (f2_t){x.z, x.w};
+            acc = acc + p01.x;
+            acc = acc + p01.y;
+            acc = acc + p23.x;
+            acc = acc + p23.y;
+        }
+        float qq = __shfl(acc, kRsRows);
+        if (tid >= nr) return 0.0f;
+        for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+        const float na = sqrtf(qq);
+        const float nb = norms[rowid[tid]];
+        if (kind == kScoreCosine) return (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+        return (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+    }
+    if (tid >= nr) return 0.0f;
+    const float4* tr4 = tile4 + tid * ld4;
+    float acc = -0.0f, qq = -0.0f;
+    if (kind == kScoreL2) {
+        const float* tr = (const float*)tr4;
+        const float* qc = (const float*)qs4;
+        for (uint32_t j = 0; j < len; ++j) {
+            const float d = qc[j] - tr[j];
+            acc = acc + d * d;
+        }
+    } else {
+        const float* tr = (const float*)tr4;
+        const float* qc = (const float*)qs4;
+        for (uint32_t j = 0; j < len; ++j) {
+            acc = acc + qc[j] * tr[j];
+            qq = qq + qc[j] * qc[j];
+        }
+    }
+    if (kind == kScoreL2) return sqrtf(acc);
+    for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+    const float na = sqrtf(qq);
+    const float nb = norms[rowid[tid]];
+    if (kind == kScoreCosine) return (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+    return (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+}
+
+struct B1TailArgs {
+    const uint32_t* counts;   // [0] candidates in buf; zeroed by the last block
+    const uint64_t* buf;
+    uint32_t bufcap, D, R, N, W4, kout;
+    const uint4* codes;
+    uint64_t cap;
+    const uint32_t* qwords;
+    const float* rows;
+    uint64_t clen;
+    const float* norms;
+    const float* q;
+    uint64_t qlen;
+    int kind, descending, force_rescan;
+    const uint64_t* ids;
+    uint64_t row_offset;
+    float* scores;            // [bufcap] published exact scores of the buffered candidates
+    float* rscores;           // [R] scores of a rescan's rows
+    uint64_t* topr;           // [R] published sorted top-R keys (d, row, buffer index)
+    uint32_t* ticket;         // arrival counter, reset by the last block
+    uint32_t* rescans;        // diagnostics: device-side rescans
+    uint32_t* hist;           // [D+1] sample histogram, zeroed by the last block
+    uint64_t* out_ids;
+    float* out_scores;
+    uint32_t* out_n;
+    unsigned long long* clk;  // timing study only (GVDB_B1_CLK): [block0 | last block][8] wall clocks
+};
+
+// k_b1_tail: block 0 selects the exact top-R from the candidate buffer while
+// blocks 1..G re-score EVERY buffered candidate (16 per block and round), so the
+// select and the row gathers + sequential folds overlap; the last block to
+// arrive sorts the top-R by exact score.  A rescan (buffer cannot hold the
+// top-R) re-scores its R rows in block 0 itself (rare; slow, still exact).
+__global__ __launch_bounds__(256) void k_b1_tail(B1TailArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // keys | hist | bins | tile | query
+    uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
+    uint32_t* bins = hist + ((a.D + 4u) & ~3u);
+    float4* tile4 = (float4*)(bins + 2048);
+    float4* qs4 = tile4 + kRsRows * (kRsMaxLen / 4 + 1);
+    __shared__ uint32_t s_last, s_nan, rowid[kRsRows];
+    const uint32_t tid = threadIdx.x, R = a.R;
+    unsigned long long ck[6];
+    ck[0] = wall_clock64();
+    const uint32_t cnt = a.counts[0];
+    unsigned long long t_staged = 0;
+    if (blockIdx.x == 0) {
+        const bool resc = select_topr(cnt, a.buf, a.bufcap, a.D, R, a.codes, a.cap, a.N, a.W4,
+                                      (const uint4*)a.qwords, a.force_rescan != 0, sk, hist, bins, true);
+        ck[1] = wall_clock64();
+        for (uint32_t i = tid; i < R; i += 256)
+            __hip_atomic_store(a.topr + i, sk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (resc) {  // rows not from the buffer: score them here, 16 at a time
+            if (tid == 0) atomicAdd(a.rescans, 1u);
+            for (uint32_t r0 = 0; r0 < R; r0 += kRsRows) {
+                const uint32_t nr = min((uint32_t)kRsRows, R - r0);
+                __syncthreads();
+                if (tid < kRsRows) rowid[tid] = tid < nr ? (uint32_t)((sk[r0 + tid] >> 21) & 0xffffffffull) : 0u;
+                __syncthreads();
+                const float sc = rerank16(a.rows, a.clen, a.norms, a.q, a.qlen, a.kind, rowid, nr, tile4, qs4);
+                if (tid < nr)
+                    __hip_atomic_store(a.rscores + r0 + tid, sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        ck[2] = wall_clock64();
+    } else if (cnt <= a.bufcap) {
+        // candidates j = 16 (blockIdx.x - 1) + 16 G i: their exact scores
+        const uint32_t G = gridDim.x - 1;
+        for (uint32_t j0 = (blockIdx.x - 1) * kRsRows; j0 < cnt; j0 += G * kRsRows) {
+            const uint32_t nr = min((uint32_t)kRsRows, cnt - j0);
+            __syncthreads();
+            if (tid < kRsRows) rowid[tid] = tid < nr ? (uint32_t)a.buf[j0 + tid] : 0u;
+            __syncthreads();
+            const float sc = rerank16(a.rows, a.clen, a.norms, a.q, a.qlen, a.kind, rowid, nr, tile4, qs4,
+                                      &t_staged);
+            if (tid < nr) __hip_atomic_store(a.scores + j0 + tid, sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ck[1] = t_staged;
+        ck[2] = wall_clock64();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = t == gridDim.x - 1;
+        s_nan = 0u;
+    }
+    __syncthreads();
+    ck[3] = wall_clock64();
+    if (a.clk && tid == 0 && blockIdx.x <= 1)
+        for (int i = 0; i < 4; ++i) a.clk[blockIdx.x * 4 + i] = ck[i];
+    if (!s_last) return;
+    // the last block: stable sort of the top-R by exact score (ties: stage-1 rank)
+    for (uint32_t i = tid; i < R; i += 256)
+        sk[i] = __hip_atomic_load(a.topr + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    uint64_t* fk = (uint64_t*)tile4;                  // R <= kSortLdsCap keys (32 KiB of the tile region)
+    float* fsc = (float*)(fk + kSortLdsCap);          // R scores (16 KiB after them)
+    for (uint32_t i = tid; i < R; i += 256) {
+        const uint32_t idx = (uint32_t)(sk[i] & kNoIdx);
+        const float f = __hip_atomic_load(idx == kNoIdx ? a.rscores + i : a.scores + idx, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        if (f != f) s_nan = 1u;
+        uint32_t o = f32_order(f);
+        if (a.descending) o = ~o;
+        fk[i] = ((uint64_t)o << 32) | i;  // ties: stage-1 rank
+        fsc[i] = f;
+    }
+    __syncthreads();
+    select_sort(fk, R, (uint64_t*)hist);  // hist (>= 4 KiB free now) as the rank-sort scratch
+    ck[4] = wall_clock64();
+    const uint32_t take = a.kout < R ? a.kout : R;
+    if (tid < 64) {  // take(k) then drop orphan rows (index.rs:217-228), order-preserving
+        uint32_t o = 0;
+        for (uint32_t i0 = 0; i0 < take; i0 += 64) {
+            const uint32_t i = i0 + tid;
+            uint64_t id = kOrphan;
+            uint32_t rank = 0;
+            if (i < take) {
+                rank = (uint32_t)fk[i];
+                const uint32_t row = (uint32_t)((sk[rank] >> 21) & 0xffffffffull);
+                id = a.ids ? a.ids[row] : (uint64_t)row + a.row_offset;
+            }
+            const bool keep = i < take && id != kOrphan;
+            const uint64_t m = __ballot(keep);
+            const uint32_t before = __popcll(m & ((1ull << tid) - 1ull));
+            if (keep) {
+                a.out_ids[o + before] = id;
+                a.out_scores[o + before] = fsc[rank];
+            }
+            o += __popcll(m);
+        }
+        if (tid == 0 && a.out_n) a.out_n[0] = (s_nan && R >= 2) ? GVDB_N_POISONED : o;
+    }
+    // self-cleaning for the next call (visible to it across the kernel boundary)
+    for (uint32_t i = tid; i <= a.D; i += 256) a.hist[i] = 0u;
+    if (tid == 0) {
+        *(uint32_t*)a.counts = 0u;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.clk) {
+            ck[5] = wall_clock64();
+            for (int i = 0; i < 6; ++i) a.clk[8 + i] = ck[i];
+            a.clk[14] = cnt;
+        }
+    }
+}
+
+size_t b1_tail_lds(uint32_t D) {
+    return (size_t)kSelectLdsCap * 8u + (size_t)((D + 4u) & ~3u) * 4u + 2048u * 4u +
+           (size_t)(kRsRows * (kRsMaxLen / 4 + 1) + kRsMaxLen / 4) * 16u;
+}
+
+hipError_t launch_b1_search(const B1Args& b, hipStream_t s) {
+    const uint32_t W4 = code_w4(b.D);
+    if (b.ev) (void)hipEventRecord(b.ev[0], s);
+    switch (W4) {
+#define GVDB_CASE(w)                                                                                            \
+    case w:                                                                                                     \
+        hipLaunchKernelGGL((k_b1_sample<w>), dim3(b.sample_chunks), dim3(256), 0, s, b.codes, b.cap, b.N, b.D, \
+                           b.sample_stride, b.q, b.thr, b.qwords, b.hist);                                     \
+        break;
+        GVDB_CASE(1) GVDB_CASE(2) GVDB_CASE(3) GVDB_CASE(4) GVDB_CASE(6) GVDB_CASE(8)
+#undef GVDB_CASE
+        default: return hipErrorInvalidValue;
+    }
+    GVDB_LAUNCH_CHECK();
+    if (b.ev) (void)hipEventRecord(b.ev[1], s);
+    switch (W4) {
+#define GVDB_CASE(w, cpl)                                                                                        \
+    case w:                                                                                                      \
+        hipLaunchKernelGGL((k_b1_scan<w, cpl>), dim3((uint32_t)((b.N + 256ull * cpl - 1) / (256ull * cpl))),    \
+                           dim3(256), 0, s, b.codes, b.cap, b.N, b.D, b.qwords, b.hist, b.target, b.counts, b.buf, \
+                           b.bufcap);                                                                            \
+        break;
+        GVDB_CASE(1, 8) GVDB_CASE(2, 8) GVDB_CASE(3, 8) GVDB_CASE(4, 4) GVDB_CASE(6, 4) GVDB_CASE(8, 2)
+#undef GVDB_CASE
+    }
+    GVDB_LAUNCH_CHECK();
+    if (b.ev) {
+        (void)hipEventRecord(b.ev[2], s);
+        (void)hipEventRecord(b.ev[3], s);
+    }
+    B1TailArgs t{};
+    t.counts = b.counts;
+    t.buf = b.buf;
+    t.bufcap = b.bufcap;
+    t.D = b.D;
+    t.R = b.R;
+    t.N = b.N;
+    t.W4 = W4;
+    t.kout = b.kout;
+    t.codes = b.codes;
+    t.cap = b.cap;
+    t.qwords = b.qwords;
+    t.rows = b.rows;
+    t.clen = b.clen;
+    t.norms = b.norms;
+    t.q = b.q;
+    t.qlen = b.qlen;
+    t.kind = b.kind;
+    t.descending = b.descending;
+    t.force_rescan = b.force_rescan;
+    t.ids = b.ids;
+    t.row_offset = b.row_offset;
+    t.scores = b.scores;
+    t.rscores = b.rscores;
+    t.topr = b.topr;
+    t.ticket = b.ticket;
+    t.rescans = b.rescans;
+    t.hist = b.hist;
+    t.out_ids = b.out_ids;
+    t.out_scores = b.out_scores;
+    t.out_n = b.out_n;
+    t.clk = b.clk;
+    const uint32_t G = std::min<uint32_t>((b.bufcap + kRsRows - 1) / kRsRows, kB1RerankBlocks);
+    hipLaunchKernelGGL(k_b1_tail, dim3(1 + G), dim3(256), b1_tail_lds(b.D), s, t);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

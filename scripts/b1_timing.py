@@ -30,4 +30,18 @@ for i in range(Q.shape[0]):
     ix.search_device(Q[i:i + 1], 10, oi, osc, None, p)
 torch.cuda.synchronize()
 t = time.perf_counter() - t
-print(f"batch-1: {1e3 * t / Q.shape[0]:.3f} ms/query, {Q.shape[0] / t:.0f} QPS", flush=True)
+tag = os.environ.get("TAG", "")
+print(f"batch-1{tag}: {1e3 * t / Q.shape[0]:.3f} ms/query, {Q.shape[0] / t:.0f} QPS", flush=True)
+# concurrent single-query requests: S streams, each with its own output buffers
+S = int(os.environ.get("STREAMS", 0))
+if S > 1:
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    outs = [(torch.zeros((1, 10), dtype=torch.int64, device=dev), torch.zeros((1, 10), device=dev)) for _ in range(S)]
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for i in range(Q.shape[0]):
+        j = i % S
+        ix.search_device(Q[i:i + 1], 10, outs[j][0], outs[j][1], None, p, stream=streams[j].cuda_stream)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t
+    print(f"batch-1{tag} x{S} streams: {Q.shape[0] / t:.0f} QPS", flush=True)
