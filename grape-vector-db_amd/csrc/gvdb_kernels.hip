@@ -279,26 +279,42 @@ template <int W4>
 __global__ __launch_bounds__(256) void k_sample_hist(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                      uint32_t D, uint32_t stride, const uint4* __restrict__ qcodes,
                                                      uint32_t B, uint32_t QT, uint32_t* __restrict__ hist) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lh[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t lh[];  // [QT][D+1] histograms, then [QT][W4] query codes
     const uint32_t nb = D + 1u;
-    for (uint32_t i = threadIdx.x; i < QT * nb; i += 256) lh[i] = 0u;
-    __syncthreads();
+    uint4* qs = (uint4*)(lh + ((QT * nb + 3u) & ~3u));
     const uint64_t start = (uint64_t)blockIdx.x * stride;
     const uint32_t q0 = blockIdx.y * QT;
     const uint32_t qn = (B - q0) < QT ? (B - q0) : QT;
+    for (uint32_t i = threadIdx.x; i < QT * nb; i += 256) lh[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < qn * W4; i += 256) qs[i] = qcodes[(uint64_t)q0 * W4 + i];
+    __syncthreads();
+    // the next row's code planes are in flight while the current row is
+    // compared with the block's queries (about one wave per SIMD here: a
+    // load -> use chain would expose one HBM latency per row)
+    uint4 c[W4], cn[W4];
+    {
+        const uint64_t row = min(start + threadIdx.x, (uint64_t)N - 1);
+#pragma unroll
+        for (int w = 0; w < W4; ++w) c[w] = load_code_nt(codes + (uint64_t)w * cap + row);
+    }
     for (uint32_t it = 0; it < 16; ++it) {
         const uint64_t row = start + it * 256u + threadIdx.x;
         if (row >= N) break;
-        uint4 c[W4];
+        const uint64_t nrow = min(row + 256u, (uint64_t)N - 1);
+        if (it + 1 < 16) {
 #pragma unroll
-        for (int w = 0; w < W4; ++w) c[w] = codes[(uint64_t)w * cap + row];
-        for (uint32_t qi = 0; qi < qn; ++qi) {
-            const uint4* qc = qcodes + (uint64_t)(q0 + qi) * W4;
+            for (int w = 0; w < W4; ++w) cn[w] = load_code_nt(codes + (uint64_t)w * cap + nrow);
+        }
+        uint32_t qi = 0;
+        for (; qi < qn; ++qi) {
+            const uint4* qc = qs + qi * W4;
             uint32_t d = 0;
 #pragma unroll
             for (int w = 0; w < W4; ++w) d = ham4(c[w], qc[w], d);
             atomicAdd(&lh[qi * nb + d], 1u);
         }
+#pragma unroll
+        for (int w = 0; w < W4; ++w) c[w] = cn[w];
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < qn * nb; i += 256) {
@@ -1392,6 +1408,11 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
     __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+#if defined(MX3_PRIO) && MX3_PRIO == 1
+    // static priority for the younger half (waves 4-7): they lose VALU
+    // arbitration to the older half otherwise (MI355X_MICROARCH.md, two waves per SIMD)
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
     constexpr float kPadF = (float)(32 * KW);
     const int scale1 = 0x7f7f7f7f;
     // query fragments: (tile qt, k-step s, lane l) = query qt*32 + (l & 31), code word 2s + (l >> 5)
@@ -1461,6 +1482,9 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
                 // expansions (their registers would spill)
                 __builtin_amdgcn_sched_barrier(0);
                 const v4i_t b = fp4_x32(word(c, s));
+#if defined(MX3_PRIO) && MX3_PRIO == 2
+                __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
                 for (int qt = 0; qt < QH; ++qt) {
                     const int m = s * QH + qt;
@@ -1471,6 +1495,9 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __rest
                     else
                         mfma_fp4_acc(acc[qt], a, b, scale1);
                 }
+#if defined(MX3_PRIO) && MX3_PRIO == 2
+                __builtin_amdgcn_s_setprio(0);
+#endif
             }
             mfma_fp4_drain();
             // threshold epilogue of these QH query tiles
@@ -1809,10 +1836,20 @@ static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
         return v >= 1024 && v <= 36864 ? (uint32_t)v : 12288u;
     }();
     uint32_t QT = words / (a.D + 1u);
+    if (!getenv("GVDB_HIST_LDS_WORDS")) {
+        // about three blocks per CU: fewer queries per block when the sample has
+        // few chunks (1.25M-row shard, 16 chunks: 6 queries per block, 0.282 ->
+        // 0.260 ms per batch-256 step; 10M: 13, unchanged -- profiles/r02)
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint32_t want = (uint32_t)(((uint64_t)a.B * a.sample_chunks + 3ull * cus - 1) / (3ull * cus));
+        QT = std::min(QT, std::max(want, 4u));
+    }
     if (QT < 1) QT = 1;
     if (QT > 32) QT = 32;
     if (QT > a.B) QT = a.B;
-    const size_t lds = (size_t)QT * (a.D + 1u) * 4u;
+    const size_t lds = (((size_t)QT * (a.D + 1u) + 3u) & ~(size_t)3) * 4u + (size_t)QT * W4 * 16u;
     hipLaunchKernelGGL((k_sample_hist<W4>), dim3(a.sample_chunks, (a.B + QT - 1) / QT), dim3(256), lds, s, a.codes,
                        a.cap, a.N, a.D, a.sample_stride, a.qcodes, a.B, QT, a.hist);
 }
@@ -2312,32 +2349,22 @@ __global__ __launch_bounds__(kRr2Threads, 4) void k_rerank2(const float* __restr
 constexpr int kRsRows = 16;
 constexpr int kRsThreads = 256;
 constexpr uint32_t kRsMaxLen = 1024;
-__global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __restrict__ rows, uint64_t clen,
-                                                            const float* __restrict__ norms,
-                                                            const float* __restrict__ q, uint64_t qlen,
-                                                            const uint32_t* __restrict__ s1_rows, uint32_t B,
-                                                            uint32_t R, const uint32_t* __restrict__ counts, int kind,
-                                                            float* __restrict__ scores) {
-    __shared__ float4 tile4[kRsRows * (kRsMaxLen / 4 + 1)];
-    __shared__ float4 qs4[kRsMaxLen / 4];
+// Exact re-score of up to 16 rows (rows[r] for r < nr) by lanes 0..15: every
+// row load in flight at once into LDS, then each lane folds its row left to
+// right (acc = acc + q_j*x_j, qq = qq + q_j*q_j; the reference's order) with
+// the next 8 float4 of its row prefetched from LDS while the current 8 fold.
+__device__ __forceinline__ float rerank16(const float* __restrict__ rows, uint64_t clen, const float* __restrict__ norms,
+                          const float* __restrict__ qv, uint64_t qlen, int kind, const uint32_t* rowid, uint32_t nr,
+                          float4* tile4, float4* qs4, unsigned long long* t_staged = nullptr) {
     __shared__ uint64_t bases[kRsRows];
     const uint32_t tid = threadIdx.x;
-    const uint32_t ipq = (R + kRsRows - 1) / kRsRows;
-    const uint32_t qi = blockIdx.x / ipq;
-    const uint32_t r0 = (blockIdx.x % ipq) * kRsRows;
-    if (qi >= B) return;
-    const uint32_t Rq = counts ? min(counts[qi], R) : R;
-    if (r0 >= Rq) return;  // block-uniform
-    const uint64_t len = qlen < clen ? qlen : clen;  // zip() truncates
+    const uint64_t len = qlen < clen ? qlen : clen;
     const uint32_t L4 = (uint32_t)((len + 3) / 4), ld4 = L4 + 1;
     const bool vec4 = (clen & 3u) == 0;
-    const float* qv = q + (uint64_t)qi * qlen;
     const bool qvec4 = (qlen & 3u) == 0 && (((uintptr_t)qv) & 15u) == 0;
-    if (tid < kRsRows) bases[tid] = r0 + tid < Rq ? (uint64_t)s1_rows[(uint64_t)qi * R + r0 + tid] * clen : ~0ull;
+    if (tid < kRsRows) bases[tid] = tid < nr ? (uint64_t)rowid[tid] * clen : ~0ull;
     __syncthreads();
-    // every load in flight before the first LDS store (a load -> store loop
-    // would wait one full gather latency per iteration)
-    constexpr int kPer = kRsRows * (kRsMaxLen / 4) / kRsThreads;  // 16 float4 per thread
+    constexpr int kPer = kRsRows * (kRsMaxLen / 4) / kRsThreads;
     float4 v[kPer];
     const float4 qv4 = tid < L4 ? load4_guarded(qv, 0, 4ull * tid, len, qvec4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -2352,7 +2379,35 @@ __global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __rest
     }
     if (tid < L4) qs4[tid] = qv4;
     __syncthreads();
-    if (tid >= kRsRows || r0 + tid >= Rq) return;
+    if (t_staged) *t_staged = wall_clock64();
+    if (kind != kScoreL2 && (len & 3u) == 0) {
+        // one chain per lane: lanes 0..15 fold q_j*x_j of their row, lane 16
+        // folds q_j*q_j (the query norm, same for every row); the products of
+        // a float4 go out as packed multiplies, the sums stay sequential
+        if (tid > kRsRows) return 0.0f;
+        typedef float f2_t __attribute__((ext_vector_type(2)));
+        const float4* src = tid < kRsRows ? tile4 + tid * ld4 : qs4;
+        float acc = -0.0f;
+#pragma unroll 8
+        for (uint32_t c = 0; c < L4; ++c) {
+            const float4 x = src[c];
+            const float4 w = qs4[c];
+            const f2_t p01 = (f2_t){w.x, w.y} * (f2_t){x.x, x.y};
+            const f2_t p23 = (f2_t){w.z, w.w} * (f2_t){x.z, x.w};
+            acc = acc + p01.x;
+            acc = acc + p01.y;
+            acc = acc + p23.x;
+            acc = acc + p23.y;
+        }
+        float qq = __shfl(acc, kRsRows);
+        if (tid >= nr) return 0.0f;
+        for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+        const float na = sqrtf(qq);
+        const float nb = norms[rowid[tid]];
+        if (kind == kScoreCosine) return (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+        return (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+    }
+    if (tid >= nr) return 0.0f;
     const float4* tr4 = tile4 + tid * ld4;
     float acc = -0.0f, qq = -0.0f;
     if (kind == kScoreL2) {
@@ -2362,20 +2417,6 @@ __global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __rest
             const float d = qc[j] - tr[j];
             acc = acc + d * d;
         }
-    } else if ((len & 3u) == 0) {
-#pragma unroll 4
-        for (uint32_t c = 0; c < L4; ++c) {
-            const float4 x = tr4[c];
-            const float4 w = qs4[c];
-            acc = acc + w.x * x.x;
-            acc = acc + w.y * x.y;
-            acc = acc + w.z * x.z;
-            acc = acc + w.w * x.w;
-            qq = qq + w.x * w.x;
-            qq = qq + w.y * w.y;
-            qq = qq + w.z * w.z;
-            qq = qq + w.w * w.w;
-        }
     } else {
         const float* tr = (const float*)tr4;
         const float* qc = (const float*)qs4;
@@ -2384,21 +2425,35 @@ __global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __rest
             qq = qq + qc[j] * qc[j];
         }
     }
-    const uint32_t r = r0 + tid;
-    float score;
-    if (kind == kScoreL2) {
-        score = sqrtf(acc);
-    } else {
-        for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
-        const float na = sqrtf(qq);
-        const float nb = norms[s1_rows[(uint64_t)qi * R + r]];
-        if (kind == kScoreCosine) {
-            score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
-        } else {
-            score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
-        }
-    }
-    scores[(uint64_t)qi * R + r] = score;
+    if (kind == kScoreL2) return sqrtf(acc);
+    for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
+    const float na = sqrtf(qq);
+    const float nb = norms[rowid[tid]];
+    if (kind == kScoreCosine) return (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+    return (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
+}
+
+__global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __restrict__ rows, uint64_t clen,
+                                                            const float* __restrict__ norms,
+                                                            const float* __restrict__ q, uint64_t qlen,
+                                                            const uint32_t* __restrict__ s1_rows, uint32_t B,
+                                                            uint32_t R, const uint32_t* __restrict__ counts, int kind,
+                                                            float* __restrict__ scores) {
+    __shared__ float4 tile4[kRsRows * (kRsMaxLen / 4 + 1)];
+    __shared__ float4 qs4[kRsMaxLen / 4];
+    __shared__ uint32_t rowid[kRsRows];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t ipq = (R + kRsRows - 1) / kRsRows;
+    const uint32_t qi = blockIdx.x / ipq;
+    const uint32_t r0 = (blockIdx.x % ipq) * kRsRows;
+    if (qi >= B) return;
+    const uint32_t Rq = counts ? min(counts[qi], R) : R;
+    if (r0 >= Rq) return;  // block-uniform
+    const uint32_t nr = min((uint32_t)kRsRows, Rq - r0);
+    if (tid < kRsRows) rowid[tid] = tid < nr ? s1_rows[(uint64_t)qi * R + r0 + tid] : 0u;
+    __syncthreads();
+    const float sc = rerank16(rows, clen, norms, q + (uint64_t)qi * qlen, qlen, kind, rowid, nr, tile4, qs4);
+    if (tid < nr) scores[(uint64_t)qi * R + r0 + tid] = sc;
 }
 
 // GVDB_RERANK=v1: always the block-synchronous k_rerank (A/B)
@@ -2440,7 +2495,11 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
         // (flat candidate lists: ~13 % on 560K rows); the block-synchronous
         // k_rerank (128-dim chunks, shorter serial chain per item) on small
         // ones (batch-1: 34 us vs 60 us)
-        if (rerank_v2() && max_items >= 2048) {
+        static const uint64_t v2_min = [] {  // GVDB_RERANK2_MIN: items from which k_rerank2 is used (A/B)
+            const char* e = getenv("GVDB_RERANK2_MIN");
+            return e ? (uint64_t)atoll(e) : (uint64_t)2048;
+        }();
+        if (rerank_v2() && max_items >= v2_min) {
             // one item per wave; up to 4 resident blocks (16 waves) per CU
             const uint64_t blocks = (max_items + 3) / 4;
             const uint32_t grid = (uint32_t)std::min<uint64_t>(blocks, 4ull * cus);
@@ -2466,28 +2525,24 @@ __global__ __launch_bounds__(256) void k_final_sort(const float* __restrict__ sc
                                                     float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
                                                     uint32_t* __restrict__ nan_flag) {
     __shared__ uint64_t sk[kSortLdsCap];
+    __shared__ uint64_t tmp[kRankSortMax];
     __shared__ uint32_t s_nan;
     const uint32_t q = blockIdx.x;
     const float* sc = scores + (uint64_t)q * R;
     if (threadIdx.x == 0) s_nan = 0u;
     __syncthreads();
-    const uint32_t P = next_pow2(R);
-    for (uint32_t i = threadIdx.x; i < P; i += 256) {
-        uint64_t key = ~0ull;
-        if (i < R) {
-            const float f = sc[i];
-            if (f != f) s_nan = 1u;
-            uint32_t o = f32_order(f);
-            if (descending) o = ~o;
-            key = ((uint64_t)o << 32) | i;  // ties: stage-1 rank ascending (stable sort)
-        }
-        sk[i] = key;
+    for (uint32_t i = threadIdx.x; i < R; i += 256) {
+        const float f = sc[i];
+        if (f != f) s_nan = 1u;
+        uint32_t o = f32_order(f);
+        if (descending) o = ~o;
+        sk[i] = ((uint64_t)o << 32) | i;  // ties: stage-1 rank ascending (stable sort)
     }
     __syncthreads();
     if (s_nan && R >= 2) {
         if (threadIdx.x == 0) atomicOr(nan_flag, 1u);
     }
-    bitonic_sort_lds(sk, P);
+    select_sort(sk, R, tmp);  // rank counting up to kRankSortMax keys, bitonic beyond
     const uint32_t take = kout < R ? kout : R;
     // take(k) then drop orphan rows (index.rs:217-228); order-preserving
     // compaction by wave 0 with a ballot prefix.
@@ -3122,90 +3177,6 @@ __global__ __launch_bounds__(256) void k_b1_scan(const uint4* __restrict__ codes
             if (pos < bufcap) buf[pos] = ((uint64_t)d << 32) | (uint32_t)(base + (uint64_t)k * 256u + tid);
         }
     }
-}
-
-// Exact re-score of up to 16 rows (rows[r] for r < nr) by lanes 0..15: every
-// row load in flight at once into LDS, then each lane folds its row left to
-// right (acc = acc + q_j*x_j, qq = qq + q_j*q_j; the reference's order) with
-// the next 8 float4 of its row prefetched from LDS while the current 8 fold.
-__device__ __forceinline__ float rerank16(const float* __restrict__ rows, uint64_t clen, const float* __restrict__ norms,
-                          const float* __restrict__ qv, uint64_t qlen, int kind, const uint32_t* rowid, uint32_t nr,
-                          float4* tile4, float4* qs4, unsigned long long* t_staged = nullptr) {
-    __shared__ uint64_t bases[kRsRows];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t len = qlen < clen ? qlen : clen;
-    const uint32_t L4 = (uint32_t)((len + 3) / 4), ld4 = L4 + 1;
-    const bool vec4 = (clen & 3u) == 0;
-    const bool qvec4 = (qlen & 3u) == 0 && (((uintptr_t)qv) & 15u) == 0;
-    if (tid < kRsRows) bases[tid] = tid < nr ? (uint64_t)rowid[tid] * clen : ~0ull;
-    __syncthreads();
-    constexpr int kPer = kRsRows * (kRsMaxLen / 4) / kRsThreads;
-    float4 v[kPer];
-    const float4 qv4 = tid < L4 ? load4_guarded(qv, 0, 4ull * tid, len, qvec4) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const uint32_t i = tid + k * kRsThreads, r = i / L4, c = i - r * L4;
-        v[k] = i < kRsRows * L4 ? load4_guarded(rows, bases[r], 4ull * c, len, vec4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const uint32_t i = tid + k * kRsThreads, r = i / L4, c = i - r * L4;
-        if (i < kRsRows * L4) tile4[r * ld4 + c] = v[k];
-    }
-    if (tid < L4) qs4[tid] = qv4;
-    __syncthreads();
-    if (t_staged) *t_staged = wall_clock64();
-    if (kind != kScoreL2 && (len & 3u) == 0) {
-        // one chain per lane: lanes 0..15 fold q_j*x_j of their row, lane 16
-        // folds q_j*q_j (the query norm, same for every row); the products of
-        // a float4 go out as packed multiplies, the sums stay sequential
-        if (tid > kRsRows) return 0.0f;
-        typedef float f2_t __attribute__((ext_vector_type(2)));
-        const float4* src = tid < kRsRows ? tile4 + tid * ld4 : qs4;
-        float acc = -0.0f;
-#pragma unroll 8
-        for (uint32_t c = 0; c < L4; ++c) {
-            const float4 x = src[c];
-            const float4 w = qs4[c];
-            const f2_t p01 = (f2_t){w.x, w.y} * (f2_t){x.x, x.y};
-            const f2_t p23 = (f2_t){w.z, w.w} * (f2_t){x.z, x.w};
-            acc = acc + p01.x;
-            acc = acc + p01.y;
-            acc = acc + p23.x;
-            acc = acc + p23.y;
-        }
-        float qq = __shfl(acc, kRsRows);
-        if (tid >= nr) return 0.0f;
-        for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
-        const float na = sqrtf(qq);
-        const float nb = norms[rowid[tid]];
-        if (kind == kScoreCosine) return (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
-        return (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
-    }
-    if (tid >= nr) return 0.0f;
-    const float4* tr4 = tile4 + tid * ld4;
-    float acc = -0.0f, qq = -0.0f;
-    if (kind == kScoreL2) {
-        const float* tr = (const float*)tr4;
-        const float* qc = (const float*)qs4;
-        for (uint32_t j = 0; j < len; ++j) {
-            const float d = qc[j] - tr[j];
-            acc = acc + d * d;
-        }
-    } else {
-        const float* tr = (const float*)tr4;
-        const float* qc = (const float*)qs4;
-        for (uint32_t j = 0; j < len; ++j) {
-            acc = acc + qc[j] * tr[j];
-            qq = qq + qc[j] * qc[j];
-        }
-    }
-    if (kind == kScoreL2) return sqrtf(acc);
-    for (uint64_t j = len; j < qlen; ++j) qq = qq + qv[j] * qv[j];  // query longer than rows
-    const float na = sqrtf(qq);
-    const float nb = norms[rowid[tid]];
-    if (kind == kScoreCosine) return (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
-    return (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc / (na * nb));
 }
 
 struct B1TailArgs {
