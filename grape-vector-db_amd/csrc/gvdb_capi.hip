@@ -244,6 +244,7 @@ struct ShardView {
 };
 
 constexpr uint32_t kExactN = 262144;  // below this the "sample" is the whole shard
+constexpr uint64_t kFlatScoreBytes = 1ull << 30;  // dense score block cap of the exact flat scan
 
 // Stage-1 sampling plan: S rows in 4096-row chunks spread over the shard.
 // sample_div: the sample is ~N/sample_div rows (32; 64 for large batches,
@@ -1143,20 +1144,28 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
         flat_fallbacks().fetch_add(1);
     }
     if (sp.mode == GVDB_SEARCH_FLAT) {
+        // exact scan + radix select, in query groups whose dense score block
+        // stays within kFlatScoreBytes (1 GiB: 26 queries per group at 10M rows)
+        // instead of one B x N block (10 GB at B = 256)
+        const uint64_t per_q = std::max<uint64_t>(ix->n * 4, 1);
+        const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(B, kFlatScoreBytes / per_q));
         HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
-        HIP_TRY(ws.scores.ensure(B * ix->n * 4), "alloc flat scores");
+        HIP_TRY(ws.scores.ensure(G * per_q), "alloc flat scores");
         HIP_TRY(ws.flags.ensure(16), "alloc flags");
         HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
         HIP_TRY(launch_row_norms(d_q, B, dim, ws.qnorm.as<float>(), s), "qnorm");
-        HIP_TRY(launch_flat_scores(d_q, (uint32_t)B, ws.qnorm.as<float>(), ix->rows, (uint32_t)ix->n, dim, ix->norms,
-                                   kind, nullptr, ws.scores.as<float>(), s),
-                "flat scores");
         const size_t need = flat_select_bytes((uint32_t)ix->n);
         HIP_TRY(ws.sort_tmp.ensure(need), "alloc sort tmp");
-        HIP_TRY(launch_flat_select(ws.scores.as<float>(), (uint32_t)B, (uint32_t)ix->n, (uint32_t)k, descending, 0, 0.0f,
-                                   ix->ids, d_ids, d_scores, d_n, ws.sort_tmp.p, ws.sort_tmp.n,
-                                   ws.flags.as<uint32_t>() + 1, s),
-                "flat select");
+        for (uint64_t g0 = 0; g0 < B; g0 += G) {
+            const uint32_t bg = (uint32_t)std::min<uint64_t>(G, B - g0);
+            HIP_TRY(launch_flat_scores(d_q + g0 * dim, bg, ws.qnorm.as<float>() + g0, ix->rows, (uint32_t)ix->n, dim,
+                                       ix->norms, kind, nullptr, ws.scores.as<float>(), s),
+                    "flat scores");
+            HIP_TRY(launch_flat_select(ws.scores.as<float>(), bg, (uint32_t)ix->n, (uint32_t)k, descending, 0, 0.0f,
+                                       ix->ids, d_ids + g0 * k, d_scores + g0 * k, d_n ? d_n + g0 : nullptr,
+                                       ws.sort_tmp.p, ws.sort_tmp.n, ws.flags.as<uint32_t>() + 1, s),
+                    "flat select");
+        }
         HIP_TRY(hipStreamSynchronize(s), "sync");
         return GVDB_OK;
     }

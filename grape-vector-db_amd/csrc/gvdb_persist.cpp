@@ -47,6 +47,8 @@ struct gvdb_persist_reader {
     std::vector<uint8_t> buf;  // undecoded bytes [pos, buf.size())
     size_t pos = 0;
     bool eof = false;
+    std::string zerr;     // a zlib error met while reading (distinct from a clean end of stream)
+    bool drained = false; // the stream was read to its end after the last entry (trailer checked)
 };
 
 namespace {
@@ -94,6 +96,11 @@ bool fill(gvdb_persist_reader* r, size_t need) {
         if (got <= 0) {
             r->eof = true;
             r->buf.resize(have);
+            if (got < 0) {
+                int err = 0;
+                const char* m = gzerror(r->f, &err);
+                r->zerr = m ? m : "zlib error";
+            }
         } else {
             r->buf.resize(have + (size_t)got);
         }
@@ -101,12 +108,34 @@ bool fill(gvdb_persist_reader* r, size_t need) {
     return r->buf.size() >= need;
 }
 
-gvdb_status truncated() { return report_status(GVDB_ERR_STORAGE, "index file truncated or not in postcard format"); }
+gvdb_status truncated(const gvdb_persist_reader* r) {
+    if (!r->zerr.empty()) return report_status(GVDB_ERR_STORAGE, "index file: " + r->zerr);
+    return report_status(GVDB_ERR_STORAGE, "index file truncated or not in postcard format");
+}
+
+// After the last entry: read the gzip stream to its end so the trailer (CRC-32,
+// length) is verified, as GzDecoder::read_to_end does (query.rs:355-373).
+gvdb_status drain_and_check(gvdb_persist_reader* r) {
+    if (r->drained) return GVDB_OK;
+    r->drained = true;
+    std::vector<uint8_t> sink(1u << 20);
+    while (!r->eof) {
+        const int got = gzread(r->f, sink.data(), (unsigned)sink.size());
+        if (got < 0) {
+            int err = 0;
+            const char* m = gzerror(r->f, &err);
+            r->zerr = m ? m : "zlib error";
+        }
+        if (got <= 0) r->eof = true;
+    }
+    if (!r->zerr.empty()) return report_status(GVDB_ERR_STORAGE, "index file: " + r->zerr);
+    return GVDB_OK;
+}
 
 gvdb_status get_varint(gvdb_persist_reader* r, uint64_t* v) {
     uint64_t x = 0;
     for (int sh = 0; sh < 70; sh += 7) {
-        if (!fill(r, 1)) return truncated();
+        if (!fill(r, 1)) return truncated(r);
         const uint8_t c = r->buf[r->pos++];
         if (sh == 63 && c > 1) return report_status(GVDB_ERR_STORAGE, "varint overflows u64");
         x |= (uint64_t)(c & 0x7f) << sh;
@@ -119,7 +148,7 @@ gvdb_status get_varint(gvdb_persist_reader* r, uint64_t* v) {
 }
 
 gvdb_status get_bytes(gvdb_persist_reader* r, size_t n, const uint8_t** p) {
-    if (!fill(r, n)) return truncated();
+    if (!fill(r, n)) return truncated(r);
     *p = r->buf.data() + r->pos;
     r->pos += n;
     return GVDB_OK;
@@ -161,6 +190,9 @@ gvdb_status gvdb_persist_append(gvdb_persist_writer* w, const float* rows, uint6
     if (!w || (n && (!rows || !id_blob || !id_offs))) return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (w->written + n > w->declared)
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "more vectors appended than declared at create");
+    if (n && dim != w->dim)  // the header states w->dim: a row of another length makes an invalid file
+        return report_status(GVDB_ERR_DIMENSION_MISMATCH, "appended rows have dimension " + std::to_string(dim) +
+                                                              ", the file header states " + std::to_string(w->dim));
     for (uint64_t i = 0; i < n; ++i) {
         if (id_offs[i + 1] < id_offs[i]) return report_status(GVDB_ERR_INVALID_ARGUMENT, "id offsets not ascending");
         put_str(w->buf, id_blob + id_offs[i], (size_t)(id_offs[i + 1] - id_offs[i]));
@@ -261,6 +293,7 @@ gvdb_status gvdb_persist_next(gvdb_persist_reader* r, float* rows, uint32_t dim,
         ++r->read;
     }
     *n_out = n;
+    if (r->read == r->count) return drain_and_check(r);
     return GVDB_OK;
 }
 

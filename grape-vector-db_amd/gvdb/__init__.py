@@ -273,6 +273,7 @@ class GpuVectorIndex:
         check(self._lib.gvdb_index_create(C.byref(p), C.byref(h)))
         self._h = h
         self.device = device
+        self._threshold = threshold
         self.params = params or SearchParams()
         self._id_of: dict = {}       # str -> u64
         self._str_of: List[str] = []  # u64 -> str
@@ -466,7 +467,11 @@ class GpuVectorIndex:
     def load_index(self, path: str, batch: int = 1 << 16) -> "PersistMetadata":
         """query.rs:335-409: read the file, check its dimension against this
         index's (DimensionMismatch), then replace the contents with its
-        vectors in file order.  Returns the stored metadata."""
+        vectors in file order.  Returns the stored metadata.  The file is
+        decoded into a staging index first and swapped in only after its last
+        entry and the gzip trailer are read, so a truncated or corrupt file
+        leaves this index as it was (the reference decodes the whole file
+        before touching the index, query.rs:355-373)."""
         m = _ffi.gvdb_persist_meta()
         cnt = C.c_uint64()
         r = C.c_void_p()
@@ -476,8 +481,8 @@ class GpuVectorIndex:
             mine = self.get_stats().dimension
             if mine and mine != D:
                 raise DimensionMismatch(f"Dimension mismatch: expected {mine}, actual {D}", mine, D)
-            self.clear()
-            self._id_of, self._str_of = {}, []
+            stage = GpuVectorIndex(dimension=0, threshold=self._threshold, device=self.device,
+                                   capacity_hint=int(cnt.value), params=self.params)
             rows = np.empty((batch, D), np.float32)
             offs = np.empty(batch + 1, np.uint64)
             cap = batch * 64
@@ -490,9 +495,14 @@ class GpuVectorIndex:
                     break
                 raw = blob.raw
                 names = [raw[int(offs[i]):int(offs[i + 1])].decode() for i in range(n)]
-                self.add_batch(np.array([self._u64(x) for x in names], np.uint64), rows[:n])
+                stage.add_batch(np.array([stage._u64(x) for x in names], np.uint64), rows[:n])
         finally:
             self._lib.gvdb_persist_free(r)
+        # swap: this object takes the staged index, the staging object the old one
+        self._h, stage._h = stage._h, self._h
+        self._id_of, stage._id_of = stage._id_of, self._id_of
+        self._str_of, stage._str_of = stage._str_of, self._str_of
+        del stage
         return PersistMetadata(int(m.dimension), int(m.total_points), m.created_at.decode(),
                                HnswConfig(int(m.m), int(m.ef_construction), int(m.ef_search), int(m.max_layers)))
 

@@ -194,6 +194,35 @@ def test_errors(gvdb_lib_path, tmp_path):
         check(L.gvdb_persist_close(w))
 
 
+def test_gzip_trailer_is_checked(gvdb_lib_path, tmp_path):
+    """A CRC-32 mismatch in the gzip trailer is a zlib error reported as
+    Storage (GzDecoder::read_to_end verifies the trailer), not a truncation."""
+    from gvdb import StorageError
+
+    L = _lib(gvdb_lib_path)
+    path = str(tmp_path / "crc.bin")
+    po.write_file(path, po.encode(4, 2, "t", (1, 2, 3, 4), [("a", [1, 2, 3, 4]), ("b", [5, 6, 7, 8])]))
+    raw = bytearray(open(path, "rb").read())
+    raw[-8] ^= 0xFF  # first byte of the CRC-32
+    open(path, "wb").write(bytes(raw))
+    with pytest.raises(StorageError) as e:
+        _read(L, path)
+    assert "truncated" not in str(e.value)
+
+
+def test_append_checks_header_dimension(gvdb_lib_path, tmp_path):
+    from gvdb import DimensionMismatch, check
+
+    L = _lib(gvdb_lib_path)
+    w = C.c_void_p()
+    check(L.gvdb_persist_create(str(tmp_path / "d.bin").encode(), C.byref(_meta(4, 1)), 1, -1, C.byref(w)))
+    rows = np.zeros((1, 3), np.float32)
+    offs = np.array([0, 1], np.uint64)
+    with pytest.raises(DimensionMismatch):
+        check(L.gvdb_persist_append(w, rows.ctypes.data, 1, 3, b"a", offs.ctypes.data))
+    L.gvdb_persist_close(w)
+
+
 def test_large_payload_streams(gvdb_lib_path, tmp_path):
     # > 64 MiB of postcard payload: several writer flushes and reader refills
     L = _lib(gvdb_lib_path)
@@ -253,3 +282,32 @@ def test_gpu_save_load_round_trip(tmp_path):
     assert s1.tobytes() == s2.tobytes()
     with pytest.raises(gvdb.DimensionMismatch):
         gvdb.GpuVectorIndex(dimension=D + 1).load_index(path)
+
+
+@pytest.mark.gpu
+def test_gpu_failed_load_leaves_index_intact(tmp_path):
+    """load_index decodes into a staging index: a truncated file raises
+    Storage and the index keeps its previous contents (query.rs:355-373 decodes
+    the whole file before it touches the index)."""
+    import gvdb
+
+    rng = np.random.default_rng(12)
+    D = 32
+    rows = rng.standard_normal((300, D)).astype(np.float32)
+    ix = gvdb.GpuVectorIndex(dimension=D)
+    ix.add_vectors([(f"k{i}", rows[i]) for i in range(300)])
+    good = str(tmp_path / "good.gvdb")
+    ix.save_index(good)
+    full = po.read_file(good)
+    bad = str(tmp_path / "bad.gvdb")
+    po.write_file(bad, full[: len(full) * 2 // 3])
+    ix2 = gvdb.GpuVectorIndex(dimension=D)
+    ix2.add_vectors([("keep-me", rows[0]), ("and-me", rows[1])])
+    before = ix2.get_all_vectors()
+    with pytest.raises(gvdb.StorageError):
+        ix2.load_index(bad)
+    after = ix2.get_all_vectors()
+    assert [s for s, _ in after] == [s for s, _ in before] == ["and-me", "keep-me"]
+    assert ix2.search(rows[1], 1)[0][0] == "and-me"
+    ix2.load_index(good)  # a good file still loads afterwards
+    assert ix2.len() == 300
