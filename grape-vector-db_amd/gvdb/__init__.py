@@ -31,6 +31,7 @@ __all__ = [
     "VectorDbError", "IndexNotBuilt", "DimensionMismatch", "InvalidVectorDimension", "QuantizationError",
     "IndexError_", "DeviceError", "BinaryQuantizationConfig", "BinaryVector", "BinaryQuantizer",
     "IndexStats", "GpuVectorIndex", "HnswVectorIndex", "SearchParams", "flat_search", "topk_merge", "lib",
+    "BinaryVectorStore", "QueryEngineConfig", "QueryEngine",
 ]
 
 
@@ -228,6 +229,50 @@ class BinaryQuantizer:
 
     def get_cache_stats(self):
         return {"enabled": self.config.enable_cache, "size": 0, "capacity": 10000 if self.config.enable_cache else 0}
+
+
+class BinaryVectorStore:
+    """quantization.rs:286-354: BinaryVectors with their string ids, plus the
+    reference's validation and memory accounting.  Host-side bookkeeping: the
+    GPU layout of the same codes is the word-major SoA plane set of a
+    GpuVectorIndex; :meth:`to_index` builds one."""
+
+    def __init__(self, config: Optional[BinaryQuantizationConfig] = None):
+        self.config = config or BinaryQuantizationConfig()
+        self.vectors: List[BinaryVector] = []
+        self.metadata: List[str] = []
+
+    def add_vector(self, vector: BinaryVector, id: str) -> None:  # 306-310
+        self.vectors.append(vector)
+        self.metadata.append(id)
+
+    def get_vector(self, index: int) -> Optional[BinaryVector]:  # 313-315 (Option<&BinaryVector>)
+        return self.vectors[index] if 0 <= index < len(self.vectors) else None
+
+    def len(self) -> int:
+        return len(self.vectors)
+
+    def __len__(self) -> int:
+        return len(self.vectors)
+
+    def is_empty(self) -> bool:
+        return not self.vectors
+
+    def get_config(self) -> BinaryQuantizationConfig:
+        return self.config
+
+    def validate_vector(self, vector: BinaryVector) -> None:  # 333-347
+        if vector.dimension == 0:
+            raise InvalidVectorDimension("binary vector of dimension 0")
+
+    def memory_usage(self) -> int:  # 350-353: code bytes + id bytes (UTF-8 length of a Rust String)
+        return sum(v.byte_size() for v in self.vectors) + sum(len(m.encode()) for m in self.metadata)
+
+    def multi_stage_search(self, query_binary: BinaryVector, original_query: Sequence[float],
+                           original_candidates) -> List[Tuple[int, float]]:
+        """BinaryQuantizer::multi_stage_search over this store's codes (GPU)."""
+        return BinaryQuantizer(self.config).multi_stage_search(query_binary, self.vectors, original_query,
+                                                               original_candidates)
 
 
 # ---------------------------------------------------------------------------
@@ -542,6 +587,55 @@ def utc_now_rfc3339() -> str:
 
 
 HnswVectorIndex = GpuVectorIndex
+
+
+@dataclass
+class QueryEngineConfig:
+    """query_engine.rs:9-32 (defaults 24-32)."""
+    default_limit: int = 10
+    default_threshold: float = 0.7
+    text_weight: float = 0.3
+    enable_cache: bool = True
+    cache_size: int = 1000
+
+
+class QueryEngine:
+    """query_engine.rs:117-147 ``vector_search``: limit defaults to 10 and the
+    threshold to 0.7, then the store's exact cosine search keeps scores >=
+    threshold, descending, truncated to limit (storage.rs:296-339).  Here the
+    store is a GPU index searched exactly (GVDB_SEARCH_FLAT, cosine): its top
+    ``limit`` filtered by the threshold is the same list, since scores that
+    pass form a prefix of the descending order.  Results are cached per
+    (query bits, limit, threshold) like the reference's cache (query_engine.rs:126-145)."""
+
+    def __init__(self, index: GpuVectorIndex, config: Optional[QueryEngineConfig] = None):
+        self.index = index
+        self.config = config or QueryEngineConfig()
+        self._cache: "dict" = {}
+
+    def vector_search(self, query_vector: Sequence[float], limit: Optional[int] = None,
+                      threshold: Optional[float] = None) -> List[Tuple[str, float]]:
+        limit = self.config.default_limit if limit is None else int(limit)
+        thr = np.float32(self.config.default_threshold if threshold is None else threshold)
+        q = _f32(query_vector).reshape(1, -1)
+        key = (q.tobytes(), limit, float(thr))
+        if self.config.enable_cache and key in self._cache:
+            return list(self._cache[key])
+        if limit == 0:
+            out: List[Tuple[str, float]] = []
+        else:
+            ids, sc, n = self.index.search_batch(q, limit, SearchParams(mode=_ffi.GVDB_SEARCH_FLAT,
+                                                                        metric=_ffi.GVDB_METRIC_COSINE))
+            out = [(self.index._str_of[int(ids[0, i])], float(sc[0, i])) for i in range(int(n[0]))
+                   if np.float32(sc[0, i]) >= thr]
+        if self.config.enable_cache:
+            if len(self._cache) >= self.config.cache_size:
+                self._cache.pop(next(iter(self._cache)))
+            self._cache[key] = list(out)
+        return out
+
+    def clear_cache(self) -> None:
+        self._cache.clear()
 
 
 # ---------------------------------------------------------------------------
