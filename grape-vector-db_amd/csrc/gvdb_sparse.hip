@@ -6,26 +6,34 @@
 //     BM25Parameters k1 = 1.2, b = 0.75 (49-53);
 //   * HybridSearchEngine::rrf_fusion (src/hybrid.rs:422-488).
 //
-// Layout in HBM: a document-major forward index (CSR over document SLOTS,
-// slot = first add of a document id): ptr[u64 N+1], term[u32 nnz], tf[f32],
-// dl[f32] (dl per entry: a re-added id carries each add's document_length).
-// A slot's entries are sorted by (term, add order), so the k-th entry of a
-// term in a slot is the slot's k-th occurrence in that term's posting list.
+// Layout in HBM.  The host keeps the authoritative document-major CSR over
+// document SLOTS (slot = first add of a document id; a slot's entries sorted
+// by (term, add order)), mirrored to the device as ptr / term / tf / dl.  From
+// it the device builds, whenever the index changed, the term-major INVERTED
+// index the reference searches (sparse.rs:167-190): per term one posting run
+// of (slot u32, tf f32, dl f32) in SoA arrays, slots ascending (a re-added id's
+// entries adjacent, in add order).  A stable radix sort of the entries by
+// term gives exactly that order.
 //
-// Search = document-at-a-time over the forward index for a batch of queries
-// (the reference walks postings term-at-a-time into a HashMap; per document
-// the contributions are added in query-term order either way, so the sums are
-// bit-identical):  for every (document, query) pair a lane binary-searches
-// each query term among the document's terms (staged in LDS per 64-document
-// tile) and folds  acc = acc + (q_tf * tfc) * idf  in query order, exactly the
-// reference's f32 expression (no FMA: -ffp-contract=off).  idf is computed on
-// the host per (query, term) with the same logf the Rust f32::ln calls.
-// Selection: a sample pass scores every `every`-th tile and the k-th largest
-// sampled key (score, then slot ascending) is a lower bound tau of the k-th
-// best key (k documents reach it); the emit pass keeps documents with
-// key >= tau (~k * every of them), an LDS sort orders them.  Exact for every
-// input: a query whose candidates overflow the buffer is answered by a dense
-// key array + radix sort.
+// Search = term-at-a-time, as the reference, over document CHUNKS of 128
+// slots.  Per launch group (<= 64 queries, <= 512 distinct terms):
+//   k_ta_dir     one pass over the group's posting runs records, per (chunk,
+//                term), the first and last posting inside the chunk;
+//   k_bm25_taat  per chunk: stage the chunk's postings of every group term in
+//                LDS (tf_component evaluated once per posting), then round r
+//                adds each query's r-th term into per-(query, slot) LDS
+//                accumulators.  Query q's rounds all run in wave q % 8, so a
+//                document's f32 sum folds its contributions in query-term
+//                order and, per term, in posting order: the reference's
+//                `*scores.entry(id).or_insert(0.0) += s`, bit for bit
+//                (no FMA: -ffp-contract=off; idf from the host's logf, the
+//                function Rust's f32::ln calls);
+//   selection    a sample pass (every `every`-th chunk) gives, per query, a
+//                lower bound tau of the limit-th best key (score, then slot
+//                ascending); the emit pass keeps keys >= tau, an LDS sort
+//                orders them.  Exact for every input: a query whose
+//                candidates overflow the buffer is answered from a dense key
+//                array + radix sort.
 //
 // Deterministic choices where the reference uses HashMap order (its results
 // vary run to run there): equal scores order by slot; avgdl's f32 fold runs
@@ -37,6 +45,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -50,14 +59,21 @@ using namespace gvdb;
 
 namespace {
 
-constexpr uint32_t kSpTile = 64;        // documents per tile (one per lane of a wave)
-constexpr uint32_t kSpThreads = 512;    // 8 query groups x 64 documents: 16 waves per CU at 2 blocks (the loop is latency-bound)
-constexpr uint32_t kSpEnt = 4096;       // staged term entries per tile (else read from HBM)
-constexpr uint32_t kSpQT = 1024;        // query terms per launch group (LDS)
-constexpr uint32_t kSpU = 512;          // distinct terms per launch group (LDS match map)
-constexpr uint32_t kSpMaxB = 256;       // queries per launch group
-constexpr uint32_t kSpCand = 4096;      // candidates per query (LDS sort)
-constexpr uint32_t kSpTopLocal = 8;     // per-thread keys kept by the tau pass
+constexpr uint32_t kTaCh = 128;                 // document slots per chunk (one LDS accumulator row per query)
+constexpr uint32_t kTaRow = kTaCh + 1;          // accumulator row stride: queries' rows start on different banks
+constexpr uint32_t kTaThreads = 512;            // 8 waves; wave w owns queries w, w + 8, ...
+constexpr uint32_t kTaWaves = kTaThreads / 64;
+constexpr uint32_t kTaQ = 64;                   // queries per launch group (<= 8 per wave)
+constexpr uint32_t kTaStage = 4096;             // postings staged per chunk (more: read from HBM in the rounds)
+constexpr uint32_t kTaGrp = 8;                  // sample pass: one max key per 8 slots
+constexpr uint32_t kTaSent = 0x7fbadbadu;       // "no posting yet": a signalling NaN, never an arithmetic result
+constexpr uint32_t kSpQT = 1024;                // query terms per launch group (LDS)
+constexpr uint32_t kSpU = 512;                  // distinct terms per launch group
+constexpr uint32_t kSpCand = 4096;              // candidates per query (LDS sort)
+constexpr uint32_t kSpTopLocal = 8;             // per-thread keys kept by the tau pass
+static_assert(kSpU <= kTaThreads, "one thread per group term in the directory row");
+static_assert(kTaQ <= kTaWaves * 8, "a wave's queries sit in lanes 0..7");
+static_assert(kTaCh <= 256, "staged slots are bytes");
 
 // total order of a BM25 score (NaN lowest: 0), then slot ascending
 __device__ __forceinline__ uint64_t sp_key(float s, uint32_t slot) {
@@ -72,197 +88,312 @@ __device__ __forceinline__ float sp_score(uint64_t key) {
 }
 __device__ __forceinline__ uint32_t sp_slot(uint64_t key) { return ~(uint32_t)key; }
 
-struct SpArgs {
-    const uint64_t* ptr;   // [N+1]
-    const uint32_t* term;  // [nnz]
-    const float* tf;
-    const float* dl;
-    uint32_t N;            // slots
-    const uint32_t* qp;    // [B+1] offsets into qb/qv/qidf
-    const uint16_t* qb;    // index of each query term in ut
-    const uint32_t* ut;    // the group's distinct live terms, ascending
+// ---------------------------------------------------------------------------
+// inverted index build: entries sorted (stable) by term -> posting runs
+// ---------------------------------------------------------------------------
+__global__ void k_inv_prep(const uint64_t* __restrict__ ptr, uint32_t N, uint32_t* __restrict__ eslot,
+                           uint32_t* __restrict__ iota) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= N) return;
+    for (uint64_t e = ptr[s], e1 = ptr[s + 1]; e < e1; ++e) {
+        eslot[e] = s;
+        iota[e] = (uint32_t)e;
+    }
+}
+
+__global__ void k_inv_gather(const uint32_t* __restrict__ order, const uint32_t* __restrict__ eslot,
+                             const float* __restrict__ tf, const float* __restrict__ dl, uint64_t E,
+                             uint32_t* __restrict__ pslot, float* __restrict__ ptf, float* __restrict__ pdl) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t e = order[i];
+        pslot[i] = eslot[e];
+        ptf[i] = tf[e];
+        pdl[i] = dl[e];
+    }
+}
+
+struct TaArgs {
+    const uint32_t* pslot;  // inverted index: posting slot / tf / document_length
+    const float* ptf;
+    const float* pdl;
+    uint32_t N;             // slots
+    uint32_t nchunks;
+    const uint64_t* toff;   // [nu] first posting of each group term
+    const uint64_t* gpre;   // [nu+1] prefix of the group terms' posting counts (directory pass)
+    uint32_t* first;        // [nchunks][nu] first / last posting (relative to toff) inside a chunk
+    uint32_t* last;
     uint32_t nu;
+    const uint32_t* qp;     // [B+1] offsets into qb/qv/qidf
+    const uint16_t* qb;     // group-term index of each query term
     const float* qv;
     const float* qidf;
     uint32_t B;
     float k1, b, avgdl;
-    uint32_t every;        // sample pass: tile stride
-    uint64_t* smp;         // sample: [B][S] keys (0 = unmatched)
+    uint32_t every;         // sample pass: chunk stride
+    uint64_t* smp;          // sample: [B][S] keys (0 = unmatched)
     uint32_t S;
-    const uint64_t* tau;   // emit: [B]
-    uint32_t* counts;      // emit: [B]
-    uint64_t* cand;        // emit: [B][kSpCand]
-    uint64_t* dense;       // dense mode: [N] keys of query `dense_q`
+    const uint64_t* tau;    // emit: [B]
+    uint32_t* counts;       // emit: [B]
+    uint64_t* cand;         // emit: [B][kSpCand]
+    uint64_t* dense;        // dense mode: [N] keys of query `dense_q`
     uint32_t dense_q;
 };
 
-// MODE 0: sample (every `every`-th tile -> smp), 1: emit (key >= tau ->
-// cand), 2: dense keys of one query.
-// Per 64-document tile: the documents' term lists are staged in LDS, then a
-// (document x batch-term) match map is built -- each entry looks its term up
-// once among the batch's distinct terms `ut` (sorted, <= kSpU) and records its
-// position (first entry of a run; 255 = "search", for documents past 254
-// entries).  Scoring a (document, query) pair is then one LDS byte per query
-// term instead of a binary search.
+// Directory: one thread per posting of the group's terms; the posting that
+// opens (closes) a chunk's run writes first (last).  `first` is preset to
+// ~0 = "no posting of the term in the chunk".
+__global__ __launch_bounds__(256) void k_ta_dir(TaArgs a) {
+    __shared__ uint64_t s_pre[kSpU + 1];
+    const uint32_t nu = a.nu;
+    for (uint32_t i = threadIdx.x; i <= nu; i += 256u) s_pre[i] = a.gpre[i];
+    __syncthreads();
+    const uint64_t P = s_pre[nu];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < P; i += (uint64_t)gridDim.x * 256u) {
+        uint32_t lo = 0, hi = nu;  // the last term whose run starts at or before i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= i) lo = mid; else hi = mid;
+        }
+        const uint32_t j = (uint32_t)(i - s_pre[lo]);
+        const uint32_t len = (uint32_t)(s_pre[lo + 1] - s_pre[lo]);
+        const uint32_t* run = a.pslot + a.toff[lo];
+        const uint32_t c = run[j] / kTaCh;
+        const uint32_t pc = j ? run[j - 1] / kTaCh : 0xffffffffu;
+        const uint32_t nc = j + 1 < len ? run[j + 1] / kTaCh : 0xffffffffu;
+        if (c != pc) a.first[(uint64_t)c * nu + lo] = j;
+        if (c != nc) a.last[(uint64_t)c * nu + lo] = j;
+    }
+}
+
+// MODE 0: sample (every `every`-th chunk -> per 8 slots the max key -> smp),
+// 1: emit (key >= tau -> cand), 2: dense keys of query `dense_q`.
 template <int MODE>
-__global__ __launch_bounds__(kSpThreads, 2) void k_bm25(SpArgs a) {
-    __shared__ uint32_t s_qp[kSpMaxB + 1];
-    __shared__ uint64_t s_tau[MODE == 1 ? kSpMaxB : 1];  // emit thresholds, staged once
+__global__ __launch_bounds__(kTaThreads, 2) void k_bm25_taat(TaArgs a) {
+    __shared__ float s_acc[kTaQ * kTaRow];
+    __shared__ uint32_t s_qp[kTaQ + 1];
     __shared__ uint16_t s_qb[kSpQT];
     __shared__ float s_qv[kSpQT], s_qidf[kSpQT];
-    __shared__ uint32_t s_ut[kSpU];
-    __shared__ uint32_t s_ent[kSpEnt];
-    __shared__ float s_tfc[kSpEnt];  // tf_component of each staged entry (query-independent)
-    __shared__ uint32_t s_dp[kSpTile + 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_map[kSpTile * kSpU];
-    const uint32_t tid = threadIdx.x, doc = tid & (kSpTile - 1), qg = tid / kSpTile;
+    __shared__ uint64_t s_tau[MODE == 1 ? kTaQ : 1];
+    __shared__ uint32_t s_n[kSpU], s_soff[kSpU + 1];
+    __shared__ uint64_t s_pf[kSpU];
+    __shared__ uint32_t s_wsum[kTaWaves];
+    __shared__ uint8_t st_slot[kTaStage];
+    __shared__ float st_tfc[kTaStage];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t B = a.B, nu = a.nu;
-    for (uint32_t i = tid; i <= B; i += kSpThreads) s_qp[i] = a.qp[i];
+    for (uint32_t i = tid; i <= B; i += kTaThreads) s_qp[i] = a.qp[i];
     if constexpr (MODE == 1)
-        for (uint32_t i = tid; i < B; i += kSpThreads) s_tau[i] = a.tau[i];
-    for (uint32_t i = tid; i < nu; i += kSpThreads) s_ut[i] = a.ut[i];
+        for (uint32_t i = tid; i < B; i += kTaThreads) s_tau[i] = a.tau[i];
     __syncthreads();
     const uint32_t nqt = s_qp[B];
-    for (uint32_t i = tid; i < nqt; i += kSpThreads) {
+    for (uint32_t i = tid; i < nqt; i += kTaThreads) {
         s_qb[i] = a.qb[i];
         s_qv[i] = a.qv[i];
         s_qidf[i] = a.qidf[i];
     }
     const float k1 = a.k1, b = a.b, avgdl = a.avgdl;
     const float k1p1 = k1 + 1.0f, omb = 1.0f - b;  // (k1 + 1.0), (1.0 - b) as the reference evaluates them
-    const uint32_t ntiles_all = (a.N + kSpTile - 1) / kSpTile;
+    // calculate_bm25_score's tf_component (sparse.rs:215-218): per posting
+    auto tfc_of = [&](float tfv, float dlv) { return (tfv * k1p1) / (tfv + k1 * (omb + b * (dlv / avgdl))); };
+    // this wave's queries: lane m < 8 holds query wave + 8 m
+    const uint32_t myq = wave + kTaWaves * lane;
+    const bool has_q = lane < 8u && myq < B && (MODE != 2 || myq == a.dense_q);
     const uint32_t every = MODE == 0 ? a.every : 1u;
-    const uint32_t ntiles = (ntiles_all + every - 1) / every;
-    const uint32_t map_words = (kSpTile * nu + 3) / 4;
-    for (uint32_t j = blockIdx.x; j < ntiles; j += gridDim.x) {
-        const uint32_t d0 = j * every * kSpTile;
-        const uint32_t nd = min(kSpTile, a.N - d0);
-        __syncthreads();  // previous tile's LDS readers are done
-        if (tid <= nd) s_dp[tid] = (uint32_t)(a.ptr[d0 + tid] - a.ptr[d0]);
-        for (uint32_t i = tid; i < map_words; i += kSpThreads) ((uint32_t*)s_map)[i] = 0u;
+    const uint32_t nj = (a.nchunks + every - 1) / every;
+    for (uint32_t jj = blockIdx.x; jj < nj; jj += gridDim.x) {
+        const uint32_t c = jj * every, c0 = c * kTaCh;
+        __syncthreads();  // the previous chunk's readers are done (and the query tables are visible)
+        // directory row -> postings per group term in this chunk, staging offsets
+        uint32_t n = 0;
+        if (tid < nu) {
+            const uint64_t row = (uint64_t)c * nu + tid;
+            const uint32_t f = a.first[row];
+            uint64_t pf = 0;
+            if (f != 0xffffffffu) {
+                n = a.last[row] - f + 1u;
+                pf = a.toff[tid] + f;
+            }
+            s_n[tid] = n;
+            s_pf[tid] = pf;
+        }
+        uint32_t x = n;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wsum[wave] = x;
+        for (uint32_t i = tid; i < B * kTaRow; i += kTaThreads) s_acc[i] = __uint_as_float(kTaSent);
         __syncthreads();
-        const uint64_t base = a.ptr[d0];
-        const uint32_t E = s_dp[nd];
-        const bool staged = E <= kSpEnt;
-        // calculate_bm25_score's tf_component (sparse.rs:215-218) depends on the
-        // entry only: evaluated once per staged entry
-        auto tfc_of = [&](uint64_t g) {
-            const float tfv = a.tf[g], dlv = a.dl[g];
-            return (tfv * k1p1) / (tfv + k1 * (omb + b * (dlv / avgdl)));
-        };
+        uint32_t T = 0, wb = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kTaWaves; ++w) {
+            const uint32_t sw = s_wsum[w];
+            wb += w < wave ? sw : 0u;
+            T += sw;
+        }
+        if (tid < nu) s_soff[tid] = wb + x - n;
+        if (tid == 0) s_soff[nu] = T;
+        __syncthreads();
+        const bool staged = T <= kTaStage;
         if (staged) {
-            // all loads first (up to kSpEnt / kSpThreads per thread in flight),
-            // then the arithmetic: a load-compute-store loop would serialise
-            // one HBM latency per entry
-            constexpr uint32_t kPer = kSpEnt / kSpThreads;
-            uint32_t tv[kPer];
-            float fv[kPer], dv[kPer];
+            // all loads first (kPer per thread in flight), then the arithmetic
+            constexpr uint32_t kPer = kTaStage / kTaThreads;
+            uint32_t sv[kPer];
+            float tv[kPer], dv[kPer];
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k) {
-                const uint32_t i = tid + k * kSpThreads;
-                if (i < E) {
-                    tv[k] = a.term[base + i];
-                    fv[k] = a.tf[base + i];
-                    dv[k] = a.dl[base + i];
-                }
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kPer; ++k) {
-                const uint32_t i = tid + k * kSpThreads;
-                if (i < E) {
-                    s_ent[i] = tv[k];
-                    s_tfc[i] = (fv[k] * k1p1) / (fv[k] + k1 * (omb + b * (dv[k] / avgdl)));
-                }
-            }
-        }
-        __syncthreads();
-        auto term_at = [&](uint32_t e) { return staged ? s_ent[e] : a.term[base + e]; };
-        const bool live = doc < nd;
-        const uint32_t lo0 = live ? s_dp[doc] : 0u, hi0 = live ? s_dp[doc + 1] : 0u;
-        // match map: 8 threads per document walk its entries
-#ifndef BM_ABL
-#define BM_ABL 0
-#endif
-        for (uint32_t e = lo0 + qg; e < hi0 && !(BM_ABL & 1); e += kSpThreads / kSpTile) {
-            const uint32_t t = term_at(e);
-            if (e > lo0 && term_at(e - 1) == t) continue;  // not the first of a run (re-added id)
-            uint32_t lo = 0, hi = nu;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_ut[mid] < t) lo = mid + 1; else hi = mid;
-            }
-            if (lo < nu && s_ut[lo] == t) s_map[lo * kSpTile + doc] = (uint8_t)min(e - lo0 + 1u, 255u);
-        }
-        __syncthreads();
-        const uint32_t slot = d0 + doc;
-        const uint32_t qbeg = MODE == 2 ? a.dense_q : qg, qstep = MODE == 2 ? B + 1 : kSpThreads / kSpTile;
-        for (uint32_t q = qbeg; q < B && !(BM_ABL & 2); q += qstep) {
-            if (MODE == 2 && qg != 0) break;
-            float acc = 0.0f;
-            bool hit = false;
-            const uint32_t p0 = s_qp[q], p1 = s_qp[q + 1];
-            for (uint32_t pc = p0; pc < p1; pc += 8) {
-                // 8 map lookups in flight, then the contributions in query-term order
-                uint32_t vv[8];
-#pragma unroll
-                for (uint32_t i = 0; i < 8; ++i) {
-                    const bool in = pc + i < p1;
-                    const uint32_t ub = in ? s_qb[pc + i] : 0u;
-                    vv[i] = in && live ? ((uint32_t)s_map[ub * kSpTile + doc] | (ub << 8)) : 0u;
-                }
-                // fast path, all reads independent: a staged document whose
-                // entry for the term is the whole run (v < 255 and the next
-                // entry holds another term) contributes tf_component[e] once
-                float tf8[8];
-                bool one8[8];
-#pragma unroll
-                for (uint32_t i = 0; i < 8; ++i) {
-                    const uint32_t v = vv[i] & 255u;
-                    const uint32_t e = lo0 + (v ? v - 1 : 0);
-                    const bool cand = staged && v != 0 && v != 255;
-                    tf8[i] = cand ? s_tfc[e] : 0.0f;
-                    one8[i] = cand && (e + 1 >= hi0 || s_ent[e + 1] != s_ut[vv[i] >> 8]);
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < 8; ++i) {
-                    const uint32_t v = vv[i] & 255u;
-                    if (v == 0) continue;
-                    const uint32_t p = pc + i;
-                    if (one8[i]) {
-                        const float sc = s_qv[p] * tf8[i] * s_qidf[p];
-                        acc = hit ? acc + sc : 0.0f + sc;
-                        hit = true;
-                        continue;
+                const uint32_t i = tid + k * kTaThreads;
+                sv[k] = 0u;
+                tv[k] = dv[k] = 0.0f;
+                if (i < T) {
+                    uint32_t lo = 0, hi = nu;  // the last term whose staging range starts at or before i
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_soff[mid] <= i) lo = mid; else hi = mid;
                     }
-                    const uint32_t t = s_ut[vv[i] >> 8];
-                    uint32_t e = lo0 + v - 1;
-                    if (v == 255) {  // long document: lower_bound(t)
-                        uint32_t lo = lo0, hi = hi0;
-                        while (lo < hi) {
-                            const uint32_t mid = (lo + hi) >> 1;
-                            if (term_at(mid) < t) lo = mid + 1; else hi = mid;
+                    const uint64_t g = s_pf[lo] + (i - s_soff[lo]);
+                    sv[k] = a.pslot[g];
+                    tv[k] = a.ptf[g];
+                    dv[k] = a.pdl[g];
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint32_t i = tid + k * kTaThreads;
+                if (i < T) {
+                    st_slot[i] = (uint8_t)(sv[k] - c0);
+                    st_tfc[i] = tfc_of(tv[k], dv[k]);
+                }
+            }
+            __syncthreads();
+        }
+        // Rounds (sparse.rs:167-190): round r adds every query's r-th term.
+        // Items of a round = (query, posting) pairs over the wave's queries;
+        // distinct items touch distinct (query, slot) accumulators except a
+        // re-added document's adjacent postings, which the run's first item
+        // folds in order.
+        uint32_t qp0 = 0, qlen = 0;
+        if (has_q) {
+            qp0 = s_qp[myq];
+            qlen = s_qp[myq + 1] - qp0;
+        }
+        uint32_t rmax = qlen;
+#pragma unroll
+        for (uint32_t o = 1; o < 8; o <<= 1) rmax = max(rmax, (uint32_t)__shfl_xor(rmax, o));
+        rmax = __builtin_amdgcn_readfirstlane(rmax);
+        auto rounds = [&](auto staged_tag) {
+            constexpr bool ST = decltype(staged_tag)::value;
+            auto slot_at = [&](uint64_t i) -> uint32_t { return ST ? (uint32_t)st_slot[i] : a.pslot[i] - c0; };
+            auto tfc_at = [&](uint64_t i) -> float { return ST ? st_tfc[i] : tfc_of(a.ptf[i], a.pdl[i]); };
+            for (uint32_t r = 0; r < rmax; ++r) {
+                uint32_t cnt = 0;
+                uint64_t base = 0;
+                float v = 0.0f, idf = 0.0f;
+                if (r < qlen) {
+                    const uint32_t p = qp0 + r, u = s_qb[p];
+                    cnt = s_n[u];
+                    base = ST ? (uint64_t)s_soff[u] : s_pf[u];
+                    v = s_qv[p];
+                    idf = s_qidf[p];
+                }
+                uint32_t inc = cnt;
+#pragma unroll
+                for (uint32_t o = 1; o < 8; o <<= 1) {
+                    const uint32_t y = __shfl_up(inc, o);
+                    if (lane >= o) inc += y;
+                }
+                uint32_t e[8];
+#pragma unroll
+                for (uint32_t m = 0; m < 8; ++m) e[m] = __builtin_amdgcn_readlane(inc, m);
+                const uint32_t tot = e[7];
+                const uint32_t base_lo = (uint32_t)base, base_hi = (uint32_t)(base >> 32);
+                constexpr uint32_t kU = 4;
+                for (uint32_t it0 = 0; it0 < tot; it0 += 64u * kU) {
+                    uint32_t ap[kU], jx[kU], cm[kU], sl[kU];
+                    uint64_t ix[kU];
+                    float vm[kU], dm[kU], tf[kU], ac[kU];
+                    bool ok[kU];
+#pragma unroll
+                    for (uint32_t u = 0; u < kU; ++u) {
+                        const uint32_t it = it0 + u * 64u + lane;
+                        uint32_t m = 0, start = 0;
+#pragma unroll
+                        for (uint32_t mm = 0; mm < 7; ++mm)
+                            if (it >= e[mm]) {
+                                m = mm + 1;
+                                start = e[mm];
+                            }
+                        jx[u] = it - start;
+                        cm[u] = __shfl(cnt, m);
+                        vm[u] = __shfl(v, m);
+                        dm[u] = __shfl(idf, m);
+                        const uint64_t bm = (uint64_t)(uint32_t)__shfl(base_lo, m) |
+                                            ((uint64_t)(uint32_t)__shfl(base_hi, m) << 32);
+                        ix[u] = bm + jx[u];
+                        ok[u] = it < tot;
+                        ap[u] = (wave + kTaWaves * m) * kTaRow;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < kU; ++u) {
+                        sl[u] = ok[u] ? slot_at(ix[u]) : 0u;
+                        const uint32_t prev = ok[u] && jx[u] > 0 ? slot_at(ix[u] - 1) : 0xffffffffu;
+                        ok[u] = ok[u] && prev != sl[u];  // not the first of a re-added document's run: folded by it
+                        tf[u] = ok[u] ? tfc_at(ix[u]) : 0.0f;
+                        ap[u] += sl[u];
+                        ac[u] = ok[u] ? s_acc[ap[u]] : 0.0f;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < kU; ++u) {
+                        if (!ok[u]) continue;
+                        // calculate_bm25_score: query_tf * tf_component * idf;
+                        // `or_insert(0.0) += s`: the first contribution is 0.0 + s
+                        float acc = ac[u];
+                        const float s0 = vm[u] * tf[u] * dm[u];
+                        acc = __float_as_uint(acc) == kTaSent ? 0.0f + s0 : acc + s0;
+                        for (uint32_t t = jx[u] + 1; t < cm[u] && slot_at(ix[u] - jx[u] + t) == sl[u]; ++t) {
+                            const float s1 = vm[u] * tfc_at(ix[u] - jx[u] + t) * dm[u];
+                            acc = acc + s1;
                         }
-                        e = lo;
-                    }
-                    for (; e < hi0 && term_at(e) == t; ++e) {
-                        const float tfc = staged ? s_tfc[e] : tfc_of(base + e);
-                        // calculate_bm25_score (sparse.rs:206-222): query_tf * tf_component * idf
-                        const float sc = s_qv[p] * tfc * s_qidf[p];
-                        acc = hit ? acc + sc : 0.0f + sc;  // or_insert(0.0) += s
-                        hit = true;
+                        s_acc[ap[u]] = acc;
                     }
                 }
             }
-            const uint64_t key = hit && live ? sp_key(acc, slot) : 0ull;
-            if (MODE == 0) {
-                a.smp[(uint64_t)q * a.S + (uint64_t)j * kSpTile + doc] = key;
-            } else if (MODE == 1) {
-                if (key != 0 && key >= s_tau[q]) {
+        };
+        if (staged)
+            rounds(std::true_type{});
+        else
+            rounds(std::false_type{});
+        __syncthreads();
+        if constexpr (MODE == 0) {
+            constexpr uint32_t G = kTaCh / kTaGrp;
+            for (uint32_t i = tid; i < B * G; i += kTaThreads) {
+                const uint32_t q = i / G, g = i % G;
+                uint64_t best = 0;
+#pragma unroll
+                for (uint32_t s = 0; s < kTaGrp; ++s) {
+                    const uint32_t slot = g * kTaGrp + s;
+                    const float f = s_acc[q * kTaRow + slot];
+                    if (__float_as_uint(f) != kTaSent) best = max(best, sp_key(f, c0 + slot));
+                }
+                a.smp[(uint64_t)q * a.S + (uint64_t)jj * G + g] = best;
+            }
+        } else if constexpr (MODE == 1) {
+            for (uint32_t i = tid; i < B * kTaCh; i += kTaThreads) {
+                const uint32_t q = i / kTaCh, slot = i % kTaCh;
+                const float f = s_acc[q * kTaRow + slot];
+                if (__float_as_uint(f) == kTaSent) continue;
+                const uint64_t key = sp_key(f, c0 + slot);
+                if (key >= s_tau[q]) {
                     const uint32_t pos = atomicAdd(&a.counts[q], 1u);
                     if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key;
                 }
-            } else {
-                if (live) a.dense[slot] = key;
+            }
+        } else {
+            for (uint32_t slot = tid; slot < kTaCh; slot += kTaThreads) {
+                if (c0 + slot >= a.N) continue;
+                const float f = s_acc[a.dense_q * kTaRow + slot];
+                a.dense[c0 + slot] = __float_as_uint(f) == kTaSent ? 0ull : sp_key(f, c0 + slot);
             }
         }
     }
@@ -280,14 +411,21 @@ __global__ __launch_bounds__(256) void k_bm25_tau(const uint64_t* __restrict__ s
 #pragma unroll
     for (uint32_t i = 0; i < kSpTopLocal; ++i) top[i] = 0;
     const uint64_t* src = smp + (uint64_t)q * S;
-    for (uint32_t i = tid; i < S; i += 256u) {
-        uint64_t k = src[i];
-        if (k <= top[kSpTopLocal - 1]) continue;
+    constexpr uint32_t kIn = 8;  // loads in flight per thread
+    for (uint32_t i0 = tid; i0 < S; i0 += 256u * kIn) {
+        uint64_t kv[kIn];
 #pragma unroll
-        for (uint32_t j = 0; j < kSpTopLocal; ++j) {
-            const uint64_t hi = k > top[j] ? k : top[j], lo = k > top[j] ? top[j] : k;
-            top[j] = hi;
-            k = lo;
+        for (uint32_t u = 0; u < kIn; ++u) kv[u] = i0 + u * 256u < S ? src[i0 + u * 256u] : 0ull;
+#pragma unroll
+        for (uint32_t u = 0; u < kIn; ++u) {
+            uint64_t k = kv[u];
+            if (k <= top[kSpTopLocal - 1]) continue;
+#pragma unroll
+            for (uint32_t j = 0; j < kSpTopLocal; ++j) {
+                const uint64_t hi = k > top[j] ? k : top[j], lo = k > top[j] ? top[j] : k;
+                top[j] = hi;
+                k = lo;
+            }
         }
     }
 #pragma unroll
@@ -349,12 +487,34 @@ __global__ void k_bm25_emit_dense(const uint64_t* __restrict__ sorted, uint32_t 
 
 // ---------------------------------------------------------------------------
 // RRF (hybrid.rs:422-488), one block per query.  Items = the three lists
-// concatenated (dense, sparse, text); the first occurrence of an id owns it.
-// score: the LAST dense occurrence (HashMap::insert replaces) or else the
-// first other occurrence, then += every later sparse / text occurrence in
-// order; ties by first appearance.
+// concatenated (dense, sparse, text).  An LDS sort of (id, item index) makes
+// every id's occurrences one run in list order; the run's first item owns the
+// document: score = the LAST dense occurrence's 1/(k + rank + 1) (HashMap::
+// insert replaces) or else the first other occurrence's, then += every later
+// sparse / text occurrence in order; ties by first appearance.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kRrfMax = 1024;  // items per query (LDS)
+constexpr uint32_t kRrfMax = 4096;  // items per query (dynamic LDS: 24 B per item)
+
+__device__ void bitonic_pairs_lds(uint64_t* id, uint16_t* ix, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t p = threadIdx.x; p < P / 2; p += blockDim.x) {
+                const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                const uint32_t hi = lo | j;
+                const uint64_t a = id[lo], b = id[hi];
+                const uint16_t ia = ix[lo], ib = ix[hi];
+                const bool gt = a > b || (a == b && ia > ib);
+                if (gt == ((lo & k) == 0)) {
+                    id[lo] = b;
+                    id[hi] = a;
+                    ix[lo] = ib;
+                    ix[hi] = ia;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
 
 __global__ __launch_bounds__(256) void k_rrf(const uint64_t* __restrict__ ids0, const float* __restrict__ sc0,
                                              const uint32_t* __restrict__ n0, uint32_t st0,
@@ -362,73 +522,81 @@ __global__ __launch_bounds__(256) void k_rrf(const uint64_t* __restrict__ ids0, 
                                              const uint32_t* __restrict__ n1, uint32_t st1,
                                              const uint64_t* __restrict__ ids2, const float* __restrict__ sc2,
                                              const uint32_t* __restrict__ n2, uint32_t st2, float k, uint32_t limit,
-                                             uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
-                                             float* __restrict__ out_raw, uint32_t* __restrict__ out_n) {
-    __shared__ uint64_t s_id[kRrfMax];
-    __shared__ float s_raw[kRrfMax];
-    __shared__ float s_score[kRrfMax];
-    __shared__ float s_bd[3][kRrfMax];
-    __shared__ uint64_t s_key[kRrfMax];
+                                             uint32_t pmax, uint64_t* __restrict__ out_ids,
+                                             float* __restrict__ out_scores, float* __restrict__ out_raw,
+                                             uint32_t* __restrict__ out_n) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t rrf_lds[];
+    uint64_t* s_id = rrf_lds;                     // [pmax] item ids, sorted with their item index
+    uint64_t* s_key = s_id + pmax;                // [pmax] (score desc, owner item) per document
+    float* s_sc = (float*)(s_key + pmax);         // [pmax] fused score, at the owner item
+    uint16_t* s_ix = (uint16_t*)(s_sc + pmax);    // [pmax] item index of s_id
+    uint16_t* s_run = s_ix + pmax;                // [pmax] owner item -> its run in s_id
     __shared__ uint32_t s_cnt;
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
     const uint32_t a = n0 ? min(n0[q], st0) : 0u, b = n1 ? min(n1[q], st1) : 0u, c = n2 ? min(n2[q], st2) : 0u;
-    const uint32_t n = min(a + b + c, kRrfMax);
-    for (uint32_t i = tid; i < n; i += 256u) {
-        const uint32_t l = i < a ? 0u : i < a + b ? 1u : 2u;
-        const uint32_t r = l == 0 ? i : l == 1 ? i - a : i - a - b;
-        s_id[i] = l == 0 ? ids0[(uint64_t)q * st0 + r] : l == 1 ? ids1[(uint64_t)q * st1 + r] : ids2[(uint64_t)q * st2 + r];
-        s_raw[i] = l == 0 ? sc0[(uint64_t)q * st0 + r] : l == 1 ? sc1[(uint64_t)q * st1 + r] : sc2[(uint64_t)q * st2 + r];
+    const uint32_t n = a + b + c;  // <= pmax (host: sum of strides)
+    auto list_of = [&](uint32_t i) { return i < a ? 0u : i < a + b ? 1u : 2u; };
+    auto rank_of = [&](uint32_t i) { return i < a ? i : i < a + b ? i - a : i - a - b; };
+    auto raw_of = [&](uint32_t i) {
+        const uint32_t l = list_of(i), r = rank_of(i);
+        return l == 0 ? sc0[(uint64_t)q * st0 + r] : l == 1 ? sc1[(uint64_t)q * st1 + r] : sc2[(uint64_t)q * st2 + r];
+    };
+    auto rrf = [&](uint32_t i) { return 1.0f / (k + (float)(rank_of(i) + 1u)); };  // 1.0 / (k + (rank + 1) as f32)
+    const uint32_t P = next_pow2(n < 2u ? 2u : n);
+    for (uint32_t i = tid; i < P; i += 256u) {
+        uint64_t id = ~0ull;
+        if (i < n) {
+            const uint32_t l = list_of(i), r = rank_of(i);
+            id = l == 0 ? ids0[(uint64_t)q * st0 + r] : l == 1 ? ids1[(uint64_t)q * st1 + r] : ids2[(uint64_t)q * st2 + r];
+        }
+        s_id[i] = id;
+        s_ix[i] = i < n ? (uint16_t)i : (uint16_t)0xffffu;
     }
     if (tid == 0) s_cnt = 0;
     __syncthreads();
-    auto rrf = [&](uint32_t i) {  // 1.0 / (k + (rank + 1) as f32)
-        const uint32_t r = i < a ? i : i < a + b ? i - a : i - a - b;
-        return 1.0f / (k + (float)(r + 1u));
-    };
-    for (uint32_t i = tid; i < n; i += 256u) {
-        bool owner = true;
-        for (uint32_t j = 0; j < i && owner; ++j) owner = s_id[j] != s_id[i];
-        if (!owner) continue;
-        const uint64_t id = s_id[i];
+    bitonic_pairs_lds(s_id, s_ix, P);
+    for (uint32_t p = tid; p < n; p += 256u) {
+        const uint64_t id = s_id[p];
+        if (p > 0 && s_id[p - 1] == id) continue;  // not the first occurrence
+        uint32_t t = p;
         int32_t last_dense = -1;  // dense: HashMap::insert replaces (hybrid.rs:432-445)
-        for (uint32_t j = 0; j < a; ++j)
-            if (s_id[j] == id) last_dense = (int32_t)j;
+        for (; t < n && s_id[t] == id && s_ix[t] < a; ++t) last_dense = s_ix[t];
         float score = 0.0f;
         bool have = false;
-        float bd[3] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
         if (last_dense >= 0) {
             score = rrf((uint32_t)last_dense);
-            bd[0] = s_raw[last_dense];
             have = true;
         }
-        for (uint32_t j = a; j < n; ++j) {  // sparse, then text: insert or += (447-478)
-            if (s_id[j] != id) continue;
-            const float r = rrf(j);
+        for (; t < n && s_id[t] == id; ++t) {  // sparse, then text: insert or += (447-478)
+            const float r = rrf(s_ix[t]);
             score = have ? score + r : r;
             have = true;
-            bd[j < a + b ? 1 : 2] = s_raw[j];
         }
-        s_score[i] = score;
-        s_bd[0][i] = bd[0];
-        s_bd[1][i] = bd[1];
-        s_bd[2][i] = bd[2];
+        const uint32_t owner = s_ix[p];
+        s_run[owner] = (uint16_t)p;
+        s_sc[owner] = score;
         const uint32_t pos = atomicAdd(&s_cnt, 1u);
-        s_key[pos] = ((uint64_t)(~f32_order(score)) << 32) | i;  // score desc, first appearance asc
+        s_key[pos] = ((uint64_t)(~f32_order(score)) << 32) | owner;  // score desc, first appearance asc
     }
     __syncthreads();
     const uint32_t m = s_cnt;
-    const uint32_t P = next_pow2(m < 2u ? 2u : m);
-    for (uint32_t i = m + tid; i < P; i += 256u) s_key[i] = ~0ull;
+    const uint32_t P2 = next_pow2(m < 2u ? 2u : m);
+    for (uint32_t i = m + tid; i < P2; i += 256u) s_key[i] = ~0ull;
     __syncthreads();
-    bitonic_sort_lds(s_key, P);
+    bitonic_sort_lds(s_key, P2);
     const uint32_t take = min(limit, m);
     for (uint32_t t = tid; t < take; t += 256u) {
-        const uint32_t i = (uint32_t)s_key[t];
+        const uint32_t owner = (uint32_t)s_key[t];
+        const uint32_t p = s_run[owner];
         const uint64_t o = (uint64_t)q * limit + t;
-        out_ids[o] = s_id[i];
-        out_scores[o] = s_score[i];
-        if (out_raw)
-            for (int l = 0; l < 3; ++l) out_raw[o * 3 + l] = s_bd[l][i];
+        const uint64_t id = s_id[p];
+        out_ids[o] = id;
+        out_scores[o] = s_sc[owner];
+        if (out_raw) {  // ScoreBreakdown: the last occurrence per list
+            float bd[3] = {__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+            for (uint32_t u = p; u < n && s_id[u] == id; ++u) bd[list_of(s_ix[u])] = raw_of(s_ix[u]);
+            for (int l = 0; l < 3; ++l) out_raw[o * 3 + l] = bd[l];
+        }
     }
     if (tid == 0) out_n[q] = take;
 }
@@ -460,6 +628,12 @@ struct gvdb_sparse {
     uint64_t cap_ptr = 0, cap_ids = 0, cap_term = 0, cap_tf = 0, cap_dl = 0;
     uint64_t up_slots = 0, up_ent = 0;  // uploaded prefix (append-only adds)
     bool dirty = true;                  // full re-upload needed
+    // term-major inverted index (device), rebuilt from the mirror after a change
+    uint32_t* d_pslot = nullptr;
+    float *d_ptf = nullptr, *d_pdl = nullptr;
+    uint64_t cap_post = 0, cap_ptf = 0, cap_pdl = 0;
+    uint64_t version = 0, inv_version = ~0ull;
+    std::unordered_map<uint32_t, uint64_t> toff;  // term -> its first posting
     // search scratch
     void* scratch = nullptr;
     size_t scratch_n = 0;
@@ -526,6 +700,65 @@ gvdb_status upload(gvdb_sparse* sp) {
     return GVDB_OK;
 }
 
+// Term-major posting runs from the forward mirror: entries stably sorted by
+// term (a slot's entries are (term, add order) and slots ascend, so each run
+// is slot-ascending with a re-added id's entries adjacent in add order), then
+// gathered into (slot, tf, dl).  Run offsets = prefix of the host's posting
+// counts over ascending terms.
+gvdb_status build_inverted(gvdb_sparse* sp, hipStream_t s) {
+    if (sp->inv_version == sp->version) return GVDB_OK;
+    const uint64_t N = sp->slot_id.size(), E = sp->term.size();
+    std::vector<std::pair<uint32_t, uint64_t>> runs(sp->plen.begin(), sp->plen.end());
+    std::sort(runs.begin(), runs.end());
+    uint64_t off = 0;
+    sp->toff.clear();
+    sp->toff.reserve(runs.size());
+    for (const auto& r : runs) {
+        sp->toff[r.first] = off;
+        off += r.second;
+    }
+    if (off != E) return report_status(GVDB_ERR_INDEX, "posting counts disagree with the forward index");
+    if (E > 0x7fffffffull) return report_status(GVDB_ERR_INVALID_ARGUMENT, "more than 2^31 - 1 posting entries");
+    if (E == 0) {
+        sp->inv_version = sp->version;
+        return GVDB_OK;
+    }
+    const uint32_t max_term = runs.empty() ? 0u : runs.back().first;
+    int end_bit = 1;
+    while (end_bit < 32 && (max_term >> end_bit)) ++end_bit;
+    size_t cub_bytes = 0;
+    SP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)E, 0, end_bit, s),
+           "inverted sort size");
+    SP_TRY(grow(sp->d_pslot, sp->cap_post, E, 0), "alloc posting slots");
+    SP_TRY(grow(sp->d_ptf, sp->cap_ptf, E, 0), "alloc posting tf");
+    SP_TRY(grow(sp->d_pdl, sp->cap_pdl, E, 0), "alloc posting dl");
+    char* tmp = nullptr;
+    const size_t a4 = ((size_t)E * 4 + 255) & ~(size_t)255;
+    SP_TRY(hipMalloc((void**)&tmp, 4 * a4 + cub_bytes), "alloc inverted build");
+    uint32_t* eslot = (uint32_t*)tmp;
+    uint32_t* iota = (uint32_t*)(tmp + a4);
+    uint32_t* keys = (uint32_t*)(tmp + 2 * a4);
+    uint32_t* order = (uint32_t*)(tmp + 3 * a4);
+    hipError_t e = hipSuccess;
+    hipLaunchKernelGGL(k_inv_prep, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, sp->d_ptr, (uint32_t)N, eslot,
+                       iota);
+    e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairs(tmp + 4 * a4, cub_bytes, sp->d_term, keys, iota, order, (int)E, 0,
+                                               end_bit, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_inv_gather, dim3(2048), dim3(256), 0, s, order, eslot, sp->d_tf, sp->d_dl, E, sp->d_pslot,
+                           sp->d_ptf, sp->d_pdl);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return sp_dev(e, "build inverted index");
+    sp->inv_version = sp->version;
+    return GVDB_OK;
+}
+
 uint32_t sp_grid(uint32_t tiles) {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
@@ -533,6 +766,34 @@ uint32_t sp_grid(uint32_t tiles) {
     return std::max<uint32_t>(1, std::min<uint32_t>(tiles, 2u * (uint32_t)cus));
 }
 
+// items per query bounded by the list strides: dynamic LDS for the next power of two
+gvdb_status rrf_capacity(const uint32_t* n0, uint32_t st0, const uint32_t* n1, uint32_t st1, const uint32_t* n2,
+                         uint32_t st2, uint32_t* pmax) {
+    const uint64_t cap = (n0 ? (uint64_t)st0 : 0) + (n1 ? (uint64_t)st1 : 0) + (n2 ? (uint64_t)st2 : 0);
+    if (cap > kRrfMax)
+        return report_status(GVDB_ERR_INVALID_ARGUMENT,
+                             "rrf: the three list strides sum to " + std::to_string(cap) + " items, more than 4096");
+    uint32_t p = 2;
+    while (p < cap) p <<= 1;
+    *pmax = p;
+    return GVDB_OK;
+}
+
+// gvdb_rrf_fuse's staging: one HBM buffer and stream per device, reused
+struct RrfPool {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    char* buf = nullptr;
+    size_t cap = 0;
+};
+RrfPool& rrf_pool(int dev) {
+    static std::mutex m;
+    static std::map<int, RrfPool*> pools;  // process lifetime
+    std::lock_guard<std::mutex> g(m);
+    RrfPool*& p = pools[dev];
+    if (!p) p = new RrfPool();
+    return *p;
+}
 }  // namespace
 
 extern "C" {
@@ -547,7 +808,7 @@ gvdb_status gvdb_sparse_create(const gvdb_bm25_params* p, gvdb_sparse** out) {
     }
     hipError_t e = hipSetDevice(sp->device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&sp->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&sp->h_fail, kSpMaxB * 4, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&sp->h_fail, kTaQ * 4, hipHostMallocDefault);
     if (e != hipSuccess) {
         delete sp;
         return sp_dev(e, "gvdb_sparse_create");
@@ -560,7 +821,7 @@ void gvdb_sparse_destroy(gvdb_sparse* sp) {
     if (!sp) return;
     (void)hipSetDevice(sp->device);
     for (void* p : {(void*)sp->d_ptr, (void*)sp->d_term, (void*)sp->d_tf, (void*)sp->d_dl, (void*)sp->d_ids,
-                    sp->scratch})
+                    (void*)sp->d_pslot, (void*)sp->d_ptf, (void*)sp->d_pdl, sp->scratch})
         if (p) (void)hipFree(p);
     if (sp->h_fail) (void)hipHostFree(sp->h_fail);
     if (sp->stream) (void)hipStreamDestroy(sp->stream);
@@ -626,6 +887,7 @@ gvdb_status gvdb_sparse_add_document(gvdb_sparse* sp, uint64_t doc_id, const uin
     }
     sp->total_documents += 1;
     sp->avgdl = sp->total_length / (float)sp->total_documents;  // sparse.rs:102-104
+    ++sp->version;
     return GVDB_OK;
 }
 
@@ -692,6 +954,7 @@ gvdb_status gvdb_sparse_add_documents(gvdb_sparse* sp, const uint64_t* doc_ids, 
             }
             sp->total_documents += n_docs;
             if (sp->total_documents) sp->avgdl = sp->total_length / (float)sp->total_documents;
+            ++sp->version;
             return GVDB_OK;
         }
     }
@@ -743,6 +1006,7 @@ gvdb_status gvdb_sparse_remove_document(gvdb_sparse* sp, uint64_t doc_id, int32_
     sp->total_documents = sp->total_documents > 0 ? sp->total_documents - 1 : 0;
     sp->recompute_length();
     sp->avgdl = sp->total_documents > 0 ? sp->total_length / (float)sp->total_documents : 0.0f;
+    ++sp->version;
     if (removed) *removed = 1;
     return GVDB_OK;
 }
@@ -772,6 +1036,7 @@ void gvdb_sparse_clear(gvdb_sparse* sp) {
     sp->total_length = 0.0f;
     sp->avgdl = 0.0f;
     sp->dirty = true;
+    ++sp->version;
 }
 
 // SparseIndex::search_bm25 (sparse.rs:151-198) for B queries in CSR
@@ -787,28 +1052,30 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
     if (B == 0 || limit == 0 || sp->total_documents == 0 || sp->slot_id.empty()) return GVDB_OK;
     SP_TRY(hipSetDevice(sp->device), "hipSetDevice");
     gvdb_status st = upload(sp);
+    if (st == GVDB_OK) st = build_inverted(sp, sp->stream);
     if (st != GVDB_OK) return st;
     const uint32_t N = (uint32_t)sp->slot_id.size();
     const uint32_t L = (uint32_t)limit;
-    const uint32_t ntiles = (N + kSpTile - 1) / kSpTile;
+    const uint32_t nchunks = (N + kTaCh - 1) / kTaCh;
     // sample stride: expected candidates ~ limit * every, kept well under kSpCand
     uint32_t every = std::max<uint32_t>(1u, std::min<uint32_t>(32u, kSpCand / std::max<uint32_t>(1u, 4u * L)));
-    if (ntiles <= 8u * every) every = 1;  // small index: the sample is the whole index
-    const uint32_t S = ((ntiles + every - 1) / every) * kSpTile;
+    if (nchunks <= 8u * every) every = 1;  // small index: the sample is the whole index
+    const uint32_t nsamp = (nchunks + every - 1) / every;
+    const uint32_t S = nsamp * (kTaCh / kTaGrp);
     hipStream_t s = sp->stream;
     uint64_t q0 = 0;
     std::vector<uint32_t> h_qp;
     std::vector<uint32_t> h_qt;
     std::vector<float> h_qv, h_qidf;
     while (q0 < B) {
-        // launch group: <= kSpMaxB queries and <= kSpQT live query terms
+        // launch group: <= kTaQ queries, <= kSpQT live query terms, <= kSpU distinct terms
         h_qp.assign(1, 0);
         h_qt.clear();
         h_qv.clear();
         h_qidf.clear();
         std::vector<uint32_t> group_terms;  // distinct live terms of the group
         uint64_t q1 = q0;
-        while (q1 < B && q1 - q0 < kSpMaxB) {
+        while (q1 < B && q1 - q0 < kTaQ) {
             std::vector<uint32_t> t;
             std::vector<float> v, idf;
             for (uint64_t p = q_ptr[q1]; p < q_ptr[q1 + 1]; ++p) {
@@ -849,11 +1116,20 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         std::vector<uint16_t> h_qb(nqt);
         for (uint32_t i = 0; i < nqt; ++i)
             h_qb[i] = (uint16_t)(std::lower_bound(group_terms.begin(), group_terms.end(), h_qt[i]) - group_terms.begin());
-        // scratch: qp | qt | qv | qidf | tau | counts | fail | out_n | smp | cand | out ids | out scores
+        std::vector<uint64_t> h_toff(nu), h_gpre(nu + 1, 0);
+        for (uint32_t u = 0; u < nu; ++u) {
+            h_toff[u] = sp->toff.at(group_terms[u]);
+            h_gpre[u + 1] = h_gpre[u] + sp->plen.at(group_terms[u]);
+        }
+        // scratch: qp | qb | qv | qidf | toff | gpre | tau | counts | fail | out_n | first | last | smp | cand |
+        //          out ids | out scores
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-        const size_t o_qp = 0, o_ut = o_qp + al((Bg + 1) * 4), o_qt = o_ut + al(nu * 4 + 4), o_qv = o_qt + al(nqt * 4 + 4),
-                     o_qidf = o_qv + al(nqt * 4 + 4), o_tau = o_qidf + al(nqt * 4 + 4), o_cnt = o_tau + al(Bg * 8),
-                     o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_smp = o_n + al(Bg * 4),
+        const size_t dir = (size_t)nchunks * nu * 4;
+        const size_t o_qp = 0, o_qb = o_qp + al((Bg + 1) * 4), o_qv = o_qb + al(nqt * 2 + 4),
+                     o_qidf = o_qv + al(nqt * 4 + 4), o_toff = o_qidf + al(nqt * 4 + 4),
+                     o_gpre = o_toff + al(nu * 8 + 8), o_tau = o_gpre + al((nu + 1) * 8), o_cnt = o_tau + al(Bg * 8),
+                     o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_first = o_n + al(Bg * 4),
+                     o_last = o_first + al(dir + 4), o_smp = o_last + al(dir + 4),
                      o_cand = o_smp + al((size_t)Bg * S * 8), o_oi = o_cand + al((size_t)Bg * kSpCand * 8),
                      o_os = o_oi + al((size_t)Bg * L * 8), total = o_os + al((size_t)Bg * L * 4);
         if (total > sp->scratch_n) {
@@ -866,22 +1142,26 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         char* base = (char*)sp->scratch;
         SP_TRY(hipMemcpyAsync(base + o_qp, h_qp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
         if (nqt) {
-            SP_TRY(hipMemcpyAsync(base + o_qt, h_qb.data(), nqt * 2, hipMemcpyHostToDevice, s), "qb");
-            SP_TRY(hipMemcpyAsync(base + o_ut, group_terms.data(), nu * 4, hipMemcpyHostToDevice, s), "ut");
+            SP_TRY(hipMemcpyAsync(base + o_qb, h_qb.data(), nqt * 2, hipMemcpyHostToDevice, s), "qb");
             SP_TRY(hipMemcpyAsync(base + o_qv, h_qv.data(), nqt * 4, hipMemcpyHostToDevice, s), "qv");
             SP_TRY(hipMemcpyAsync(base + o_qidf, h_qidf.data(), nqt * 4, hipMemcpyHostToDevice, s), "qidf");
+            SP_TRY(hipMemcpyAsync(base + o_toff, h_toff.data(), nu * 8, hipMemcpyHostToDevice, s), "toff");
+            SP_TRY(hipMemcpyAsync(base + o_gpre, h_gpre.data(), (nu + 1) * 8, hipMemcpyHostToDevice, s), "gpre");
         }
         SP_TRY(hipMemsetAsync(base + o_cnt, 0, Bg * 4, s), "counts");
-        SpArgs a{};
-        a.ptr = sp->d_ptr;
-        a.term = sp->d_term;
-        a.tf = sp->d_tf;
-        a.dl = sp->d_dl;
+        TaArgs a{};
+        a.pslot = sp->d_pslot;
+        a.ptf = sp->d_ptf;
+        a.pdl = sp->d_pdl;
         a.N = N;
-        a.qp = (const uint32_t*)(base + o_qp);
-        a.qb = (const uint16_t*)(base + o_qt);
-        a.ut = (const uint32_t*)(base + o_ut);
+        a.nchunks = nchunks;
+        a.toff = (const uint64_t*)(base + o_toff);
+        a.gpre = (const uint64_t*)(base + o_gpre);
+        a.first = (uint32_t*)(base + o_first);
+        a.last = (uint32_t*)(base + o_last);
         a.nu = nu;
+        a.qp = (const uint32_t*)(base + o_qp);
+        a.qb = (const uint16_t*)(base + o_qb);
         a.qv = (const float*)(base + o_qv);
         a.qidf = (const float*)(base + o_qidf);
         a.B = Bg;
@@ -894,12 +1174,18 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         a.tau = (const uint64_t*)(base + o_tau);
         a.counts = (uint32_t*)(base + o_cnt);
         a.cand = (uint64_t*)(base + o_cand);
-        const uint32_t stiles = (ntiles + every - 1) / every;
-        hipLaunchKernelGGL(k_bm25<0>, dim3(sp_grid(stiles)), dim3(kSpThreads), 0, s, a);
+        if (nu) {
+            SP_TRY(hipMemsetAsync(a.first, 0xff, dir, s), "directory");
+            const uint64_t P = h_gpre[nu];
+            const uint32_t dgrid = (uint32_t)std::min<uint64_t>((P + 255) / 256, 8u * sp_grid(1u << 30));
+            hipLaunchKernelGGL(k_ta_dir, dim3(std::max<uint32_t>(1u, dgrid)), dim3(256), 0, s, a);
+            SP_TRY(hipGetLastError(), "bm25 directory");
+        }
+        hipLaunchKernelGGL(k_bm25_taat<0>, dim3(sp_grid(nsamp)), dim3(kTaThreads), 0, s, a);
         SP_TRY(hipGetLastError(), "bm25 sample");
         hipLaunchKernelGGL(k_bm25_tau, dim3(Bg), dim3(256), 0, s, a.smp, S, L, (uint64_t*)(base + o_tau));
         SP_TRY(hipGetLastError(), "bm25 tau");
-        hipLaunchKernelGGL(k_bm25<1>, dim3(sp_grid(ntiles)), dim3(kSpThreads), 0, s, a);
+        hipLaunchKernelGGL(k_bm25_taat<1>, dim3(sp_grid(nchunks)), dim3(kTaThreads), 0, s, a);
         SP_TRY(hipGetLastError(), "bm25 emit");
         uint64_t* d_oi = (uint64_t*)(base + o_oi);
         float* d_os = (float*)(base + o_os);
@@ -924,7 +1210,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             void* ct = (char*)tmp + (size_t)N * 16 + 256;
             a.dense = k0;
             a.dense_q = q;
-            hipLaunchKernelGGL(k_bm25<2>, dim3(sp_grid(ntiles)), dim3(kSpThreads), 0, s, a);
+            hipLaunchKernelGGL(k_bm25_taat<2>, dim3(sp_grid(nchunks)), dim3(kTaThreads), 0, s, a);
             hipError_t e = hipGetLastError();
             hipcub::DoubleBuffer<uint64_t> db(k0, k1);
             if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortKeysDescending(ct, cub_bytes, db, (int)N, 0, 64, s);
@@ -953,17 +1239,22 @@ gvdb_status gvdb_rrf_fuse_device(const uint64_t* d_dense_ids, const float* d_den
                                  float k, uint64_t limit, uint64_t* d_out_ids, float* d_out_scores,
                                  float* d_out_breakdown, uint32_t* d_out_n, void* stream) {
     if (B == 0) return GVDB_OK;
-    if (!d_out_n || (limit && (!d_out_ids || !d_out_scores)) || limit > 0xffffffffull)
+    if (!d_out_n || (limit && (!d_out_ids || !d_out_scores)) || limit > 0xffffffffull || B > 0x7fffffffull)
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "bad output arguments");
-    hipLaunchKernelGGL(k_rrf, dim3((uint32_t)B), dim3(256), 0, (hipStream_t)stream, d_dense_ids, d_dense_scores,
-                       d_dense_n, dense_stride, d_sparse_ids, d_sparse_scores, d_sparse_n, sparse_stride, d_text_ids,
-                       d_text_scores, d_text_n, text_stride, k, (uint32_t)limit, d_out_ids, d_out_scores,
-                       d_out_breakdown, d_out_n);
+    uint32_t pmax = 0;
+    gvdb_status st = rrf_capacity(d_dense_n, dense_stride, d_sparse_n, sparse_stride, d_text_n, text_stride, &pmax);
+    if (st != GVDB_OK) return st;
+    hipLaunchKernelGGL(k_rrf, dim3((uint32_t)B), dim3(256), (size_t)pmax * 24, (hipStream_t)stream, d_dense_ids,
+                       d_dense_scores, d_dense_n, dense_stride, d_sparse_ids, d_sparse_scores, d_sparse_n,
+                       sparse_stride, d_text_ids, d_text_scores, d_text_n, text_stride, k, (uint32_t)limit, pmax,
+                       d_out_ids, d_out_scores, d_out_breakdown, d_out_n);
     SP_TRY(hipGetLastError(), "rrf");
     return GVDB_OK;
 }
 
-// Host-pointer form: stages the lists through HBM on a private stream.
+
+// Host-pointer form: stages the lists through a per-device pooled HBM buffer
+// on a pooled stream (no allocation per call once the buffer is large enough).
 gvdb_status gvdb_rrf_fuse(const uint64_t* dense_ids, const float* dense_scores, const uint32_t* dense_n,
                           uint32_t dense_stride, const uint64_t* sparse_ids, const float* sparse_scores,
                           const uint32_t* sparse_n, uint32_t sparse_stride, const uint64_t* text_ids,
@@ -972,6 +1263,9 @@ gvdb_status gvdb_rrf_fuse(const uint64_t* dense_ids, const float* dense_scores, 
                           uint32_t* out_n) {
     if (B == 0) return GVDB_OK;
     if (!out_n || (limit && (!out_ids || !out_scores))) return report_status(GVDB_ERR_INVALID_ARGUMENT, "null output");
+    uint32_t pmax = 0;
+    gvdb_status st = rrf_capacity(dense_n, dense_stride, sparse_n, sparse_stride, text_n, text_stride, &pmax);
+    if (st != GVDB_OK) return st;
     struct L {
         const uint64_t* ids;
         const float* sc;
@@ -980,27 +1274,35 @@ gvdb_status gvdb_rrf_fuse(const uint64_t* dense_ids, const float* dense_scores, 
     } lists[3] = {{dense_ids, dense_scores, dense_n, dense_stride},
                   {sparse_ids, sparse_scores, sparse_n, sparse_stride},
                   {text_ids, text_scores, text_n, text_stride}};
+    auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
     size_t bytes = 0;
     for (const L& l : lists)
-        if (l.n) bytes += B * 4 + (size_t)B * l.st * 12 + 768;
-    bytes += (size_t)B * limit * (8 + 4 + 12) + B * 4 + 1024;
-    char* d = nullptr;
-    hipStream_t s = nullptr;
-    SP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "rrf stream");
-    hipError_t e = hipMalloc((void**)&d, bytes);
-    if (e != hipSuccess) {
-        (void)hipStreamDestroy(s);
-        return sp_dev(e, "alloc rrf");
+        if (l.n) bytes += al(B * 4) + al((size_t)B * l.st * 8) + al((size_t)B * l.st * 4);
+    bytes += al((size_t)B * limit * 8) + al((size_t)B * limit * 4) + al((size_t)B * limit * 12) + al(B * 4);
+    int dev = 0;
+    SP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    RrfPool& pool = rrf_pool(dev);
+    std::lock_guard<std::mutex> g(pool.mu);
+    if (!pool.stream) SP_TRY(hipStreamCreateWithFlags(&pool.stream, hipStreamNonBlocking), "rrf stream");
+    if (bytes > pool.cap) {
+        if (pool.buf) (void)hipFree(pool.buf);
+        pool.buf = nullptr;
+        pool.cap = 0;
+        const size_t want = std::max(bytes, (size_t)1 << 20);
+        SP_TRY(hipMalloc((void**)&pool.buf, want), "alloc rrf");
+        pool.cap = want;
     }
-    char* p = d;
+    hipStream_t s = pool.stream;
+    char* p = pool.buf;
     auto take = [&](size_t n) {
         char* r = p;
-        p += (n + 255) & ~(size_t)255;
+        p += al(n);
         return r;
     };
     const uint64_t* dl_ids[3] = {nullptr, nullptr, nullptr};
     const float* dl_sc[3] = {nullptr, nullptr, nullptr};
     const uint32_t* dl_n[3] = {nullptr, nullptr, nullptr};
+    hipError_t e = hipSuccess;
     for (int i = 0; i < 3 && e == hipSuccess; ++i) {
         const L& l = lists[i];
         if (!l.n) continue;
@@ -1016,9 +1318,9 @@ gvdb_status gvdb_rrf_fuse(const uint64_t* dense_ids, const float* dense_scores, 
     }
     uint64_t* oi = (uint64_t*)take((size_t)B * limit * 8);
     float* os = (float*)take((size_t)B * limit * 4);
-    float* ob = out_breakdown ? (float*)take((size_t)B * limit * 12) : nullptr;
+    float* ob = (float*)take((size_t)B * limit * 12);
     uint32_t* on = (uint32_t*)take(B * 4);
-    gvdb_status st = GVDB_OK;
+    if (!out_breakdown) ob = nullptr;
     if (e == hipSuccess)
         st = gvdb_rrf_fuse_device(dl_ids[0], dl_sc[0], dl_n[0], dense_stride, dl_ids[1], dl_sc[1], dl_n[1], sparse_stride,
                                   dl_ids[2], dl_sc[2], dl_n[2], text_stride, B, k, limit, oi, os, ob, on, s);
@@ -1027,10 +1329,10 @@ gvdb_status gvdb_rrf_fuse(const uint64_t* dense_ids, const float* dense_scores, 
         if (e == hipSuccess && limit) e = hipMemcpyAsync(out_scores, os, (size_t)B * limit * 4, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess && ob) e = hipMemcpyAsync(out_breakdown, ob, (size_t)B * limit * 12, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipMemcpyAsync(out_n, on, B * 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
     }
-    (void)hipFree(d);
-    (void)hipStreamDestroy(s);
+    // the pooled buffer is reused by the next call: drain the stream whatever happened
+    const hipError_t e2 = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = e2;
     if (e != hipSuccess) return sp_dev(e, "rrf");
     return st;
 }

@@ -194,3 +194,57 @@ def test_hybrid_engine_rrf(gvdb_mod, sp_mod, oracle_mod):
         assert [d for d, _, _ in out[qi]] == [f"doc{w[0]}" for w in want]
         assert np.array([s for _, s, _ in out[qi]], np.float32).tobytes() == \
             np.array([w[1] for w in want], np.float32).tobytes()
+
+
+def test_bm25_unstaged_chunks(sp_mod, oracle_mod):
+    """Documents with ~80 distinct terms of a 400-term vocabulary and 64
+    queries of 8 terms: a 128-document chunk holds more postings of the
+    group's terms than the 4096-entry LDS stage, so the rounds read the
+    posting runs from HBM (k_bm25_taat's unstaged path)."""
+    docs = zipf_docs(31, 6000, 400, 160, a=0.3)
+    assert np.mean([t.size for t, _, _ in docs]) > 60
+    g, o = build(sp_mod, oracle_mod, docs)
+    check_batch(sp_mod, g, o, queries(32, 64, 400, 6, 10), 30)
+
+
+def test_bm25_batch_groups_and_repeated_terms(sp_mod, oracle_mod):
+    """150 queries (three launch groups of <= 64), every query repeating a
+    term (each occurrence adds again, sparse.rs:167-190), re-added ids (a
+    second posting of the same document in a run)."""
+    docs = zipf_docs(33, 20_000, 3000, 30)
+    g, o = build(sp_mod, oracle_mod, docs)
+    for i in (5, 129, 130, 19_999):
+        t, v, dl = docs[(i * 7) % len(docs)]
+        g.add_documents_u64(np.array([i], np.uint64), np.array([0, t.size], np.uint64), t, v, np.array([dl]))
+        o.add_document(i, t, v, dl)
+    qs = []
+    for t, v in queries(34, 150, 3000, 2, 7):
+        qs.append((np.append(t, t[0]).astype(np.uint32), np.append(v, np.float32(0.25)).astype(np.float32)))
+    check_batch(sp_mod, g, o, qs, 12)
+
+
+def test_rrf_large_lists_match_oracle(sp_mod, oracle_mod):
+    """limit 400 -> 800-entry dense / sparse lists (more than the old 1024-item
+    cap in total) with overlapping and repeated ids."""
+    r = np.random.default_rng(41)
+    B = 6
+    D, S, T = [], [], []
+    for _ in range(B):
+        mk = lambda n: [(int(x), float(r.random())) for x in r.integers(0, 1500, n)]  # noqa: E731
+        D.append(mk(800))
+        S.append(mk(800))
+        T.append(mk(int(r.integers(0, 300))))
+    got = sp_mod.rrf_fuse(D, S, T, 60.0, 400)
+    for b in range(B):
+        want = oracle_mod.rrf_fusion(D[b], S[b], T[b], 60.0)[:400]
+        assert [x[0] for x in got[b]] == [w[0] for w in want], b
+        assert np.array([x[1] for x in got[b]], np.float32).tobytes() == \
+            np.array([w[1] for w in want], np.float32).tobytes()
+        for x, w in zip(got[b], want):
+            assert same([np.nan if v is None else v for v in x[2]], w[2:])
+
+
+def test_rrf_over_capacity_is_an_error(sp_mod):
+    big = [[(i, 1.0) for i in range(2100)]]
+    with pytest.raises(Exception, match="4096"):
+        sp_mod.rrf_fuse(big, big, [], 60.0, 10)
