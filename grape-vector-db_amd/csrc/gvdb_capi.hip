@@ -280,15 +280,16 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t sample_div, uint32_t& chunks
 // sit contiguously in ws.zero (flags[0] = any stage-1 failure, flags[1] = NaN).
 gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D, uint32_t R, uint32_t N,
                            hipStream_t s) {
-    // GVDB_SCAN=valu forces the popcount scan for every batch size, =i8 the
-    // i8-MFMA scan instead of the FP4 one (A/B runs); default: FP4 MFMA for
-    // large batches
+    // GVDB_SCAN=valu forces the popcount scan for every batch size; default:
+    // FP4 MFMA for large batches.  The A/B variants (=i8, =fp4u, =fp4lds)
+    // exist only in a `make VARIANTS=1` build.
     const char* scan = getenv("GVDB_SCAN");
-    s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0
-                  : (scan && strcmp(scan, "i8") == 0)  ? 2
-                  : (scan && strcmp(scan, "fp4u") == 0) ? 3
-                  : (scan && strcmp(scan, "fp4lds") == 0) ? 4
-                                                        : 1;
+    s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0 : 1;
+#ifdef GVDB_SCAN_VARIANTS
+    if (scan && strcmp(scan, "i8") == 0) s1.use_mfma = 2;
+    if (scan && strcmp(scan, "fp4u") == 0) s1.use_mfma = 3;
+    if (scan && strcmp(scan, "fp4lds") == 0) s1.use_mfma = 4;
+#endif
     const char* dbg = getenv("GVDB_SCAN_DBG");  // ablation timing only (results invalid when set)
     s1.dbg = dbg ? atoi(dbg) : 0;
     s1.force_rescan = getenv_flag("GVDB_FORCE_RESCAN") ? 1 : 0;  // tests of the device-side fallback

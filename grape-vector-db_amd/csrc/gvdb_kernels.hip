@@ -785,6 +785,7 @@ __device__ __forceinline__ v4i_t pm1_x16(uint32_t h16) {
     return r;
 }
 
+#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
 constexpr int kMfThreads = 512;
 constexpr int kMxDepth = 4;
 constexpr int kMxLdsDepth = 3;  // k-steps of B-fragment LDS prefetch in k_scan_mx2
@@ -905,6 +906,7 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mfma(const uint4* __rest
         __syncthreads();
     }
 }
+#endif  // GVDB_SCAN_VARIANTS
 
 // ----------------------------------------------------------------------------
 // k_scan_mx — the large-batch stage-1 filter on block-scaled FP4 MFMA.
@@ -958,6 +960,7 @@ __device__ __forceinline__ void mfma_fp4_acc(v16f_t& d, const v4i_t& a, const v4
 }
 __device__ __forceinline__ void mfma_fp4_drain() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); }
 
+#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
 template <int W4>
 __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                           const uint32_t* __restrict__ qwords,
@@ -1064,6 +1067,7 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restri
         __syncthreads();
     }
 }
+#endif  // GVDB_SCAN_VARIANTS
 
 // k_scan_mx2: the FP4 scan with staggered wave halves.  8 waves per CU, one
 // 32-query tile each; waves w and w+4 share a SIMD.  Every tile both halves
@@ -1075,6 +1079,7 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restri
 // MFMAs instead of all waves alternating between the two phases together.
 // Each half keeps ONE register set for its codes (expanded, then reloaded:
 // no register moves, which would wait on the loads).  One barrier per tile.
+#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
 template <int W4>
 __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restrict__ codes, uint64_t cap,
                                                            uint32_t N, const uint32_t* __restrict__ qwords,
@@ -1320,6 +1325,7 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restr
         if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
     }
 }
+#endif  // GVDB_SCAN_VARIANTS
 
 // Block-aggregated flush of the per-wave staged emits (k_scan_mx3/mx4): one
 // LDS atomic per entry gives its rank within (block, query), then ONE global
@@ -1773,6 +1779,7 @@ static void launch_scan_mx4_t(const Stage1Args& a, hipStream_t s) {
     }
 }
 
+#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
 template <int W4>
 static void launch_scan_mx2_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
@@ -1787,7 +1794,9 @@ static void launch_scan_mx2_t(const Stage1Args& a, hipStream_t s) {
                            a.buf + (uint64_t)g * a.bufcap, a.bufcap, a.dbg);
     }
 }
+#endif  // GVDB_SCAN_VARIANTS
 
+#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
 template <int W4>
 static void launch_scan_mx_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
@@ -1802,7 +1811,9 @@ static void launch_scan_mx_t(const Stage1Args& a, hipStream_t s) {
                            a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
 }
+#endif  // GVDB_SCAN_VARIANTS
 
+#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
 template <int W4>
 static void launch_scan_mfma_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
@@ -1818,6 +1829,7 @@ static void launch_scan_mfma_t(const Stage1Args& a, hipStream_t s) {
                            a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
 }
+#endif  // GVDB_SCAN_VARIANTS
 
 template <int W4, int CPL>
 static void launch_scan_t(const Stage1Args& a, hipStream_t s) {
@@ -1891,6 +1903,7 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 24: launch_scan_mx4_t<24, 6, 2>(a, s); break;
             default: launch_scan_mx4_t<32, 8, 1>(a, s); break;
         }
+#ifdef GVDB_SCAN_VARIANTS
     } else if (mfma && a.use_mfma == 2) {  // i8 MFMA variant (A/B comparison)
         switch (W4) {
             case 2: launch_scan_mfma_t<2>(a, s); break;
@@ -1912,19 +1925,13 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 4: launch_scan_mx2_t<4>(a, s); break;
             default: launch_scan_mx2_t<6>(a, s); break;
         }
+#endif  // GVDB_SCAN_VARIANTS
     } else if (mfma) {  // FP4 block-scaled MFMA, candidates in registers (default for large batches)
         switch (W4) {
             case 2: launch_scan_mx3_t<2>(a, s); break;
             case 3: launch_scan_mx3_t<3>(a, s); break;
             case 4: launch_scan_mx3_t<4>(a, s); break;
             default: launch_scan_mx3_t<6>(a, s); break;
-        }
-    } else if (false) {
-        switch (W4) {
-            case 2: launch_scan_mx2_t<2>(a, s); break;
-            case 3: launch_scan_mx2_t<3>(a, s); break;
-            case 4: launch_scan_mx2_t<4>(a, s); break;
-            default: launch_scan_mx2_t<6>(a, s); break;
         }
     } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \
@@ -3056,7 +3063,6 @@ hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, ui
 // atomic add per block, and the block whose add came last reads them with
 // agent-scope atomic loads (MI355X_MICROARCH.md, valid hand-off forms, row 1).
 // ============================================================================
-constexpr uint32_t kB1Chunk = 1024;  // sample rows per k_b1_sample block (4 per thread)
 
 // Query -> 4*W4 Msb0 code words in LDS (pad words zero), by the whole block.
 // 256-thread blocks, D <= 1024: every query load is issued before the first
@@ -3400,5 +3406,10 @@ hipError_t launch_b1_search(const B1Args& b, hipStream_t s) {
 }  // namespace gvdb
 
 extern "C" int gvdb_debug_stamps(unsigned long long* out) {
+#ifdef GVDB_SCAN_VARIANTS
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(gvdb::g_stamps), sizeof(gvdb::g_stamps));
+#else
+    (void)out;
+    return -1;  // k_scan_mx2's stamps exist only in a VARIANTS=1 build
+#endif
 }

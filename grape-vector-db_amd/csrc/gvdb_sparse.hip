@@ -59,21 +59,21 @@ using namespace gvdb;
 
 namespace {
 
-constexpr uint32_t kTaCh = 128;                 // document slots per chunk (one LDS accumulator row per query)
-constexpr uint32_t kTaRow = kTaCh + 1;          // accumulator row stride: queries' rows start on different banks
-constexpr uint32_t kTaThreads = 512;            // 8 waves; wave w owns queries w, w + 8, ...
+constexpr uint32_t kTaCh = 64;                  // document slots per chunk: one per lane
+constexpr uint32_t kTaThreads = 1024;           // one block per CU: 16 waves; wave w owns queries w, w + 16, ...
 constexpr uint32_t kTaWaves = kTaThreads / 64;
-constexpr uint32_t kTaQ = 64;                   // queries per launch group (<= 8 per wave)
-constexpr uint32_t kTaStage = 4096;             // postings staged per chunk (more: read from HBM in the rounds)
+constexpr uint32_t kTaQW = 4;                   // queries per wave
+constexpr uint32_t kTaQ = kTaWaves * kTaQW;     // queries per launch group
+constexpr uint32_t kTaStage = 4096;             // postings per chunk staged through registers (more: from HBM)
 constexpr uint32_t kTaGrp = 8;                  // sample pass: one max key per 8 slots
-constexpr uint32_t kTaSent = 0x7fbadbadu;       // "no posting yet": a signalling NaN, never an arithmetic result
+constexpr uint32_t kTaDirPer = 4;               // directory pass: postings per thread
+constexpr uint32_t kTaSent = 0x7fbadbadu;       // accumulator "no posting yet": a signalling NaN, never an arithmetic result
 constexpr uint32_t kSpQT = 1024;                // query terms per launch group (LDS)
-constexpr uint32_t kSpU = 512;                  // distinct terms per launch group
+constexpr uint32_t kSpU = 511;                  // distinct terms per launch group (map row kSpU stays empty)
 constexpr uint32_t kSpCand = 4096;              // candidates per query (LDS sort)
 constexpr uint32_t kSpTopLocal = 8;             // per-thread keys kept by the tau pass
-static_assert(kSpU <= kTaThreads, "one thread per group term in the directory row");
-static_assert(kTaQ <= kTaWaves * 8, "a wave's queries sit in lanes 0..7");
-static_assert(kTaCh <= 256, "staged slots are bytes");
+static_assert(kSpU < kTaThreads, "one thread per group term in the directory row");
+static_assert(kTaCh == 64, "a chunk slot is a lane");
 
 // total order of a BM25 score (NaN lowest: 0), then slot ascending
 __device__ __forceinline__ uint64_t sp_key(float s, uint32_t slot) {
@@ -101,14 +101,16 @@ __global__ void k_inv_prep(const uint64_t* __restrict__ ptr, uint32_t N, uint32_
     }
 }
 
-__global__ void k_inv_gather(const uint32_t* __restrict__ order, const uint32_t* __restrict__ eslot,
-                             const float* __restrict__ tf, const float* __restrict__ dl, uint64_t E,
-                             uint32_t* __restrict__ pslot, float* __restrict__ ptf, float* __restrict__ pdl) {
+__global__ void k_inv_gather(const uint32_t* __restrict__ order, const uint32_t* __restrict__ keys,
+                             const uint32_t* __restrict__ eslot, const float* __restrict__ tf,
+                             const float* __restrict__ dl, uint64_t E, uint32_t* __restrict__ pslot,
+                             float* __restrict__ ptf, float* __restrict__ pdl, uint32_t* __restrict__ runs) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t e = order[i];
-        pslot[i] = eslot[e];
+        const uint32_t e = order[i], s = eslot[e];
+        pslot[i] = s;
         ptf[i] = tf[e];
         pdl[i] = dl[e];
+        if (i > 0 && keys[i] == keys[i - 1] && eslot[order[i - 1]] == s) *runs = 1u;  // same term, same document
     }
 }
 
@@ -119,14 +121,14 @@ struct TaArgs {
     uint32_t N;             // slots
     uint32_t nchunks;
     const uint64_t* toff;   // [nu] first posting of each group term
-    const uint64_t* gpre;   // [nu+1] prefix of the group terms' posting counts (directory pass)
-    uint32_t* first;        // [nchunks][nu] first / last posting (relative to toff) inside a chunk
+    const uint64_t* gpre;   // [nu+1] prefix of the group terms' posting counts
+    const uint64_t* gpre4;  // [nu+1] prefix of ceil(count / kTaDirPer) (directory pass threads)
+    uint32_t* first;        // [nu][nchunks] first / last posting (relative to toff) inside a chunk
     uint32_t* last;
     uint32_t nu;
-    const uint32_t* qp;     // [B+1] offsets into qb/qv/qidf
-    const uint16_t* qb;     // group-term index of each query term
-    const float* qv;
-    const float* qidf;
+    const uint32_t* qp;     // [B+1] offsets into qrec
+    const uint4* qrec;      // [nqt+1] per query term: (group term, q_tf bits, idf bits, 0); [nqt] = the empty row
+    uint32_t nqt;
     uint32_t B;
     float k1, b, avgdl;
     uint32_t every;         // sample pass: chunk stride
@@ -137,266 +139,339 @@ struct TaArgs {
     uint64_t* cand;         // emit: [B][kSpCand]
     uint64_t* dense;        // dense mode: [N] keys of query `dense_q`
     uint32_t dense_q;
+    uint32_t runs;          // the index holds a (term, document) run longer than one posting (a re-added id)
+    uint32_t abl;           // timing probe only (GVDB_BM25_ABL): 1 skip rounds, 2 skip staging loads, 4 skip dir loads,
+                            // 8 phase clocks into prof
+    uint64_t* prof;         // [gridDim][8] cycles per phase (wave 0), with abl & 8
 };
 
-// Directory: one thread per posting of the group's terms; the posting that
-// opens (closes) a chunk's run writes first (last).  `first` is preset to
-// ~0 = "no posting of the term in the chunk".
+// Directory: each thread takes kTaDirPer consecutive postings of one term; the
+// posting that opens (closes) a chunk's run writes first (last).  `first` is
+// preset to ~0 = "no posting of the term in the chunk".  Term-major rows, so a
+// dense term's consecutive chunks are written by neighbouring threads.
 __global__ __launch_bounds__(256) void k_ta_dir(TaArgs a) {
-    __shared__ uint64_t s_pre[kSpU + 1];
+    __shared__ uint64_t s_pre4[kSpU + 2], s_pre[kSpU + 2];
     const uint32_t nu = a.nu;
-    for (uint32_t i = threadIdx.x; i <= nu; i += 256u) s_pre[i] = a.gpre[i];
+    for (uint32_t i = threadIdx.x; i <= nu; i += 256u) {
+        s_pre4[i] = a.gpre4[i];
+        s_pre[i] = a.gpre[i];
+    }
     __syncthreads();
-    const uint64_t P = s_pre[nu];
-    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < P; i += (uint64_t)gridDim.x * 256u) {
-        uint32_t lo = 0, hi = nu;  // the last term whose run starts at or before i
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_pre[mid] <= i) lo = mid; else hi = mid;
-        }
-        const uint32_t j = (uint32_t)(i - s_pre[lo]);
-        const uint32_t len = (uint32_t)(s_pre[lo + 1] - s_pre[lo]);
-        const uint32_t* run = a.pslot + a.toff[lo];
-        const uint32_t c = run[j] / kTaCh;
-        const uint32_t pc = j ? run[j - 1] / kTaCh : 0xffffffffu;
-        const uint32_t nc = j + 1 < len ? run[j + 1] / kTaCh : 0xffffffffu;
-        if (c != pc) a.first[(uint64_t)c * nu + lo] = j;
-        if (c != nc) a.last[(uint64_t)c * nu + lo] = j;
+    const uint64_t gi = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (gi >= s_pre4[nu]) return;
+    uint32_t lo = 0, hi = nu;  // the last term whose thread range starts at or before gi
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_pre4[mid] <= gi) lo = mid; else hi = mid;
+    }
+    const uint32_t len = (uint32_t)(s_pre[lo + 1] - s_pre[lo]);
+    const uint32_t j0 = (uint32_t)(gi - s_pre4[lo]) * kTaDirPer;
+    const uint32_t* run = a.pslot + a.toff[lo];
+    uint32_t ch[kTaDirPer + 2];  // chunks of postings j0-1 .. j0+kTaDirPer
+#pragma unroll
+    for (uint32_t k = 0; k < kTaDirPer + 2; ++k) {
+        const uint32_t j = j0 + k - 1;  // j0 - 1 wraps to ~0 for j0 == 0
+        ch[k] = (k > 0 || j0 > 0) && j0 + k - 1 < len ? run[j] / kTaCh : 0xffffffffu;
+    }
+    uint32_t* fr = a.first + (uint64_t)lo * a.nchunks;
+    uint32_t* lr = a.last + (uint64_t)lo * a.nchunks;
+#pragma unroll
+    for (uint32_t k = 1; k <= kTaDirPer; ++k) {
+        if (j0 + k - 1 >= len) break;
+        if (ch[k] != ch[k - 1]) fr[ch[k]] = j0 + k - 1;
+        if (ch[k] != ch[k + 1]) lr[ch[k]] = j0 + k - 1;
     }
 }
 
 // MODE 0: sample (every `every`-th chunk -> per 8 slots the max key -> smp),
 // 1: emit (key >= tau -> cand), 2: dense keys of query `dense_q`.
+//
+// One block per CU walks a contiguous range of 64-slot chunks.  Per chunk:
+//   1. directory row -> each group term's postings in the chunk;
+//   2. a (term x slot) LDS map receives tf_component (calculate_bm25_score's
+//      query-independent part, sparse.rs:215-218) of each (term, document)'s
+//      first posting; kTaSent = no posting;
+//   3. rounds: lane = slot, wave w owns queries w + 16 m (m < 4),
+//      accumulators in registers.  Round r adds query q's r-th term: one map
+//      read, acc = acc + q_tf * tfc * idf -- per document exactly the
+//      reference's fold (sparse.rs:167-190).  A re-added document's run of
+//      postings (rare: the index records whether any exists) is folded from
+//      the posting run in HBM, in order;
+//   4. selection by the mode.
+// Software pipeline: while chunk j's rounds run, the postings of chunk j+1
+// and the directory entries of chunk j+2 are in flight into registers.
 template <int MODE>
-__global__ __launch_bounds__(kTaThreads, 2) void k_bm25_taat(TaArgs a) {
-    __shared__ float s_acc[kTaQ * kTaRow];
-    __shared__ uint32_t s_qp[kTaQ + 1];
-    __shared__ uint16_t s_qb[kSpQT];
-    __shared__ float s_qv[kSpQT], s_qidf[kSpQT];
+__global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_tmap[(kSpU + 1) * kTaCh];  // row kSpU: the empty row
     __shared__ uint64_t s_tau[MODE == 1 ? kTaQ : 1];
-    __shared__ uint32_t s_n[kSpU], s_soff[kSpU + 1];
-    __shared__ uint64_t s_pf[kSpU];
-    __shared__ uint32_t s_wsum[kTaWaves];
-    __shared__ uint8_t st_slot[kTaStage];
-    __shared__ float st_tfc[kTaStage];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    __shared__ uint32_t s_n[2][kSpU + 1], s_soff[2][kSpU + 1];  // double-buffered: chunk j / j+1
+    __shared__ uint64_t s_pf[2][kSpU + 1];
+    __shared__ uint32_t s_wsum[2][kTaWaves];
+    __shared__ uint32_t s_slow;
+    typedef const uint32_t __attribute__((address_space(4)))* cu32;
+    const cu32 qp = (cu32)(uintptr_t)a.qp;  // read-only query tables: scalar loads
+    const cu32 qr32 = (cu32)(uintptr_t)a.qrec;
+    auto qrec_at = [&](uint32_t p) { return make_uint4(qr32[4 * p], qr32[4 * p + 1], qr32[4 * p + 2], 0u); };
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t B = a.B, nu = a.nu;
-    for (uint32_t i = tid; i <= B; i += kTaThreads) s_qp[i] = a.qp[i];
     if constexpr (MODE == 1)
         for (uint32_t i = tid; i < B; i += kTaThreads) s_tau[i] = a.tau[i];
-    __syncthreads();
-    const uint32_t nqt = s_qp[B];
-    for (uint32_t i = tid; i < nqt; i += kTaThreads) {
-        s_qb[i] = a.qb[i];
-        s_qv[i] = a.qv[i];
-        s_qidf[i] = a.qidf[i];
-    }
+    if (tid < kTaCh) s_tmap[kSpU * kTaCh + tid] = __uint_as_float(kTaSent);
     const float k1 = a.k1, b = a.b, avgdl = a.avgdl;
     const float k1p1 = k1 + 1.0f, omb = 1.0f - b;  // (k1 + 1.0), (1.0 - b) as the reference evaluates them
-    // calculate_bm25_score's tf_component (sparse.rs:215-218): per posting
     auto tfc_of = [&](float tfv, float dlv) { return (tfv * k1p1) / (tfv + k1 * (omb + b * (dlv / avgdl))); };
-    // this wave's queries: lane m < 8 holds query wave + 8 m
-    const uint32_t myq = wave + kTaWaves * lane;
-    const bool has_q = lane < 8u && myq < B && (MODE != 2 || myq == a.dense_q);
+    // this wave's queries (uniform): term range of query wave + 16 m
+    uint32_t qp0[kTaQW], ql[kTaQW], rmax = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < kTaQW; ++m) {
+        const uint32_t q = wave + kTaWaves * m;
+        const bool live = q < B && (MODE != 2 || q == a.dense_q);
+        qp0[m] = live ? qp[q] : 0u;
+        ql[m] = live ? qp[q + 1] - qp0[m] : 0u;
+        rmax = max(rmax, ql[m]);
+    }
+    const uint32_t pdummy = a.nqt;  // qrec[nqt]: the empty map row, q_tf = idf = 0
+    // the wave's query terms, lane-resident: lane 16 m + r holds query m's r-th term (r < 16)
+    uint32_t lr_u, lr_v, lr_idf;
+    {
+        const uint32_t m = lane >> 4, r = lane & 15u;
+        const uint4 rec = qrec_at(r < ql[m & 3] ? qp0[m & 3] + r : pdummy);
+        lr_u = rec.x;
+        lr_v = rec.y;
+        lr_idf = rec.z;
+    }
+    const uint64_t my_toff = tid < nu ? a.toff[tid] : 0ull;
     const uint32_t every = MODE == 0 ? a.every : 1u;
     const uint32_t nj = (a.nchunks + every - 1) / every;
-    for (uint32_t jj = blockIdx.x; jj < nj; jj += gridDim.x) {
-        const uint32_t c = jj * every, c0 = c * kTaCh;
-        __syncthreads();  // the previous chunk's readers are done (and the query tables are visible)
-        // directory row -> postings per group term in this chunk, staging offsets
-        uint32_t n = 0;
-        if (tid < nu) {
-            const uint64_t row = (uint64_t)c * nu + tid;
-            const uint32_t f = a.first[row];
-            uint64_t pf = 0;
-            if (f != 0xffffffffu) {
-                n = a.last[row] - f + 1u;
-                pf = a.toff[tid] + f;
-            }
-            s_n[tid] = n;
-            s_pf[tid] = pf;
+    // contiguous chunk range per block: the directory's term-major rows are read sequentially
+    const uint32_t jb = (uint32_t)((uint64_t)nj * blockIdx.x / gridDim.x);
+    const uint32_t je = (uint32_t)((uint64_t)nj * (blockIdx.x + 1) / gridDim.x);
+    uint64_t ph[4] = {0, 0, 0, 0}, tprev = 0;
+    auto mark = [&](int k) {
+        if (a.abl & 8) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (k >= 0) ph[k] += t - tprev;
+            tprev = t;
         }
-        uint32_t x = n;
+    };
+    // ---- pipeline stages
+    uint32_t dfirst = 0xffffffffu, dlast = 0;  // directory entries of one chunk (thread tid < nu: term tid)
+    auto load_dir = [&](uint32_t jx) {
+        dfirst = 0xffffffffu;
+        dlast = 0;
+        if (jx < je && tid < nu && !(a.abl & 4)) {
+            const uint64_t o = (uint64_t)tid * a.nchunks + (uint64_t)jx * every;
+            dfirst = a.first[o];
+            dlast = a.last[o];
+        }
+    };
+    uint32_t scan_x = 0, scan_n = 0;
+    auto prefix1 = [&](uint32_t bf) {  // wave scan of the per-term counts
+        scan_n = dfirst != 0xffffffffu ? dlast - dfirst + 1u : 0u;
+        uint32_t x = scan_n;
 #pragma unroll
         for (uint32_t o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o);
             if (lane >= o) x += y;
         }
-        if (lane == 63) s_wsum[wave] = x;
-        for (uint32_t i = tid; i < B * kTaRow; i += kTaThreads) s_acc[i] = __uint_as_float(kTaSent);
-        __syncthreads();
+        scan_x = x;
+        if (lane == 63) s_wsum[bf][wave] = x;
+    };
+    auto prefix2 = [&](uint32_t bf) {  // after a barrier: block offsets
         uint32_t T = 0, wb = 0;
 #pragma unroll
         for (uint32_t w = 0; w < kTaWaves; ++w) {
-            const uint32_t sw = s_wsum[w];
+            const uint32_t sw = s_wsum[bf][w];
             wb += w < wave ? sw : 0u;
             T += sw;
         }
-        if (tid < nu) s_soff[tid] = wb + x - n;
-        if (tid == 0) s_soff[nu] = T;
+        if (tid < nu) {
+            s_soff[bf][tid] = wb + scan_x - scan_n;
+            s_n[bf][tid] = scan_n;
+            s_pf[bf][tid] = scan_n ? my_toff + dfirst : 0ull;
+        }
+        if (tid == 0) s_soff[bf][nu] = T;
+    };
+    auto term_of = [&](uint32_t bf, uint32_t i) {  // the last term whose range starts at or before i
+        uint32_t lo = 0, hi = nu;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_soff[bf][mid] <= i) lo = mid; else hi = mid;
+        }
+        return lo;
+    };
+    constexpr uint32_t kPer = kTaStage / kTaThreads;
+    uint32_t sv[kPer], uv[kPer], jv[kPer], pv[kPer], nv[kPer];
+    float tv[kPer], dv[kPer];
+    auto load_stage = [&](uint32_t bf) {
+        const uint32_t T = s_soff[bf][nu];
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t i = tid + k * kTaThreads;
+            sv[k] = uv[k] = jv[k] = 0u;
+            pv[k] = nv[k] = 0xffffffffu;
+            tv[k] = dv[k] = 0.0f;
+            if (i < T) {
+                const uint32_t u = term_of(bf, i), j = i - s_soff[bf][u];
+                const uint64_t g = s_pf[bf][u] + j;
+                uv[k] = u;
+                jv[k] = j;
+                if (a.abl & 2) {
+                    sv[k] = (uint32_t)g;
+                    continue;
+                }
+                sv[k] = a.pslot[g];
+                tv[k] = a.ptf[g];
+                dv[k] = a.pdl[g];
+                if (a.runs) {  // neighbours in the run: a re-added document repeats its slot
+                    if (j > 0) pv[k] = a.pslot[g - 1];
+                    if (j + 1 < s_n[bf][u]) nv[k] = a.pslot[g + 1];
+                }
+            }
+        }
+    };
+    // ---- prologue: chunk jb's offsets and postings, chunk jb+1's directory entries
+    uint32_t cur = 0;
+    if (jb < je) {
+        load_dir(jb);
+        prefix1(0);
         __syncthreads();
-        const bool staged = T <= kTaStage;
-        if (staged) {
-            // all loads first (kPer per thread in flight), then the arithmetic
-            constexpr uint32_t kPer = kTaStage / kTaThreads;
-            uint32_t sv[kPer];
-            float tv[kPer], dv[kPer];
+        prefix2(0);
+        __syncthreads();
+        load_stage(0);
+        load_dir(jb + 1);
+    }
+    for (uint32_t jj = jb; jj < je; ++jj, cur ^= 1u) {
+        const uint32_t nxt = cur ^ 1u, c0 = jj * every * kTaCh;
+        const uint32_t T = s_soff[cur][nu];
+        __syncthreads();  // (1) the previous chunk's rounds are done: the map is free
+        mark(-1);
+        {
+            uint4* mp = (uint4*)s_tmap;
+            const uint4 sent4 = make_uint4(kTaSent, kTaSent, kTaSent, kTaSent);
+            for (uint32_t i = tid; i < nu * (kTaCh / 4); i += kTaThreads) mp[i] = sent4;
+        }
+        if (tid == 0) s_slow = 0;
+        prefix1(nxt);  // directory of chunk jj+1 (loaded one chunk ago)
+        __syncthreads();  // (2)
+        mark(0);
+        {
+            bool slow = false;
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k) {
                 const uint32_t i = tid + k * kTaThreads;
-                sv[k] = 0u;
-                tv[k] = dv[k] = 0.0f;
-                if (i < T) {
-                    uint32_t lo = 0, hi = nu;  // the last term whose staging range starts at or before i
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_soff[mid] <= i) lo = mid; else hi = mid;
+                if (i < T && pv[k] != sv[k]) s_tmap[uv[k] * kTaCh + (sv[k] - c0)] = tfc_of(tv[k], dv[k]);
+                slow = slow || (i < T && nv[k] == sv[k]);
+            }
+            for (uint32_t i = kTaStage + tid; i < T; i += kTaThreads) {  // past the register stage: from HBM
+                const uint32_t u = term_of(cur, i), j = i - s_soff[cur][u];
+                const uint64_t g = s_pf[cur][u] + j;
+                const uint32_t s = a.pslot[g];
+                if (j == 0 || a.pslot[g - 1] != s) s_tmap[u * kTaCh + (s - c0)] = tfc_of(a.ptf[g], a.pdl[g]);
+                slow = slow || (j + 1 < s_n[cur][u] && a.pslot[g + 1] == s);
+            }
+            if (slow) s_slow = 1u;
+        }
+        prefix2(nxt);
+        __syncthreads();  // (3)
+        mark(1);
+        load_stage(nxt);  // chunk jj+1's postings: consumed after this chunk's rounds
+        load_dir(jj + 2);
+        // 3. rounds; acc = kTaSent until the document's first contribution
+        float acc[kTaQW];
+#pragma unroll
+        for (uint32_t m = 0; m < kTaQW; ++m) acc[m] = __uint_as_float(kTaSent);
+        if (a.abl & 1) {
+        } else if (!s_slow && rmax <= 16) {
+            // 8 rounds at a time: all 4 x 8 map reads issued, then the folds in
+            // round order per query; a finished query reads the empty row.
+            // Branch-free: the terms come from lane-resident registers.
+            for (uint32_t rb = 0; rb < rmax; rb += 8) {
+                float tf[kTaQW][8];
+#pragma unroll
+                for (uint32_t m = 0; m < kTaQW; ++m)
+#pragma unroll
+                    for (uint32_t k = 0; k < 8; ++k) {
+                        const uint32_t r = rb + k;
+                        const uint32_t uu = __builtin_amdgcn_readlane(lr_u, m * 16 + (r & 15u));
+                        tf[m][k] = s_tmap[(r < ql[m] ? uu : kSpU) * kTaCh + lane];
                     }
-                    const uint64_t g = s_pf[lo] + (i - s_soff[lo]);
-                    sv[k] = a.pslot[g];
-                    tv[k] = a.ptf[g];
-                    dv[k] = a.pdl[g];
-                }
-            }
 #pragma unroll
-            for (uint32_t k = 0; k < kPer; ++k) {
-                const uint32_t i = tid + k * kTaThreads;
-                if (i < T) {
-                    st_slot[i] = (uint8_t)(sv[k] - c0);
-                    st_tfc[i] = tfc_of(tv[k], dv[k]);
-                }
-            }
-            __syncthreads();
-        }
-        // Rounds (sparse.rs:167-190): round r adds every query's r-th term.
-        // Items of a round = (query, posting) pairs over the wave's queries;
-        // distinct items touch distinct (query, slot) accumulators except a
-        // re-added document's adjacent postings, which the run's first item
-        // folds in order.
-        uint32_t qp0 = 0, qlen = 0;
-        if (has_q) {
-            qp0 = s_qp[myq];
-            qlen = s_qp[myq + 1] - qp0;
-        }
-        uint32_t rmax = qlen;
+                for (uint32_t m = 0; m < kTaQW; ++m)
 #pragma unroll
-        for (uint32_t o = 1; o < 8; o <<= 1) rmax = max(rmax, (uint32_t)__shfl_xor(rmax, o));
-        rmax = __builtin_amdgcn_readfirstlane(rmax);
-        auto rounds = [&](auto staged_tag) {
-            constexpr bool ST = decltype(staged_tag)::value;
-            auto slot_at = [&](uint64_t i) -> uint32_t { return ST ? (uint32_t)st_slot[i] : a.pslot[i] - c0; };
-            auto tfc_at = [&](uint64_t i) -> float { return ST ? st_tfc[i] : tfc_of(a.ptf[i], a.pdl[i]); };
+                    for (uint32_t k = 0; k < 8; ++k) {
+                        const uint32_t ln = m * 16 + ((rb + k) & 15u);
+                        const float v = __uint_as_float(__builtin_amdgcn_readlane(lr_v, ln));
+                        const float idf = __uint_as_float(__builtin_amdgcn_readlane(lr_idf, ln));
+                        // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`
+                        const bool hit = __float_as_uint(tf[m][k]) != kTaSent;
+                        const float sc = v * tf[m][k] * idf;
+                        const float first = 0.0f + sc, more = acc[m] + sc;
+                        const float nvl = __float_as_uint(acc[m]) == kTaSent ? first : more;
+                        acc[m] = hit ? nvl : acc[m];
+                    }
+            }
+        } else {
+            // a re-added document's run (every posting of (term, document) in run order, from HBM),
+            // or a query with more than 16 live terms
             for (uint32_t r = 0; r < rmax; ++r) {
-                uint32_t cnt = 0;
-                uint64_t base = 0;
-                float v = 0.0f, idf = 0.0f;
-                if (r < qlen) {
-                    const uint32_t p = qp0 + r, u = s_qb[p];
-                    cnt = s_n[u];
-                    base = ST ? (uint64_t)s_soff[u] : s_pf[u];
-                    v = s_qv[p];
-                    idf = s_qidf[p];
-                }
-                uint32_t inc = cnt;
 #pragma unroll
-                for (uint32_t o = 1; o < 8; o <<= 1) {
-                    const uint32_t y = __shfl_up(inc, o);
-                    if (lane >= o) inc += y;
-                }
-                uint32_t e[8];
-#pragma unroll
-                for (uint32_t m = 0; m < 8; ++m) e[m] = __builtin_amdgcn_readlane(inc, m);
-                const uint32_t tot = e[7];
-                const uint32_t base_lo = (uint32_t)base, base_hi = (uint32_t)(base >> 32);
-                constexpr uint32_t kU = 4;
-                for (uint32_t it0 = 0; it0 < tot; it0 += 64u * kU) {
-                    uint32_t ap[kU], jx[kU], cm[kU], sl[kU];
-                    uint64_t ix[kU];
-                    float vm[kU], dm[kU], tf[kU], ac[kU];
-                    bool ok[kU];
-#pragma unroll
-                    for (uint32_t u = 0; u < kU; ++u) {
-                        const uint32_t it = it0 + u * 64u + lane;
-                        uint32_t m = 0, start = 0;
-#pragma unroll
-                        for (uint32_t mm = 0; mm < 7; ++mm)
-                            if (it >= e[mm]) {
-                                m = mm + 1;
-                                start = e[mm];
-                            }
-                        jx[u] = it - start;
-                        cm[u] = __shfl(cnt, m);
-                        vm[u] = __shfl(v, m);
-                        dm[u] = __shfl(idf, m);
-                        const uint64_t bm = (uint64_t)(uint32_t)__shfl(base_lo, m) |
-                                            ((uint64_t)(uint32_t)__shfl(base_hi, m) << 32);
-                        ix[u] = bm + jx[u];
-                        ok[u] = it < tot;
-                        ap[u] = (wave + kTaWaves * m) * kTaRow;
+                for (uint32_t m = 0; m < kTaQW; ++m) {
+                    const uint4 rec = qrec_at(r < ql[m] ? qp0[m] + r : pdummy);
+                    const uint32_t u = rec.x;
+                    const float t = s_tmap[u * kTaCh + lane];
+                    if (__float_as_uint(t) == kTaSent) continue;
+                    const float v = __uint_as_float(rec.y), idf = __uint_as_float(rec.z);
+                    if (!s_slow) {  // one posting per (term, document)
+                        const float sc = v * t * idf;
+                        acc[m] = __float_as_uint(acc[m]) == kTaSent ? 0.0f + sc : acc[m] + sc;
+                        continue;
                     }
-#pragma unroll
-                    for (uint32_t u = 0; u < kU; ++u) {
-                        sl[u] = ok[u] ? slot_at(ix[u]) : 0u;
-                        const uint32_t prev = ok[u] && jx[u] > 0 ? slot_at(ix[u] - 1) : 0xffffffffu;
-                        ok[u] = ok[u] && prev != sl[u];  // not the first of a re-added document's run: folded by it
-                        tf[u] = ok[u] ? tfc_at(ix[u]) : 0.0f;
-                        ap[u] += sl[u];
-                        ac[u] = ok[u] ? s_acc[ap[u]] : 0.0f;
+                    const uint32_t n = s_n[cur][u];
+                    const uint64_t pf = s_pf[cur][u];
+                    uint32_t lo = 0, hi = n;  // lower_bound(slot) in the term's postings of this chunk
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (a.pslot[pf + mid] < c0 + lane) lo = mid + 1; else hi = mid;
                     }
-#pragma unroll
-                    for (uint32_t u = 0; u < kU; ++u) {
-                        if (!ok[u]) continue;
-                        // calculate_bm25_score: query_tf * tf_component * idf;
-                        // `or_insert(0.0) += s`: the first contribution is 0.0 + s
-                        float acc = ac[u];
-                        const float s0 = vm[u] * tf[u] * dm[u];
-                        acc = __float_as_uint(acc) == kTaSent ? 0.0f + s0 : acc + s0;
-                        for (uint32_t t = jx[u] + 1; t < cm[u] && slot_at(ix[u] - jx[u] + t) == sl[u]; ++t) {
-                            const float s1 = vm[u] * tfc_at(ix[u] - jx[u] + t) * dm[u];
-                            acc = acc + s1;
-                        }
-                        s_acc[ap[u]] = acc;
+                    for (uint32_t j = lo; j < n && a.pslot[pf + j] == c0 + lane; ++j) {
+                        const float sc = v * tfc_of(a.ptf[pf + j], a.pdl[pf + j]) * idf;
+                        acc[m] = __float_as_uint(acc[m]) == kTaSent ? 0.0f + sc : acc[m] + sc;
                     }
                 }
             }
-        };
-        if (staged)
-            rounds(std::true_type{});
-        else
-            rounds(std::false_type{});
-        __syncthreads();
-        if constexpr (MODE == 0) {
-            constexpr uint32_t G = kTaCh / kTaGrp;
-            for (uint32_t i = tid; i < B * G; i += kTaThreads) {
-                const uint32_t q = i / G, g = i % G;
-                uint64_t best = 0;
+        }
+        mark(2);
+        // 4. selection: (query wave + 16 m, slot c0 + lane)
+        const uint32_t slot = c0 + lane;
 #pragma unroll
-                for (uint32_t s = 0; s < kTaGrp; ++s) {
-                    const uint32_t slot = g * kTaGrp + s;
-                    const float f = s_acc[q * kTaRow + slot];
-                    if (__float_as_uint(f) != kTaSent) best = max(best, sp_key(f, c0 + slot));
+        for (uint32_t m = 0; m < kTaQW; ++m) {
+            const uint32_t q = wave + kTaWaves * m;
+            if (q >= B) break;
+            const uint64_t key = __float_as_uint(acc[m]) != kTaSent ? sp_key(acc[m], slot) : 0ull;
+            if constexpr (MODE == 0) {
+                uint64_t best = key;
+#pragma unroll
+                for (uint32_t o = 1; o < kTaGrp; o <<= 1) {
+                    const uint32_t lo32 = __shfl_xor((uint32_t)best, o), hi32 = __shfl_xor((uint32_t)(best >> 32), o);
+                    best = max(best, ((uint64_t)hi32 << 32) | lo32);
                 }
-                a.smp[(uint64_t)q * a.S + (uint64_t)jj * G + g] = best;
-            }
-        } else if constexpr (MODE == 1) {
-            for (uint32_t i = tid; i < B * kTaCh; i += kTaThreads) {
-                const uint32_t q = i / kTaCh, slot = i % kTaCh;
-                const float f = s_acc[q * kTaRow + slot];
-                if (__float_as_uint(f) == kTaSent) continue;
-                const uint64_t key = sp_key(f, c0 + slot);
-                if (key >= s_tau[q]) {
+                if ((lane & (kTaGrp - 1)) == 0)
+                    a.smp[(uint64_t)q * a.S + (uint64_t)jj * (kTaCh / kTaGrp) + lane / kTaGrp] = best;
+            } else if constexpr (MODE == 1) {
+                if (key != 0ull && key >= s_tau[q]) {
                     const uint32_t pos = atomicAdd(&a.counts[q], 1u);
                     if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key;
                 }
-            }
-        } else {
-            for (uint32_t slot = tid; slot < kTaCh; slot += kTaThreads) {
-                if (c0 + slot >= a.N) continue;
-                const float f = s_acc[a.dense_q * kTaRow + slot];
-                a.dense[c0 + slot] = __float_as_uint(f) == kTaSent ? 0ull : sp_key(f, c0 + slot);
+            } else {
+                if (q == a.dense_q && slot < a.N) a.dense[slot] = key;
             }
         }
+        mark(3);
     }
+    if ((a.abl & 8) && tid == 0)
+        for (int k = 0; k < 4; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
 }
 
 // tau[q] = the kk-th largest sampled key (0 when fewer than kk matched): each
@@ -633,6 +708,7 @@ struct gvdb_sparse {
     float *d_ptf = nullptr, *d_pdl = nullptr;
     uint64_t cap_post = 0, cap_ptf = 0, cap_pdl = 0;
     uint64_t version = 0, inv_version = ~0ull;
+    bool runs = false;  // some (term, document) has more than one posting (re-added ids)
     std::unordered_map<uint32_t, uint64_t> toff;  // term -> its first posting
     // search scratch
     void* scratch = nullptr;
@@ -735,7 +811,8 @@ gvdb_status build_inverted(gvdb_sparse* sp, hipStream_t s) {
     SP_TRY(grow(sp->d_pdl, sp->cap_pdl, E, 0), "alloc posting dl");
     char* tmp = nullptr;
     const size_t a4 = ((size_t)E * 4 + 255) & ~(size_t)255;
-    SP_TRY(hipMalloc((void**)&tmp, 4 * a4 + cub_bytes), "alloc inverted build");
+    SP_TRY(hipMalloc((void**)&tmp, 4 * a4 + cub_bytes + 256), "alloc inverted build");
+    uint32_t* d_runs = (uint32_t*)(tmp + 4 * a4 + ((cub_bytes + 255) & ~(size_t)255));
     uint32_t* eslot = (uint32_t*)tmp;
     uint32_t* iota = (uint32_t*)(tmp + a4);
     uint32_t* keys = (uint32_t*)(tmp + 2 * a4);
@@ -748,22 +825,29 @@ gvdb_status build_inverted(gvdb_sparse* sp, hipStream_t s) {
         e = hipcub::DeviceRadixSort::SortPairs(tmp + 4 * a4, cub_bytes, sp->d_term, keys, iota, order, (int)E, 0,
                                                end_bit, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_inv_gather, dim3(2048), dim3(256), 0, s, order, eslot, sp->d_tf, sp->d_dl, E, sp->d_pslot,
-                           sp->d_ptf, sp->d_pdl);
-        e = hipGetLastError();
+        e = hipMemsetAsync(d_runs, 0, 4, s);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_inv_gather, dim3(2048), dim3(256), 0, s, order, keys, eslot, sp->d_tf, sp->d_dl, E,
+                               sp->d_pslot, sp->d_ptf, sp->d_pdl, d_runs);
+            e = hipGetLastError();
+        }
     }
+    uint32_t h_runs = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h_runs, d_runs, 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) sp->runs = h_runs != 0;
     (void)hipFree(tmp);
     if (e != hipSuccess) return sp_dev(e, "build inverted index");
     sp->inv_version = sp->version;
     return GVDB_OK;
 }
 
+// k_bm25_taat: one resident block per CU (its LDS map), each a contiguous chunk range
 uint32_t sp_grid(uint32_t tiles) {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::max<uint32_t>(1, std::min<uint32_t>(tiles, 2u * (uint32_t)cus));
+    return std::max<uint32_t>(1, std::min<uint32_t>(tiles, (uint32_t)cus));
 }
 
 // items per query bounded by the list strides: dynamic LDS for the next power of two
@@ -1113,21 +1197,28 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         const uint32_t Bg = (uint32_t)(q1 - q0);
         const uint32_t nqt = (uint32_t)h_qt.size();
         const uint32_t nu = (uint32_t)group_terms.size();
-        std::vector<uint16_t> h_qb(nqt);
-        for (uint32_t i = 0; i < nqt; ++i)
-            h_qb[i] = (uint16_t)(std::lower_bound(group_terms.begin(), group_terms.end(), h_qt[i]) - group_terms.begin());
-        std::vector<uint64_t> h_toff(nu), h_gpre(nu + 1, 0);
-        for (uint32_t u = 0; u < nu; ++u) {
-            h_toff[u] = sp->toff.at(group_terms[u]);
-            h_gpre[u + 1] = h_gpre[u] + sp->plen.at(group_terms[u]);
+        std::vector<uint32_t> h_qrec(4 * (nqt + 1), 0u);  // (group term, q_tf, idf, 0); [nqt]: the empty row
+        for (uint32_t i = 0; i < nqt; ++i) {
+            h_qrec[4 * i] =
+                (uint32_t)(std::lower_bound(group_terms.begin(), group_terms.end(), h_qt[i]) - group_terms.begin());
+            std::memcpy(&h_qrec[4 * i + 1], &h_qv[i], 4);
+            std::memcpy(&h_qrec[4 * i + 2], &h_qidf[i], 4);
         }
-        // scratch: qp | qb | qv | qidf | toff | gpre | tau | counts | fail | out_n | first | last | smp | cand |
+        h_qrec[4 * nqt] = kSpU;
+        std::vector<uint64_t> h_toff(nu), h_gpre(nu + 1, 0), h_gpre4(nu + 1, 0);
+        for (uint32_t u = 0; u < nu; ++u) {
+            const uint64_t len = sp->plen.at(group_terms[u]);
+            h_toff[u] = sp->toff.at(group_terms[u]);
+            h_gpre[u + 1] = h_gpre[u] + len;
+            h_gpre4[u + 1] = h_gpre4[u] + (len + kTaDirPer - 1) / kTaDirPer;
+        }
+        // scratch: qp | qrec | toff | gpre | gpre4 | tau | counts | fail | out_n | first | last | smp | cand |
         //          out ids | out scores
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
         const size_t dir = (size_t)nchunks * nu * 4;
-        const size_t o_qp = 0, o_qb = o_qp + al((Bg + 1) * 4), o_qv = o_qb + al(nqt * 2 + 4),
-                     o_qidf = o_qv + al(nqt * 4 + 4), o_toff = o_qidf + al(nqt * 4 + 4),
-                     o_gpre = o_toff + al(nu * 8 + 8), o_tau = o_gpre + al((nu + 1) * 8), o_cnt = o_tau + al(Bg * 8),
+        const size_t o_qp = 0, o_qrec = o_qp + al((Bg + 1) * 4), o_toff = o_qrec + al((nqt + 1) * 16),
+                     o_gpre = o_toff + al(nu * 8 + 8), o_gpre4 = o_gpre + al((nu + 1) * 8),
+                     o_tau = o_gpre4 + al((nu + 1) * 8), o_cnt = o_tau + al(Bg * 8),
                      o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_first = o_n + al(Bg * 4),
                      o_last = o_first + al(dir + 4), o_smp = o_last + al(dir + 4),
                      o_cand = o_smp + al((size_t)Bg * S * 8), o_oi = o_cand + al((size_t)Bg * kSpCand * 8),
@@ -1141,12 +1232,11 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         }
         char* base = (char*)sp->scratch;
         SP_TRY(hipMemcpyAsync(base + o_qp, h_qp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
+        SP_TRY(hipMemcpyAsync(base + o_qrec, h_qrec.data(), (nqt + 1) * 16, hipMemcpyHostToDevice, s), "qrec");
         if (nqt) {
-            SP_TRY(hipMemcpyAsync(base + o_qb, h_qb.data(), nqt * 2, hipMemcpyHostToDevice, s), "qb");
-            SP_TRY(hipMemcpyAsync(base + o_qv, h_qv.data(), nqt * 4, hipMemcpyHostToDevice, s), "qv");
-            SP_TRY(hipMemcpyAsync(base + o_qidf, h_qidf.data(), nqt * 4, hipMemcpyHostToDevice, s), "qidf");
             SP_TRY(hipMemcpyAsync(base + o_toff, h_toff.data(), nu * 8, hipMemcpyHostToDevice, s), "toff");
             SP_TRY(hipMemcpyAsync(base + o_gpre, h_gpre.data(), (nu + 1) * 8, hipMemcpyHostToDevice, s), "gpre");
+            SP_TRY(hipMemcpyAsync(base + o_gpre4, h_gpre4.data(), (nu + 1) * 8, hipMemcpyHostToDevice, s), "gpre4");
         }
         SP_TRY(hipMemsetAsync(base + o_cnt, 0, Bg * 4, s), "counts");
         TaArgs a{};
@@ -1157,13 +1247,14 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         a.nchunks = nchunks;
         a.toff = (const uint64_t*)(base + o_toff);
         a.gpre = (const uint64_t*)(base + o_gpre);
+        a.gpre4 = (const uint64_t*)(base + o_gpre4);
         a.first = (uint32_t*)(base + o_first);
         a.last = (uint32_t*)(base + o_last);
         a.nu = nu;
         a.qp = (const uint32_t*)(base + o_qp);
-        a.qb = (const uint16_t*)(base + o_qb);
-        a.qv = (const float*)(base + o_qv);
-        a.qidf = (const float*)(base + o_qidf);
+        a.qrec = (const uint4*)(base + o_qrec);
+        a.nqt = nqt;
+        a.runs = sp->runs ? 1u : 0u;
         a.B = Bg;
         a.k1 = sp->k1;
         a.b = sp->b;
@@ -1174,11 +1265,25 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         a.tau = (const uint64_t*)(base + o_tau);
         a.counts = (uint32_t*)(base + o_cnt);
         a.cand = (uint64_t*)(base + o_cand);
+        {
+            static const uint32_t abl = [] {
+                const char* e = getenv("GVDB_BM25_ABL");
+                return e ? (uint32_t)atoi(e) : 0u;
+            }();
+            a.abl = abl;
+        }
+        std::vector<uint64_t> h_prof;
+        uint64_t* d_prof = nullptr;
+        if (a.abl & 8) {
+            SP_TRY(hipMalloc((void**)&d_prof, 1024 * 8 * 8), "prof");
+            SP_TRY(hipMemsetAsync(d_prof, 0, 1024 * 8 * 8, s), "prof");
+            a.prof = d_prof;
+        }
         if (nu) {
             SP_TRY(hipMemsetAsync(a.first, 0xff, dir, s), "directory");
-            const uint64_t P = h_gpre[nu];
-            const uint32_t dgrid = (uint32_t)std::min<uint64_t>((P + 255) / 256, 8u * sp_grid(1u << 30));
-            hipLaunchKernelGGL(k_ta_dir, dim3(std::max<uint32_t>(1u, dgrid)), dim3(256), 0, s, a);
+            const uint64_t threads = h_gpre4[nu];
+            if (threads > 0xffffffffull * 256) return report_status(GVDB_ERR_INVALID_ARGUMENT, "posting runs too long");
+            hipLaunchKernelGGL(k_ta_dir, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, a);
             SP_TRY(hipGetLastError(), "bm25 directory");
         }
         hipLaunchKernelGGL(k_bm25_taat<0>, dim3(sp_grid(nsamp)), dim3(kTaThreads), 0, s, a);
@@ -1187,6 +1292,18 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         SP_TRY(hipGetLastError(), "bm25 tau");
         hipLaunchKernelGGL(k_bm25_taat<1>, dim3(sp_grid(nchunks)), dim3(kTaThreads), 0, s, a);
         SP_TRY(hipGetLastError(), "bm25 emit");
+        if (d_prof) {
+            h_prof.resize(1024 * 8);
+            SP_TRY(hipMemcpyAsync(h_prof.data(), d_prof, 1024 * 8 * 8, hipMemcpyDeviceToHost, s), "prof");
+            SP_TRY(hipStreamSynchronize(s), "prof");
+            double acc[4] = {0, 0, 0, 0};
+            const uint32_t G = sp_grid(nchunks);
+            for (uint32_t g = 0; g < G; ++g)
+                for (int k = 0; k < 4; ++k) acc[k] += (double)h_prof[g * 8 + k];
+            fprintf(stderr, "[bm25 prof] per block, shader clock cycles: dir %.0f stage %.0f rounds %.0f select %.0f\n",
+                    acc[0] / G, acc[1] / G, acc[2] / G, acc[3] / G);
+            (void)hipFree(d_prof);
+        }
         uint64_t* d_oi = (uint64_t*)(base + o_oi);
         float* d_os = (float*)(base + o_os);
         uint32_t* d_n = (uint32_t*)(base + o_n);

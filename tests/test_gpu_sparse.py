@@ -248,3 +248,12 @@ def test_rrf_over_capacity_is_an_error(sp_mod):
     big = [[(i, 1.0) for i in range(2100)]]
     with pytest.raises(Exception, match="4096"):
         sp_mod.rrf_fuse(big, big, [], 60.0, 10)
+
+
+def test_bm25_long_queries(sp_mod, oracle_mod):
+    """Queries of 17-60 live terms (past the 16 lane-resident rounds of the
+    fast path), mixed with short ones in the same launch group."""
+    docs = zipf_docs(35, 15_000, 1500, 40)
+    g, o = build(sp_mod, oracle_mod, docs)
+    qs = queries(36, 20, 1500, 17, 61) + queries(37, 20, 1500, 1, 5)
+    check_batch(sp_mod, g, o, qs, 15)
