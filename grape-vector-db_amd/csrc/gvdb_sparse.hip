@@ -64,14 +64,14 @@ constexpr uint32_t kTaThreads = 1024;           // one block per CU: 16 waves; w
 constexpr uint32_t kTaWaves = kTaThreads / 64;
 constexpr uint32_t kTaQW = 4;                   // queries per wave
 constexpr uint32_t kTaQ = kTaWaves * kTaQW;     // queries per launch group
-constexpr uint32_t kTaStage = 4096;             // postings per chunk staged through registers (more: from HBM)
+constexpr uint32_t kTaStage = 4096;             // entries per chunk staged through registers (more: from HBM)
 constexpr uint32_t kTaGrp = 8;                  // sample pass: one max key per 8 slots
-constexpr uint32_t kTaDirPer = 4;               // directory pass: postings per thread
-constexpr uint32_t kTaSent = 0x7fbadbadu;       // accumulator "no posting yet": a signalling NaN, never an arithmetic result
+constexpr uint32_t kTaCptrLds = 512;            // chunks per block (their ranges cached in LDS)
+constexpr uint32_t kTaSent = 0x7fbadbadu;       // map "no posting": a signalling NaN, never an arithmetic result
 constexpr uint32_t kSpQT = 1024;                // query terms per launch group (LDS)
 constexpr uint32_t kSpU = 511;                  // distinct terms per launch group (map row kSpU stays empty)
 constexpr uint32_t kSpCand = 4096;              // candidates per query (LDS sort)
-constexpr uint32_t kSpTopLocal = 8;             // per-thread keys kept by the tau pass
+constexpr uint32_t kSpTopLocal = 2;             // per-thread keys kept by the tau pass
 static_assert(kSpU < kTaThreads, "one thread per group term in the directory row");
 static_assert(kTaCh == 64, "a chunk slot is a lane");
 
@@ -89,48 +89,64 @@ __device__ __forceinline__ float sp_score(uint64_t key) {
 __device__ __forceinline__ uint32_t sp_slot(uint64_t key) { return ~(uint32_t)key; }
 
 // ---------------------------------------------------------------------------
-// inverted index build: entries sorted (stable) by term -> posting runs
+// Blocked inverted index: the entries of each 64-slot chunk sorted by (term,
+// slot, add order) -- the inverted index restricted to the chunk's documents
+// -- by one stable radix sort of (chunk, term) keys over the slot-ordered
+// forward entries.  A chunk's entries stay the forward range
+// [ptr[64c], ptr[64c + 64]).
 // ---------------------------------------------------------------------------
-__global__ void k_inv_prep(const uint64_t* __restrict__ ptr, uint32_t N, uint32_t* __restrict__ eslot,
-                           uint32_t* __restrict__ iota) {
+__global__ void k_blk_keys(const uint64_t* __restrict__ ptr, uint32_t N, const uint32_t* __restrict__ term,
+                           uint64_t* __restrict__ keys, uint32_t* __restrict__ iota, uint32_t* __restrict__ eslot) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= N) return;
     for (uint64_t e = ptr[s], e1 = ptr[s + 1]; e < e1; ++e) {
-        eslot[e] = s;
+        keys[e] = ((uint64_t)(s / kTaCh) << 32) | term[e];
         iota[e] = (uint32_t)e;
+        eslot[e] = s;
     }
 }
 
-__global__ void k_inv_gather(const uint32_t* __restrict__ order, const uint32_t* __restrict__ keys,
+__global__ void k_blk_gather(const uint32_t* __restrict__ order, const uint64_t* __restrict__ keys,
                              const uint32_t* __restrict__ eslot, const float* __restrict__ tf,
-                             const float* __restrict__ dl, uint64_t E, uint32_t* __restrict__ pslot,
-                             float* __restrict__ ptf, float* __restrict__ pdl, uint32_t* __restrict__ runs) {
+                             const float* __restrict__ dl, uint64_t E, uint32_t* __restrict__ cterm,
+                             uint8_t* __restrict__ cslot, float* __restrict__ ctf, float* __restrict__ cdl,
+                             uint32_t* __restrict__ runs) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t e = order[i], s = eslot[e];
-        pslot[i] = s;
-        ptf[i] = tf[e];
-        pdl[i] = dl[e];
+        cterm[i] = (uint32_t)keys[i];
+        cslot[i] = (uint8_t)(s % kTaCh);
+        ctf[i] = tf[e];
+        cdl[i] = dl[e];
         if (i > 0 && keys[i] == keys[i - 1] && eslot[order[i - 1]] == s) *runs = 1u;  // same term, same document
     }
 }
 
+// tf_component of every entry for the index's current avgdl (calculate_bm25_score,
+// sparse.rs:215-218: (tf * (k1 + 1)) / (tf + k1 * (1 - b + b * (dl / avgdl))))
+__global__ void k_blk_tfc(const float* __restrict__ ctf, const float* __restrict__ cdl, uint64_t E, float k1, float b,
+                          float avgdl, float* __restrict__ ctfc) {
+    const float k1p1 = k1 + 1.0f, omb = 1.0f - b;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
+        const float t = ctf[i];
+        ctfc[i] = (t * k1p1) / (t + k1 * (omb + b * (cdl[i] / avgdl)));
+    }
+}
+
 struct TaArgs {
-    const uint32_t* pslot;  // inverted index: posting slot / tf / document_length
-    const float* ptf;
-    const float* pdl;
+    const uint64_t* cptr;   // [nchunks+1] entry range of each chunk (= forward ptr every 64 slots)
+    const uint32_t* cterm;  // blocked entries: term, slot within the chunk, tf_component
+    const uint8_t* cslot;
+    const float* ctfc;
     uint32_t N;             // slots
     uint32_t nchunks;
-    const uint64_t* toff;   // [nu] first posting of each group term
-    const uint64_t* gpre;   // [nu+1] prefix of the group terms' posting counts
-    const uint64_t* gpre4;  // [nu+1] prefix of ceil(count / kTaDirPer) (directory pass threads)
-    uint32_t* first;        // [nu][nchunks] first / last posting (relative to toff) inside a chunk
-    uint32_t* last;
+    uint64_t n_entries;     // > 0
+    const uint32_t* ut;     // [nu] the group's distinct live terms
     uint32_t nu;
     const uint32_t* qp;     // [B+1] offsets into qrec
+    const uint32_t* perm;   // [B] query of each wave slot (w + 16 m)
     const uint4* qrec;      // [nqt+1] per query term: (group term, q_tf bits, idf bits, 0); [nqt] = the empty row
     uint32_t nqt;
     uint32_t B;
-    float k1, b, avgdl;
     uint32_t every;         // sample pass: chunk stride
     uint64_t* smp;          // sample: [B][S] keys (0 = unmatched)
     uint32_t S;
@@ -139,98 +155,89 @@ struct TaArgs {
     uint64_t* cand;         // emit: [B][kSpCand]
     uint64_t* dense;        // dense mode: [N] keys of query `dense_q`
     uint32_t dense_q;
-    uint32_t runs;          // the index holds a (term, document) run longer than one posting (a re-added id)
-    uint32_t abl;           // timing probe only (GVDB_BM25_ABL): 1 skip rounds, 2 skip staging loads, 4 skip dir loads,
-                            // 8 phase clocks into prof
+    uint32_t runs;          // the index holds a (term, document) run longer than one entry (a re-added id)
+    uint32_t abl;           // timing probe only (GVDB_BM25_ABL): 1 skip rounds, 2 skip entry loads, 8 phase clocks
     uint64_t* prof;         // [gridDim][8] cycles per phase (wave 0), with abl & 8
 };
 
-// Directory: each thread takes kTaDirPer consecutive postings of one term; the
-// posting that opens (closes) a chunk's run writes first (last).  `first` is
-// preset to ~0 = "no posting of the term in the chunk".  Term-major rows, so a
-// dense term's consecutive chunks are written by neighbouring threads.
-__global__ __launch_bounds__(256) void k_ta_dir(TaArgs a) {
-    __shared__ uint64_t s_pre4[kSpU + 2], s_pre[kSpU + 2];
-    const uint32_t nu = a.nu;
-    for (uint32_t i = threadIdx.x; i <= nu; i += 256u) {
-        s_pre4[i] = a.gpre4[i];
-        s_pre[i] = a.gpre[i];
-    }
-    __syncthreads();
-    const uint64_t gi = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (gi >= s_pre4[nu]) return;
-    uint32_t lo = 0, hi = nu;  // the last term whose thread range starts at or before gi
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_pre4[mid] <= gi) lo = mid; else hi = mid;
-    }
-    const uint32_t len = (uint32_t)(s_pre[lo + 1] - s_pre[lo]);
-    const uint32_t j0 = (uint32_t)(gi - s_pre4[lo]) * kTaDirPer;
-    const uint32_t* run = a.pslot + a.toff[lo];
-    uint32_t ch[kTaDirPer + 2];  // chunks of postings j0-1 .. j0+kTaDirPer
-#pragma unroll
-    for (uint32_t k = 0; k < kTaDirPer + 2; ++k) {
-        const uint32_t j = j0 + k - 1;  // j0 - 1 wraps to ~0 for j0 == 0
-        ch[k] = (k > 0 || j0 > 0) && j0 + k - 1 < len ? run[j] / kTaCh : 0xffffffffu;
-    }
-    uint32_t* fr = a.first + (uint64_t)lo * a.nchunks;
-    uint32_t* lr = a.last + (uint64_t)lo * a.nchunks;
-#pragma unroll
-    for (uint32_t k = 1; k <= kTaDirPer; ++k) {
-        if (j0 + k - 1 >= len) break;
-        if (ch[k] != ch[k - 1]) fr[ch[k]] = j0 + k - 1;
-        if (ch[k] != ch[k + 1]) lr[ch[k]] = j0 + k - 1;
-    }
-}
+constexpr uint32_t kHashSlots = 1024;  // LDS open-addressing table of the group's terms (load <= 1/2)
+__device__ __forceinline__ uint32_t term_hash(uint32_t t) { return (t * 0x9E3779B1u) >> 22; }
 
 // MODE 0: sample (every `every`-th chunk -> per 8 slots the max key -> smp),
 // 1: emit (key >= tau -> cand), 2: dense keys of query `dense_q`.
 //
 // One block per CU walks a contiguous range of 64-slot chunks.  Per chunk:
-//   1. directory row -> each group term's postings in the chunk;
-//   2. a (term x slot) LDS map receives tf_component (calculate_bm25_score's
-//      query-independent part, sparse.rs:215-218) of each (term, document)'s
-//      first posting; kTaSent = no posting;
-//   3. rounds: lane = slot, wave w owns queries w + 16 m (m < 4),
+//   1. its blocked entries (all terms, ~30 per document) stream in; an LDS
+//      hash of the group's terms keeps those of the batch, whose
+//      tf_component lands in an LDS (group term x slot) map (kTaSent = no
+//      posting; the first entry of a re-added document's run);
+//   2. rounds: lane = slot, wave w owns queries w + 16 m (m < 4),
 //      accumulators in registers.  Round r adds query q's r-th term: one map
 //      read, acc = acc + q_tf * tfc * idf -- per document exactly the
-//      reference's fold (sparse.rs:167-190).  A re-added document's run of
-//      postings (rare: the index records whether any exists) is folded from
-//      the posting run in HBM, in order;
-//   4. selection by the mode.
-// Software pipeline: while chunk j's rounds run, the postings of chunk j+1
-// and the directory entries of chunk j+2 are in flight into registers.
+//      reference's fold (sparse.rs:167-190; acc starts at 0.0 = or_insert);
+//      a run of several entries (rare: the index records whether any exists)
+//      is folded from HBM in order;
+//   3. selection by the mode.
+// Software pipeline: while chunk j's rounds run, chunk j+1's entries are in
+// flight into registers.
 template <int MODE>
 __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     __shared__ __attribute__((aligned(16))) float s_tmap[(kSpU + 1) * kTaCh];  // row kSpU: the empty row
-    __shared__ uint64_t s_tau[MODE == 1 ? kTaQ : 1];
-    __shared__ uint32_t s_n[2][kSpU + 1], s_soff[2][kSpU + 1];  // double-buffered: chunk j / j+1
-    __shared__ uint64_t s_pf[2][kSpU + 1];
-    __shared__ uint32_t s_wsum[2][kTaWaves];
+    __shared__ uint32_t s_hkey[kHashSlots];
+    __shared__ uint32_t s_ut[kSpU];  // group term index -> term
+    __shared__ uint16_t s_hval[kHashSlots];
     __shared__ uint32_t s_slow;
+    __shared__ uint64_t s_cptr[2 * (kTaCptrLds + 1)];  // the block's chunk ranges (no HBM round trip per chunk)
     typedef const uint32_t __attribute__((address_space(4)))* cu32;
     const cu32 qp = (cu32)(uintptr_t)a.qp;  // read-only query tables: scalar loads
     const cu32 qr32 = (cu32)(uintptr_t)a.qrec;
     auto qrec_at = [&](uint32_t p) { return make_uint4(qr32[4 * p], qr32[4 * p + 1], qr32[4 * p + 2], 0u); };
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t B = a.B, nu = a.nu;
-    if constexpr (MODE == 1)
-        for (uint32_t i = tid; i < B; i += kTaThreads) s_tau[i] = a.tau[i];
-    if (tid < kTaCh) s_tmap[kSpU * kTaCh + tid] = __uint_as_float(kTaSent);
-    const float k1 = a.k1, b = a.b, avgdl = a.avgdl;
-    const float k1p1 = k1 + 1.0f, omb = 1.0f - b;  // (k1 + 1.0), (1.0 - b) as the reference evaluates them
-    auto tfc_of = [&](float tfv, float dlv) { return (tfv * k1p1) / (tfv + k1 * (omb + b * (dlv / avgdl))); };
-    // this wave's queries (uniform): term range of query wave + 16 m
-    uint32_t qp0[kTaQW], ql[kTaQW], rmax = 0;
+    const uint32_t nu = a.nu;
+    for (uint32_t i = tid; i < (kSpU + 1) * kTaCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
+    for (uint32_t i = tid; i < kHashSlots; i += kTaThreads) s_hkey[i] = 0xffffffffu;
+    __syncthreads();
+    // the group's terms (distinct): linear probing; 0xffffffff marks empty, so
+    // that term id itself is looked up through the sorted list instead
+    bool max_term = false;
+    if (tid < nu) {
+        const uint32_t t = a.ut[tid];
+        s_ut[tid] = t;
+        if (t == 0xffffffffu) {
+            max_term = true;
+        } else {
+            uint32_t h = term_hash(t);
+            while (atomicCAS(&s_hkey[h], 0xffffffffu, t) != 0xffffffffu) h = (h + 1) & (kHashSlots - 1);
+            s_hval[h] = (uint16_t)tid;
+        }
+    }
+    const bool has_max_term = __syncthreads_or(max_term);
+    auto group_of = [&](uint32_t t) -> uint32_t {  // group term index, or kSpU (not in the batch)
+        if (t == 0xffffffffu) return has_max_term ? nu - 1 : kSpU;  // the sorted list's last entry
+        uint32_t h = term_hash(t);
+        while (true) {
+            const uint32_t k = s_hkey[h];
+            if (k == t) return s_hval[h];
+            if (k == 0xffffffffu) return kSpU;
+            h = (h + 1) & (kHashSlots - 1);
+        }
+    };
+    // this wave's queries (uniform): wave slot w + 16 m holds query perm[w + 16 m]
+    // (the host balances the slots' total terms across waves)
+    const cu32 perm = (cu32)(uintptr_t)a.perm;
+    uint32_t qid[kTaQW], qp0[kTaQW], ql[kTaQW], rmax = 0;
 #pragma unroll
     for (uint32_t m = 0; m < kTaQW; ++m) {
-        const uint32_t q = wave + kTaWaves * m;
-        const bool live = q < B && (MODE != 2 || q == a.dense_q);
-        qp0[m] = live ? qp[q] : 0u;
-        ql[m] = live ? qp[q + 1] - qp0[m] : 0u;
+        qid[m] = perm[wave + kTaWaves * m];  // 0xffffffff: an empty slot
+        const bool live = qid[m] != 0xffffffffu && (MODE != 2 || qid[m] == a.dense_q);
+        qp0[m] = live ? qp[qid[m]] : 0u;
+        ql[m] = live ? qp[qid[m] + 1] - qp0[m] : 0u;
         rmax = max(rmax, ql[m]);
     }
+    uint64_t tau[kTaQW];
+#pragma unroll
+    for (uint32_t m = 0; m < kTaQW; ++m) tau[m] = MODE == 1 && qid[m] != 0xffffffffu ? a.tau[qid[m]] : 0ull;
     const uint32_t pdummy = a.nqt;  // qrec[nqt]: the empty map row, q_tf = idf = 0
     // the wave's query terms, lane-resident: lane 16 m + r holds query m's r-th term (r < 16)
     uint32_t lr_u, lr_v, lr_idf;
@@ -241,10 +248,9 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         lr_v = rec.y;
         lr_idf = rec.z;
     }
-    const uint64_t my_toff = tid < nu ? a.toff[tid] : 0ull;
     const uint32_t every = MODE == 0 ? a.every : 1u;
     const uint32_t nj = (a.nchunks + every - 1) / every;
-    // contiguous chunk range per block: the directory's term-major rows are read sequentially
+    // contiguous chunk range per block
     const uint32_t jb = (uint32_t)((uint64_t)nj * blockIdx.x / gridDim.x);
     const uint32_t je = (uint32_t)((uint64_t)nj * (blockIdx.x + 1) / gridDim.x);
     uint64_t ph[4] = {0, 0, 0, 0}, tprev = 0;
@@ -255,201 +261,166 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             tprev = t;
         }
     };
-    // ---- pipeline stages
-    uint32_t dfirst = 0xffffffffu, dlast = 0;  // directory entries of one chunk (thread tid < nu: term tid)
-    auto load_dir = [&](uint32_t jx) {
-        dfirst = 0xffffffffu;
-        dlast = 0;
-        if (jx < je && tid < nu && !(a.abl & 4)) {
-            const uint64_t o = (uint64_t)tid * a.nchunks + (uint64_t)jx * every;
-            dfirst = a.first[o];
-            dlast = a.last[o];
-        }
-    };
-    uint32_t scan_x = 0, scan_n = 0;
-    auto prefix1 = [&](uint32_t bf) {  // wave scan of the per-term counts
-        scan_n = dfirst != 0xffffffffu ? dlast - dfirst + 1u : 0u;
-        uint32_t x = scan_n;
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        scan_x = x;
-        if (lane == 63) s_wsum[bf][wave] = x;
-    };
-    auto prefix2 = [&](uint32_t bf) {  // after a barrier: block offsets
-        uint32_t T = 0, wb = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kTaWaves; ++w) {
-            const uint32_t sw = s_wsum[bf][w];
-            wb += w < wave ? sw : 0u;
-            T += sw;
-        }
-        if (tid < nu) {
-            s_soff[bf][tid] = wb + scan_x - scan_n;
-            s_n[bf][tid] = scan_n;
-            s_pf[bf][tid] = scan_n ? my_toff + dfirst : 0ull;
-        }
-        if (tid == 0) s_soff[bf][nu] = T;
-    };
-    auto term_of = [&](uint32_t bf, uint32_t i) {  // the last term whose range starts at or before i
-        uint32_t lo = 0, hi = nu;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_soff[bf][mid] <= i) lo = mid; else hi = mid;
-        }
-        return lo;
-    };
+    // the host sizes the grid so that a block's range fits (je - jb <= kTaCptrLds)
+    for (uint32_t i = tid; i <= je - jb; i += kTaThreads) {
+        const uint64_t c = (uint64_t)(jb + i) * every;
+        s_cptr[2 * i] = a.cptr[min(c, (uint64_t)a.nchunks)];
+        s_cptr[2 * i + 1] = a.cptr[min(c + 1, (uint64_t)a.nchunks)];
+    }
+    __syncthreads();
+    // ---- a chunk's entries through registers, two chunks ahead (double buffer)
     constexpr uint32_t kPer = kTaStage / kTaThreads;
-    uint32_t sv[kPer], uv[kPer], jv[kPer], pv[kPer], nv[kPer];
-    float tv[kPer], dv[kPer];
-    auto load_stage = [&](uint32_t bf) {
-        const uint32_t T = s_soff[bf][nu];
+    struct Stage {
+        uint32_t t[kPer], s[kPer];  // term, slot
+        float f[kPer];              // tf_component
+        uint64_t e0, e1;            // entry range
+    };
+    Stage st0, st1;
+    uint32_t cell[kPer];  // map cells this thread wrote for the current chunk (unwritten after its rounds)
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) cell[k] = 0xffffffffu;
+    auto load_entries = [&](Stage& sg, uint32_t jx) {
+        sg.e0 = sg.e1 = 0;
+        if (jx < je) {
+            sg.e0 = s_cptr[2 * (jx - jb)];
+            sg.e1 = s_cptr[2 * (jx - jb) + 1];
+        }
+        // unconditional loads (an index past the range reads a valid entry that
+        // the build skips): no use and no register write before the chunk's
+        // turn, so the loads stay in flight
+        const uint64_t last = a.n_entries - 1;
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
-            const uint32_t i = tid + k * kTaThreads;
-            sv[k] = uv[k] = jv[k] = 0u;
-            pv[k] = nv[k] = 0xffffffffu;
-            tv[k] = dv[k] = 0.0f;
-            if (i < T) {
-                const uint32_t u = term_of(bf, i), j = i - s_soff[bf][u];
-                const uint64_t g = s_pf[bf][u] + j;
-                uv[k] = u;
-                jv[k] = j;
-                if (a.abl & 2) {
-                    sv[k] = (uint32_t)g;
-                    continue;
-                }
-                sv[k] = a.pslot[g];
-                tv[k] = a.ptf[g];
-                dv[k] = a.pdl[g];
-                if (a.runs) {  // neighbours in the run: a re-added document repeats its slot
-                    if (j > 0) pv[k] = a.pslot[g - 1];
-                    if (j + 1 < s_n[bf][u]) nv[k] = a.pslot[g + 1];
-                }
-            }
+            const uint64_t i = min(sg.e0 + tid + k * kTaThreads, last);
+            sg.t[k] = a.cterm[i];
+            sg.s[k] = a.cslot[i];
+            sg.f[k] = a.ctfc[i];
         }
     };
-    // ---- prologue: chunk jb's offsets and postings, chunk jb+1's directory entries
-    uint32_t cur = 0;
-    if (jb < je) {
-        load_dir(jb);
-        prefix1(0);
-        __syncthreads();
-        prefix2(0);
-        __syncthreads();
-        load_stage(0);
-        load_dir(jb + 1);
-    }
-    for (uint32_t jj = jb; jj < je; ++jj, cur ^= 1u) {
-        const uint32_t nxt = cur ^ 1u, c0 = jj * every * kTaCh;
-        const uint32_t T = s_soff[cur][nu];
-        __syncthreads();  // (1) the previous chunk's rounds are done: the map is free
+    bool prev_overflow = false;
+    auto chunk = [&](Stage& sg, uint32_t jj) {
+        const uint32_t c0 = jj * every * kTaCh;
+        const uint64_t ce0 = sg.e0, ce1 = sg.e1;
+        __syncthreads();  // (1) the previous chunk's rounds are done
         mark(-1);
-        {
-            uint4* mp = (uint4*)s_tmap;
-            const uint4 sent4 = make_uint4(kTaSent, kTaSent, kTaSent, kTaSent);
-            for (uint32_t i = tid; i < nu * (kTaCh / 4); i += kTaThreads) mp[i] = sent4;
+        if (prev_overflow) {  // cells written past the register stage are not tracked: clear the rows
+            for (uint32_t i = tid; i < nu * kTaCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k)
+                if (cell[k] != 0xffffffffu) s_tmap[cell[k]] = __uint_as_float(kTaSent);
         }
         if (tid == 0) s_slow = 0;
-        prefix1(nxt);  // directory of chunk jj+1 (loaded one chunk ago)
-        __syncthreads();  // (2)
+        __syncthreads();  // (2) the map is clean
         mark(0);
         {
             bool slow = false;
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k) {
-                const uint32_t i = tid + k * kTaThreads;
-                if (i < T && pv[k] != sv[k]) s_tmap[uv[k] * kTaCh + (sv[k] - c0)] = tfc_of(tv[k], dv[k]);
-                slow = slow || (i < T && nv[k] == sv[k]);
+                cell[k] = 0xffffffffu;
+                const uint64_t i = ce0 + tid + k * kTaThreads;
+                if (i >= ce1) continue;
+                const uint32_t g = group_of(sg.t[k]);
+                if (g == kSpU) continue;
+                if (a.runs) {  // a re-added document: only the first entry of its run enters the map
+                    if (i + 1 < ce1 && a.cterm[i + 1] == sg.t[k] && a.cslot[i + 1] == sg.s[k]) slow = true;
+                    if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) continue;
+                }
+                cell[k] = g * kTaCh + sg.s[k];
+                s_tmap[cell[k]] = sg.f[k];
             }
-            for (uint32_t i = kTaStage + tid; i < T; i += kTaThreads) {  // past the register stage: from HBM
-                const uint32_t u = term_of(cur, i), j = i - s_soff[cur][u];
-                const uint64_t g = s_pf[cur][u] + j;
-                const uint32_t s = a.pslot[g];
-                if (j == 0 || a.pslot[g - 1] != s) s_tmap[u * kTaCh + (s - c0)] = tfc_of(a.ptf[g], a.pdl[g]);
-                slow = slow || (j + 1 < s_n[cur][u] && a.pslot[g + 1] == s);
+            for (uint64_t i = ce0 + kTaStage + tid; i < ce1; i += kTaThreads) {  // past the register stage
+                const uint32_t g = group_of(a.cterm[i]);
+                if (g == kSpU) continue;
+                const uint32_t s = a.cslot[i];
+                if (i > ce0 && a.cterm[i - 1] == a.cterm[i] && a.cslot[i - 1] == s) {
+                    slow = true;
+                    continue;
+                }
+                s_tmap[g * kTaCh + s] = a.ctfc[i];
+                slow = slow || (i + 1 < ce1 && a.cterm[i + 1] == a.cterm[i] && a.cslot[i + 1] == s);
             }
             if (slow) s_slow = 1u;
         }
-        prefix2(nxt);
-        __syncthreads();  // (3)
+        __syncthreads();  // (3) the chunk's map is built
         mark(1);
-        load_stage(nxt);  // chunk jj+1's postings: consumed after this chunk's rounds
-        load_dir(jj + 2);
-        // 3. rounds; acc = kTaSent until the document's first contribution
+        prev_overflow = ce1 - ce0 > kTaStage;
+        load_entries(sg, jj + 2);  // in flight during this chunk's and the next chunk's rounds
+        // 2. rounds, per query m in its term order
         float acc[kTaQW];
+        uint64_t hit[kTaQW];  // lane masks
 #pragma unroll
-        for (uint32_t m = 0; m < kTaQW; ++m) acc[m] = __uint_as_float(kTaSent);
+        for (uint32_t m = 0; m < kTaQW; ++m) {
+            acc[m] = 0.0f;
+            hit[m] = 0;
+        }
         if (a.abl & 1) {
         } else if (!s_slow && rmax <= 16) {
-            // 8 rounds at a time: all 4 x 8 map reads issued, then the folds in
-            // round order per query; a finished query reads the empty row.
-            // Branch-free: the terms come from lane-resident registers.
-            for (uint32_t rb = 0; rb < rmax; rb += 8) {
-                float tf[kTaQW][8];
+            // 4 terms at a time: the 4 map reads issued together, then the folds in order
 #pragma unroll
-                for (uint32_t m = 0; m < kTaQW; ++m)
+            for (uint32_t m = 0; m < kTaQW; ++m) {
+                for (uint32_t rb = 0; rb < ql[m]; rb += 4) {
+                    float tf[4];
 #pragma unroll
-                    for (uint32_t k = 0; k < 8; ++k) {
+                    for (uint32_t k = 0; k < 4; ++k) {
                         const uint32_t r = rb + k;
                         const uint32_t uu = __builtin_amdgcn_readlane(lr_u, m * 16 + (r & 15u));
-                        tf[m][k] = s_tmap[(r < ql[m] ? uu : kSpU) * kTaCh + lane];
+                        tf[k] = s_tmap[(r < ql[m] ? uu : kSpU) * kTaCh + lane];
                     }
 #pragma unroll
-                for (uint32_t m = 0; m < kTaQW; ++m)
-#pragma unroll
-                    for (uint32_t k = 0; k < 8; ++k) {
+                    for (uint32_t k = 0; k < 4; ++k) {
                         const uint32_t ln = m * 16 + ((rb + k) & 15u);
                         const float v = __uint_as_float(__builtin_amdgcn_readlane(lr_v, ln));
                         const float idf = __uint_as_float(__builtin_amdgcn_readlane(lr_idf, ln));
-                        // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`
-                        const bool hit = __float_as_uint(tf[m][k]) != kTaSent;
-                        const float sc = v * tf[m][k] * idf;
-                        const float first = 0.0f + sc, more = acc[m] + sc;
-                        const float nvl = __float_as_uint(acc[m]) == kTaSent ? first : more;
-                        acc[m] = hit ? nvl : acc[m];
+                        // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`.
+                        // acc starts at +0.0 and never holds -0.0, so adding 0.0 for a
+                        // miss leaves it unchanged and the first hit is 0.0 + s
+                        const bool h = __float_as_uint(tf[k]) != kTaSent;
+                        const float sc = v * tf[k] * idf;
+                        acc[m] = acc[m] + (h ? sc : 0.0f);
+                        hit[m] |= __ballot(h);
                     }
+                }
             }
         } else {
-            // a re-added document's run (every posting of (term, document) in run order, from HBM),
-            // or a query with more than 16 live terms
-            for (uint32_t r = 0; r < rmax; ++r) {
+            // a re-added document's run (every entry of (term, document) in order, from HBM), or a query
+            // with more than 16 live terms
 #pragma unroll
-                for (uint32_t m = 0; m < kTaQW; ++m) {
-                    const uint4 rec = qrec_at(r < ql[m] ? qp0[m] + r : pdummy);
+            for (uint32_t m = 0; m < kTaQW; ++m) {
+                for (uint32_t r = 0; r < ql[m]; ++r) {
+                    const uint4 rec = qrec_at(qp0[m] + r);
                     const uint32_t u = rec.x;
                     const float t = s_tmap[u * kTaCh + lane];
-                    if (__float_as_uint(t) == kTaSent) continue;
+                    const bool h = __float_as_uint(t) != kTaSent;
+                    hit[m] |= __ballot(h);
+                    if (!h) continue;
                     const float v = __uint_as_float(rec.y), idf = __uint_as_float(rec.z);
-                    if (!s_slow) {  // one posting per (term, document)
-                        const float sc = v * t * idf;
-                        acc[m] = __float_as_uint(acc[m]) == kTaSent ? 0.0f + sc : acc[m] + sc;
+                    if (!s_slow) {
+                        acc[m] = acc[m] + v * t * idf;
                         continue;
                     }
-                    const uint32_t n = s_n[cur][u];
-                    const uint64_t pf = s_pf[cur][u];
-                    uint32_t lo = 0, hi = n;  // lower_bound(slot) in the term's postings of this chunk
+                    // the chunk's entries are sorted by (term, slot): lower_bound((term, lane))
+                    const uint32_t term = s_ut[u];
+                    uint64_t lo = ce0, hi = ce1;
                     while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (a.pslot[pf + mid] < c0 + lane) lo = mid + 1; else hi = mid;
+                        const uint64_t mid = (lo + hi) >> 1;
+                        const uint32_t mt = a.cterm[mid];
+                        if (mt < term || (mt == term && a.cslot[mid] < lane)) lo = mid + 1; else hi = mid;
                     }
-                    for (uint32_t j = lo; j < n && a.pslot[pf + j] == c0 + lane; ++j) {
-                        const float sc = v * tfc_of(a.ptf[pf + j], a.pdl[pf + j]) * idf;
-                        acc[m] = __float_as_uint(acc[m]) == kTaSent ? 0.0f + sc : acc[m] + sc;
-                    }
+                    for (uint64_t i = lo; i < ce1 && a.cterm[i] == term && a.cslot[i] == lane; ++i)
+                        acc[m] = acc[m] + v * a.ctfc[i] * idf;
                 }
             }
         }
         mark(2);
-        // 4. selection: (query wave + 16 m, slot c0 + lane)
+        // 3. selection: (query qid[m], slot c0 + lane)
         const uint32_t slot = c0 + lane;
 #pragma unroll
         for (uint32_t m = 0; m < kTaQW; ++m) {
-            const uint32_t q = wave + kTaWaves * m;
-            if (q >= B) break;
-            const uint64_t key = __float_as_uint(acc[m]) != kTaSent ? sp_key(acc[m], slot) : 0ull;
+            const uint32_t q = qid[m];
+            if (q == 0xffffffffu) continue;
+            const bool h = (hit[m] >> lane) & 1ull;
+            const uint64_t key = h ? sp_key(acc[m], slot) : 0ull;
             if constexpr (MODE == 0) {
                 uint64_t best = key;
 #pragma unroll
@@ -460,7 +431,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                 if ((lane & (kTaGrp - 1)) == 0)
                     a.smp[(uint64_t)q * a.S + (uint64_t)jj * (kTaCh / kTaGrp) + lane / kTaGrp] = best;
             } else if constexpr (MODE == 1) {
-                if (key != 0ull && key >= s_tau[q]) {
+                if (key != 0ull && key >= tau[m]) {
                     const uint32_t pos = atomicAdd(&a.counts[q], 1u);
                     if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key;
                 }
@@ -469,32 +440,38 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             }
         }
         mark(3);
+    };
+    if (jb < je) load_entries(st0, jb);
+    if (jb + 1 < je) load_entries(st1, jb + 1);
+    for (uint32_t jj = jb; jj < je; jj += 2) {
+        chunk(st0, jj);
+        if (jj + 1 < je) chunk(st1, jj + 1);
     }
     if ((a.abl & 8) && tid == 0)
         for (int k = 0; k < 4; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
 }
 
 // tau[q] = the kk-th largest sampled key (0 when fewer than kk matched): each
-// thread keeps its top kSpTopLocal keys, an LDS sort of all of them follows.
-// Any kk keys it keeps are real documents, so tau never exceeds the true
-// kk-th best key; dropped keys only lower it (more candidates, still exact).
-__global__ __launch_bounds__(256) void k_bm25_tau(const uint64_t* __restrict__ smp, uint32_t S, uint32_t kk,
-                                                  uint64_t* __restrict__ tau) {
-    __shared__ uint64_t keys[256 * kSpTopLocal];
+// of 1024 threads keeps its top kSpTopLocal keys, an LDS sort of all of them
+// follows.  Any kk keys it keeps are real documents, so tau never exceeds the
+// true kk-th best key; dropped keys only lower it (more candidates, still exact).
+constexpr uint32_t kTauThreads = 1024;
+__global__ __launch_bounds__(kTauThreads) void k_bm25_tau(const uint64_t* __restrict__ smp, uint32_t S, uint32_t kk,
+                                                          uint64_t* __restrict__ tau) {
+    __shared__ uint64_t keys[kTauThreads * kSpTopLocal];
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
     uint64_t top[kSpTopLocal];
 #pragma unroll
     for (uint32_t i = 0; i < kSpTopLocal; ++i) top[i] = 0;
     const uint64_t* src = smp + (uint64_t)q * S;
     constexpr uint32_t kIn = 8;  // loads in flight per thread
-    for (uint32_t i0 = tid; i0 < S; i0 += 256u * kIn) {
+    for (uint32_t i0 = tid; i0 < S; i0 += kTauThreads * kIn) {
         uint64_t kv[kIn];
 #pragma unroll
-        for (uint32_t u = 0; u < kIn; ++u) kv[u] = i0 + u * 256u < S ? src[i0 + u * 256u] : 0ull;
+        for (uint32_t u = 0; u < kIn; ++u) kv[u] = i0 + u * kTauThreads < S ? src[i0 + u * kTauThreads] : 0ull;
 #pragma unroll
         for (uint32_t u = 0; u < kIn; ++u) {
             uint64_t k = kv[u];
-            if (k <= top[kSpTopLocal - 1]) continue;
 #pragma unroll
             for (uint32_t j = 0; j < kSpTopLocal; ++j) {
                 const uint64_t hi = k > top[j] ? k : top[j], lo = k > top[j] ? top[j] : k;
@@ -506,8 +483,8 @@ __global__ __launch_bounds__(256) void k_bm25_tau(const uint64_t* __restrict__ s
 #pragma unroll
     for (uint32_t i = 0; i < kSpTopLocal; ++i) keys[tid * kSpTopLocal + i] = ~top[i];
     __syncthreads();
-    bitonic_sort_lds(keys, 256 * kSpTopLocal);
-    if (tid == 0) tau[q] = kk >= 1 && kk <= 256 * kSpTopLocal ? ~keys[kk - 1] : 0ull;
+    bitonic_sort_lds(keys, kTauThreads * kSpTopLocal);
+    if (tid == 0) tau[q] = kk >= 1 && kk <= kTauThreads * kSpTopLocal ? ~keys[kk - 1] : 0ull;
 }
 
 // Per query: sort the candidates (descending key) and emit the first `limit`.
@@ -703,13 +680,16 @@ struct gvdb_sparse {
     uint64_t cap_ptr = 0, cap_ids = 0, cap_term = 0, cap_tf = 0, cap_dl = 0;
     uint64_t up_slots = 0, up_ent = 0;  // uploaded prefix (append-only adds)
     bool dirty = true;                  // full re-upload needed
-    // term-major inverted index (device), rebuilt from the mirror after a change
-    uint32_t* d_pslot = nullptr;
-    float *d_ptf = nullptr, *d_pdl = nullptr;
-    uint64_t cap_post = 0, cap_ptf = 0, cap_pdl = 0;
-    uint64_t version = 0, inv_version = ~0ull;
-    bool runs = false;  // some (term, document) has more than one posting (re-added ids)
-    std::unordered_map<uint32_t, uint64_t> toff;  // term -> its first posting
+    // blocked inverted index (device), rebuilt from the mirror after a change:
+    // per 64-slot chunk its entries by (term, slot, add order)
+    uint64_t* d_cptr = nullptr;
+    uint32_t* d_cterm = nullptr;
+    uint8_t* d_cslot = nullptr;
+    float *d_ctf = nullptr, *d_cdl = nullptr, *d_ctfc = nullptr;
+    uint64_t cap_cptr = 0, cap_cterm = 0, cap_cslot = 0, cap_ctf = 0, cap_cdl = 0, cap_ctfc = 0;
+    uint64_t version = 0, inv_version = ~0ull, tfc_version = ~0ull;
+    uint32_t tfc_avgdl = 0;  // the avgdl bits d_ctfc was computed with
+    bool runs = false;       // some (term, document) has more than one entry (re-added ids)
     // search scratch
     void* scratch = nullptr;
     size_t scratch_n = 0;
@@ -776,78 +756,86 @@ gvdb_status upload(gvdb_sparse* sp) {
     return GVDB_OK;
 }
 
-// Term-major posting runs from the forward mirror: entries stably sorted by
-// term (a slot's entries are (term, add order) and slots ascend, so each run
-// is slot-ascending with a re-added id's entries adjacent in add order), then
-// gathered into (slot, tf, dl).  Run offsets = prefix of the host's posting
-// counts over ascending terms.
-gvdb_status build_inverted(gvdb_sparse* sp, hipStream_t s) {
-    if (sp->inv_version == sp->version) return GVDB_OK;
+__global__ void k_blk_cptr(const uint64_t* __restrict__ ptr, uint32_t N, uint32_t nchunks, uint64_t* __restrict__ cptr) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c <= nchunks) cptr[c] = ptr[min((uint64_t)c * kTaCh, (uint64_t)N)];
+}
+
+// The blocked inverted index from the forward mirror (one stable radix sort
+// of (chunk, term) keys; the forward entries are slot-ordered, each slot's by
+// (term, add order)), and tf_component of every entry for the current avgdl.
+gvdb_status build_blocked(gvdb_sparse* sp, hipStream_t s) {
     const uint64_t N = sp->slot_id.size(), E = sp->term.size();
-    std::vector<std::pair<uint32_t, uint64_t>> runs(sp->plen.begin(), sp->plen.end());
-    std::sort(runs.begin(), runs.end());
-    uint64_t off = 0;
-    sp->toff.clear();
-    sp->toff.reserve(runs.size());
-    for (const auto& r : runs) {
-        sp->toff[r.first] = off;
-        off += r.second;
-    }
-    if (off != E) return report_status(GVDB_ERR_INDEX, "posting counts disagree with the forward index");
-    if (E > 0x7fffffffull) return report_status(GVDB_ERR_INVALID_ARGUMENT, "more than 2^31 - 1 posting entries");
-    if (E == 0) {
-        sp->inv_version = sp->version;
-        return GVDB_OK;
-    }
-    const uint32_t max_term = runs.empty() ? 0u : runs.back().first;
-    int end_bit = 1;
-    while (end_bit < 32 && (max_term >> end_bit)) ++end_bit;
-    size_t cub_bytes = 0;
-    SP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                              (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)E, 0, end_bit, s),
-           "inverted sort size");
-    SP_TRY(grow(sp->d_pslot, sp->cap_post, E, 0), "alloc posting slots");
-    SP_TRY(grow(sp->d_ptf, sp->cap_ptf, E, 0), "alloc posting tf");
-    SP_TRY(grow(sp->d_pdl, sp->cap_pdl, E, 0), "alloc posting dl");
-    char* tmp = nullptr;
-    const size_t a4 = ((size_t)E * 4 + 255) & ~(size_t)255;
-    SP_TRY(hipMalloc((void**)&tmp, 4 * a4 + cub_bytes + 256), "alloc inverted build");
-    uint32_t* d_runs = (uint32_t*)(tmp + 4 * a4 + ((cub_bytes + 255) & ~(size_t)255));
-    uint32_t* eslot = (uint32_t*)tmp;
-    uint32_t* iota = (uint32_t*)(tmp + a4);
-    uint32_t* keys = (uint32_t*)(tmp + 2 * a4);
-    uint32_t* order = (uint32_t*)(tmp + 3 * a4);
-    hipError_t e = hipSuccess;
-    hipLaunchKernelGGL(k_inv_prep, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, sp->d_ptr, (uint32_t)N, eslot,
-                       iota);
-    e = hipGetLastError();
-    if (e == hipSuccess)
-        e = hipcub::DeviceRadixSort::SortPairs(tmp + 4 * a4, cub_bytes, sp->d_term, keys, iota, order, (int)E, 0,
-                                               end_bit, s);
-    if (e == hipSuccess) {
-        e = hipMemsetAsync(d_runs, 0, 4, s);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_inv_gather, dim3(2048), dim3(256), 0, s, order, keys, eslot, sp->d_tf, sp->d_dl, E,
-                               sp->d_pslot, sp->d_ptf, sp->d_pdl, d_runs);
-            e = hipGetLastError();
+    const uint32_t nchunks = (uint32_t)((N + kTaCh - 1) / kTaCh);
+    if (sp->inv_version != sp->version) {
+        if (E > 0x7fffffffull) return report_status(GVDB_ERR_INVALID_ARGUMENT, "more than 2^31 - 1 posting entries");
+        SP_TRY(grow(sp->d_cptr, sp->cap_cptr, (uint64_t)nchunks + 1, 0), "alloc chunk ptr");
+        hipLaunchKernelGGL(k_blk_cptr, dim3(nchunks / 256 + 1), dim3(256), 0, s, sp->d_ptr, (uint32_t)N, nchunks,
+                           sp->d_cptr);
+        SP_TRY(hipGetLastError(), "chunk ptr");
+        uint32_t h_runs = 0;
+        if (E > 0) {
+            int end_bit = 32;
+            while (end_bit < 64 && ((uint64_t)nchunks >> (end_bit - 32))) ++end_bit;
+            size_t cub_bytes = 0;
+            SP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                      (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)E, 0, end_bit,
+                                                      s),
+                   "blocked sort size");
+            SP_TRY(grow(sp->d_cterm, sp->cap_cterm, E, 0), "alloc blocked terms");
+            SP_TRY(grow(sp->d_cslot, sp->cap_cslot, E, 0), "alloc blocked slots");
+            SP_TRY(grow(sp->d_ctf, sp->cap_ctf, E, 0), "alloc blocked tf");
+            SP_TRY(grow(sp->d_cdl, sp->cap_cdl, E, 0), "alloc blocked dl");
+            SP_TRY(grow(sp->d_ctfc, sp->cap_ctfc, E, 0), "alloc blocked tfc");
+            const size_t a8 = ((size_t)E * 8 + 255) & ~(size_t)255, a4 = ((size_t)E * 4 + 255) & ~(size_t)255;
+            char* tmp = nullptr;
+            SP_TRY(hipMalloc((void**)&tmp, 2 * a8 + 3 * a4 + cub_bytes + 256), "alloc blocked build");
+            uint64_t* keys = (uint64_t*)tmp;
+            uint64_t* skeys = (uint64_t*)(tmp + a8);
+            uint32_t* iota = (uint32_t*)(tmp + 2 * a8);
+            uint32_t* order = (uint32_t*)(tmp + 2 * a8 + a4);
+            uint32_t* eslot = (uint32_t*)(tmp + 2 * a8 + 2 * a4);
+            uint32_t* d_runs = (uint32_t*)(tmp + 2 * a8 + 3 * a4);
+            void* ct = tmp + 2 * a8 + 3 * a4 + 256;
+            hipLaunchKernelGGL(k_blk_keys, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, sp->d_ptr, (uint32_t)N,
+                               sp->d_term, keys, iota, eslot);
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess)
+                e = hipcub::DeviceRadixSort::SortPairs(ct, cub_bytes, keys, skeys, iota, order, (int)E, 0, end_bit, s);
+            if (e == hipSuccess) e = hipMemsetAsync(d_runs, 0, 4, s);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_blk_gather, dim3(2048), dim3(256), 0, s, order, skeys, eslot, sp->d_tf, sp->d_dl,
+                                   E, sp->d_cterm, sp->d_cslot, sp->d_ctf, sp->d_cdl, d_runs);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(&h_runs, d_runs, 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            (void)hipFree(tmp);
+            if (e != hipSuccess) return sp_dev(e, "build blocked index");
         }
+        sp->runs = h_runs != 0;
+        sp->inv_version = sp->version;
     }
-    uint32_t h_runs = 0;
-    if (e == hipSuccess) e = hipMemcpyAsync(&h_runs, d_runs, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e == hipSuccess) sp->runs = h_runs != 0;
-    (void)hipFree(tmp);
-    if (e != hipSuccess) return sp_dev(e, "build inverted index");
-    sp->inv_version = sp->version;
+    uint32_t avg_bits;
+    std::memcpy(&avg_bits, &sp->avgdl, 4);
+    if (E > 0 && (sp->tfc_version != sp->version || sp->tfc_avgdl != avg_bits)) {
+        hipLaunchKernelGGL(k_blk_tfc, dim3(2048), dim3(256), 0, s, sp->d_ctf, sp->d_cdl, E, sp->k1, sp->b, sp->avgdl,
+                           sp->d_ctfc);
+        SP_TRY(hipGetLastError(), "blocked tf_component");
+        sp->tfc_version = sp->version;
+        sp->tfc_avgdl = avg_bits;
+    }
     return GVDB_OK;
 }
 
-// k_bm25_taat: one resident block per CU (its LDS map), each a contiguous chunk range
+// k_bm25_taat: one resident block per CU (its LDS map), each a contiguous range of
+// at most kTaCptrLds chunks (more blocks than CUs for very large indexes)
 uint32_t sp_grid(uint32_t tiles) {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::max<uint32_t>(1, std::min<uint32_t>(tiles, (uint32_t)cus));
+    const uint32_t need = (tiles + kTaCptrLds - 1) / kTaCptrLds;
+    return std::max<uint32_t>(1, std::max(need, std::min<uint32_t>(tiles, (uint32_t)cus)));
 }
 
 // items per query bounded by the list strides: dynamic LDS for the next power of two
@@ -905,7 +893,8 @@ void gvdb_sparse_destroy(gvdb_sparse* sp) {
     if (!sp) return;
     (void)hipSetDevice(sp->device);
     for (void* p : {(void*)sp->d_ptr, (void*)sp->d_term, (void*)sp->d_tf, (void*)sp->d_dl, (void*)sp->d_ids,
-                    (void*)sp->d_pslot, (void*)sp->d_ptf, (void*)sp->d_pdl, sp->scratch})
+                    (void*)sp->d_cptr, (void*)sp->d_cterm, (void*)sp->d_cslot, (void*)sp->d_ctf, (void*)sp->d_cdl,
+                    (void*)sp->d_ctfc, sp->scratch})
         if (p) (void)hipFree(p);
     if (sp->h_fail) (void)hipHostFree(sp->h_fail);
     if (sp->stream) (void)hipStreamDestroy(sp->stream);
@@ -1133,10 +1122,11 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
     if (limit > 0xffffffffull) return report_status(GVDB_ERR_INVALID_ARGUMENT, "limit too large");
     std::lock_guard<std::mutex> g(sp->mu);
     for (uint64_t q = 0; q < B; ++q) out_n[q] = 0;
-    if (B == 0 || limit == 0 || sp->total_documents == 0 || sp->slot_id.empty()) return GVDB_OK;
+    // no entries: no document matches any term (the reference's map stays empty)
+    if (B == 0 || limit == 0 || sp->total_documents == 0 || sp->slot_id.empty() || sp->term.empty()) return GVDB_OK;
     SP_TRY(hipSetDevice(sp->device), "hipSetDevice");
     gvdb_status st = upload(sp);
-    if (st == GVDB_OK) st = build_inverted(sp, sp->stream);
+    if (st == GVDB_OK) st = build_blocked(sp, sp->stream);
     if (st != GVDB_OK) return st;
     const uint32_t N = (uint32_t)sp->slot_id.size();
     const uint32_t L = (uint32_t)limit;
@@ -1205,22 +1195,32 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             std::memcpy(&h_qrec[4 * i + 2], &h_qidf[i], 4);
         }
         h_qrec[4 * nqt] = kSpU;
-        std::vector<uint64_t> h_toff(nu), h_gpre(nu + 1, 0), h_gpre4(nu + 1, 0);
-        for (uint32_t u = 0; u < nu; ++u) {
-            const uint64_t len = sp->plen.at(group_terms[u]);
-            h_toff[u] = sp->toff.at(group_terms[u]);
-            h_gpre[u + 1] = h_gpre[u] + len;
-            h_gpre4[u + 1] = h_gpre4[u] + (len + kTaDirPer - 1) / kTaDirPer;
+        // wave slots w + 16 m: longest-processing-time assignment of the queries to the
+        // 16 waves (each wave's rounds cost about the sum of its queries' term counts)
+        std::vector<uint32_t> h_perm(kTaQ, 0xffffffffu);
+        {
+            std::vector<uint32_t> order(Bg);
+            for (uint32_t q = 0; q < Bg; ++q) order[q] = q;
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+                return h_qp[x + 1] - h_qp[x] > h_qp[y + 1] - h_qp[y];
+            });
+            const uint32_t nw = std::min<uint32_t>(kTaWaves, Bg);
+            std::vector<uint32_t> load(nw, 0), cnt(nw, 0);
+            for (uint32_t q : order) {
+                uint32_t best = 0xffffffffu;
+                for (uint32_t w = 0; w < nw; ++w)
+                    if (cnt[w] < kTaQW && (best == 0xffffffffu || load[w] < load[best])) best = w;
+                h_perm[best + kTaWaves * cnt[best]] = q;
+                load[best] += h_qp[q + 1] - h_qp[q];
+                ++cnt[best];
+            }
         }
-        // scratch: qp | qrec | toff | gpre | gpre4 | tau | counts | fail | out_n | first | last | smp | cand |
-        //          out ids | out scores
+        // scratch: qp | perm | qrec | ut | tau | counts | fail | out_n | smp | cand | out ids | out scores
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-        const size_t dir = (size_t)nchunks * nu * 4;
-        const size_t o_qp = 0, o_qrec = o_qp + al((Bg + 1) * 4), o_toff = o_qrec + al((nqt + 1) * 16),
-                     o_gpre = o_toff + al(nu * 8 + 8), o_gpre4 = o_gpre + al((nu + 1) * 8),
-                     o_tau = o_gpre4 + al((nu + 1) * 8), o_cnt = o_tau + al(Bg * 8),
-                     o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_first = o_n + al(Bg * 4),
-                     o_last = o_first + al(dir + 4), o_smp = o_last + al(dir + 4),
+        const size_t o_qp = 0, o_perm = o_qp + al((Bg + 1) * 4), o_qrec = o_perm + al(kTaQ * 4),
+                     o_ut = o_qrec + al((nqt + 1) * 16),
+                     o_tau = o_ut + al(nu * 4 + 4), o_cnt = o_tau + al(Bg * 8),
+                     o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_smp = o_n + al(Bg * 4),
                      o_cand = o_smp + al((size_t)Bg * S * 8), o_oi = o_cand + al((size_t)Bg * kSpCand * 8),
                      o_os = o_oi + al((size_t)Bg * L * 8), total = o_os + al((size_t)Bg * L * 4);
         if (total > sp->scratch_n) {
@@ -1233,32 +1233,25 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         char* base = (char*)sp->scratch;
         SP_TRY(hipMemcpyAsync(base + o_qp, h_qp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
         SP_TRY(hipMemcpyAsync(base + o_qrec, h_qrec.data(), (nqt + 1) * 16, hipMemcpyHostToDevice, s), "qrec");
-        if (nqt) {
-            SP_TRY(hipMemcpyAsync(base + o_toff, h_toff.data(), nu * 8, hipMemcpyHostToDevice, s), "toff");
-            SP_TRY(hipMemcpyAsync(base + o_gpre, h_gpre.data(), (nu + 1) * 8, hipMemcpyHostToDevice, s), "gpre");
-            SP_TRY(hipMemcpyAsync(base + o_gpre4, h_gpre4.data(), (nu + 1) * 8, hipMemcpyHostToDevice, s), "gpre4");
-        }
+        SP_TRY(hipMemcpyAsync(base + o_perm, h_perm.data(), kTaQ * 4, hipMemcpyHostToDevice, s), "perm");
+        if (nu) SP_TRY(hipMemcpyAsync(base + o_ut, group_terms.data(), nu * 4, hipMemcpyHostToDevice, s), "ut");
         SP_TRY(hipMemsetAsync(base + o_cnt, 0, Bg * 4, s), "counts");
         TaArgs a{};
-        a.pslot = sp->d_pslot;
-        a.ptf = sp->d_ptf;
-        a.pdl = sp->d_pdl;
+        a.cptr = sp->d_cptr;
+        a.cterm = sp->d_cterm;
+        a.cslot = sp->d_cslot;
+        a.ctfc = sp->d_ctfc;
         a.N = N;
         a.nchunks = nchunks;
-        a.toff = (const uint64_t*)(base + o_toff);
-        a.gpre = (const uint64_t*)(base + o_gpre);
-        a.gpre4 = (const uint64_t*)(base + o_gpre4);
-        a.first = (uint32_t*)(base + o_first);
-        a.last = (uint32_t*)(base + o_last);
+        a.n_entries = sp->term.size();
+        a.ut = (const uint32_t*)(base + o_ut);
         a.nu = nu;
         a.qp = (const uint32_t*)(base + o_qp);
         a.qrec = (const uint4*)(base + o_qrec);
+        a.perm = (const uint32_t*)(base + o_perm);
         a.nqt = nqt;
         a.runs = sp->runs ? 1u : 0u;
         a.B = Bg;
-        a.k1 = sp->k1;
-        a.b = sp->b;
-        a.avgdl = sp->avgdl;
         a.every = every;
         a.smp = (uint64_t*)(base + o_smp);
         a.S = S;
@@ -1279,16 +1272,9 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             SP_TRY(hipMemsetAsync(d_prof, 0, 1024 * 8 * 8, s), "prof");
             a.prof = d_prof;
         }
-        if (nu) {
-            SP_TRY(hipMemsetAsync(a.first, 0xff, dir, s), "directory");
-            const uint64_t threads = h_gpre4[nu];
-            if (threads > 0xffffffffull * 256) return report_status(GVDB_ERR_INVALID_ARGUMENT, "posting runs too long");
-            hipLaunchKernelGGL(k_ta_dir, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, a);
-            SP_TRY(hipGetLastError(), "bm25 directory");
-        }
         hipLaunchKernelGGL(k_bm25_taat<0>, dim3(sp_grid(nsamp)), dim3(kTaThreads), 0, s, a);
         SP_TRY(hipGetLastError(), "bm25 sample");
-        hipLaunchKernelGGL(k_bm25_tau, dim3(Bg), dim3(256), 0, s, a.smp, S, L, (uint64_t*)(base + o_tau));
+        hipLaunchKernelGGL(k_bm25_tau, dim3(Bg), dim3(kTauThreads), 0, s, a.smp, S, L, (uint64_t*)(base + o_tau));
         SP_TRY(hipGetLastError(), "bm25 tau");
         hipLaunchKernelGGL(k_bm25_taat<1>, dim3(sp_grid(nchunks)), dim3(kTaThreads), 0, s, a);
         SP_TRY(hipGetLastError(), "bm25 emit");
