@@ -133,12 +133,12 @@ __global__ void k_blk_tfc(const float* __restrict__ ctf, const float* __restrict
 }
 
 struct TaArgs {
-    const uint64_t* cptr;   // [nchunks+1] entry range of each chunk (= forward ptr every 64 slots)
+    const uint64_t* cptr;   // [nchunks+1] entry range of each blocked-index chunk (= forward ptr every 64 slots)
     const uint32_t* cterm;  // blocked entries: term, slot within the chunk, tf_component
     const uint8_t* cslot;
     const float* ctfc;
     uint32_t N;             // slots
-    uint32_t nchunks;
+    uint32_t nchunks;       // blocked-index (64-slot) chunks
     uint64_t n_entries;     // > 0
     const uint32_t* ut;     // [nu] the group's distinct live terms
     uint32_t nu;
@@ -165,41 +165,45 @@ __device__ __forceinline__ uint32_t term_hash(uint32_t t) { return (t * 0x9E3779
 
 // MODE 0: sample (every `every`-th chunk -> per 8 slots the max key -> smp),
 // 1: emit (key >= tau -> cand), 2: dense keys of query `dense_q`.
+// SPL slots per lane: a chunk of 64 SPL documents (1 or 2 blocked-index
+// chunks); the LDS map then has 512 / SPL rows (group terms + the empty row).
 //
-// One block per CU walks a contiguous range of 64-slot chunks.  Per chunk:
+// One block per CU walks a contiguous range of chunks.  Per chunk:
 //   1. its blocked entries (all terms, ~30 per document) stream in; an LDS
 //      hash of the group's terms keeps those of the batch, whose
 //      tf_component lands in an LDS (group term x slot) map (kTaSent = no
 //      posting; the first entry of a re-added document's run);
-//   2. rounds: lane = slot, wave w owns queries w + 16 m (m < 4),
-//      accumulators in registers.  Round r adds query q's r-th term: one map
-//      read, acc = acc + q_tf * tfc * idf -- per document exactly the
-//      reference's fold (sparse.rs:167-190; acc starts at 0.0 = or_insert);
-//      a run of several entries (rare: the index records whether any exists)
-//      is folded from HBM in order;
+//   2. rounds: lane = SPL slots, wave w owns 4 queries (host-balanced),
+//      accumulators in registers.  Query q's terms in order: one map read,
+//      acc = acc + q_tf * tfc * idf -- per document exactly the reference's
+//      fold (sparse.rs:167-190; acc starts at 0.0 = or_insert).  A run of
+//      several entries (rare: the index records whether any exists) is folded
+//      from HBM in order;
 //   3. selection by the mode.
-// Software pipeline: while chunk j's rounds run, chunk j+1's entries are in
-// flight into registers.
-template <int MODE>
+// Software pipeline: a chunk's entries are loaded two chunks ahead.
+template <int MODE, int SPL>
 __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
-    __shared__ __attribute__((aligned(16))) float s_tmap[(kSpU + 1) * kTaCh];  // row kSpU: the empty row
+    constexpr uint32_t kCh = kTaCh * SPL;          // slots per chunk
+    constexpr uint32_t kRows = 512u / SPL;         // map rows: 128 KB
+    constexpr uint32_t kEmpty = kRows - 1;         // the empty row
+    __shared__ __attribute__((aligned(16))) float s_tmap[kRows * kCh];
     __shared__ uint32_t s_hkey[kHashSlots];
-    __shared__ uint32_t s_ut[kSpU];  // group term index -> term
     __shared__ uint16_t s_hval[kHashSlots];
+    __shared__ uint32_t s_ut[kRows];  // group term index -> term
     __shared__ uint32_t s_slow;
-    __shared__ uint64_t s_cptr[2 * (kTaCptrLds + 1)];  // the block's chunk ranges (no HBM round trip per chunk)
+    __shared__ uint64_t s_cptr[(SPL + 1) * (kTaCptrLds + 1)];  // the block's chunk (sub-)ranges
     typedef const uint32_t __attribute__((address_space(4)))* cu32;
     const cu32 qp = (cu32)(uintptr_t)a.qp;  // read-only query tables: scalar loads
     const cu32 qr32 = (cu32)(uintptr_t)a.qrec;
     auto qrec_at = [&](uint32_t p) { return make_uint4(qr32[4 * p], qr32[4 * p + 1], qr32[4 * p + 2], 0u); };
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t nu = a.nu;
-    for (uint32_t i = tid; i < (kSpU + 1) * kTaCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
+    const uint32_t nu = a.nu;  // < kRows (host)
+    for (uint32_t i = tid; i < kRows * kCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
     for (uint32_t i = tid; i < kHashSlots; i += kTaThreads) s_hkey[i] = 0xffffffffu;
     __syncthreads();
     // the group's terms (distinct): linear probing; 0xffffffff marks empty, so
-    // that term id itself is looked up through the sorted list instead
+    // that term id itself is found as the sorted list's last entry
     bool max_term = false;
     if (tid < nu) {
         const uint32_t t = a.ut[tid];
@@ -213,13 +217,13 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         }
     }
     const bool has_max_term = __syncthreads_or(max_term);
-    auto group_of = [&](uint32_t t) -> uint32_t {  // group term index, or kSpU (not in the batch)
-        if (t == 0xffffffffu) return has_max_term ? nu - 1 : kSpU;  // the sorted list's last entry
+    auto group_of = [&](uint32_t t) -> uint32_t {  // group term index, or kEmpty (not in the batch)
+        if (t == 0xffffffffu) return has_max_term ? nu - 1 : kEmpty;
         uint32_t h = term_hash(t);
         while (true) {
             const uint32_t k = s_hkey[h];
             if (k == t) return s_hval[h];
-            if (k == 0xffffffffu) return kSpU;
+            if (k == 0xffffffffu) return kEmpty;
             h = (h + 1) & (kHashSlots - 1);
         }
     };
@@ -238,21 +242,29 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     uint64_t tau[kTaQW];
 #pragma unroll
     for (uint32_t m = 0; m < kTaQW; ++m) tau[m] = MODE == 1 && qid[m] != 0xffffffffu ? a.tau[qid[m]] : 0ull;
-    const uint32_t pdummy = a.nqt;  // qrec[nqt]: the empty map row, q_tf = idf = 0
-    // the wave's query terms, lane-resident: lane 16 m + r holds query m's r-th term (r < 16)
-    uint32_t lr_u, lr_v, lr_idf;
+    // the wave's query terms, lane-resident: lane 16 m + r holds query m's r-th term (r < 16):
+    // map row offset (the empty row past the query's end), q_tf, idf
+    uint32_t lr_row, lr_v, lr_idf;
     {
         const uint32_t m = lane >> 4, r = lane & 15u;
-        const uint4 rec = qrec_at(r < ql[m & 3] ? qp0[m & 3] + r : pdummy);
-        lr_u = rec.x;
+        const bool in = r < ql[m & 3];
+        const uint4 rec = qrec_at(in ? qp0[m & 3] + r : a.nqt);
+        lr_row = (in ? rec.x : kEmpty) * kCh;
         lr_v = rec.y;
         lr_idf = rec.z;
     }
     const uint32_t every = MODE == 0 ? a.every : 1u;
-    const uint32_t nj = (a.nchunks + every - 1) / every;
-    // contiguous chunk range per block
+    const uint32_t nchunks = (a.nchunks + SPL - 1) / SPL;  // in chunks of kCh slots
+    const uint32_t nj = (nchunks + every - 1) / every;
+    // contiguous chunk range per block (the host sizes the grid: je - jb <= kTaCptrLds)
     const uint32_t jb = (uint32_t)((uint64_t)nj * blockIdx.x / gridDim.x);
     const uint32_t je = (uint32_t)((uint64_t)nj * (blockIdx.x + 1) / gridDim.x);
+    for (uint32_t i = tid; i < je - jb; i += kTaThreads) {
+        const uint64_t c = (uint64_t)(jb + i) * every * SPL;  // in blocked-index chunks
+#pragma unroll
+        for (uint32_t h = 0; h <= SPL; ++h) s_cptr[(SPL + 1) * i + h] = a.cptr[min(c + h, (uint64_t)a.nchunks)];
+    }
+    __syncthreads();
     uint64_t ph[4] = {0, 0, 0, 0}, tprev = 0;
     auto mark = [&](int k) {
         if (a.abl & 8) {
@@ -261,37 +273,24 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             tprev = t;
         }
     };
-    // the host sizes the grid so that a block's range fits (je - jb <= kTaCptrLds)
-    for (uint32_t i = tid; i <= je - jb; i += kTaThreads) {
-        const uint64_t c = (uint64_t)(jb + i) * every;
-        s_cptr[2 * i] = a.cptr[min(c, (uint64_t)a.nchunks)];
-        s_cptr[2 * i + 1] = a.cptr[min(c + 1, (uint64_t)a.nchunks)];
-    }
-    __syncthreads();
     // ---- a chunk's entries through registers, two chunks ahead (double buffer)
     constexpr uint32_t kPer = kTaStage / kTaThreads;
     struct Stage {
-        uint32_t t[kPer], s[kPer];  // term, slot
+        uint32_t t[kPer], s[kPer];  // term, slot within the blocked-index chunk
         float f[kPer];              // tf_component
-        uint64_t e0, e1;            // entry range
     };
     Stage st0, st1;
     uint32_t cell[kPer];  // map cells this thread wrote for the current chunk (unwritten after its rounds)
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) cell[k] = 0xffffffffu;
+    const uint64_t last = a.n_entries - 1;
     auto load_entries = [&](Stage& sg, uint32_t jx) {
-        sg.e0 = sg.e1 = 0;
-        if (jx < je) {
-            sg.e0 = s_cptr[2 * (jx - jb)];
-            sg.e1 = s_cptr[2 * (jx - jb) + 1];
-        }
-        // unconditional loads (an index past the range reads a valid entry that
-        // the build skips): no use and no register write before the chunk's
-        // turn, so the loads stay in flight
-        const uint64_t last = a.n_entries - 1;
+        // unconditional loads (an index past the range reads a valid entry that the
+        // build skips): no use and no register write before the chunk's turn
+        const uint64_t e0 = jx < je ? s_cptr[(SPL + 1) * (jx - jb)] : 0ull;
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
-            const uint64_t i = min(sg.e0 + tid + k * kTaThreads, last);
+            const uint64_t i = min(e0 + tid + k * kTaThreads, last);
             sg.t[k] = a.cterm[i];
             sg.s[k] = a.cslot[i];
             sg.f[k] = a.ctfc[i];
@@ -299,12 +298,14 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     };
     bool prev_overflow = false;
     auto chunk = [&](Stage& sg, uint32_t jj) {
-        const uint32_t c0 = jj * every * kTaCh;
-        const uint64_t ce0 = sg.e0, ce1 = sg.e1;
+        const uint32_t c0 = jj * every * kCh;
+        const uint64_t* cr = &s_cptr[(SPL + 1) * (jj - jb)];
+        const uint64_t ce0 = cr[0], ce1 = cr[SPL], cmid = cr[1];  // cmid: start of the second sub-chunk
+        auto slot_in_chunk = [&](uint64_t i, uint32_t s) { return SPL == 2 && i >= cmid ? s + kTaCh : s; };
         __syncthreads();  // (1) the previous chunk's rounds are done
         mark(-1);
         if (prev_overflow) {  // cells written past the register stage are not tracked: clear the rows
-            for (uint32_t i = tid; i < nu * kTaCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
+            for (uint32_t i = tid; i < nu * kCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
         } else {
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k)
@@ -321,23 +322,23 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                 const uint64_t i = ce0 + tid + k * kTaThreads;
                 if (i >= ce1) continue;
                 const uint32_t g = group_of(sg.t[k]);
-                if (g == kSpU) continue;
+                if (g == kEmpty) continue;
                 if (a.runs) {  // a re-added document: only the first entry of its run enters the map
                     if (i + 1 < ce1 && a.cterm[i + 1] == sg.t[k] && a.cslot[i + 1] == sg.s[k]) slow = true;
                     if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) continue;
                 }
-                cell[k] = g * kTaCh + sg.s[k];
+                cell[k] = g * kCh + slot_in_chunk(i, sg.s[k]);
                 s_tmap[cell[k]] = sg.f[k];
             }
             for (uint64_t i = ce0 + kTaStage + tid; i < ce1; i += kTaThreads) {  // past the register stage
                 const uint32_t g = group_of(a.cterm[i]);
-                if (g == kSpU) continue;
+                if (g == kEmpty) continue;
                 const uint32_t s = a.cslot[i];
                 if (i > ce0 && a.cterm[i - 1] == a.cterm[i] && a.cslot[i - 1] == s) {
                     slow = true;
                     continue;
                 }
-                s_tmap[g * kTaCh + s] = a.ctfc[i];
+                s_tmap[g * kCh + slot_in_chunk(i, s)] = a.ctfc[i];
                 slow = slow || (i + 1 < ce1 && a.cterm[i + 1] == a.cterm[i] && a.cslot[i + 1] == s);
             }
             if (slow) s_slow = 1u;
@@ -346,39 +347,49 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         mark(1);
         prev_overflow = ce1 - ce0 > kTaStage;
         load_entries(sg, jj + 2);  // in flight during this chunk's and the next chunk's rounds
-        // 2. rounds, per query m in its term order
-        float acc[kTaQW];
-        uint64_t hit[kTaQW];  // lane masks
+        // 2. rounds, per query m in its term order; lane holds slots SPL*lane + h
+        float acc[kTaQW][SPL];
+        uint64_t hit[kTaQW][SPL];  // lane masks
 #pragma unroll
-        for (uint32_t m = 0; m < kTaQW; ++m) {
-            acc[m] = 0.0f;
-            hit[m] = 0;
-        }
+        for (uint32_t m = 0; m < kTaQW; ++m)
+#pragma unroll
+            for (uint32_t h = 0; h < SPL; ++h) {
+                acc[m][h] = 0.0f;
+                hit[m][h] = 0;
+            }
         if (a.abl & 1) {
         } else if (!s_slow && rmax <= 16) {
-            // 4 terms at a time: the 4 map reads issued together, then the folds in order
+            // 4 terms at a time: the map reads issued together, then the folds in order
 #pragma unroll
             for (uint32_t m = 0; m < kTaQW; ++m) {
                 for (uint32_t rb = 0; rb < ql[m]; rb += 4) {
-                    float tf[4];
+                    float tf[4][SPL];
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) {
-                        const uint32_t r = rb + k;
-                        const uint32_t uu = __builtin_amdgcn_readlane(lr_u, m * 16 + (r & 15u));
-                        tf[k] = s_tmap[(r < ql[m] ? uu : kSpU) * kTaCh + lane];
+                        const uint32_t row = __builtin_amdgcn_readlane(lr_row, m * 16 + ((rb + k) & 15u));
+                        if constexpr (SPL == 2) {
+                            const float2 t2 = *(const float2*)&s_tmap[row + 2 * lane];
+                            tf[k][0] = t2.x;
+                            tf[k][1 % SPL] = t2.y;
+                        } else {
+                            tf[k][0] = s_tmap[row + lane];
+                        }
                     }
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) {
                         const uint32_t ln = m * 16 + ((rb + k) & 15u);
                         const float v = __uint_as_float(__builtin_amdgcn_readlane(lr_v, ln));
                         const float idf = __uint_as_float(__builtin_amdgcn_readlane(lr_idf, ln));
-                        // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`.
-                        // acc starts at +0.0 and never holds -0.0, so adding 0.0 for a
-                        // miss leaves it unchanged and the first hit is 0.0 + s
-                        const bool h = __float_as_uint(tf[k]) != kTaSent;
-                        const float sc = v * tf[k] * idf;
-                        acc[m] = acc[m] + (h ? sc : 0.0f);
-                        hit[m] |= __ballot(h);
+#pragma unroll
+                        for (uint32_t h = 0; h < SPL; ++h) {
+                            // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`.
+                            // acc starts at +0.0 and never holds -0.0, so adding 0.0 for a
+                            // miss leaves it unchanged and the first hit is 0.0 + s
+                            const bool hh = __float_as_uint(tf[k][h]) != kTaSent;
+                            const float sc = v * tf[k][h] * idf;
+                            acc[m][h] = acc[m][h] + (hh ? sc : 0.0f);
+                            hit[m][h] |= __ballot(hh);
+                        }
                     }
                 }
             }
@@ -389,60 +400,74 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             for (uint32_t m = 0; m < kTaQW; ++m) {
                 for (uint32_t r = 0; r < ql[m]; ++r) {
                     const uint4 rec = qrec_at(qp0[m] + r);
-                    const uint32_t u = rec.x;
-                    const float t = s_tmap[u * kTaCh + lane];
-                    const bool h = __float_as_uint(t) != kTaSent;
-                    hit[m] |= __ballot(h);
-                    if (!h) continue;
                     const float v = __uint_as_float(rec.y), idf = __uint_as_float(rec.z);
-                    if (!s_slow) {
-                        acc[m] = acc[m] + v * t * idf;
-                        continue;
+#pragma unroll
+                    for (uint32_t h = 0; h < SPL; ++h) {
+                        const uint32_t sl = SPL * lane + h;  // slot within the chunk
+                        const float t = s_tmap[rec.x * kCh + sl];
+                        const bool hh = __float_as_uint(t) != kTaSent;
+                        hit[m][h] |= __ballot(hh);
+                        if (!hh) continue;
+                        if (!s_slow) {
+                            acc[m][h] = acc[m][h] + v * t * idf;
+                            continue;
+                        }
+                        // the sub-chunk's entries are sorted by (term, slot): lower_bound((term, slot))
+                        const uint32_t term = s_ut[rec.x], sub = sl / kTaCh, ss = sl % kTaCh;
+                        const uint64_t r0 = cr[sub], r1 = cr[sub + 1];
+                        uint64_t lo = r0, hi = r1;
+                        while (lo < hi) {
+                            const uint64_t mid = (lo + hi) >> 1;
+                            const uint32_t mt = a.cterm[mid];
+                            if (mt < term || (mt == term && a.cslot[mid] < ss)) lo = mid + 1; else hi = mid;
+                        }
+                        for (uint64_t i = lo; i < r1 && a.cterm[i] == term && a.cslot[i] == ss; ++i)
+                            acc[m][h] = acc[m][h] + v * a.ctfc[i] * idf;
                     }
-                    // the chunk's entries are sorted by (term, slot): lower_bound((term, lane))
-                    const uint32_t term = s_ut[u];
-                    uint64_t lo = ce0, hi = ce1;
-                    while (lo < hi) {
-                        const uint64_t mid = (lo + hi) >> 1;
-                        const uint32_t mt = a.cterm[mid];
-                        if (mt < term || (mt == term && a.cslot[mid] < lane)) lo = mid + 1; else hi = mid;
-                    }
-                    for (uint64_t i = lo; i < ce1 && a.cterm[i] == term && a.cslot[i] == lane; ++i)
-                        acc[m] = acc[m] + v * a.ctfc[i] * idf;
                 }
             }
         }
         mark(2);
-        // 3. selection: (query qid[m], slot c0 + lane)
-        const uint32_t slot = c0 + lane;
+        // 3. selection: (query qid[m], slot c0 + SPL lane + h)
 #pragma unroll
         for (uint32_t m = 0; m < kTaQW; ++m) {
             const uint32_t q = qid[m];
             if (q == 0xffffffffu) continue;
-            const bool h = (hit[m] >> lane) & 1ull;
-            const uint64_t key = h ? sp_key(acc[m], slot) : 0ull;
-            if constexpr (MODE == 0) {
-                uint64_t best = key;
+            uint64_t key[SPL];
 #pragma unroll
-                for (uint32_t o = 1; o < kTaGrp; o <<= 1) {
+            for (uint32_t h = 0; h < SPL; ++h)
+                key[h] = (hit[m][h] >> lane) & 1ull ? sp_key(acc[m][h], c0 + SPL * lane + h) : 0ull;
+            if constexpr (MODE == 0) {
+                uint64_t best = key[0];
+#pragma unroll
+                for (uint32_t h = 1; h < SPL; ++h) best = max(best, key[h]);
+                constexpr uint32_t kLanes = kTaGrp / SPL;  // lanes per group of 8 slots
+#pragma unroll
+                for (uint32_t o = 1; o < kLanes; o <<= 1) {
                     const uint32_t lo32 = __shfl_xor((uint32_t)best, o), hi32 = __shfl_xor((uint32_t)(best >> 32), o);
                     best = max(best, ((uint64_t)hi32 << 32) | lo32);
                 }
-                if ((lane & (kTaGrp - 1)) == 0)
-                    a.smp[(uint64_t)q * a.S + (uint64_t)jj * (kTaCh / kTaGrp) + lane / kTaGrp] = best;
+                if ((lane & (kLanes - 1)) == 0)
+                    a.smp[(uint64_t)q * a.S + (uint64_t)jj * (kCh / kTaGrp) + lane / kLanes] = best;
             } else if constexpr (MODE == 1) {
-                if (key != 0ull && key >= tau[m]) {
-                    const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-                    if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key;
-                }
+#pragma unroll
+                for (uint32_t h = 0; h < SPL; ++h)
+                    if (key[h] != 0ull && key[h] >= tau[m]) {
+                        const uint32_t pos = atomicAdd(&a.counts[q], 1u);
+                        if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key[h];
+                    }
             } else {
-                if (q == a.dense_q && slot < a.N) a.dense[slot] = key;
+#pragma unroll
+                for (uint32_t h = 0; h < SPL; ++h) {
+                    const uint32_t slot = c0 + SPL * lane + h;
+                    if (q == a.dense_q && slot < a.N) a.dense[slot] = key[h];
+                }
             }
         }
         mark(3);
     };
-    if (jb < je) load_entries(st0, jb);
-    if (jb + 1 < je) load_entries(st1, jb + 1);
+    load_entries(st0, jb);
+    load_entries(st1, jb + 1);
     for (uint32_t jj = jb; jj < je; jj += 2) {
         chunk(st0, jj);
         if (jj + 1 < je) chunk(st1, jj + 1);
@@ -1130,12 +1155,13 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
     if (st != GVDB_OK) return st;
     const uint32_t N = (uint32_t)sp->slot_id.size();
     const uint32_t L = (uint32_t)limit;
-    const uint32_t nchunks = (N + kTaCh - 1) / kTaCh;
-    // sample stride: expected candidates ~ limit * every, kept well under kSpCand
-    uint32_t every = std::max<uint32_t>(1u, std::min<uint32_t>(32u, kSpCand / std::max<uint32_t>(1u, 4u * L)));
-    if (nchunks <= 8u * every) every = 1;  // small index: the sample is the whole index
-    const uint32_t nsamp = (nchunks + every - 1) / every;
-    const uint32_t S = nsamp * (kTaCh / kTaGrp);
+    const uint32_t nblk = (N + kTaCh - 1) / kTaCh;  // blocked-index chunks
+    // distinct terms per launch group before a new group starts (GVDB_BM25_GROUP_TERMS, timing knob)
+    static const size_t group_cap = [] {
+        const char* e = getenv("GVDB_BM25_GROUP_TERMS");
+        const long v = e ? atol(e) : 0;
+        return v >= 16 && v <= (long)kSpU ? (size_t)v : (size_t)255;  // 255: the 2-slot map (profiles/r02)
+    }();
     hipStream_t s = sp->stream;
     uint64_t q0 = 0;
     std::vector<uint32_t> h_qp;
@@ -1173,9 +1199,10 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
                 u.erase(std::unique(u.begin(), u.end()), u.end());
                 if (u.size() > kSpU) {
                     if (q1 == q0)
-                        return report_status(GVDB_ERR_INVALID_ARGUMENT, "query has more than 512 distinct terms");
+                        return report_status(GVDB_ERR_INVALID_ARGUMENT, "query has more than 511 distinct terms");
                     break;
                 }
+                if (u.size() > group_cap && q1 > q0) break;  // keep the group in the 2-slot map
                 group_terms.swap(u);
             }
             h_qt.insert(h_qt.end(), t.begin(), t.end());
@@ -1187,6 +1214,25 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         const uint32_t Bg = (uint32_t)(q1 - q0);
         const uint32_t nqt = (uint32_t)h_qt.size();
         const uint32_t nu = (uint32_t)group_terms.size();
+        // two slots per lane (128-document chunks) while the map's 256 rows hold the group
+        const uint32_t spl = nu < 256 ? 2u : 1u;
+        const uint32_t nchunks = (nblk + spl - 1) / spl;
+        // sample stride: expected candidates ~ limit * every, kept well under kSpCand
+        uint32_t every = std::max<uint32_t>(1u, std::min<uint32_t>(32u, kSpCand / std::max<uint32_t>(1u, 4u * L)));
+        if (nchunks <= 8u * every) every = 1;  // small index: the sample is the whole index
+        const uint32_t nsamp = (nchunks + every - 1) / every;
+        const uint32_t S = nsamp * (kTaCh * spl / kTaGrp);
+        auto launch_taat = [&](int mode, uint32_t grid, const TaArgs& ta) {
+            if (spl == 2) {
+                if (mode == 0) hipLaunchKernelGGL((k_bm25_taat<0, 2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+                if (mode == 1) hipLaunchKernelGGL((k_bm25_taat<1, 2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+                if (mode == 2) hipLaunchKernelGGL((k_bm25_taat<2, 2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+            } else {
+                if (mode == 0) hipLaunchKernelGGL((k_bm25_taat<0, 1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+                if (mode == 1) hipLaunchKernelGGL((k_bm25_taat<1, 1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+                if (mode == 2) hipLaunchKernelGGL((k_bm25_taat<2, 1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+            }
+        };
         std::vector<uint32_t> h_qrec(4 * (nqt + 1), 0u);  // (group term, q_tf, idf, 0); [nqt]: the empty row
         for (uint32_t i = 0; i < nqt; ++i) {
             h_qrec[4 * i] =
@@ -1194,7 +1240,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             std::memcpy(&h_qrec[4 * i + 1], &h_qv[i], 4);
             std::memcpy(&h_qrec[4 * i + 2], &h_qidf[i], 4);
         }
-        h_qrec[4 * nqt] = kSpU;
+        h_qrec[4 * nqt] = 0u;  // the kernel maps a finished query's rounds to the empty row
         // wave slots w + 16 m: longest-processing-time assignment of the queries to the
         // 16 waves (each wave's rounds cost about the sum of its queries' term counts)
         std::vector<uint32_t> h_perm(kTaQ, 0xffffffffu);
@@ -1242,7 +1288,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         a.cslot = sp->d_cslot;
         a.ctfc = sp->d_ctfc;
         a.N = N;
-        a.nchunks = nchunks;
+        a.nchunks = nblk;
         a.n_entries = sp->term.size();
         a.ut = (const uint32_t*)(base + o_ut);
         a.nu = nu;
@@ -1272,11 +1318,11 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             SP_TRY(hipMemsetAsync(d_prof, 0, 1024 * 8 * 8, s), "prof");
             a.prof = d_prof;
         }
-        hipLaunchKernelGGL(k_bm25_taat<0>, dim3(sp_grid(nsamp)), dim3(kTaThreads), 0, s, a);
+        launch_taat(0, sp_grid(nsamp), a);
         SP_TRY(hipGetLastError(), "bm25 sample");
         hipLaunchKernelGGL(k_bm25_tau, dim3(Bg), dim3(kTauThreads), 0, s, a.smp, S, L, (uint64_t*)(base + o_tau));
         SP_TRY(hipGetLastError(), "bm25 tau");
-        hipLaunchKernelGGL(k_bm25_taat<1>, dim3(sp_grid(nchunks)), dim3(kTaThreads), 0, s, a);
+        launch_taat(1, sp_grid(nchunks), a);
         SP_TRY(hipGetLastError(), "bm25 emit");
         if (d_prof) {
             h_prof.resize(1024 * 8);
@@ -1313,7 +1359,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             void* ct = (char*)tmp + (size_t)N * 16 + 256;
             a.dense = k0;
             a.dense_q = q;
-            hipLaunchKernelGGL(k_bm25_taat<2>, dim3(sp_grid(nchunks)), dim3(kTaThreads), 0, s, a);
+            launch_taat(2, sp_grid(nchunks), a);
             hipError_t e = hipGetLastError();
             hipcub::DoubleBuffer<uint64_t> db(k0, k1);
             if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortKeysDescending(ct, cub_bytes, db, (int)N, 0, 64, s);
