@@ -147,7 +147,7 @@ struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
-        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids;
+        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids, flt_codes;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     // Searches return without a host sync: the workspace goes back to the pool
@@ -165,7 +165,7 @@ struct Workspace {
         if (done) (void)hipEventDestroy(done);
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
                         &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
-                        &fx_scores, &flt_rows, &flt_ids, &b1})
+                        &fx_scores, &flt_rows, &flt_ids, &flt_codes, &b1})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -338,6 +338,7 @@ struct BqSearchArgs {
     uint32_t* d_out_n;
     uint32_t* d_out_dist;   // candidates mode: stage-1 order, no final sort
     uint64_t out_stride;    // candidates mode: output row stride (0 = R)
+    const uint32_t* row_map;  // filtered search: v's codes are the compacted allowed rows; subset row -> index row
 };
 
 // Stage-1 + stage-2 timing without a host round trip: events are recorded
@@ -513,7 +514,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     }
     const uint32_t W4 = code_w4(v.D);
     if (B == 1 && a.dims_match && v.D > 0 && v.D <= kB1MaxD && !a.d_qwords && !a.d_out_dist && R <= kSortLdsCap &&
-        a.qlen == v.clen && v.clen == v.D && b1_enabled())
+        a.qlen == v.clen && v.clen == v.D && !a.row_map && b1_enabled())
         return bq_search_b1(a, ws, s);
     HIP_TRY(ws.qnorm.ensure((size_t)B * 4), "alloc qnorm");
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
@@ -559,6 +560,8 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         }
     }
 
+    if (a.row_map)  // stage-1 rows are subset rows: back to index rows (order kept: the subset ascends)
+        HIP_TRY(launch_map_rows(ws.s1_rows.as<uint32_t>(), (uint64_t)B * R, a.row_map, s), "map filtered rows");
     RerankArgs rr{};
     rr.rows = v.rows;
     rr.clen = v.clen;
@@ -1229,10 +1232,17 @@ gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64
 }
 
 // Filtered search (§8(f) rank 4): the pre-mask of FilterEngine::execute_filter
-// (filtering.rs:374) -> exact scan of the allowed rows only.  The allowed ids
-// are mapped to live rows on the host (unknown ids are ignored, repeats count
-// once), sorted by row so ties keep the unfiltered scan's row order, and the
-// exact flat kernels run over that row list.
+// (filtering.rs:374) applied to the vector search.  The allowed ids map to
+// live rows on the host (unknown ids are ignored, repeats count once), sorted
+// ascending so ties keep the index's row order.  Then, by sp->mode:
+//   BQ (the reference's multi_stage_search, quantization.rs:151-193, over the
+//   subset): the allowed rows' code planes are compacted (one gather of
+//   M x 16 W4 bytes), the unchanged stage-1 kernels run over them with R from
+//   the subset size, the candidates map back to index rows, and the exact
+//   rerank + final sort read the resident rows -- memory O(M) codes, no
+//   per-row test in the unfiltered hot kernels;
+//   FLAT: the exact scan of the allowed rows, in query groups whose score
+//   block stays within kFlatScoreBytes.
 gvdb_status gvdb_index_search_filtered(const gvdb_index* ix, const float* queries, uint64_t B, uint32_t dim, uint64_t k,
                                        const gvdb_search_params* sp_in, const uint64_t* allowed, uint64_t n_allowed,
                                        uint64_t* out_ids, float* out_scores, uint32_t* out_n) {
@@ -1254,14 +1264,15 @@ gvdb_status gvdb_index_search_filtered(const gvdb_index* ix, const float* querie
         memset(out_n, 0, B * 4);
         return GVDB_OK;
     }
-    std::vector<uint64_t> sub_ids(M);
-    for (uint64_t j = 0; j < M; ++j) sub_ids[j] = ix->h_ids[rows[j]];
     gvdb_search_params sp{};
     sp.metric = GVDB_METRIC_COSINE;
+    sp.mode = GVDB_SEARCH_BQ_RERANK;
+    sp.rescore_ratio = 0.1f;
     if (sp_in) sp = *sp_in;
     const int kind = sp.metric == GVDB_METRIC_L2 ? kScoreL2
                      : sp.metric == GVDB_METRIC_COSINE_DISTANCE ? kScoreCosineDistance
                                                                  : kScoreCosine;
+    const int descending = kind == kScoreCosine;
     if ((st = set_device(ix->device)) != GVDB_OK) return st;
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
@@ -1270,32 +1281,66 @@ gvdb_status gvdb_index_search_filtered(const gvdb_index* ix, const float* querie
     g.begin(s);
     HIP_TRY(hipStreamSynchronize(ix->stream), "sync mutations");
     HIP_TRY(ws.q.ensure(B * dim * 4), "alloc queries");
-    HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
     HIP_TRY(ws.flt_rows.ensure(M * 4), "alloc filter rows");
-    HIP_TRY(ws.flt_ids.ensure(M * 8), "alloc filter ids");
-    HIP_TRY(ws.scores.ensure(B * M * 4), "alloc filtered scores");
-    HIP_TRY(ws.flags.ensure(16), "alloc flags");
-    HIP_TRY(ws.sort_tmp.ensure(flat_select_bytes((uint32_t)M)), "alloc sort tmp");
     HIP_TRY(ws.out_ids.ensure(B * k * 8), "alloc out");
     HIP_TRY(ws.out_scores.ensure(B * k * 4), "alloc out");
     HIP_TRY(ws.out_n.ensure(B * 4), "alloc out");
-    HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
     HIP_TRY(hipMemcpyAsync(ws.q.p, queries, B * dim * 4, hipMemcpyHostToDevice, s), "upload queries");
     HIP_TRY(hipMemcpyAsync(ws.flt_rows.p, rows.data(), M * 4, hipMemcpyHostToDevice, s), "upload filter rows");
-    HIP_TRY(hipMemcpyAsync(ws.flt_ids.p, sub_ids.data(), M * 8, hipMemcpyHostToDevice, s), "upload filter ids");
-    HIP_TRY(launch_row_norms(ws.q.as<float>(), B, dim, ws.qnorm.as<float>(), s), "qnorm");
-    HIP_TRY(launch_flat_scores(ws.q.as<float>(), (uint32_t)B, ws.qnorm.as<float>(), ix->rows, (uint32_t)M, dim,
-                               ix->norms, kind, ws.flt_rows.as<uint32_t>(), ws.scores.as<float>(), s),
-            "filtered scores");
-    HIP_TRY(launch_flat_select(ws.scores.as<float>(), (uint32_t)B, (uint32_t)M, (uint32_t)k, kind == kScoreCosine, 0,
-                               0.0f, ws.flt_ids.as<uint64_t>(), ws.out_ids.as<uint64_t>(), ws.out_scores.as<float>(),
-                               ws.out_n.as<uint32_t>(), ws.sort_tmp.p, ws.sort_tmp.n, ws.flags.as<uint32_t>() + 1, s),
-            "filtered select");
+    if (sp.mode == GVDB_SEARCH_FLAT) {
+        std::vector<uint64_t> sub_ids(M);
+        for (uint64_t j = 0; j < M; ++j) sub_ids[j] = ix->h_ids[rows[j]];
+        const uint64_t per_q = M * 4;
+        const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(B, kFlatScoreBytes / per_q));
+        HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
+        HIP_TRY(ws.flt_ids.ensure(M * 8), "alloc filter ids");
+        HIP_TRY(ws.scores.ensure(G * per_q), "alloc filtered scores");
+        HIP_TRY(ws.flags.ensure(16), "alloc flags");
+        HIP_TRY(ws.sort_tmp.ensure(flat_select_bytes((uint32_t)M)), "alloc sort tmp");
+        HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
+        HIP_TRY(hipMemcpyAsync(ws.flt_ids.p, sub_ids.data(), M * 8, hipMemcpyHostToDevice, s), "upload filter ids");
+        HIP_TRY(launch_row_norms(ws.q.as<float>(), B, dim, ws.qnorm.as<float>(), s), "qnorm");
+        for (uint64_t g0 = 0; g0 < B; g0 += G) {
+            const uint32_t bg = (uint32_t)std::min<uint64_t>(G, B - g0);
+            HIP_TRY(launch_flat_scores(ws.q.as<float>() + g0 * dim, bg, ws.qnorm.as<float>() + g0, ix->rows,
+                                       (uint32_t)M, dim, ix->norms, kind, ws.flt_rows.as<uint32_t>(),
+                                       ws.scores.as<float>(), s),
+                    "filtered scores");
+            HIP_TRY(launch_flat_select(ws.scores.as<float>(), bg, (uint32_t)M, (uint32_t)k, descending, 0, 0.0f,
+                                       ws.flt_ids.as<uint64_t>(), ws.out_ids.as<uint64_t>() + g0 * k,
+                                       ws.out_scores.as<float>() + g0 * k, ws.out_n.as<uint32_t>() + g0,
+                                       ws.sort_tmp.p, ws.sort_tmp.n, ws.flags.as<uint32_t>() + 1, s),
+                    "filtered select");
+        }
+    } else {
+        HIP_TRY(ws.flt_codes.ensure(M * code_w4(dim) * 16), "alloc filter codes");
+        HIP_TRY(launch_gather_code_rows(ix->codes, ix->cap, ws.flt_rows.as<uint32_t>(), (uint32_t)M, dim,
+                                        ws.flt_codes.as<uint4>(), s),
+                "gather filter codes");
+        uint64_t R = sp.rescore_count ? sp.rescore_count : rust_f32_as_usize((float)M * sp.rescore_ratio);
+        R = std::min<uint64_t>(std::max<uint64_t>(R, k), M);
+        BqSearchArgs a{};
+        a.v = ShardView{ix->rows, dim, ix->norms, ws.flt_codes.as<uint4>(), M, (uint32_t)M, dim, ix->ids, 0};
+        a.d_q = ws.q.as<float>();
+        a.qlen = dim;
+        a.B = (uint32_t)B;
+        a.thr = ix->thr;
+        a.dims_match = true;
+        a.R = (uint32_t)R;
+        a.kout = (uint32_t)k;
+        a.kind = kind;
+        a.descending = descending;
+        a.d_out_ids = ws.out_ids.as<uint64_t>();
+        a.d_out_scores = ws.out_scores.as<float>();
+        a.d_out_n = ws.out_n.as<uint32_t>();
+        a.row_map = ws.flt_rows.as<uint32_t>();
+        if ((st = bq_search(a, ws, s)) != GVDB_OK) return st;
+    }
     HIP_TRY(hipMemcpyAsync(out_ids, ws.out_ids.p, B * k * 8, hipMemcpyDeviceToHost, s), "download ids");
     HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
     HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download n");
     HIP_TRY(hipStreamSynchronize(s), "sync");
-    return GVDB_OK;
+    return check_poisoned(out_n, B);
 }
 
 gvdb_status gvdb_index_search_device(const gvdb_index* ix, const float* d_queries, uint64_t B, uint32_t dim, uint64_t k,

@@ -285,6 +285,10 @@ hipError_t launch_bq_shard_merge(const uint64_t* gids, const uint32_t* dist, con
 // ---- index maintenance -----------------------------------------------------------
 // Order-preserving gather of rows/codes/norms/ids: new row r <- old row map[r]
 // (remove_vector compaction, index.rs:245-266).
+// filtered BQ: compact the allowed rows' code planes (cap = m); map stage-1 rows back
+hipError_t launch_gather_code_rows(const uint4* codes, uint64_t cap, const uint32_t* rows, uint32_t m, uint32_t D,
+                                   uint4* ncodes, hipStream_t s);
+hipError_t launch_map_rows(uint32_t* s1_rows, uint64_t n, const uint32_t* rows, hipStream_t s);
 hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, uint4* ncodes, const float* norms,
                          float* nnorms, const uint64_t* ids, uint64_t* nids, const uint64_t* map, uint64_t m,
                          uint64_t cap, uint32_t D, hipStream_t s);

@@ -3027,6 +3027,38 @@ __global__ void k_gather_meta(const uint4* __restrict__ codes, uint4* __restrict
     nids[r] = ids[o];
 }
 
+// Filtered BQ search: the allowed rows' code planes, compacted (row list
+// ascending, so the subset keeps the index's row order), and the stage-1
+// candidates mapped back to index rows before the rerank.
+__global__ void k_gather_code_rows(const uint4* __restrict__ codes, uint64_t cap, const uint32_t* __restrict__ rows,
+                                   uint32_t m, uint32_t W4, uint4* __restrict__ ncodes) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const uint64_t o = rows[r];
+    for (uint32_t w = 0; w < W4; ++w) ncodes[(uint64_t)w * m + r] = codes[(uint64_t)w * cap + o];
+}
+
+__global__ void k_map_rows(uint32_t* __restrict__ s1_rows, uint64_t n, const uint32_t* __restrict__ rows) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) s1_rows[i] = rows[s1_rows[i]];
+}
+
+hipError_t launch_gather_code_rows(const uint4* codes, uint64_t cap, const uint32_t* rows, uint32_t m, uint32_t D,
+                                   uint4* ncodes, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_code_rows, dim3((m + 255) / 256), dim3(256), 0, s, codes, cap, rows, m, code_w4(D),
+                       ncodes);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_map_rows(uint32_t* s1_rows, uint64_t n, const uint32_t* rows, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_map_rows, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, s1_rows, n, rows);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, uint4* ncodes, const float* norms,
                          float* nnorms, const uint64_t* ids, uint64_t* nids, const uint64_t* map, uint64_t m,
                          uint64_t cap, uint32_t D, hipStream_t s) {

@@ -388,8 +388,9 @@ class GpuVectorIndex:
     def search_batch_filtered(self, queries: np.ndarray, k: int, allowed: Iterable[str],
                               params: Optional[SearchParams] = None):
         """Vector search restricted to the ids a FilterEngine::execute_filter
-        (filtering.rs:374) returned: exact scan of those rows (metric of
-        ``params``); ids the index does not hold are ignored."""
+        (filtering.rs:374) returned; ids the index does not hold are ignored.
+        ``params.mode`` BQ: multi_stage_search over those rows (R from their
+        count); FLAT: exact scan of those rows (metric of ``params``)."""
         q = _f32(queries)
         if q.ndim == 1:
             q = q.reshape(1, -1)

@@ -202,10 +202,13 @@ gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* index, const float
  * if the id was present. */
 /* Filtered search: the pre-mask of FilterEngine::execute_filter
  * (filtering.rs:374, whose Vec<String> result maps to u64 ids through the host
- * table) applied to the vector search — exact scan (the metric of
- * sp->metric; sp->mode is ignored) over the live rows whose id is in
+ * table) applied to the vector search over the live rows whose id is in
  * allowed[0..n_allowed); unknown ids are ignored, repeats count once, equal
- * scores keep row order.  Host buffers. */
+ * scores keep row order.  sp->mode BQ_RERANK: multi_stage_search
+ * (quantization.rs:151-193) over those rows, R = rescore_count or
+ * (M as f32 * rescore_ratio) as usize for M allowed rows (the allowed rows'
+ * codes are compacted on the device: O(M) extra memory); FLAT: the exact scan
+ * of those rows.  Host buffers. */
 gvdb_status gvdb_index_search_filtered(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
                                        uint64_t k, const gvdb_search_params* sp, const uint64_t* allowed,
                                        uint64_t n_allowed, uint64_t* out_ids, float* out_scores, uint32_t* out_n);

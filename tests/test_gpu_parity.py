@@ -535,6 +535,49 @@ def test_search_filtered_matches_oracle_on_subset(g, oracle_mod, metric):
     assert on[0] == 0
 
 
+@pytest.mark.parametrize("N,D,B,keep,R,metric", [
+    (3_000, 48, 5, 0.3, 40, 0),          # exact-threshold regime, cosine
+    (3_000, 48, 5, 0.3, 0, 1),           # R from the subset (M as f32 * 0.1) as usize, L2
+    (700_000, 768, 2, 0.6, 100, 0),      # sampled threshold over the 420K-row subset
+    (400_000, 768, 128, 0.8, 100, 2),    # the FP4-MFMA scan over the subset, 1 - cosine
+])
+def test_search_filtered_bq_matches_multi_stage_on_subset(g, oracle_mod, N, D, B, keep, R, metric):
+    """BQ mode + filter = multi_stage_search (quantization.rs:151-193) over the
+    allowed rows only: their codes compacted, stage 1 on them, rows mapped
+    back for the rerank; ids and scores bit-identical to the oracle run on the
+    subset (ties in subset order = index row order)."""
+    x = rng_rows(N + D, N, D, dup=30)
+    Q = rng_rows(D + 5, B, D)
+    r = np.random.default_rng(N)
+    sub = np.flatnonzero(r.random(N) < keep)
+    Q[0] = x[sub[len(sub) // 2]]
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64) * 3 + 7, x)
+    k = 10
+    sp = g.SearchParams(metric=metric, rescore_count=R)
+    allowed = (sub.astype(np.uint64) * 3 + 7)
+    ids = np.zeros((B, k), np.uint64)
+    sc = np.zeros((B, k), np.float32)
+    n = np.zeros(B, np.uint32)
+    import ctypes as C
+
+    from gvdb._ffi import ptr
+
+    c = sp.to_c()
+    g.check(ix._lib.gvdb_index_search_filtered(ix._h, ptr(Q), B, D, k, C.byref(c), ptr(allowed), allowed.size,
+                                               ptr(ids), ptr(sc), ptr(n)))
+    M = len(sub)
+    Reff = R if R else oracle_mod.rust_f32_as_usize(np.float32(M) * np.float32(0.1))
+    Reff = min(max(Reff, k), M)
+    xs = x[sub]
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(xs), Q, xs, Reff,
+                                                   kind=metric)
+    kk = min(k, Reff)
+    assert (n == kk).all()
+    assert (ids[:, :kk] == sub[ri[:, :kk].astype(np.int64)].astype(np.uint64) * 3 + 7).all()
+    assert same_f32(sc[:, :kk], rs[:, :kk])
+
+
 def test_sharded_packed_world1_equals_single_device(g):
     """ShardedBQSearch's packed path (candidates written into the all-gather
     send block, gvdb_bq_shard_merge_packed_device on it) with one rank returns
