@@ -92,7 +92,8 @@ def main():
     ap.add_argument("--b1-queries", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--hnsw-rows", type=int, default=20_000, help="corpus prefix for the CPU-HNSW leg (0 = skip)")
+    ap.add_argument("--hnsw-rows", type=int, default=100_000,
+                    help="corpus prefix for the CPU-HNSW leg and its matched-N GPU points (0 = skip)")
     ap.add_argument("--no-points", dest="points", action="store_false", help="skip the QPS/recall operating points")
     args = ap.parse_args()
 
@@ -394,13 +395,14 @@ def main():
         parity = {"queries": nq, "ids_equal": ok_ids, "cosine_bit_exact": ok_sc}
         del host_codes
 
-    # ---------------- CPU-HNSW leg: HnswVectorIndex's graph search (instant-distance
-    # restated, oracle/hnsw_oracle.cpp) on a bounded prefix of the same corpus.  A
-    # 10M-row build is out of reach (~30 thread-ms per inserted row at D=768, i.e.
-    # days), so the graph holds the first --hnsw-rows rows; its QPS there is an
-    # upper bound for 10M (search cost grows with N) and its recall is measured
-    # against the exact top-10 of that prefix.
+    # ---------------- CPU-HNSW leg at matched N: HnswVectorIndex's graph search
+    # (instant-distance 0.6.1 restated, oracle/hnsw_oracle.cpp) on the first
+    # --hnsw-rows rows of the same corpus (a 10M-row build takes days), and the
+    # GPU on THE SAME rows: a BQ rescore sweep and the exact flat search, all
+    # scored against the exact top-10 of that prefix.  gpu_vs_cpu_hnsw pairs
+    # every ef_search point with the fastest GPU point of recall >= its recall - 0.02.
     cpu_hnsw = None
+    matched = None
     if want_cpu and args.hnsw_rows > 0:
         import oracle
 
@@ -408,26 +410,67 @@ def main():
         ns = min(args.hnsw_rows, N)
         xs = np.ascontiguousarray(host_rows[:ns])
         qn = q.cpu().numpy()
+        sub_truth = np.argsort(-(qn @ xs.T), axis=1, kind="stable")[:, :k]
+        log(f"[bench] CPU-HNSW leg: building M=32 ef_construction=100 on {ns} rows ({threads} threads)")
         tb = time.perf_counter()
         h = oracle.Hnsw(xs, threads=threads)
         tb = time.perf_counter() - tb
-        h.search(qn[:threads], k=k, threads=threads)
-        th = time.perf_counter()
-        hid, _, _ = h.search(qn, k=k, threads=threads)
-        th = time.perf_counter() - th
+        hpts = []
+        for ef in (64, 100, 200, 400):
+            h.search(qn[:threads], k=k, ef_search=ef, threads=threads)
+            th = time.perf_counter()
+            hid, _, _ = h.search(qn, k=k, ef_search=ef, threads=threads)
+            th = time.perf_counter() - th
+            hpts.append({"ef_search": ef, "qps": B / th,
+                         "recall_at_10": recall_at(hid.astype(np.int64), sub_truth)})
         t1 = time.perf_counter()
-        h.search(qn[:16], k=k, threads=1)
+        h.search(qn[:16], k=k, ef_search=100, threads=1)
         t1 = (time.perf_counter() - t1) / 16
-        sub_truth = np.argsort(-(qn @ xs.T), axis=1, kind="stable")[:, :k]
+        ref = next(p for p in hpts if p["ef_search"] == 100)
         cpu_hnsw = {
-            "value": B / th, "unit": "queries/s", "cores": threads, "kind": "port",
-            "recall_at_10": recall_at(hid.astype(np.int64), sub_truth),
-            "rows": ns, "build_s": tb, "single_thread_ms_per_query": 1e3 * t1,
-            "sample": f"HNSW M=32 ef_construction=ef_search=100 (instant-distance 0.6.1 defaults, restated) built "
-                      f"on the first {ns} rows of the corpus; the {B} benchmark queries, one query per thread; "
-                      f"recall vs the exact top-{k} of those {ns} rows",
+            "value": ref["qps"], "unit": "queries/s", "cores": threads, "kind": "port",
+            "recall_at_10": ref["recall_at_10"], "rows": ns, "build_s": tb,
+            "single_thread_ms_per_query": 1e3 * t1, "points": hpts,
+            "sample": f"HNSW M=32 ef_construction=100 (instant-distance 0.6.1 defaults, restated; value at "
+                      f"ef_search=100) built on the first {ns} rows of the corpus; the {B} benchmark queries, one "
+                      f"query per thread; recall vs the exact top-{k} of those {ns} rows",
         }
-        del h, xs
+        del h
+        # the GPU on the same prefix
+        sub_ix = gvdb.GpuVectorIndex(dimension=D, capacity_hint=ns)
+        xt = torch.from_numpy(xs).to(dev)
+        sub_ix.add_device(xt, torch.arange(ns, dtype=torch.int64, device=dev))
+        del xt
+        gpts = []
+        osi = torch.zeros((B, k), dtype=torch.int64, device=dev)
+        oss = torch.zeros((B, k), dtype=torch.float32, device=dev)
+        for name, prm in [(f"bq R={r}", gvdb.SearchParams(rescore_count=r)) for r in (10, 30, 100, 300, 1000, 3000)] + \
+                [("exact flat", gvdb.SearchParams(mode=1))]:
+            sub_ix.search_device(q, k, osi, oss, None, prm)
+            torch.cuda.synchronize()
+            reps = 5
+            tp = time.perf_counter()
+            for _ in range(reps):
+                sub_ix.search_device(q, k, osi, oss, None, prm)
+            torch.cuda.synchronize()
+            tp = time.perf_counter() - tp
+            gpts.append({"search": name, "qps": B * reps / tp, "batch": B,
+                         "recall_at_10": recall_at(osi.cpu().numpy(), sub_truth)})
+        del sub_ix
+        torch.cuda.empty_cache()
+        pairs = []
+        for hp in hpts:
+            ok = [g for g in gpts if g["recall_at_10"] >= hp["recall_at_10"] - 0.02]
+            if ok:
+                best = max(ok, key=lambda g: g["qps"])
+                pairs.append({"hnsw_ef_search": hp["ef_search"], "hnsw_qps": hp["qps"],
+                              "hnsw_recall_at_10": hp["recall_at_10"], "gpu_search": best["search"],
+                              "gpu_qps": best["qps"], "gpu_recall_at_10": best["recall_at_10"],
+                              "speedup": best["qps"] / hp["qps"]})
+        matched = {"rows": ns, "gpu_points": gpts, "pairs": pairs,
+                   "note": "matched N (the same prefix rows, ids = prefix rows) and matched recall (GPU >= HNSW - 0.02); "
+                           "1M-row sweep: profiles/r02/equal_recall_1000000x768.json"}
+        del xs
 
     if rank == 0:
         line = {
@@ -460,16 +503,8 @@ def main():
             "operating_points": points,
             "cpu_hnsw": cpu_hnsw,
         }
-        if points and cpu_hnsw:
-            best = max((p for p in points if p.get("queries") == "iid" and p["recall_at_10"] >= cpu_hnsw["recall_at_10"]),
-                       key=lambda p: p["qps"], default=None)
-            if best:
-                line["gpu_vs_cpu_hnsw"] = {
-                    "gpu_search": best["search"], "gpu_qps": best["qps"], "gpu_recall_at_10": best["recall_at_10"],
-                    "cpu_hnsw_qps": cpu_hnsw["value"], "cpu_hnsw_recall_at_10": cpu_hnsw["recall_at_10"],
-                    "speedup": best["qps"] / cpu_hnsw["value"],
-                    "note": f"fastest GPU point (10M rows) with recall >= CPU HNSW's recall on {cpu_hnsw['rows']} rows",
-                }
+        if matched:
+            line["gpu_vs_cpu_hnsw"] = matched
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist
