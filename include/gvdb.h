@@ -318,9 +318,12 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
                                              void* stream);
 
 /* ---- BM25 sparse index (src/sparse.rs:29-222) ---------------------------- */
-/* SparseIndex: an HBM forward index over document slots; documents are
- * (term id, term frequency) lists with a document_length, exactly what
- * DocumentSparseRepresentation carries (types.rs:93-102). */
+/* SparseIndex: documents are (term id, term frequency) lists with a
+ * document_length, exactly what DocumentSparseRepresentation carries
+ * (types.rs:93-102).  The host keeps the document-major entries; the device
+ * holds them as a blocked inverted index (per 64-document chunk, entries by
+ * term), rebuilt lazily after a mutation.  Search is term-at-a-time per
+ * chunk (gvdb_sparse.hip). */
 typedef struct gvdb_bm25_params {  /* BM25Parameters, sparse.rs:42-53 */
     float k1;                       /* default 1.2 */
     float b;                        /* default 0.75 */
@@ -372,7 +375,9 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* index, const uint64_t* q_ptr, c
  * `limit` per query go to out_ids / out_scores [q*limit + i] and, when
  * out_breakdown is non-NULL, the raw dense / sparse / text score of each
  * result to out_breakdown[(q*limit + i)*3 + l] (NaN = absent, ScoreBreakdown).
- * At most 1024 items per query.  The _device form takes device pointers. */
+ * At most 4096 items per query: the three list strides (of the lists passed)
+ * may sum to 4096, more is GVDB_ERR_INVALID_ARGUMENT.  The _device form takes
+ * device pointers. */
 gvdb_status gvdb_rrf_fuse(const uint64_t* dense_ids, const float* dense_scores, const uint32_t* dense_n,
                           uint32_t dense_stride, const uint64_t* sparse_ids, const float* sparse_scores,
                           const uint32_t* sparse_n, uint32_t sparse_stride, const uint64_t* text_ids,
