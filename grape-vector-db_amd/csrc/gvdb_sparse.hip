@@ -48,6 +48,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -67,7 +68,6 @@ constexpr uint32_t kTaQ = kTaWaves * kTaQW;     // queries per launch group
 constexpr uint32_t kTaStage = 4096;             // entries per chunk staged through registers (more: from HBM)
 constexpr uint32_t kTaGrp = 8;                  // sample pass: one max key per 8 slots
 constexpr uint32_t kTaCptrLds = 512;            // chunks per block (their ranges cached in LDS)
-constexpr uint32_t kTaSent = 0x7fbadbadu;       // map "no posting": a signalling NaN, never an arithmetic result
 constexpr uint32_t kSpQT = 1024;                // query terms per launch group (LDS)
 constexpr uint32_t kSpU = 511;                  // distinct terms per launch group (map row kSpU stays empty)
 constexpr uint32_t kSpCand = 4096;              // candidates per query (LDS sort)
@@ -93,7 +93,9 @@ __device__ __forceinline__ uint32_t sp_slot(uint64_t key) { return ~(uint32_t)ke
 // slot, add order) -- the inverted index restricted to the chunk's documents
 // -- by one stable radix sort of (chunk, term) keys over the slot-ordered
 // forward entries.  A chunk's entries stay the forward range
-// [ptr[64c], ptr[64c + 64]).
+// [ptr[64c], ptr[64c + 64]).  Terms are stored as their rank in the index's
+// sorted vocabulary (dense ids, same order), so a search group's terms are
+// found through a direct-mapped table instead of a hash.
 // ---------------------------------------------------------------------------
 __global__ void k_blk_keys(const uint64_t* __restrict__ ptr, uint32_t N, const uint32_t* __restrict__ term,
                            uint64_t* __restrict__ keys, uint32_t* __restrict__ iota, uint32_t* __restrict__ eslot) {
@@ -108,16 +110,22 @@ __global__ void k_blk_keys(const uint64_t* __restrict__ ptr, uint32_t N, const u
 
 __global__ void k_blk_gather(const uint32_t* __restrict__ order, const uint64_t* __restrict__ keys,
                              const uint32_t* __restrict__ eslot, const float* __restrict__ tf,
-                             const float* __restrict__ dl, uint64_t E, uint32_t* __restrict__ cterm,
-                             uint8_t* __restrict__ cslot, float* __restrict__ ctf, float* __restrict__ cdl,
-                             uint32_t* __restrict__ runs) {
+                             const float* __restrict__ dl, uint64_t E, const uint32_t* __restrict__ vocab,
+                             uint32_t V, uint32_t* __restrict__ cterm, uint8_t* __restrict__ cslot,
+                             float* __restrict__ ctf, float* __restrict__ cdl, uint32_t* __restrict__ runs) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t e = order[i], s = eslot[e];
-        cterm[i] = (uint32_t)keys[i];
+        const uint32_t e = order[i], s = eslot[e], t = (uint32_t)keys[i];
+        uint32_t lo = 0, hi = V;  // lower_bound(vocab, t)
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (vocab[mid] < t) lo = mid + 1; else hi = mid;
+        }
+        if (lo >= V || vocab[lo] != t) *runs |= 2u;  // a term missing from the vocabulary
+        cterm[i] = lo;
         cslot[i] = (uint8_t)(s % kTaCh);
         ctf[i] = tf[e];
         cdl[i] = dl[e];
-        if (i > 0 && keys[i] == keys[i - 1] && eslot[order[i - 1]] == s) *runs = 1u;  // same term, same document
+        if (i > 0 && keys[i] == keys[i - 1] && eslot[order[i - 1]] == s) *runs |= 1u;  // same term, same document
     }
 }
 
@@ -132,6 +140,13 @@ __global__ void k_blk_tfc(const float* __restrict__ ctf, const float* __restrict
     }
 }
 
+// A search group's direct-mapped term table: gmap[dense term] = (epoch << 9) | group
+// term index; entries of earlier epochs read as "not in the group".
+constexpr uint32_t kGmapShift = 9;
+__global__ void k_gmap_set(uint32_t* __restrict__ gmap, const uint32_t* __restrict__ ut, uint32_t nu, uint32_t epoch) {
+    for (uint32_t i = threadIdx.x; i < nu; i += blockDim.x) gmap[ut[i]] = (epoch << kGmapShift) | i;
+}
+
 struct TaArgs {
     const uint64_t* cptr;   // [nchunks+1] entry range of each blocked-index chunk (= forward ptr every 64 slots)
     const uint32_t* cterm;  // blocked entries: term, slot within the chunk, tf_component
@@ -140,8 +155,12 @@ struct TaArgs {
     uint32_t N;             // slots
     uint32_t nchunks;       // blocked-index (64-slot) chunks
     uint64_t n_entries;     // > 0
-    const uint32_t* ut;     // [nu] the group's distinct live terms
+    const uint32_t* ut;     // [nu] the group's distinct live terms (dense ids, sorted)
     uint32_t nu;
+    const uint32_t* gmap;   // [vocabulary] (epoch << 9) | group term index
+    uint32_t epoch;
+    const uint64_t* qmask;  // [nu] the group's queries (bit = index in the group) holding each term
+    uint64_t qsel;          // queries with a non-finite q_tf or idf (bit = index in the group)
     const uint32_t* qp;     // [B+1] offsets into qrec
     const uint32_t* perm;   // [B] query of each wave slot (w + 16 m)
     const uint4* qrec;      // [nqt+1] per query term: (group term, q_tf bits, idf bits, 0); [nqt] = the empty row
@@ -156,12 +175,9 @@ struct TaArgs {
     uint64_t* dense;        // dense mode: [N] keys of query `dense_q`
     uint32_t dense_q;
     uint32_t runs;          // the index holds a (term, document) run longer than one entry (a re-added id)
-    uint32_t abl;           // timing probe only (GVDB_BM25_ABL): 1 skip rounds, 2 skip entry loads, 8 phase clocks
+    uint32_t abl;           // timing probe only (GVDB_BM25_ABL): 1 skip rounds (results invalid), 8 phase clocks
     uint64_t* prof;         // [gridDim][8] cycles per phase (wave 0), with abl & 8
 };
-
-constexpr uint32_t kHashSlots = 1024;  // LDS open-addressing table of the group's terms (load <= 1/2)
-__device__ __forceinline__ uint32_t term_hash(uint32_t t) { return (t * 0x9E3779B1u) >> 22; }
 
 // MODE 0: sample (every `every`-th chunk -> per 8 slots the max key -> smp),
 // 1: emit (key >= tau -> cand), 2: dense keys of query `dense_q`.
@@ -169,16 +185,21 @@ __device__ __forceinline__ uint32_t term_hash(uint32_t t) { return (t * 0x9E3779
 // chunks); the LDS map then has 512 / SPL rows (group terms + the empty row).
 //
 // One block per CU walks a contiguous range of chunks.  Per chunk:
-//   1. its blocked entries (all terms, ~30 per document) stream in; an LDS
-//      hash of the group's terms keeps those of the batch, whose
-//      tf_component lands in an LDS (group term x slot) map (kTaSent = no
-//      posting; the first entry of a re-added document's run);
+//   1. its blocked entries (all terms, ~30 per document) stream in; the
+//      group's direct-mapped term table (gmap, read a chunk ahead) keeps those
+//      of the batch, whose tf_component lands in an LDS (group term x slot)
+//      map (the first entry of a re-added document's run), and whose
+//      queries' bits (host mask per group term) are OR-ed into the slot's
+//      LDS hit mask: the documents each query matches;
 //   2. rounds: lane = SPL slots, wave w owns 4 queries (host-balanced),
 //      accumulators in registers.  Query q's terms in order: one map read,
 //      acc = acc + q_tf * tfc * idf -- per document exactly the reference's
-//      fold (sparse.rs:167-190; acc starts at 0.0 = or_insert).  A run of
-//      several entries (rare: the index records whether any exists) is folded
-//      from HBM in order;
+//      fold (sparse.rs:167-190; acc starts at 0.0 = or_insert).  No posting
+//      reads +0.0 (a posting's own +0.0 tfc is stored as -0.0): when q_tf and
+//      idf are finite its product is +-0.0 and acc + +-0.0 == acc (acc never
+//      holds -0.0), so the fold needs no select; queries with a non-finite
+//      q_tf or idf (host flag) select per term.  A run of several entries
+//      (rare: the index records whether any exists) is folded from HBM in order;
 //   3. selection by the mode.
 // Software pipeline: a chunk's entries are loaded two chunks ahead.
 template <int MODE, int SPL>
@@ -187,9 +208,9 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     constexpr uint32_t kRows = 512u / SPL;         // map rows: 128 KB
     constexpr uint32_t kEmpty = kRows - 1;         // the empty row
     __shared__ __attribute__((aligned(16))) float s_tmap[kRows * kCh];
-    __shared__ uint32_t s_hkey[kHashSlots];
-    __shared__ uint16_t s_hval[kHashSlots];
-    __shared__ uint32_t s_ut[kRows];  // group term index -> term
+    __shared__ uint32_t s_ut[kRows];        // group term index -> dense term
+    __shared__ uint64_t s_qmask[kRows];     // group term index -> the group's queries holding it
+    __shared__ uint64_t s_hit[kCh];         // per slot of the chunk: the queries it matches
     __shared__ uint32_t s_slow;
     __shared__ uint64_t s_cptr[(SPL + 1) * (kTaCptrLds + 1)];  // the block's chunk (sub-)ranges
     typedef const uint32_t __attribute__((address_space(4)))* cu32;
@@ -199,34 +220,15 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nu = a.nu;  // < kRows (host)
-    for (uint32_t i = tid; i < kRows * kCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
-    for (uint32_t i = tid; i < kHashSlots; i += kTaThreads) s_hkey[i] = 0xffffffffu;
-    __syncthreads();
-    // the group's terms (distinct): linear probing; 0xffffffff marks empty, so
-    // that term id itself is found as the sorted list's last entry
-    bool max_term = false;
+    for (uint32_t i = tid; i < kRows * kCh; i += kTaThreads) s_tmap[i] = 0.0f;
     if (tid < nu) {
-        const uint32_t t = a.ut[tid];
-        s_ut[tid] = t;
-        if (t == 0xffffffffu) {
-            max_term = true;
-        } else {
-            uint32_t h = term_hash(t);
-            while (atomicCAS(&s_hkey[h], 0xffffffffu, t) != 0xffffffffu) h = (h + 1) & (kHashSlots - 1);
-            s_hval[h] = (uint16_t)tid;
-        }
+        s_ut[tid] = a.ut[tid];
+        s_qmask[tid] = a.qmask[tid];
     }
-    const bool has_max_term = __syncthreads_or(max_term);
-    auto group_of = [&](uint32_t t) -> uint32_t {  // group term index, or kEmpty (not in the batch)
-        if (t == 0xffffffffu) return has_max_term ? nu - 1 : kEmpty;
-        uint32_t h = term_hash(t);
-        while (true) {
-            const uint32_t k = s_hkey[h];
-            if (k == t) return s_hval[h];
-            if (k == 0xffffffffu) return kEmpty;
-            h = (h + 1) & (kHashSlots - 1);
-        }
-    };
+    // a posting's tfc in the map: +0.0 is "no posting", so a posting's +0.0 is kept as -0.0
+    auto map_tfc = [](float f) { return __float_as_uint(f) == 0u ? -0.0f : f; };
+    // group term index of a gmap word, kEmpty for a term outside the group
+    auto group_of = [&](uint32_t gv) { return (gv >> kGmapShift) == a.epoch ? gv & ((1u << kGmapShift) - 1) : kEmpty; };
     // this wave's queries (uniform): wave slot w + 16 m holds query perm[w + 16 m]
     // (the host balances the slots' total terms across waves)
     const cu32 perm = (cu32)(uintptr_t)a.perm;
@@ -239,6 +241,9 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         ql[m] = live ? qp[qid[m] + 1] - qp0[m] : 0u;
         rmax = max(rmax, ql[m]);
     }
+    bool wave_sel = false;  // a query of the wave has a non-finite q_tf or idf: select per term
+#pragma unroll
+    for (uint32_t m = 0; m < kTaQW; ++m) wave_sel |= qid[m] != 0xffffffffu && ((a.qsel >> qid[m]) & 1ull);
     uint64_t tau[kTaQW];
 #pragma unroll
     for (uint32_t m = 0; m < kTaQW; ++m) tau[m] = MODE == 1 && qid[m] != 0xffffffffu ? a.tau[qid[m]] : 0ull;
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         for (uint32_t h = 0; h <= SPL; ++h) s_cptr[(SPL + 1) * i + h] = a.cptr[min(c + h, (uint64_t)a.nchunks)];
     }
     __syncthreads();
-    uint64_t ph[4] = {0, 0, 0, 0}, tprev = 0;
+    uint64_t ph[5] = {0, 0, 0, 0, 0}, tprev = 0;
     auto mark = [&](int k) {
         if (a.abl & 8) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -276,8 +281,9 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     // ---- a chunk's entries through registers, two chunks ahead (double buffer)
     constexpr uint32_t kPer = kTaStage / kTaThreads;
     struct Stage {
-        uint32_t t[kPer], s[kPer];  // term, slot within the blocked-index chunk
+        uint32_t t[kPer], s[kPer];  // dense term, slot within the blocked-index chunk
         float f[kPer];              // tf_component
+        uint32_t g[kPer];           // gmap word of the term (loaded a chunk ahead of the build)
     };
     Stage st0, st1;
     uint32_t cell[kPer];  // map cells this thread wrote for the current chunk (unwritten after its rounds)
@@ -289,15 +295,21 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         // build skips): no use and no register write before the chunk's turn
         const uint64_t e0 = jx < je ? s_cptr[(SPL + 1) * (jx - jb)] : 0ull;
 #pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) sg.t[k] = a.cterm[min(e0 + tid + k * kTaThreads, last)];
+#pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint64_t i = min(e0 + tid + k * kTaThreads, last);
-            sg.t[k] = a.cterm[i];
             sg.s[k] = a.cslot[i];
             sg.f[k] = a.ctfc[i];
         }
     };
+    // the group table words of a stage's terms (its entries arrived a chunk earlier)
+    auto lookup = [&](Stage& sg) {
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) sg.g[k] = a.gmap[sg.t[k]];
+    };
     bool prev_overflow = false;
-    auto chunk = [&](Stage& sg, uint32_t jj) {
+    auto chunk = [&](Stage& sg, Stage& nx, uint32_t jj) {
         const uint32_t c0 = jj * every * kCh;
         const uint64_t* cr = &s_cptr[(SPL + 1) * (jj - jb)];
         const uint64_t ce0 = cr[0], ce1 = cr[SPL], cmid = cr[1];  // cmid: start of the second sub-chunk
@@ -305,12 +317,13 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         __syncthreads();  // (1) the previous chunk's rounds are done
         mark(-1);
         if (prev_overflow) {  // cells written past the register stage are not tracked: clear the rows
-            for (uint32_t i = tid; i < nu * kCh; i += kTaThreads) s_tmap[i] = __uint_as_float(kTaSent);
+            for (uint32_t i = tid; i < nu * kCh; i += kTaThreads) s_tmap[i] = 0.0f;
         } else {
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k)
-                if (cell[k] != 0xffffffffu) s_tmap[cell[k]] = __uint_as_float(kTaSent);
+                if (cell[k] != 0xffffffffu) s_tmap[cell[k]] = 0.0f;
         }
+        if (tid < kCh) s_hit[tid] = 0ull;
         if (tid == 0) s_slow = 0;
         __syncthreads();  // (2) the map is clean
         mark(0);
@@ -320,25 +333,28 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             for (uint32_t k = 0; k < kPer; ++k) {
                 cell[k] = 0xffffffffu;
                 const uint64_t i = ce0 + tid + k * kTaThreads;
-                if (i >= ce1) continue;
-                const uint32_t g = group_of(sg.t[k]);
-                if (g == kEmpty) continue;
+                const uint32_t g = group_of(sg.g[k]);
+                if (i >= ce1 || g == kEmpty) continue;
                 if (a.runs) {  // a re-added document: only the first entry of its run enters the map
                     if (i + 1 < ce1 && a.cterm[i + 1] == sg.t[k] && a.cslot[i + 1] == sg.s[k]) slow = true;
                     if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) continue;
                 }
-                cell[k] = g * kCh + slot_in_chunk(i, sg.s[k]);
-                s_tmap[cell[k]] = sg.f[k];
+                const uint32_t sl = slot_in_chunk(i, sg.s[k]);
+                cell[k] = g * kCh + sl;
+                s_tmap[cell[k]] = map_tfc(sg.f[k]);
+                atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
             }
             for (uint64_t i = ce0 + kTaStage + tid; i < ce1; i += kTaThreads) {  // past the register stage
-                const uint32_t g = group_of(a.cterm[i]);
+                const uint32_t g = group_of(a.gmap[a.cterm[i]]);
                 if (g == kEmpty) continue;
                 const uint32_t s = a.cslot[i];
                 if (i > ce0 && a.cterm[i - 1] == a.cterm[i] && a.cslot[i - 1] == s) {
                     slow = true;
                     continue;
                 }
-                s_tmap[g * kCh + slot_in_chunk(i, s)] = a.ctfc[i];
+                const uint32_t sl = slot_in_chunk(i, s);
+                s_tmap[g * kCh + sl] = map_tfc(a.ctfc[i]);
+                atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
                 slow = slow || (i + 1 < ce1 && a.cterm[i + 1] == a.cterm[i] && a.cslot[i + 1] == s);
             }
             if (slow) s_slow = 1u;
@@ -346,20 +362,19 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         __syncthreads();  // (3) the chunk's map is built
         mark(1);
         prev_overflow = ce1 - ce0 > kTaStage;
+        lookup(nx);                // the next chunk's group words
         load_entries(sg, jj + 2);  // in flight during this chunk's and the next chunk's rounds
+        mark(4);
         // 2. rounds, per query m in its term order; lane holds slots SPL*lane + h
         float acc[kTaQW][SPL];
-        uint64_t hit[kTaQW][SPL];  // lane masks
 #pragma unroll
         for (uint32_t m = 0; m < kTaQW; ++m)
 #pragma unroll
-            for (uint32_t h = 0; h < SPL; ++h) {
-                acc[m][h] = 0.0f;
-                hit[m][h] = 0;
-            }
-        if (a.abl & 1) {
-        } else if (!s_slow && rmax <= 16) {
-            // 4 terms at a time: the map reads issued together, then the folds in order
+            for (uint32_t h = 0; h < SPL; ++h) acc[m][h] = 0.0f;
+        // 4 terms at a time: the map reads issued together, then the folds in order.
+        // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`
+        auto fast_rounds = [&](auto sel_c) {
+            constexpr bool kSel = decltype(sel_c)::value;
 #pragma unroll
             for (uint32_t m = 0; m < kTaQW; ++m) {
                 for (uint32_t rb = 0; rb < ql[m]; rb += 4) {
@@ -382,17 +397,20 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                         const float idf = __uint_as_float(__builtin_amdgcn_readlane(lr_idf, ln));
 #pragma unroll
                         for (uint32_t h = 0; h < SPL; ++h) {
-                            // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`.
-                            // acc starts at +0.0 and never holds -0.0, so adding 0.0 for a
-                            // miss leaves it unchanged and the first hit is 0.0 + s
-                            const bool hh = __float_as_uint(tf[k][h]) != kTaSent;
                             const float sc = v * tf[k][h] * idf;
-                            acc[m][h] = acc[m][h] + (hh ? sc : 0.0f);
-                            hit[m][h] |= __ballot(hh);
+                            if constexpr (kSel)
+                                acc[m][h] = acc[m][h] + (__float_as_uint(tf[k][h]) != 0u ? sc : 0.0f);
+                            else
+                                acc[m][h] = acc[m][h] + sc;  // no posting: +-0.0
                         }
                     }
                 }
             }
+        };
+        if (a.abl & 1) {
+        } else if (!s_slow && rmax <= 16) {
+            if (wave_sel) fast_rounds(std::true_type{});
+            else fast_rounds(std::false_type{});
         } else {
             // a re-added document's run (every entry of (term, document) in order, from HBM), or a query
             // with more than 16 live terms
@@ -405,9 +423,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     for (uint32_t h = 0; h < SPL; ++h) {
                         const uint32_t sl = SPL * lane + h;  // slot within the chunk
                         const float t = s_tmap[rec.x * kCh + sl];
-                        const bool hh = __float_as_uint(t) != kTaSent;
-                        hit[m][h] |= __ballot(hh);
-                        if (!hh) continue;
+                        if (__float_as_uint(t) == 0u) continue;  // no posting
                         if (!s_slow) {
                             acc[m][h] = acc[m][h] + v * t * idf;
                             continue;
@@ -429,6 +445,9 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         }
         mark(2);
         // 3. selection: (query qid[m], slot c0 + SPL lane + h)
+        uint64_t hm[SPL];
+#pragma unroll
+        for (uint32_t h = 0; h < SPL; ++h) hm[h] = s_hit[SPL * lane + h];
 #pragma unroll
         for (uint32_t m = 0; m < kTaQW; ++m) {
             const uint32_t q = qid[m];
@@ -436,7 +455,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             uint64_t key[SPL];
 #pragma unroll
             for (uint32_t h = 0; h < SPL; ++h)
-                key[h] = (hit[m][h] >> lane) & 1ull ? sp_key(acc[m][h], c0 + SPL * lane + h) : 0ull;
+                key[h] = (hm[h] >> q) & 1ull ? sp_key(acc[m][h], c0 + SPL * lane + h) : 0ull;
             if constexpr (MODE == 0) {
                 uint64_t best = key[0];
 #pragma unroll
@@ -468,12 +487,13 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     };
     load_entries(st0, jb);
     load_entries(st1, jb + 1);
+    lookup(st0);
     for (uint32_t jj = jb; jj < je; jj += 2) {
-        chunk(st0, jj);
-        if (jj + 1 < je) chunk(st1, jj + 1);
+        chunk(st0, st1, jj);
+        if (jj + 1 < je) chunk(st1, st0, jj + 1);
     }
     if ((a.abl & 8) && tid == 0)
-        for (int k = 0; k < 4; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
+        for (int k = 0; k < 5; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
 }
 
 // tau[q] = the kk-th largest sampled key (0 when fewer than kk matched): each
@@ -712,6 +732,13 @@ struct gvdb_sparse {
     uint8_t* d_cslot = nullptr;
     float *d_ctf = nullptr, *d_cdl = nullptr, *d_ctfc = nullptr;
     uint64_t cap_cptr = 0, cap_cterm = 0, cap_cslot = 0, cap_ctf = 0, cap_cdl = 0, cap_ctfc = 0;
+    // the blocked index's vocabulary (sorted distinct terms; d_cterm holds ranks in it) and
+    // the search groups' direct-mapped term table over it (epoch-tagged words)
+    std::vector<uint32_t> vocab;
+    uint32_t* d_vocab = nullptr;
+    uint32_t* d_gmap = nullptr;
+    uint64_t cap_vocab = 0, cap_gmap = 0;
+    uint32_t epoch = 0;
     uint64_t version = 0, inv_version = ~0ull, tfc_version = ~0ull;
     uint32_t tfc_avgdl = 0;  // the avgdl bits d_ctfc was computed with
     bool runs = false;       // some (term, document) has more than one entry (re-added ids)
@@ -799,6 +826,16 @@ gvdb_status build_blocked(gvdb_sparse* sp, hipStream_t s) {
                            sp->d_cptr);
         SP_TRY(hipGetLastError(), "chunk ptr");
         uint32_t h_runs = 0;
+        sp->vocab.clear();
+        for (const auto& x : sp->plen)
+            if (x.second) sp->vocab.push_back(x.first);
+        std::sort(sp->vocab.begin(), sp->vocab.end());
+        const uint64_t V = sp->vocab.size();
+        SP_TRY(grow(sp->d_vocab, sp->cap_vocab, V + 1, 0), "alloc vocabulary");
+        SP_TRY(grow(sp->d_gmap, sp->cap_gmap, V + 1, 0), "alloc group table");
+        if (V) SP_TRY(hipMemcpyAsync(sp->d_vocab, sp->vocab.data(), V * 4, hipMemcpyHostToDevice, s), "vocabulary");
+        SP_TRY(hipMemsetAsync(sp->d_gmap, 0, (V + 1) * 4, s), "group table");
+        sp->epoch = 0;
         if (E > 0) {
             int end_bit = 32;
             while (end_bit < 64 && ((uint64_t)nchunks >> (end_bit - 32))) ++end_bit;
@@ -830,15 +867,17 @@ gvdb_status build_blocked(gvdb_sparse* sp, hipStream_t s) {
             if (e == hipSuccess) e = hipMemsetAsync(d_runs, 0, 4, s);
             if (e == hipSuccess) {
                 hipLaunchKernelGGL(k_blk_gather, dim3(2048), dim3(256), 0, s, order, skeys, eslot, sp->d_tf, sp->d_dl,
-                                   E, sp->d_cterm, sp->d_cslot, sp->d_ctf, sp->d_cdl, d_runs);
+                                   E, sp->d_vocab, (uint32_t)V, sp->d_cterm, sp->d_cslot, sp->d_ctf, sp->d_cdl,
+                                   d_runs);
                 e = hipGetLastError();
             }
             if (e == hipSuccess) e = hipMemcpyAsync(&h_runs, d_runs, 4, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             (void)hipFree(tmp);
             if (e != hipSuccess) return sp_dev(e, "build blocked index");
+            if (h_runs & 2u) return report_status(GVDB_ERR_INDEX, "posting term missing from the vocabulary");
         }
-        sp->runs = h_runs != 0;
+        sp->runs = (h_runs & 1u) != 0;
         sp->inv_version = sp->version;
     }
     uint32_t avg_bits;
@@ -919,7 +958,7 @@ void gvdb_sparse_destroy(gvdb_sparse* sp) {
     (void)hipSetDevice(sp->device);
     for (void* p : {(void*)sp->d_ptr, (void*)sp->d_term, (void*)sp->d_tf, (void*)sp->d_dl, (void*)sp->d_ids,
                     (void*)sp->d_cptr, (void*)sp->d_cterm, (void*)sp->d_cslot, (void*)sp->d_ctf, (void*)sp->d_cdl,
-                    (void*)sp->d_ctfc, sp->scratch})
+                    (void*)sp->d_ctfc, (void*)sp->d_vocab, (void*)sp->d_gmap, sp->scratch})
         if (p) (void)hipFree(p);
     if (sp->h_fail) (void)hipHostFree(sp->h_fail);
     if (sp->stream) (void)hipStreamDestroy(sp->stream);
@@ -1241,6 +1280,14 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             std::memcpy(&h_qrec[4 * i + 2], &h_qidf[i], 4);
         }
         h_qrec[4 * nqt] = 0u;  // the kernel maps a finished query's rounds to the empty row
+        // per group term the queries holding it; queries whose q_tf or idf is not finite
+        std::vector<uint64_t> h_qmask(nu + 1, 0ull);
+        uint64_t qsel = 0;
+        for (uint32_t q = 0; q < Bg; ++q)
+            for (uint32_t i = h_qp[q]; i < h_qp[q + 1]; ++i) {
+                h_qmask[h_qrec[4 * i]] |= 1ull << q;
+                if (!std::isfinite(h_qv[i]) || !std::isfinite(h_qidf[i])) qsel |= 1ull << q;
+            }
         // wave slots w + 16 m: longest-processing-time assignment of the queries to the
         // 16 waves (each wave's rounds cost about the sum of its queries' term counts)
         std::vector<uint32_t> h_perm(kTaQ, 0xffffffffu);
@@ -1264,8 +1311,8 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         // scratch: qp | perm | qrec | ut | tau | counts | fail | out_n | smp | cand | out ids | out scores
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
         const size_t o_qp = 0, o_perm = o_qp + al((Bg + 1) * 4), o_qrec = o_perm + al(kTaQ * 4),
-                     o_ut = o_qrec + al((nqt + 1) * 16),
-                     o_tau = o_ut + al(nu * 4 + 4), o_cnt = o_tau + al(Bg * 8),
+                     o_ut = o_qrec + al((nqt + 1) * 16), o_qm = o_ut + al(nu * 4 + 4),
+                     o_tau = o_qm + al(nu * 8 + 8), o_cnt = o_tau + al(Bg * 8),
                      o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_smp = o_n + al(Bg * 4),
                      o_cand = o_smp + al((size_t)Bg * S * 8), o_oi = o_cand + al((size_t)Bg * kSpCand * 8),
                      o_os = o_oi + al((size_t)Bg * L * 8), total = o_os + al((size_t)Bg * L * 4);
@@ -1280,7 +1327,17 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         SP_TRY(hipMemcpyAsync(base + o_qp, h_qp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
         SP_TRY(hipMemcpyAsync(base + o_qrec, h_qrec.data(), (nqt + 1) * 16, hipMemcpyHostToDevice, s), "qrec");
         SP_TRY(hipMemcpyAsync(base + o_perm, h_perm.data(), kTaQ * 4, hipMemcpyHostToDevice, s), "perm");
+        for (auto& t : group_terms)  // dense ids (the vocabulary holds every live term; same order)
+            t = (uint32_t)(std::lower_bound(sp->vocab.begin(), sp->vocab.end(), t) - sp->vocab.begin());
         if (nu) SP_TRY(hipMemcpyAsync(base + o_ut, group_terms.data(), nu * 4, hipMemcpyHostToDevice, s), "ut");
+        if (nu) SP_TRY(hipMemcpyAsync(base + o_qm, h_qmask.data(), nu * 8, hipMemcpyHostToDevice, s), "qmask");
+        if (++sp->epoch >> (32 - kGmapShift)) {  // epoch tag wrapped: clear the table
+            SP_TRY(hipMemsetAsync(sp->d_gmap, 0, (sp->vocab.size() + 1) * 4, s), "group table");
+            sp->epoch = 1;
+        }
+        hipLaunchKernelGGL(k_gmap_set, dim3(1), dim3(512), 0, s, sp->d_gmap, (const uint32_t*)(base + o_ut), nu,
+                           sp->epoch);
+        SP_TRY(hipGetLastError(), "bm25 group table");
         SP_TRY(hipMemsetAsync(base + o_cnt, 0, Bg * 4, s), "counts");
         TaArgs a{};
         a.cptr = sp->d_cptr;
@@ -1292,6 +1349,10 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         a.n_entries = sp->term.size();
         a.ut = (const uint32_t*)(base + o_ut);
         a.nu = nu;
+        a.gmap = sp->d_gmap;
+        a.epoch = sp->epoch;
+        a.qmask = (const uint64_t*)(base + o_qm);
+        a.qsel = qsel;
         a.qp = (const uint32_t*)(base + o_qp);
         a.qrec = (const uint4*)(base + o_qrec);
         a.perm = (const uint32_t*)(base + o_perm);
@@ -1328,12 +1389,14 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             h_prof.resize(1024 * 8);
             SP_TRY(hipMemcpyAsync(h_prof.data(), d_prof, 1024 * 8 * 8, hipMemcpyDeviceToHost, s), "prof");
             SP_TRY(hipStreamSynchronize(s), "prof");
-            double acc[4] = {0, 0, 0, 0};
+            double acc[5] = {0, 0, 0, 0, 0};
             const uint32_t G = sp_grid(nchunks);
             for (uint32_t g = 0; g < G; ++g)
-                for (int k = 0; k < 4; ++k) acc[k] += (double)h_prof[g * 8 + k];
-            fprintf(stderr, "[bm25 prof] per block, shader clock cycles: dir %.0f stage %.0f rounds %.0f select %.0f\n",
-                    acc[0] / G, acc[1] / G, acc[2] / G, acc[3] / G);
+                for (int k = 0; k < 5; ++k) acc[k] += (double)h_prof[g * 8 + k];
+            fprintf(stderr,
+                    "[bm25 prof] per block, shader clock cycles: dir %.0f stage %.0f rounds %.0f select %.0f "
+                    "issue %.0f\n",
+                    acc[0] / G, acc[1] / G, acc[2] / G, acc[3] / G, acc[4] / G);
             (void)hipFree(d_prof);
         }
         uint64_t* d_oi = (uint64_t*)(base + o_oi);

@@ -50,7 +50,7 @@ def same(a, b):
 
 
 def check_batch(sp_mod, g, o, qs, limit):
-    svs = [sp_mod.SparseVector(t.tolist(), v.tolist(), 1 << 31) for t, v in qs]
+    svs = [sp_mod.SparseVector(t.tolist(), v.tolist(), 1 << 32) for t, v in qs]
     ids, sc, n = g.search_bm25_batch(svs, limit)
     for b, (t, v) in enumerate(qs):
         ri, rs = o.search(t, v, limit)
@@ -257,3 +257,25 @@ def test_bm25_long_queries(sp_mod, oracle_mod):
     g, o = build(sp_mod, oracle_mod, docs)
     qs = queries(36, 20, 1500, 17, 61) + queries(37, 20, 1500, 1, 5)
     check_batch(sp_mod, g, o, qs, 15)
+
+
+def test_bm25_special_values(sp_mod, oracle_mod):
+    """Zero, negative and infinite tf / q_tf and term ids up to 2^32 - 1: a
+    posting whose tf_component is +0.0 still matches (score 0), a non-finite
+    q_tf poisons only its own query (the per-term select path), and sparse
+    32-bit term ids map through the index's dense vocabulary."""
+    r = np.random.default_rng(31)
+    vocab = np.array([0, 1, 2, 5, 77, 1 << 20, (1 << 31) + 3, 0xFFFFFFFE, 0xFFFFFFFF], np.uint32)
+    docs = []
+    for i in range(6000):
+        t = np.unique(r.choice(vocab, size=int(r.integers(1, 6)), replace=False)).astype(np.uint32)
+        v = r.choice(np.array([0.0, 1.0, 2.5, -1.0, 0.25], np.float32), size=t.size)
+        docs.append((t, v.astype(np.float32), np.float32(r.integers(1, 20))))
+    g, o = build(sp_mod, oracle_mod, docs)
+    qs = [(np.array([0xFFFFFFFF, 1 << 20], np.uint32), np.array([1.0, 2.0], np.float32)),
+          (np.array([5, 77], np.uint32), np.array([np.inf, 1.0], np.float32)),
+          (np.array([2], np.uint32), np.array([0.0], np.float32)),
+          (np.array([(1 << 31) + 3, 0, 1], np.uint32), np.array([1.0, -2.0, 0.5], np.float32)),
+          (np.array([0xFFFFFFFE, 12345], np.uint32), np.array([np.nan, 1.0], np.float32))]
+    for limit in (7, 300):
+        check_batch(sp_mod, g, o, qs, limit)
