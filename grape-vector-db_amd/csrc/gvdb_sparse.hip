@@ -181,38 +181,45 @@ struct TaArgs {
 
 // MODE 0: sample (every `every`-th chunk -> per 8 slots the max key -> smp),
 // 1: emit (key >= tau -> cand), 2: dense keys of query `dense_q`.
-// SPL slots per lane: a chunk of 64 SPL documents (1 or 2 blocked-index
-// chunks); the LDS map then has 512 / SPL rows (group terms + the empty row).
 //
-// One block per CU walks a contiguous range of chunks.  Per chunk:
+// One block per CU walks a contiguous range of chunks of 128 documents (two
+// blocked-index chunks; lane = 2 slots).  Per chunk:
 //   1. its blocked entries (all terms, ~30 per document) stream in; the
 //      group's direct-mapped term table (gmap, read a chunk ahead) keeps those
-//      of the batch, whose tf_component lands in an LDS (group term x slot)
-//      map (the first entry of a re-added document's run), and whose
-//      queries' bits (host mask per group term) are OR-ed into the slot's
-//      LDS hit mask: the documents each query matches;
-//   2. rounds: lane = SPL slots, wave w owns 4 queries (host-balanced),
-//      accumulators in registers.  Query q's terms in order: one map read,
+//      of the batch: their tf_components are compacted into an LDS stage
+//      (per wave: ballot + one counter add) and an LDS (group term x slot) map
+//      of u16 stage offsets (0 = no posting; the first entry of a re-added
+//      document's run) points at them -- 512 rows x 128 slots in 128 KB, so
+//      one group holds up to 511 distinct terms.  The queries' bits (host mask
+//      per group term) are OR-ed into the slot's LDS hit mask: the documents
+//      each query matches;
+//   2. rounds: wave w owns 4 queries (host-balanced), accumulators in
+//      registers.  Query q's terms in order: a map read, two stage reads,
 //      acc = acc + q_tf * tfc * idf -- per document exactly the reference's
 //      fold (sparse.rs:167-190; acc starts at 0.0 = or_insert).  No posting
-//      reads +0.0 (a posting's own +0.0 tfc is stored as -0.0): when q_tf and
-//      idf are finite its product is +-0.0 and acc + +-0.0 == acc (acc never
-//      holds -0.0), so the fold needs no select; queries with a non-finite
-//      q_tf or idf (host flag) select per term.  A run of several entries
-//      (rare: the index records whether any exists) is folded from HBM in order;
+//      reads stage[0] = +0.0 (a posting's own +0.0 tfc is staged as -0.0):
+//      when q_tf and idf are finite its product is +-0.0 and acc + +-0.0 ==
+//      acc (acc never holds -0.0), so the fold needs no select; queries with a
+//      non-finite q_tf or idf (host flag) select per term.  A run of several
+//      entries (rare: the index records whether any exists) or a stage
+//      overflow is folded from HBM in order;
 //   3. selection by the mode.
 // Software pipeline: a chunk's entries are loaded two chunks ahead.
-template <int MODE, int SPL>
+constexpr uint32_t kTaSpl = 2;              // slots per lane
+constexpr uint32_t kTaRows = 512;           // map rows: group terms + the empty row
+constexpr uint32_t kTaStaged = 4096;        // staged tf_components per chunk (index 0: +0.0)
+constexpr uint16_t kTaUnstaged = 0xffffu;   // a posting past the stage (odd: never a stage offset)
+static_assert(kSpU < kTaRows, "the empty row");
+static_assert(kTaStaged * 4 <= 0xffffu, "u16 byte offsets");
+template <int MODE>
 __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
-    constexpr uint32_t kCh = kTaCh * SPL;          // slots per chunk
-    constexpr uint32_t kRows = 512u / SPL;         // map rows: 128 KB
-    constexpr uint32_t kEmpty = kRows - 1;         // the empty row
-    __shared__ __attribute__((aligned(16))) float s_tmap[kRows * kCh];
-    __shared__ uint32_t s_ut[kRows];        // group term index -> dense term
-    __shared__ uint64_t s_qmask[kRows];     // group term index -> the group's queries holding it
-    __shared__ uint64_t s_hit[kCh];         // per slot of the chunk: the queries it matches
-    __shared__ uint32_t s_slow;
-    __shared__ uint64_t s_cptr[(SPL + 1) * (kTaCptrLds + 1)];  // the block's chunk (sub-)ranges
+    constexpr uint32_t SPL = kTaSpl, kCh = kTaCh * SPL, kRows = kTaRows, kEmpty = kRows - 1;
+    __shared__ __attribute__((aligned(16))) uint16_t s_tmap[kRows * kCh];  // stage byte offset per (term, slot)
+    __shared__ __attribute__((aligned(16))) float s_tfc[kTaStaged];
+    __shared__ uint64_t s_qmask[kRows];  // group term index -> the group's queries holding it
+    __shared__ uint64_t s_hit[kCh];      // per slot of the chunk: the queries it matches
+    __shared__ uint32_t s_cptr[(SPL + 1) * (kTaCptrLds + 1)];  // the block's chunk (sub-)ranges, from cbase
+    __shared__ uint32_t s_slow, s_nst;
     typedef const uint32_t __attribute__((address_space(4)))* cu32;
     const cu32 qp = (cu32)(uintptr_t)a.qp;  // read-only query tables: scalar loads
     const cu32 qr32 = (cu32)(uintptr_t)a.qrec;
@@ -220,12 +227,11 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nu = a.nu;  // < kRows (host)
-    for (uint32_t i = tid; i < kRows * kCh; i += kTaThreads) s_tmap[i] = 0.0f;
-    if (tid < nu) {
-        s_ut[tid] = a.ut[tid];
-        s_qmask[tid] = a.qmask[tid];
-    }
-    // a posting's tfc in the map: +0.0 is "no posting", so a posting's +0.0 is kept as -0.0
+    for (uint32_t i = tid; i < kRows * kCh / 2; i += kTaThreads) ((uint32_t*)s_tmap)[i] = 0u;
+    if (tid == 0) s_tfc[0] = 0.0f;
+    if (tid < nu) s_qmask[tid] = a.qmask[tid];
+    auto tfc_at = [&](uint32_t off) { return *(const float*)((const char*)s_tfc + off); };
+    // a posting's staged tfc: +0.0 is "no posting", so a posting's +0.0 is kept as -0.0
     auto map_tfc = [](float f) { return __float_as_uint(f) == 0u ? -0.0f : f; };
     // group term index of a gmap word, kEmpty for a term outside the group
     auto group_of = [&](uint32_t gv) { return (gv >> kGmapShift) == a.epoch ? gv & ((1u << kGmapShift) - 1) : kEmpty; };
@@ -264,10 +270,12 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     // contiguous chunk range per block (the host sizes the grid: je - jb <= kTaCptrLds)
     const uint32_t jb = (uint32_t)((uint64_t)nj * blockIdx.x / gridDim.x);
     const uint32_t je = (uint32_t)((uint64_t)nj * (blockIdx.x + 1) / gridDim.x);
+    const uint64_t cbase = a.cptr[min((uint64_t)jb * every * SPL, (uint64_t)a.nchunks)];
     for (uint32_t i = tid; i < je - jb; i += kTaThreads) {
         const uint64_t c = (uint64_t)(jb + i) * every * SPL;  // in blocked-index chunks
 #pragma unroll
-        for (uint32_t h = 0; h <= SPL; ++h) s_cptr[(SPL + 1) * i + h] = a.cptr[min(c + h, (uint64_t)a.nchunks)];
+        for (uint32_t h = 0; h <= SPL; ++h)
+            s_cptr[(SPL + 1) * i + h] = (uint32_t)(a.cptr[min(c + h, (uint64_t)a.nchunks)] - cbase);
     }
     __syncthreads();
     uint64_t ph[5] = {0, 0, 0, 0, 0}, tprev = 0;
@@ -293,7 +301,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     auto load_entries = [&](Stage& sg, uint32_t jx) {
         // unconditional loads (an index past the range reads a valid entry that the
         // build skips): no use and no register write before the chunk's turn
-        const uint64_t e0 = jx < je ? s_cptr[(SPL + 1) * (jx - jb)] : 0ull;
+        const uint64_t e0 = jx < je ? cbase + s_cptr[(SPL + 1) * (jx - jb)] : 0ull;
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) sg.t[k] = a.cterm[min(e0 + tid + k * kTaThreads, last)];
 #pragma unroll
@@ -311,20 +319,23 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     bool prev_overflow = false;
     auto chunk = [&](Stage& sg, Stage& nx, uint32_t jj) {
         const uint32_t c0 = jj * every * kCh;
-        const uint64_t* cr = &s_cptr[(SPL + 1) * (jj - jb)];
-        const uint64_t ce0 = cr[0], ce1 = cr[SPL], cmid = cr[1];  // cmid: start of the second sub-chunk
-        auto slot_in_chunk = [&](uint64_t i, uint32_t s) { return SPL == 2 && i >= cmid ? s + kTaCh : s; };
+        const uint32_t* cr = &s_cptr[(SPL + 1) * (jj - jb)];
+        const uint64_t ce0 = cbase + cr[0], ce1 = cbase + cr[SPL], cmid = cbase + cr[1];  // cmid: second sub-chunk
+        auto slot_in_chunk = [&](uint64_t i, uint32_t s) { return i >= cmid ? s + kTaCh : s; };
         __syncthreads();  // (1) the previous chunk's rounds are done
         mark(-1);
         if (prev_overflow) {  // cells written past the register stage are not tracked: clear the rows
-            for (uint32_t i = tid; i < nu * kCh; i += kTaThreads) s_tmap[i] = 0.0f;
+            for (uint32_t i = tid; i < nu * kCh / 2; i += kTaThreads) ((uint32_t*)s_tmap)[i] = 0u;
         } else {
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k)
-                if (cell[k] != 0xffffffffu) s_tmap[cell[k]] = 0.0f;
+                if (cell[k] != 0xffffffffu) s_tmap[cell[k]] = 0;
         }
         if (tid < kCh) s_hit[tid] = 0ull;
-        if (tid == 0) s_slow = 0;
+        if (tid == 0) {
+            s_slow = 0;
+            s_nst = 1;
+        }
         __syncthreads();  // (2) the map is clean
         mark(0);
         {
@@ -334,14 +345,28 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                 cell[k] = 0xffffffffu;
                 const uint64_t i = ce0 + tid + k * kTaThreads;
                 const uint32_t g = group_of(sg.g[k]);
-                if (i >= ce1 || g == kEmpty) continue;
-                if (a.runs) {  // a re-added document: only the first entry of its run enters the map
+                bool take = i < ce1 && g != kEmpty;
+                if (take && a.runs) {  // a re-added document: only the first entry of its run enters the map
                     if (i + 1 < ce1 && a.cterm[i + 1] == sg.t[k] && a.cslot[i + 1] == sg.s[k]) slow = true;
-                    if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) continue;
+                    if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) take = false;
                 }
+                // stage position: the wave's takers in lane order after one counter add
+                const uint64_t bal = __ballot(take);
+                uint32_t base = 0;
+                if (lane == 0 && bal) base = atomicAdd(&s_nst, (uint32_t)__popcll(bal));
+                base = __builtin_amdgcn_readfirstlane(base);
+                const uint32_t pos =
+                    base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                if (!take) continue;
                 const uint32_t sl = slot_in_chunk(i, sg.s[k]);
                 cell[k] = g * kCh + sl;
-                s_tmap[cell[k]] = map_tfc(sg.f[k]);
+                if (pos < kTaStaged) {
+                    s_tfc[pos] = map_tfc(sg.f[k]);
+                    s_tmap[cell[k]] = (uint16_t)(pos * 4);
+                } else {
+                    s_tmap[cell[k]] = kTaUnstaged;
+                    slow = true;
+                }
                 atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
             }
             for (uint64_t i = ce0 + kTaStage + tid; i < ce1; i += kTaThreads) {  // past the register stage
@@ -353,7 +378,14 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     continue;
                 }
                 const uint32_t sl = slot_in_chunk(i, s);
-                s_tmap[g * kCh + sl] = map_tfc(a.ctfc[i]);
+                const uint32_t pos = atomicAdd(&s_nst, 1u);
+                if (pos < kTaStaged) {
+                    s_tfc[pos] = map_tfc(a.ctfc[i]);
+                    s_tmap[g * kCh + sl] = (uint16_t)(pos * 4);
+                } else {
+                    s_tmap[g * kCh + sl] = kTaUnstaged;
+                    slow = true;
+                }
                 atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
                 slow = slow || (i + 1 < ce1 && a.cterm[i + 1] == a.cterm[i] && a.cslot[i + 1] == s);
             }
@@ -371,24 +403,24 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         for (uint32_t m = 0; m < kTaQW; ++m)
 #pragma unroll
             for (uint32_t h = 0; h < SPL; ++h) acc[m][h] = 0.0f;
-        // 4 terms at a time: the map reads issued together, then the folds in order.
-        // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`
+        // 4 terms at a time: the map reads issued together, then the stage reads, then the
+        // folds in order.  calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`
         auto fast_rounds = [&](auto sel_c) {
             constexpr bool kSel = decltype(sel_c)::value;
 #pragma unroll
             for (uint32_t m = 0; m < kTaQW; ++m) {
                 for (uint32_t rb = 0; rb < ql[m]; rb += 4) {
-                    float tf[4][SPL];
+                    uint32_t off[4];
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) {
                         const uint32_t row = __builtin_amdgcn_readlane(lr_row, m * 16 + ((rb + k) & 15u));
-                        if constexpr (SPL == 2) {
-                            const float2 t2 = *(const float2*)&s_tmap[row + 2 * lane];
-                            tf[k][0] = t2.x;
-                            tf[k][1 % SPL] = t2.y;
-                        } else {
-                            tf[k][0] = s_tmap[row + lane];
-                        }
+                        off[k] = *(const uint32_t*)&s_tmap[row + 2 * lane];
+                    }
+                    float tf[4][SPL];
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k) {
+                        tf[k][0] = tfc_at(off[k] & 0xffffu);
+                        tf[k][1] = tfc_at(off[k] >> 16);
                     }
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) {
@@ -399,7 +431,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                         for (uint32_t h = 0; h < SPL; ++h) {
                             const float sc = v * tf[k][h] * idf;
                             if constexpr (kSel)
-                                acc[m][h] = acc[m][h] + (__float_as_uint(tf[k][h]) != 0u ? sc : 0.0f);
+                                acc[m][h] = acc[m][h] + (((off[k] >> (16 * h)) & 0xffffu) != 0u ? sc : 0.0f);
                             else
                                 acc[m][h] = acc[m][h] + sc;  // no posting: +-0.0
                         }
@@ -412,8 +444,8 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             if (wave_sel) fast_rounds(std::true_type{});
             else fast_rounds(std::false_type{});
         } else {
-            // a re-added document's run (every entry of (term, document) in order, from HBM), or a query
-            // with more than 16 live terms
+            // a re-added document's run (every entry of (term, document) in order, from HBM), a stage
+            // overflow, or a query with more than 16 live terms
 #pragma unroll
             for (uint32_t m = 0; m < kTaQW; ++m) {
                 for (uint32_t r = 0; r < ql[m]; ++r) {
@@ -422,15 +454,15 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
 #pragma unroll
                     for (uint32_t h = 0; h < SPL; ++h) {
                         const uint32_t sl = SPL * lane + h;  // slot within the chunk
-                        const float t = s_tmap[rec.x * kCh + sl];
-                        if (__float_as_uint(t) == 0u) continue;  // no posting
+                        const uint32_t off = s_tmap[rec.x * kCh + sl];
+                        if (off == 0u) continue;  // no posting
                         if (!s_slow) {
-                            acc[m][h] = acc[m][h] + v * t * idf;
+                            acc[m][h] = acc[m][h] + v * tfc_at(off) * idf;
                             continue;
                         }
                         // the sub-chunk's entries are sorted by (term, slot): lower_bound((term, slot))
-                        const uint32_t term = s_ut[rec.x], sub = sl / kTaCh, ss = sl % kTaCh;
-                        const uint64_t r0 = cr[sub], r1 = cr[sub + 1];
+                        const uint32_t term = a.ut[rec.x], sub = sl / kTaCh, ss = sl % kTaCh;
+                        const uint64_t r0 = cbase + cr[sub], r1 = cbase + cr[sub + 1];
                         uint64_t lo = r0, hi = r1;
                         while (lo < hi) {
                             const uint64_t mid = (lo + hi) >> 1;
@@ -1195,12 +1227,6 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
     const uint32_t N = (uint32_t)sp->slot_id.size();
     const uint32_t L = (uint32_t)limit;
     const uint32_t nblk = (N + kTaCh - 1) / kTaCh;  // blocked-index chunks
-    // distinct terms per launch group before a new group starts (GVDB_BM25_GROUP_TERMS, timing knob)
-    static const size_t group_cap = [] {
-        const char* e = getenv("GVDB_BM25_GROUP_TERMS");
-        const long v = e ? atol(e) : 0;
-        return v >= 16 && v <= (long)kSpU ? (size_t)v : (size_t)255;  // 255: the 2-slot map (profiles/r02)
-    }();
     hipStream_t s = sp->stream;
     uint64_t q0 = 0;
     std::vector<uint32_t> h_qp;
@@ -1241,7 +1267,6 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
                         return report_status(GVDB_ERR_INVALID_ARGUMENT, "query has more than 511 distinct terms");
                     break;
                 }
-                if (u.size() > group_cap && q1 > q0) break;  // keep the group in the 2-slot map
                 group_terms.swap(u);
             }
             h_qt.insert(h_qt.end(), t.begin(), t.end());
@@ -1253,24 +1278,16 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         const uint32_t Bg = (uint32_t)(q1 - q0);
         const uint32_t nqt = (uint32_t)h_qt.size();
         const uint32_t nu = (uint32_t)group_terms.size();
-        // two slots per lane (128-document chunks) while the map's 256 rows hold the group
-        const uint32_t spl = nu < 256 ? 2u : 1u;
-        const uint32_t nchunks = (nblk + spl - 1) / spl;
+        const uint32_t nchunks = (nblk + kTaSpl - 1) / kTaSpl;  // 128-document chunks
         // sample stride: expected candidates ~ limit * every, kept well under kSpCand
         uint32_t every = std::max<uint32_t>(1u, std::min<uint32_t>(32u, kSpCand / std::max<uint32_t>(1u, 4u * L)));
         if (nchunks <= 8u * every) every = 1;  // small index: the sample is the whole index
         const uint32_t nsamp = (nchunks + every - 1) / every;
-        const uint32_t S = nsamp * (kTaCh * spl / kTaGrp);
+        const uint32_t S = nsamp * (kTaCh * kTaSpl / kTaGrp);
         auto launch_taat = [&](int mode, uint32_t grid, const TaArgs& ta) {
-            if (spl == 2) {
-                if (mode == 0) hipLaunchKernelGGL((k_bm25_taat<0, 2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
-                if (mode == 1) hipLaunchKernelGGL((k_bm25_taat<1, 2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
-                if (mode == 2) hipLaunchKernelGGL((k_bm25_taat<2, 2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
-            } else {
-                if (mode == 0) hipLaunchKernelGGL((k_bm25_taat<0, 1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
-                if (mode == 1) hipLaunchKernelGGL((k_bm25_taat<1, 1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
-                if (mode == 2) hipLaunchKernelGGL((k_bm25_taat<2, 1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
-            }
+            if (mode == 0) hipLaunchKernelGGL((k_bm25_taat<0>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+            if (mode == 1) hipLaunchKernelGGL((k_bm25_taat<1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
+            if (mode == 2) hipLaunchKernelGGL((k_bm25_taat<2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
         };
         std::vector<uint32_t> h_qrec(4 * (nqt + 1), 0u);  // (group term, q_tf, idf, 0); [nqt]: the empty row
         for (uint32_t i = 0; i < nqt; ++i) {
