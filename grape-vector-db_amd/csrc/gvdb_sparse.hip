@@ -163,7 +163,8 @@ struct TaArgs {
     uint64_t qsel;          // queries with a non-finite q_tf or idf (bit = index in the group)
     const uint32_t* qp;     // [B+1] offsets into qrec
     const uint32_t* perm;   // [B] query of each wave slot (w + 16 m)
-    const uint4* qrec;      // [nqt+1] per query term: (group term, q_tf bits, idf bits, 0); [nqt] = the empty row
+    const uint4* qrec;      // [nqt+4] per query term: (group term, q_tf bits, idf bits, map row bytes), each
+                            // query's padded with empty records (empty row, 0, 0) to a multiple of 4; [nqt, nqt+4) empty
     uint32_t nqt;
     uint32_t B;
     uint32_t every;         // sample pass: chunk stride
@@ -204,11 +205,13 @@ struct TaArgs {
 //      entries (rare: the index records whether any exists) or a stage
 //      overflow is folded from HBM in order;
 //   3. selection by the mode.
-// Software pipeline: a chunk's entries are loaded two chunks ahead.
+// Software pipeline: a chunk's entries are loaded three chunks ahead, their
+// group words one chunk ahead; emitted candidates pool in LDS.
 constexpr uint32_t kTaSpl = 2;              // slots per lane
 constexpr uint32_t kTaRows = 512;           // map rows: group terms + the empty row
 constexpr uint32_t kTaStaged = 4096;        // staged tf_components per chunk (index 0: +0.0)
 constexpr uint16_t kTaUnstaged = 0xffffu;   // a posting past the stage (odd: never a stage offset)
+constexpr uint32_t kTaPool = 448;           // emit: candidates pooled in LDS per block (more: direct)
 static_assert(kSpU < kTaRows, "the empty row");
 static_assert(kTaStaged * 4 <= 0xffffu, "u16 byte offsets");
 template <int MODE>
@@ -219,16 +222,23 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     __shared__ uint64_t s_qmask[kRows];  // group term index -> the group's queries holding it
     __shared__ uint64_t s_hit[kCh];      // per slot of the chunk: the queries it matches
     __shared__ uint32_t s_cptr[(SPL + 1) * (kTaCptrLds + 1)];  // the block's chunk (sub-)ranges, from cbase
-    __shared__ uint32_t s_slow, s_nst;
+    __shared__ uint32_t s_slow, s_nst, s_npool;
+    __shared__ uint64_t s_pkey[kTaPool];  // emit: the block's candidates (key, query), flushed at the end
+    __shared__ uint8_t s_pq[kTaPool];
     typedef const uint32_t __attribute__((address_space(4)))* cu32;
     const cu32 qp = (cu32)(uintptr_t)a.qp;  // read-only query tables: scalar loads
     const cu32 qr32 = (cu32)(uintptr_t)a.qrec;
-    auto qrec_at = [&](uint32_t p) { return make_uint4(qr32[4 * p], qr32[4 * p + 1], qr32[4 * p + 2], 0u); };
+    auto qrec_at = [&](uint32_t p) {
+        return make_uint4(qr32[4 * p], qr32[4 * p + 1], qr32[4 * p + 2], qr32[4 * p + 3]);
+    };
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nu = a.nu;  // < kRows (host)
     for (uint32_t i = tid; i < kRows * kCh / 2; i += kTaThreads) ((uint32_t*)s_tmap)[i] = 0u;
-    if (tid == 0) s_tfc[0] = 0.0f;
+    if (tid == 0) {
+        s_tfc[0] = 0.0f;
+        s_npool = 0;
+    }
     if (tid < nu) s_qmask[tid] = a.qmask[tid];
     auto tfc_at = [&](uint32_t off) { return *(const float*)((const char*)s_tfc + off); };
     // a posting's staged tfc: +0.0 is "no posting", so a posting's +0.0 is kept as -0.0
@@ -253,16 +263,23 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     uint64_t tau[kTaQW];
 #pragma unroll
     for (uint32_t m = 0; m < kTaQW; ++m) tau[m] = MODE == 1 && qid[m] != 0xffffffffu ? a.tau[qid[m]] : 0ull;
-    // the wave's query terms, lane-resident: lane 16 m + r holds query m's r-th term (r < 16):
-    // map row offset (the empty row past the query's end), q_tf, idf
+    // the wave's query terms, lane-resident: lane 16 m + r holds query m's r-th (padded) term
+    // record: map row bytes, q_tf, idf (the empty record past the query's end)
     uint32_t lr_row, lr_v, lr_idf;
     {
         const uint32_t m = lane >> 4, r = lane & 15u;
-        const bool in = r < ql[m & 3];
-        const uint4 rec = qrec_at(in ? qp0[m & 3] + r : a.nqt);
-        lr_row = (in ? rec.x : kEmpty) * kCh;
+        const uint4 rec = qrec_at(r < ql[m & 3] ? qp0[m & 3] + r : a.nqt);
+        lr_row = rec.w;
         lr_v = rec.y;
         lr_idf = rec.z;
+    }
+    // emit: a score below tau's cannot pass (acc is never -0.0; a NaN tau score passes every hit)
+    float thr[kTaQW];
+    bool loose[kTaQW];
+#pragma unroll
+    for (uint32_t m = 0; m < kTaQW; ++m) {
+        loose[m] = (tau[m] >> 32) == 0;
+        thr[m] = loose[m] ? 0.0f : sp_score(tau[m]);
     }
     const uint32_t every = MODE == 0 ? a.every : 1u;
     const uint32_t nchunks = (a.nchunks + SPL - 1) / SPL;  // in chunks of kCh slots
@@ -286,14 +303,14 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             tprev = t;
         }
     };
-    // ---- a chunk's entries through registers, two chunks ahead (double buffer)
+    // ---- a chunk's entries through registers, three chunks ahead (triple buffer)
     constexpr uint32_t kPer = kTaStage / kTaThreads;
     struct Stage {
         uint32_t t[kPer], s[kPer];  // dense term, slot within the blocked-index chunk
         float f[kPer];              // tf_component
         uint32_t g[kPer];           // gmap word of the term (loaded a chunk ahead of the build)
     };
-    Stage st0, st1;
+    Stage st0, st1, st2;
     uint32_t cell[kPer];  // map cells this thread wrote for the current chunk (unwritten after its rounds)
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) cell[k] = 0xffffffffu;
@@ -311,7 +328,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             sg.f[k] = a.ctfc[i];
         }
     };
-    // the group table words of a stage's terms (its entries arrived a chunk earlier)
+    // the group table words of a stage's terms (its entries were issued two chunks earlier)
     auto lookup = [&](Stage& sg) {
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) sg.g[k] = a.gmap[sg.t[k]];
@@ -340,24 +357,34 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         mark(0);
         {
             bool slow = false;
+            bool take[kPer];
+            uint32_t gk[kPer], pre[kPer], tot = 0;
+            uint64_t bal[kPer];
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint64_t i = ce0 + tid + k * kTaThreads;
+                gk[k] = group_of(sg.g[k]);
+                take[k] = i < ce1 && gk[k] != kEmpty;
+                if (take[k] && a.runs) {  // a re-added document: only the first entry of its run enters the map
+                    if (i + 1 < ce1 && a.cterm[i + 1] == sg.t[k] && a.cslot[i + 1] == sg.s[k]) slow = true;
+                    if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) take[k] = false;
+                }
+                bal[k] = __ballot(take[k]);
+                pre[k] = tot;
+                tot += (uint32_t)__popcll(bal[k]);
+            }
+            // stage positions: the wave's takers in (k, lane) order after one counter add
+            uint32_t base = 0;
+            if (lane == 0 && tot) base = atomicAdd(&s_nst, tot);
+            base = __builtin_amdgcn_readfirstlane(base);
 #pragma unroll
             for (uint32_t k = 0; k < kPer; ++k) {
                 cell[k] = 0xffffffffu;
+                if (!take[k]) continue;
                 const uint64_t i = ce0 + tid + k * kTaThreads;
-                const uint32_t g = group_of(sg.g[k]);
-                bool take = i < ce1 && g != kEmpty;
-                if (take && a.runs) {  // a re-added document: only the first entry of its run enters the map
-                    if (i + 1 < ce1 && a.cterm[i + 1] == sg.t[k] && a.cslot[i + 1] == sg.s[k]) slow = true;
-                    if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) take = false;
-                }
-                // stage position: the wave's takers in lane order after one counter add
-                const uint64_t bal = __ballot(take);
-                uint32_t base = 0;
-                if (lane == 0 && bal) base = atomicAdd(&s_nst, (uint32_t)__popcll(bal));
-                base = __builtin_amdgcn_readfirstlane(base);
-                const uint32_t pos =
-                    base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                if (!take) continue;
+                const uint32_t g = gk[k];
+                const uint32_t pos = base + pre[k] +
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
                 const uint32_t sl = slot_in_chunk(i, sg.s[k]);
                 cell[k] = g * kCh + sl;
                 if (pos < kTaStaged) {
@@ -395,7 +422,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         mark(1);
         prev_overflow = ce1 - ce0 > kTaStage;
         lookup(nx);                // the next chunk's group words
-        load_entries(sg, jj + 2);  // in flight during this chunk's and the next chunk's rounds
+        load_entries(sg, jj + 3);  // in flight during the next two chunks
         mark(4);
         // 2. rounds, per query m in its term order; lane holds slots SPL*lane + h
         float acc[kTaQW][SPL];
@@ -413,8 +440,8 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     uint32_t off[4];
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) {
-                        const uint32_t row = __builtin_amdgcn_readlane(lr_row, m * 16 + ((rb + k) & 15u));
-                        off[k] = *(const uint32_t*)&s_tmap[row + 2 * lane];
+                        const uint32_t rowb = __builtin_amdgcn_readlane(lr_row, m * 16 + ((rb + k) & 15u));
+                        off[k] = *(const uint32_t*)((const char*)s_tmap + rowb + 4 * lane);
                     }
                     float tf[4][SPL];
 #pragma unroll
@@ -484,10 +511,36 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         for (uint32_t m = 0; m < kTaQW; ++m) {
             const uint32_t q = qid[m];
             if (q == 0xffffffffu) continue;
+            bool hb[SPL];
+#pragma unroll
+            for (uint32_t h = 0; h < SPL; ++h) hb[h] = (hm[h] >> q) & 1ull;
+            if constexpr (MODE == 1) {
+                bool pass[SPL], any = false;
+#pragma unroll
+                for (uint32_t h = 0; h < SPL; ++h) {
+                    pass[h] = hb[h] && (loose[m] || acc[m][h] >= thr[m]);
+                    any |= pass[h];
+                }
+                if (__ballot(any) == 0ull) continue;  // usual: no document of the chunk reaches tau
+#pragma unroll
+                for (uint32_t h = 0; h < SPL; ++h) {
+                    const uint64_t key = pass[h] ? sp_key(acc[m][h], c0 + SPL * lane + h) : 0ull;
+                    if (key != 0ull && key >= tau[m]) {
+                        const uint32_t pp = atomicAdd(&s_npool, 1u);
+                        if (pp < kTaPool) {
+                            s_pkey[pp] = key;
+                            s_pq[pp] = (uint8_t)q;
+                        } else {
+                            const uint32_t pos = atomicAdd(&a.counts[q], 1u);
+                            if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key;
+                        }
+                    }
+                }
+                continue;
+            }
             uint64_t key[SPL];
 #pragma unroll
-            for (uint32_t h = 0; h < SPL; ++h)
-                key[h] = (hm[h] >> q) & 1ull ? sp_key(acc[m][h], c0 + SPL * lane + h) : 0ull;
+            for (uint32_t h = 0; h < SPL; ++h) key[h] = hb[h] ? sp_key(acc[m][h], c0 + SPL * lane + h) : 0ull;
             if constexpr (MODE == 0) {
                 uint64_t best = key[0];
 #pragma unroll
@@ -500,13 +553,6 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                 }
                 if ((lane & (kLanes - 1)) == 0)
                     a.smp[(uint64_t)q * a.S + (uint64_t)jj * (kCh / kTaGrp) + lane / kLanes] = best;
-            } else if constexpr (MODE == 1) {
-#pragma unroll
-                for (uint32_t h = 0; h < SPL; ++h)
-                    if (key[h] != 0ull && key[h] >= tau[m]) {
-                        const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-                        if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = key[h];
-                    }
             } else {
 #pragma unroll
                 for (uint32_t h = 0; h < SPL; ++h) {
@@ -519,10 +565,21 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     };
     load_entries(st0, jb);
     load_entries(st1, jb + 1);
+    load_entries(st2, jb + 2);
     lookup(st0);
-    for (uint32_t jj = jb; jj < je; jj += 2) {
+    for (uint32_t jj = jb; jj < je; jj += 3) {
         chunk(st0, st1, jj);
-        if (jj + 1 < je) chunk(st1, st0, jj + 1);
+        if (jj + 1 < je) chunk(st1, st2, jj + 1);
+        if (jj + 2 < je) chunk(st2, st0, jj + 2);
+    }
+    if constexpr (MODE == 1) {  // the pooled candidates
+        __syncthreads();
+        const uint32_t n = min(s_npool, kTaPool);
+        for (uint32_t i = tid; i < n; i += kTaThreads) {
+            const uint32_t q = s_pq[i];
+            const uint32_t pos = atomicAdd(&a.counts[q], 1u);
+            if (pos < kSpCand) a.cand[(uint64_t)q * kSpCand + pos] = s_pkey[i];
+        }
     }
     if ((a.abl & 8) && tid == 0)
         for (int k = 0; k < 5; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
@@ -1276,7 +1333,6 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             ++q1;
         }
         const uint32_t Bg = (uint32_t)(q1 - q0);
-        const uint32_t nqt = (uint32_t)h_qt.size();
         const uint32_t nu = (uint32_t)group_terms.size();
         const uint32_t nchunks = (nblk + kTaSpl - 1) / kTaSpl;  // 128-document chunks
         // sample stride: expected candidates ~ limit * every, kept well under kSpCand
@@ -1289,22 +1345,32 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             if (mode == 1) hipLaunchKernelGGL((k_bm25_taat<1>), dim3(grid), dim3(kTaThreads), 0, s, ta);
             if (mode == 2) hipLaunchKernelGGL((k_bm25_taat<2>), dim3(grid), dim3(kTaThreads), 0, s, ta);
         };
-        std::vector<uint32_t> h_qrec(4 * (nqt + 1), 0u);  // (group term, q_tf, idf, 0); [nqt]: the empty row
-        for (uint32_t i = 0; i < nqt; ++i) {
-            h_qrec[4 * i] =
-                (uint32_t)(std::lower_bound(group_terms.begin(), group_terms.end(), h_qt[i]) - group_terms.begin());
-            std::memcpy(&h_qrec[4 * i + 1], &h_qv[i], 4);
-            std::memcpy(&h_qrec[4 * i + 2], &h_qidf[i], 4);
-        }
-        h_qrec[4 * nqt] = 0u;  // the kernel maps a finished query's rounds to the empty row
-        // per group term the queries holding it; queries whose q_tf or idf is not finite
+        // per query its term records (group term, q_tf, idf, map row bytes), padded with empty
+        // records (the empty row, never written; q_tf = idf = 0) to a multiple of 4 -- the
+        // kernel's batches -- plus one more; per group term the queries holding it; the
+        // queries whose q_tf or idf is not finite
+        std::vector<uint32_t> h_pqp(1, 0u), h_qrec;
         std::vector<uint64_t> h_qmask(nu + 1, 0ull);
         uint64_t qsel = 0;
-        for (uint32_t q = 0; q < Bg; ++q)
+        auto push_rec = [&](uint32_t g, float v, float idf) {
+            uint32_t r[4] = {g, 0u, 0u, g * kTaCh * kTaSpl * 2};
+            std::memcpy(&r[1], &v, 4);
+            std::memcpy(&r[2], &idf, 4);
+            h_qrec.insert(h_qrec.end(), r, r + 4);
+        };
+        for (uint32_t q = 0; q < Bg; ++q) {
             for (uint32_t i = h_qp[q]; i < h_qp[q + 1]; ++i) {
-                h_qmask[h_qrec[4 * i]] |= 1ull << q;
+                const uint32_t g =
+                    (uint32_t)(std::lower_bound(group_terms.begin(), group_terms.end(), h_qt[i]) - group_terms.begin());
+                push_rec(g, h_qv[i], h_qidf[i]);
+                h_qmask[g] |= 1ull << q;
                 if (!std::isfinite(h_qv[i]) || !std::isfinite(h_qidf[i])) qsel |= 1ull << q;
             }
+            while ((h_qrec.size() / 4) % 4) push_rec(kTaRows - 1, 0.0f, 0.0f);
+            h_pqp.push_back((uint32_t)(h_qrec.size() / 4));
+        }
+        const uint32_t nrec = (uint32_t)(h_qrec.size() / 4);
+        for (int k = 0; k < 4; ++k) push_rec(kTaRows - 1, 0.0f, 0.0f);  // [nrec, nrec + 4): a whole empty batch
         // wave slots w + 16 m: longest-processing-time assignment of the queries to the
         // 16 waves (each wave's rounds cost about the sum of its queries' term counts)
         std::vector<uint32_t> h_perm(kTaQ, 0xffffffffu);
@@ -1328,7 +1394,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         // scratch: qp | perm | qrec | ut | tau | counts | fail | out_n | smp | cand | out ids | out scores
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
         const size_t o_qp = 0, o_perm = o_qp + al((Bg + 1) * 4), o_qrec = o_perm + al(kTaQ * 4),
-                     o_ut = o_qrec + al((nqt + 1) * 16), o_qm = o_ut + al(nu * 4 + 4),
+                     o_ut = o_qrec + al((nrec + 4) * 16), o_qm = o_ut + al(nu * 4 + 4),
                      o_tau = o_qm + al(nu * 8 + 8), o_cnt = o_tau + al(Bg * 8),
                      o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_smp = o_n + al(Bg * 4),
                      o_cand = o_smp + al((size_t)Bg * S * 8), o_oi = o_cand + al((size_t)Bg * kSpCand * 8),
@@ -1341,8 +1407,8 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             sp->scratch_n = total;
         }
         char* base = (char*)sp->scratch;
-        SP_TRY(hipMemcpyAsync(base + o_qp, h_qp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
-        SP_TRY(hipMemcpyAsync(base + o_qrec, h_qrec.data(), (nqt + 1) * 16, hipMemcpyHostToDevice, s), "qrec");
+        SP_TRY(hipMemcpyAsync(base + o_qp, h_pqp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
+        SP_TRY(hipMemcpyAsync(base + o_qrec, h_qrec.data(), (nrec + 4) * 16, hipMemcpyHostToDevice, s), "qrec");
         SP_TRY(hipMemcpyAsync(base + o_perm, h_perm.data(), kTaQ * 4, hipMemcpyHostToDevice, s), "perm");
         for (auto& t : group_terms)  // dense ids (the vocabulary holds every live term; same order)
             t = (uint32_t)(std::lower_bound(sp->vocab.begin(), sp->vocab.end(), t) - sp->vocab.begin());
@@ -1373,7 +1439,7 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         a.qp = (const uint32_t*)(base + o_qp);
         a.qrec = (const uint4*)(base + o_qrec);
         a.perm = (const uint32_t*)(base + o_perm);
-        a.nqt = nqt;
+        a.nqt = nrec;
         a.runs = sp->runs ? 1u : 0u;
         a.B = Bg;
         a.every = every;
