@@ -122,7 +122,7 @@ __global__ void k_blk_gather(const uint32_t* __restrict__ order, const uint64_t*
         }
         if (lo >= V || vocab[lo] != t) *runs |= 2u;  // a term missing from the vocabulary
         cterm[i] = lo;
-        cslot[i] = (uint8_t)(s % kTaCh);
+        cslot[i] = (uint8_t)(s % (2 * kTaCh));  // slot within the search's 128-document chunk
         ctf[i] = tf[e];
         cdl[i] = dl[e];
         if (i > 0 && keys[i] == keys[i - 1] && eslot[order[i - 1]] == s) *runs |= 1u;  // same term, same document
@@ -136,7 +136,10 @@ __global__ void k_blk_tfc(const float* __restrict__ ctf, const float* __restrict
     const float k1p1 = k1 + 1.0f, omb = 1.0f - b;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E; i += (uint64_t)gridDim.x * blockDim.x) {
         const float t = ctf[i];
-        ctfc[i] = (t * k1p1) / (t + k1 * (omb + b * (cdl[i] / avgdl)));
+        const float c = (t * k1p1) / (t + k1 * (omb + b * (cdl[i] / avgdl)));
+        // +0.0 is kept as -0.0 (the search's map reads +0.0 as "no posting"): q_tf * c * idf is then
+        // +-0.0 or the same NaN either way, and acc + +-0.0 == acc (acc never holds -0.0)
+        ctfc[i] = __float_as_uint(c) == 0u ? -0.0f : c;
     }
 }
 
@@ -198,7 +201,7 @@ struct TaArgs {
 //      registers.  Query q's terms in order: a map read, two stage reads,
 //      acc = acc + q_tf * tfc * idf -- per document exactly the reference's
 //      fold (sparse.rs:167-190; acc starts at 0.0 = or_insert).  No posting
-//      reads stage[0] = +0.0 (a posting's own +0.0 tfc is staged as -0.0):
+//      reads stage[0] = +0.0 (the index keeps a posting's +0.0 tfc as -0.0):
 //      when q_tf and idf are finite its product is +-0.0 and acc + +-0.0 ==
 //      acc (acc never holds -0.0), so the fold needs no select; queries with a
 //      non-finite q_tf or idf (host flag) select per term.  A run of several
@@ -206,7 +209,7 @@ struct TaArgs {
 //      overflow is folded from HBM in order;
 //   3. selection by the mode.
 // Software pipeline: a chunk's entries are loaded three chunks ahead, their
-// group words one chunk ahead; emitted candidates pool in LDS.
+// group words two chunks ahead; emitted candidates pool in LDS.
 constexpr uint32_t kTaSpl = 2;              // slots per lane
 constexpr uint32_t kTaRows = 512;           // map rows: group terms + the empty row
 constexpr uint32_t kTaStaged = 4096;        // staged tf_components per chunk (index 0: +0.0)
@@ -241,8 +244,6 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     }
     if (tid < nu) s_qmask[tid] = a.qmask[tid];
     auto tfc_at = [&](uint32_t off) { return *(const float*)((const char*)s_tfc + off); };
-    // a posting's staged tfc: +0.0 is "no posting", so a posting's +0.0 is kept as -0.0
-    auto map_tfc = [](float f) { return __float_as_uint(f) == 0u ? -0.0f : f; };
     // group term index of a gmap word, kEmpty for a term outside the group
     auto group_of = [&](uint32_t gv) { return (gv >> kGmapShift) == a.epoch ? gv & ((1u << kGmapShift) - 1) : kEmpty; };
     // this wave's queries (uniform): wave slot w + 16 m holds query perm[w + 16 m]
@@ -328,17 +329,17 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             sg.f[k] = a.ctfc[i];
         }
     };
-    // the group table words of a stage's terms (its entries were issued two chunks earlier)
+    // the group table words of a stage's terms, two chunks before its build
     auto lookup = [&](Stage& sg) {
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) sg.g[k] = a.gmap[sg.t[k]];
     };
     bool prev_overflow = false;
-    auto chunk = [&](Stage& sg, Stage& nx, uint32_t jj) {
+    auto chunk = [&](Stage& sg, Stage& nx2, uint32_t jj) {
         const uint32_t c0 = jj * every * kCh;
         const uint32_t* cr = &s_cptr[(SPL + 1) * (jj - jb)];
-        const uint64_t ce0 = cbase + cr[0], ce1 = cbase + cr[SPL], cmid = cbase + cr[1];  // cmid: second sub-chunk
-        auto slot_in_chunk = [&](uint64_t i, uint32_t s) { return i >= cmid ? s + kTaCh : s; };
+        const uint64_t ce0 = cbase + cr[0], ce1 = cbase + cr[SPL];
+        const uint32_t cn = cr[SPL] - cr[0];  // the chunk's entries
         __syncthreads();  // (1) the previous chunk's rounds are done
         mark(-1);
         if (prev_overflow) {  // cells written past the register stage are not tracked: clear the rows
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             for (uint32_t k = 0; k < kPer; ++k) {
                 const uint64_t i = ce0 + tid + k * kTaThreads;
                 gk[k] = group_of(sg.g[k]);
-                take[k] = i < ce1 && gk[k] != kEmpty;
+                take[k] = tid + k * kTaThreads < cn && gk[k] != kEmpty;
                 if (take[k] && a.runs) {  // a re-added document: only the first entry of its run enters the map
                     if (i + 1 < ce1 && a.cterm[i + 1] == sg.t[k] && a.cslot[i + 1] == sg.s[k]) slow = true;
                     if (i > ce0 && a.cterm[i - 1] == sg.t[k] && a.cslot[i - 1] == sg.s[k]) take[k] = false;
@@ -381,14 +382,13 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             for (uint32_t k = 0; k < kPer; ++k) {
                 cell[k] = 0xffffffffu;
                 if (!take[k]) continue;
-                const uint64_t i = ce0 + tid + k * kTaThreads;
                 const uint32_t g = gk[k];
                 const uint32_t pos = base + pre[k] +
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
-                const uint32_t sl = slot_in_chunk(i, sg.s[k]);
+                const uint32_t sl = sg.s[k];
                 cell[k] = g * kCh + sl;
                 if (pos < kTaStaged) {
-                    s_tfc[pos] = map_tfc(sg.f[k]);
+                    s_tfc[pos] = sg.f[k];
                     s_tmap[cell[k]] = (uint16_t)(pos * 4);
                 } else {
                     s_tmap[cell[k]] = kTaUnstaged;
@@ -404,10 +404,10 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     slow = true;
                     continue;
                 }
-                const uint32_t sl = slot_in_chunk(i, s);
+                const uint32_t sl = s;
                 const uint32_t pos = atomicAdd(&s_nst, 1u);
                 if (pos < kTaStaged) {
-                    s_tfc[pos] = map_tfc(a.ctfc[i]);
+                    s_tfc[pos] = a.ctfc[i];
                     s_tmap[g * kCh + sl] = (uint16_t)(pos * 4);
                 } else {
                     s_tmap[g * kCh + sl] = kTaUnstaged;
@@ -420,8 +420,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         }
         __syncthreads();  // (3) the chunk's map is built
         mark(1);
-        prev_overflow = ce1 - ce0 > kTaStage;
-        lookup(nx);                // the next chunk's group words
+        prev_overflow = cn > kTaStage;
         load_entries(sg, jj + 3);  // in flight during the next two chunks
         mark(4);
         // 2. rounds, per query m in its term order; lane holds slots SPL*lane + h
@@ -488,7 +487,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                             continue;
                         }
                         // the sub-chunk's entries are sorted by (term, slot): lower_bound((term, slot))
-                        const uint32_t term = a.ut[rec.x], sub = sl / kTaCh, ss = sl % kTaCh;
+                        const uint32_t term = a.ut[rec.x], sub = sl / kTaCh, ss = sl;
                         const uint64_t r0 = cbase + cr[sub], r1 = cbase + cr[sub + 1];
                         uint64_t lo = r0, hi = r1;
                         while (lo < hi) {
@@ -562,15 +561,17 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             }
         }
         mark(3);
+        lookup(nx2);  // the group words of chunk jj + 2 (its entries were issued a chunk ago)
     };
     load_entries(st0, jb);
     load_entries(st1, jb + 1);
     load_entries(st2, jb + 2);
     lookup(st0);
+    lookup(st1);
     for (uint32_t jj = jb; jj < je; jj += 3) {
-        chunk(st0, st1, jj);
-        if (jj + 1 < je) chunk(st1, st2, jj + 1);
-        if (jj + 2 < je) chunk(st2, st0, jj + 2);
+        chunk(st0, st2, jj);
+        if (jj + 1 < je) chunk(st1, st0, jj + 1);
+        if (jj + 2 < je) chunk(st2, st1, jj + 2);
     }
     if constexpr (MODE == 1) {  // the pooled candidates
         __syncthreads();
