@@ -224,6 +224,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     __shared__ __attribute__((aligned(16))) float s_tfc[kTaStaged];
     __shared__ uint64_t s_qmask[kRows];  // group term index -> the group's queries holding it
     __shared__ uint64_t s_hit[kCh];      // per slot of the chunk: the queries it matches
+    __shared__ __attribute__((aligned(4))) uint8_t s_present[kRows];  // group terms with a posting in the chunk
     __shared__ uint32_t s_cptr[(SPL + 1) * (kTaCptrLds + 1)];  // the block's chunk (sub-)ranges, from cbase
     __shared__ uint32_t s_slow, s_nst, s_npool;
     __shared__ uint64_t s_pkey[kTaPool];  // emit: the block's candidates (key, query), flushed at the end
@@ -266,11 +267,12 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     for (uint32_t m = 0; m < kTaQW; ++m) tau[m] = MODE == 1 && qid[m] != 0xffffffffu ? a.tau[qid[m]] : 0ull;
     // the wave's query terms, lane-resident: lane 16 m + r holds query m's r-th (padded) term
     // record: map row bytes, q_tf, idf (the empty record past the query's end)
-    uint32_t lr_row, lr_v, lr_idf;
+    uint32_t lr_row, lr_v, lr_idf, lr_g;
     {
         const uint32_t m = lane >> 4, r = lane & 15u;
         const uint4 rec = qrec_at(r < ql[m & 3] ? qp0[m & 3] + r : a.nqt);
         lr_row = rec.w;
+        lr_g = rec.x;
         lr_v = rec.y;
         lr_idf = rec.z;
     }
@@ -350,6 +352,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                 if (cell[k] != 0xffffffffu) s_tmap[cell[k]] = 0;
         }
         if (tid < kCh) s_hit[tid] = 0ull;
+        if (tid < kRows / 4) ((uint32_t*)s_present)[tid] = 0u;
         if (tid == 0) {
             s_slow = 0;
             s_nst = 1;
@@ -395,6 +398,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     slow = true;
                 }
                 atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
+                s_present[g] = 1;
             }
             for (uint64_t i = ce0 + kTaStage + tid; i < ce1; i += kTaThreads) {  // past the register stage
                 const uint32_t g = group_of(a.gmap[a.cterm[i]]);
@@ -414,6 +418,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     slow = true;
                 }
                 atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
+                s_present[g] = 1;
                 slow = slow || (i + 1 < ce1 && a.cterm[i + 1] == a.cterm[i] && a.cslot[i + 1] == s);
             }
             if (slow) s_slow = 1u;
@@ -429,40 +434,52 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         for (uint32_t m = 0; m < kTaQW; ++m)
 #pragma unroll
             for (uint32_t h = 0; h < SPL; ++h) acc[m][h] = 0.0f;
-        // 4 terms at a time: the map reads issued together, then the stage reads, then the
-        // folds in order.  calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`
+        // Only the query terms with a posting in the chunk (a term without one adds +-0.0, or is
+        // skipped by the select: either way acc is unchanged), in term order, N <= 4 at a time:
+        // the map reads issued together, then the stage reads, then the folds in order.
+        // calculate_bm25_score: query_tf * tf_component * idf; `or_insert(0.0) += s`
         auto fast_rounds = [&](auto sel_c) {
             constexpr bool kSel = decltype(sel_c)::value;
+            const uint64_t pm = __ballot(s_present[lr_g] != 0);  // lane 16 m + r: query m's term r
+            auto batch = [&](auto n_c, uint32_t m, uint32_t& bits) {
+                constexpr uint32_t N = decltype(n_c)::value;
+                uint32_t ln[N], off[N];
 #pragma unroll
-            for (uint32_t m = 0; m < kTaQW; ++m) {
-                for (uint32_t rb = 0; rb < ql[m]; rb += 4) {
-                    uint32_t off[4];
+                for (uint32_t k = 0; k < N; ++k) {
+                    const uint32_t b = (uint32_t)__builtin_ctz(bits);
+                    bits &= bits - 1;
+                    ln[k] = __builtin_amdgcn_readfirstlane(m * 16 + b);
+                    const uint32_t rowb = __builtin_amdgcn_readlane(lr_row, ln[k]);
+                    off[k] = *(const uint32_t*)((const char*)s_tmap + rowb + 4 * lane);
+                }
+                float tf[N][SPL];
 #pragma unroll
-                    for (uint32_t k = 0; k < 4; ++k) {
-                        const uint32_t rowb = __builtin_amdgcn_readlane(lr_row, m * 16 + ((rb + k) & 15u));
-                        off[k] = *(const uint32_t*)((const char*)s_tmap + rowb + 4 * lane);
-                    }
-                    float tf[4][SPL];
+                for (uint32_t k = 0; k < N; ++k) {
+                    tf[k][0] = tfc_at(off[k] & 0xffffu);
+                    tf[k][1] = tfc_at(off[k] >> 16);
+                }
 #pragma unroll
-                    for (uint32_t k = 0; k < 4; ++k) {
-                        tf[k][0] = tfc_at(off[k] & 0xffffu);
-                        tf[k][1] = tfc_at(off[k] >> 16);
-                    }
+                for (uint32_t k = 0; k < N; ++k) {
+                    const float v = __uint_as_float(__builtin_amdgcn_readlane(lr_v, ln[k]));
+                    const float idf = __uint_as_float(__builtin_amdgcn_readlane(lr_idf, ln[k]));
 #pragma unroll
-                    for (uint32_t k = 0; k < 4; ++k) {
-                        const uint32_t ln = m * 16 + ((rb + k) & 15u);
-                        const float v = __uint_as_float(__builtin_amdgcn_readlane(lr_v, ln));
-                        const float idf = __uint_as_float(__builtin_amdgcn_readlane(lr_idf, ln));
-#pragma unroll
-                        for (uint32_t h = 0; h < SPL; ++h) {
-                            const float sc = v * tf[k][h] * idf;
-                            if constexpr (kSel)
-                                acc[m][h] = acc[m][h] + (((off[k] >> (16 * h)) & 0xffffu) != 0u ? sc : 0.0f);
-                            else
-                                acc[m][h] = acc[m][h] + sc;  // no posting: +-0.0
-                        }
+                    for (uint32_t h = 0; h < SPL; ++h) {
+                        const float sc = v * tf[k][h] * idf;
+                        if constexpr (kSel)
+                            acc[m][h] = acc[m][h] + (((off[k] >> (16 * h)) & 0xffffu) != 0u ? sc : 0.0f);
+                        else
+                            acc[m][h] = acc[m][h] + sc;  // no posting in this slot: +-0.0
                     }
                 }
+            };
+#pragma unroll
+            for (uint32_t m = 0; m < kTaQW; ++m) {
+                uint32_t bits = __builtin_amdgcn_readfirstlane((uint32_t)(pm >> (16 * m)) & 0xffffu);
+                while (__builtin_popcount(bits) >= 4) batch(std::integral_constant<uint32_t, 4>{}, m, bits);
+                const uint32_t rest = __builtin_popcount(bits);
+                if (rest == 3) batch(std::integral_constant<uint32_t, 3>{}, m, bits);
+                else if (rest == 2) batch(std::integral_constant<uint32_t, 2>{}, m, bits);
+                else if (rest == 1) batch(std::integral_constant<uint32_t, 1>{}, m, bits);
             }
         };
         if (a.abl & 1) {
