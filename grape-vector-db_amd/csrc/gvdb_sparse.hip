@@ -146,8 +146,11 @@ __global__ void k_blk_tfc(const float* __restrict__ ctf, const float* __restrict
 // A search group's direct-mapped term table: gmap[dense term] = (epoch << 9) | group
 // term index; entries of earlier epochs read as "not in the group".
 constexpr uint32_t kGmapShift = 9;
-__global__ void k_gmap_set(uint32_t* __restrict__ gmap, const uint32_t* __restrict__ ut, uint32_t nu, uint32_t epoch) {
+// (and zeroes the group's candidate counters)
+__global__ void k_gmap_set(uint32_t* __restrict__ gmap, const uint32_t* __restrict__ ut, uint32_t nu, uint32_t epoch,
+                           uint32_t* __restrict__ counts, uint32_t B) {
     for (uint32_t i = threadIdx.x; i < nu; i += blockDim.x) gmap[ut[i]] = (epoch << kGmapShift) | i;
+    for (uint32_t i = threadIdx.x; i < B; i += blockDim.x) counts[i] = 0u;
 }
 
 struct TaArgs {
@@ -852,7 +855,8 @@ struct gvdb_sparse {
     // search scratch
     void* scratch = nullptr;
     size_t scratch_n = 0;
-    uint32_t* h_fail = nullptr;
+    char* h_io = nullptr;  // pinned staging of a launch group's inputs and outputs
+    size_t h_io_n = 0;
     uint64_t dense_fallbacks = 0;
 
     // avgdl's fold order: storage order = slot order, each slot's entries by
@@ -1051,7 +1055,6 @@ gvdb_status gvdb_sparse_create(const gvdb_bm25_params* p, gvdb_sparse** out) {
     }
     hipError_t e = hipSetDevice(sp->device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&sp->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&sp->h_fail, kTaQ * 4, hipHostMallocDefault);
     if (e != hipSuccess) {
         delete sp;
         return sp_dev(e, "gvdb_sparse_create");
@@ -1067,7 +1070,7 @@ void gvdb_sparse_destroy(gvdb_sparse* sp) {
                     (void*)sp->d_cptr, (void*)sp->d_cterm, (void*)sp->d_cslot, (void*)sp->d_ctf, (void*)sp->d_cdl,
                     (void*)sp->d_ctfc, (void*)sp->d_vocab, (void*)sp->d_gmap, sp->scratch})
         if (p) (void)hipFree(p);
-    if (sp->h_fail) (void)hipHostFree(sp->h_fail);
+    if (sp->h_io) (void)hipHostFree(sp->h_io);
     if (sp->stream) (void)hipStreamDestroy(sp->stream);
     delete sp;
 }
@@ -1409,14 +1412,16 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
                 ++cnt[best];
             }
         }
-        // scratch: qp | perm | qrec | ut | tau | counts | fail | out_n | smp | cand | out ids | out scores
+        // scratch: [qp | perm | qrec | ut | qmask] (one upload) | tau | counts | smp | cand |
+        // [fail | out_n | out ids | out scores] (one download)
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
         const size_t o_qp = 0, o_perm = o_qp + al((Bg + 1) * 4), o_qrec = o_perm + al(kTaQ * 4),
                      o_ut = o_qrec + al((nrec + 4) * 16), o_qm = o_ut + al(nu * 4 + 4),
-                     o_tau = o_qm + al(nu * 8 + 8), o_cnt = o_tau + al(Bg * 8),
-                     o_fail = o_cnt + al(Bg * 4), o_n = o_fail + al(Bg * 4), o_smp = o_n + al(Bg * 4),
-                     o_cand = o_smp + al((size_t)Bg * S * 8), o_oi = o_cand + al((size_t)Bg * kSpCand * 8),
-                     o_os = o_oi + al((size_t)Bg * L * 8), total = o_os + al((size_t)Bg * L * 4);
+                     o_tau = o_qm + al(nu * 8 + 8), o_cnt = o_tau + al(Bg * 8), o_smp = o_cnt + al(Bg * 4),
+                     o_cand = o_smp + al((size_t)Bg * S * 8), o_fail = o_cand + al((size_t)Bg * kSpCand * 8),
+                     o_n = o_fail + al(Bg * 4), o_oi = o_n + al(Bg * 4), o_os = o_oi + al((size_t)Bg * L * 8),
+                     total = o_os + al((size_t)Bg * L * 4);
+        const size_t in_bytes = o_tau, out_bytes = total - o_fail;
         if (total > sp->scratch_n) {
             if (sp->scratch) (void)hipFree(sp->scratch);
             sp->scratch = nullptr;
@@ -1424,22 +1429,32 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             SP_TRY(hipMalloc(&sp->scratch, total), "alloc bm25 scratch");
             sp->scratch_n = total;
         }
+        const size_t io_need = std::max(in_bytes, out_bytes);
+        if (io_need > sp->h_io_n) {
+            if (sp->h_io) (void)hipHostFree(sp->h_io);
+            sp->h_io = nullptr;
+            sp->h_io_n = 0;
+            SP_TRY(hipHostMalloc((void**)&sp->h_io, io_need, hipHostMallocDefault), "alloc bm25 staging");
+            sp->h_io_n = io_need;
+        }
         char* base = (char*)sp->scratch;
-        SP_TRY(hipMemcpyAsync(base + o_qp, h_pqp.data(), (Bg + 1) * 4, hipMemcpyHostToDevice, s), "qp");
-        SP_TRY(hipMemcpyAsync(base + o_qrec, h_qrec.data(), (nrec + 4) * 16, hipMemcpyHostToDevice, s), "qrec");
-        SP_TRY(hipMemcpyAsync(base + o_perm, h_perm.data(), kTaQ * 4, hipMemcpyHostToDevice, s), "perm");
+        char* hio = sp->h_io;
+        SP_TRY(hipStreamSynchronize(s), "sync");  // the staging buffer's previous download was consumed
         for (auto& t : group_terms)  // dense ids (the vocabulary holds every live term; same order)
             t = (uint32_t)(std::lower_bound(sp->vocab.begin(), sp->vocab.end(), t) - sp->vocab.begin());
-        if (nu) SP_TRY(hipMemcpyAsync(base + o_ut, group_terms.data(), nu * 4, hipMemcpyHostToDevice, s), "ut");
-        if (nu) SP_TRY(hipMemcpyAsync(base + o_qm, h_qmask.data(), nu * 8, hipMemcpyHostToDevice, s), "qmask");
+        std::memcpy(hio + o_qp, h_pqp.data(), (Bg + 1) * 4);
+        std::memcpy(hio + o_perm, h_perm.data(), kTaQ * 4);
+        std::memcpy(hio + o_qrec, h_qrec.data(), (nrec + 4) * 16);
+        if (nu) std::memcpy(hio + o_ut, group_terms.data(), nu * 4);
+        if (nu) std::memcpy(hio + o_qm, h_qmask.data(), nu * 8);
+        SP_TRY(hipMemcpyAsync(base, hio, in_bytes, hipMemcpyHostToDevice, s), "bm25 inputs");
         if (++sp->epoch >> (32 - kGmapShift)) {  // epoch tag wrapped: clear the table
             SP_TRY(hipMemsetAsync(sp->d_gmap, 0, (sp->vocab.size() + 1) * 4, s), "group table");
             sp->epoch = 1;
         }
         hipLaunchKernelGGL(k_gmap_set, dim3(1), dim3(512), 0, s, sp->d_gmap, (const uint32_t*)(base + o_ut), nu,
-                           sp->epoch);
+                           sp->epoch, (uint32_t*)(base + o_cnt), Bg);
         SP_TRY(hipGetLastError(), "bm25 group table");
-        SP_TRY(hipMemsetAsync(base + o_cnt, 0, Bg * 4, s), "counts");
         TaArgs a{};
         a.cptr = sp->d_cptr;
         a.cterm = sp->d_cterm;
@@ -1507,11 +1522,14 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
         hipLaunchKernelGGL(k_bm25_final, dim3(Bg), dim3(256), 0, s, a.cand, a.counts, L, sp->d_ids, d_oi, d_os, d_n,
                            d_fail);
         SP_TRY(hipGetLastError(), "bm25 final");
-        SP_TRY(hipMemcpyAsync(sp->h_fail, d_fail, Bg * 4, hipMemcpyDeviceToHost, s), "fail flags");
+        SP_TRY(hipMemcpyAsync(hio, base + o_fail, out_bytes, hipMemcpyDeviceToHost, s), "bm25 outputs");
         SP_TRY(hipStreamSynchronize(s), "sync");
+        const uint32_t* h_failv = (const uint32_t*)hio;
+        bool any_fail = false;
         // exact fallback for overflowing queries: dense keys + radix sort
         for (uint32_t q = 0; q < Bg; ++q) {
-            if (!sp->h_fail[q]) continue;
+            if (!h_failv[q]) continue;
+            any_fail = true;
             ++sp->dense_fallbacks;
             size_t cub_bytes = 0;
             hipcub::DoubleBuffer<uint64_t> kb(nullptr, nullptr);
@@ -1536,10 +1554,13 @@ gvdb_status gvdb_sparse_search_bm25(gvdb_sparse* sp, const uint64_t* q_ptr, cons
             (void)hipFree(tmp);
             if (e != hipSuccess) return sp_dev(e, "bm25 dense fallback");
         }
-        SP_TRY(hipMemcpyAsync(out_ids + q0 * L, d_oi, (size_t)Bg * L * 8, hipMemcpyDeviceToHost, s), "out ids");
-        SP_TRY(hipMemcpyAsync(out_scores + q0 * L, d_os, (size_t)Bg * L * 4, hipMemcpyDeviceToHost, s), "out scores");
-        SP_TRY(hipMemcpyAsync(out_n + q0, d_n, (size_t)Bg * 4, hipMemcpyDeviceToHost, s), "out n");
-        SP_TRY(hipStreamSynchronize(s), "sync");
+        if (any_fail) {  // the fallback rewrote some outputs
+            SP_TRY(hipMemcpyAsync(hio, base + o_fail, out_bytes, hipMemcpyDeviceToHost, s), "bm25 outputs");
+            SP_TRY(hipStreamSynchronize(s), "sync");
+        }
+        std::memcpy(out_ids + q0 * L, hio + (o_oi - o_fail), (size_t)Bg * L * 8);
+        std::memcpy(out_scores + q0 * L, hio + (o_os - o_fail), (size_t)Bg * L * 4);
+        std::memcpy(out_n + q0, hio + (o_n - o_fail), (size_t)Bg * 4);
         q0 = q1;
     }
     return GVDB_OK;
