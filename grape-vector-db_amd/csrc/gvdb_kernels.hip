@@ -2774,10 +2774,194 @@ __global__ void k_emit_flat(const uint32_t* __restrict__ ranks, const float* __r
     if (threadIdx.x == 0 && out_n) *out_n = o < limit ? o : limit;
 }
 
+// The same selection for limit <= kFlatTopkCap and N <= kFlatTopkMaxN, every
+// query of the batch in ONE launch (one block per query) instead of a radix
+// sort per query: the kept entries' (order key, row) pairs are totally ordered
+// exactly as the stable key sort orders them, so the first `limit` kept
+// entries are the `limit` smallest pairs.  The keys are staged in LDS (N <=
+// kFlatTopkStage; else re-read from L2), a 4-digit radix select finds the
+// limit-th smallest key K, then the entries below K and the lowest-row entries
+// equal to K (ordered compaction, chunk by chunk) are collected and sorted in
+// LDS.  NaN flags as k_make_keys.
+constexpr uint32_t kFlatTopkCap = 1024;
+constexpr uint32_t kFlatTopkBuf = 2048;  // collected entries (>= kFlatTopkCap)
+constexpr uint32_t kFlatTopkStage = 16384;
+constexpr uint32_t kFlatTopkMaxN = 262144;
+constexpr uint32_t kFlatTopkThreads = 1024;
+template <bool STAGED>
+__global__ __launch_bounds__(kFlatTopkThreads) void k_flat_topk(const float* __restrict__ scores, uint32_t N, uint32_t limit,
+                                                   int descending, int has_threshold, float threshold,
+                                                   const uint64_t* __restrict__ ids, uint64_t* __restrict__ out_idx,
+                                                   float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
+                                                   uint32_t* __restrict__ nan_flag) {
+    constexpr uint32_t kKeys = STAGED ? kFlatTopkStage : 1u;
+    __shared__ uint32_t s_key[kKeys];
+    __shared__ uint32_t s_kept[STAGED ? kFlatTopkStage / 32 : 1u];
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t cand[kFlatTopkBuf];
+    __shared__ uint32_t s_total, s_nan, s_prefix, s_need, s_nc, s_wc[kFlatTopkThreads / 64];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const float* sc = scores + (uint64_t)q * N;
+    auto load = [&](uint32_t i, uint32_t& key, bool& nan) {  // kept (threshold, mapped row) and its order key
+        const float f = sc[i];
+        const uint64_t id = ids ? ids[i] : (uint64_t)i;
+        const uint32_t o = f32_order(f);
+        key = descending ? ~o : o;
+        nan = f != f;
+        return (!has_threshold || !(f < threshold)) && id != kOrphan;
+    };
+    auto get = [&](uint32_t i, uint32_t& key) {
+        if constexpr (STAGED) {
+            key = s_key[i];
+            return ((s_kept[i >> 5] >> (i & 31u)) & 1u) != 0u;
+        } else {
+            bool nan;
+            return load(i, key, nan);
+        }
+    };
+    if (tid == 0) {
+        s_total = 0;
+        s_nan = 0;
+        s_prefix = 0;
+        s_nc = 0;
+    }
+    __syncthreads();
+    uint32_t kept = 0;
+    bool nan = false;
+    constexpr uint32_t kU = 8;  // loads in flight per thread
+    for (uint32_t i0 = tid; i0 < N; i0 += kFlatTopkThreads * kU) {
+        uint32_t key[kU];
+        bool kp[kU], nn[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t i = i0 + kFlatTopkThreads * u;
+            kp[u] = i < N && load(min(i, N - 1), key[u], nn[u]);
+            nn[u] = i < N && nn[u];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t i = i0 + kFlatTopkThreads * u;
+            kept += kp[u] ? 1u : 0u;
+            nan |= nn[u];
+            if constexpr (STAGED) {  // the wave's 64 consecutive rows: two bitmap words
+                if (i < N) s_key[i] = key[u];
+                const uint64_t b = __ballot(kp[u]);
+                const uint32_t w0 = (i - lane) >> 5;
+                if (lane == 0 && w0 < kFlatTopkStage / 32) s_kept[w0] = (uint32_t)b;
+                if (lane == 32 && w0 + 1 < kFlatTopkStage / 32) s_kept[w0 + 1] = (uint32_t)(b >> 32);
+            }
+        }
+    }
+    atomicAdd(&s_total, kept);
+    if (nan) s_nan = 1u;
+    __syncthreads();
+    const uint32_t want = min(s_total, limit);
+    if (tid == 0) {
+        if (s_nan && N >= 2) {
+            atomicOr(nan_flag, 1u);
+            atomicOr(nan_flag + 1, 1u);
+        }
+        if (out_n) out_n[q] = want;
+        s_need = want;
+    }
+    if (want == 0) return;
+    // radix select of the want-th smallest key among the kept entries
+    uint32_t mask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        const uint32_t prefix = s_prefix;
+        for (uint32_t i = tid; i < N; i += kFlatTopkThreads) {
+            uint32_t key;
+            if (get(i, key) && (key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        // the digit whose cumulative count reaches s_need: a scan of the 256 bins (waves 0-3)
+        const uint32_t v = tid < 256 ? hist[tid] : 0u, need = s_need;
+        uint32_t incl = v;
+#pragma unroll
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(incl, off);
+            if (lane >= off) incl += t;
+        }
+        if (lane == 63 && wv < 4) s_wc[wv] = incl;
+        __syncthreads();
+        for (uint32_t w = 0; w < wv && w < 4; ++w) incl += s_wc[w];
+        const uint32_t excl = incl - v;
+        if (tid < 256 && excl < need && need <= incl) {
+            s_need = need - excl;
+            s_prefix = prefix | (tid << shift);
+        }
+        mask |= 255u << shift;
+        __syncthreads();
+    }
+    const uint32_t K = s_prefix;
+    // collect every kept entry below K and those equal to K (their sort by row
+    // keeps the lowest rows first); past the buffer (massive ties) the equal
+    // ones are taken again in row order, chunk by chunk
+    for (uint32_t i = tid; i < N; i += kFlatTopkThreads) {
+        uint32_t key;
+        if (get(i, key) && key <= K) {
+            const uint32_t c = atomicAdd(&s_nc, 1u);
+            if (c < kFlatTopkBuf) cand[c] = ((uint64_t)key << 32) | i;
+        }
+    }
+    __syncthreads();
+    uint32_t nc = s_nc;
+    if (nc > kFlatTopkBuf) {
+        __syncthreads();
+        if (tid == 0) s_nc = 0;
+        __syncthreads();
+        uint32_t eq_left = s_need;
+        for (uint32_t base = 0; base < N; base += kFlatTopkThreads) {
+            const uint32_t i = base + tid;
+            uint32_t key = 0;
+            const bool k = i < N && get(i, key);
+            if (k && key < K) cand[atomicAdd(&s_nc, 1u)] = ((uint64_t)key << 32) | i;
+            if (eq_left == 0) continue;  // (block-uniform)
+            const bool eq = k && key == K;
+            const uint64_t m = __ballot(eq);
+            if (lane == 0) s_wc[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t before = 0, tot = 0;
+            for (uint32_t w = 0; w < kFlatTopkThreads / 64; ++w) {
+                before += w < wv ? s_wc[w] : 0u;
+                tot += s_wc[w];
+            }
+            const uint32_t r = before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (eq && r < eq_left) cand[atomicAdd(&s_nc, 1u)] = ((uint64_t)key << 32) | i;
+            eq_left = tot < eq_left ? eq_left - tot : 0u;
+            __syncthreads();
+        }
+        __syncthreads();
+        nc = s_nc;  // == want
+    }
+    const uint32_t P = next_pow2(nc);
+    for (uint32_t j = nc + tid; j < P; j += kFlatTopkThreads) cand[j] = ~0ull;
+    __syncthreads();
+    bitonic_sort_lds(cand, P);
+    for (uint32_t j = tid; j < want; j += kFlatTopkThreads) {
+        const uint32_t i = (uint32_t)cand[j];
+        out_idx[(uint64_t)q * limit + j] = ids ? ids[i] : (uint64_t)i;
+        out_scores[(uint64_t)q * limit + j] = sc[i];
+    }
+}
+
 hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint32_t limit, int descending,
                               int has_threshold, float threshold, const uint64_t* ids, uint64_t* out_idx,
                               float* out_scores, uint32_t* out_n, void* tmp, size_t tmp_bytes, uint32_t* nan_flag,
                               hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (limit <= kFlatTopkCap && N <= kFlatTopkMaxN && !getenv("GVDB_FLAT_SORT")) {
+        if (N <= kFlatTopkStage)
+            hipLaunchKernelGGL(k_flat_topk<true>, dim3(B), dim3(kFlatTopkThreads), 0, s, scores, N, limit, descending,
+                               has_threshold, threshold, ids, out_idx, out_scores, out_n, nan_flag);
+        else
+            hipLaunchKernelGGL(k_flat_topk<false>, dim3(B), dim3(kFlatTopkThreads), 0, s, scores, N, limit, descending,
+                               has_threshold, threshold, ids, out_idx, out_scores, out_n, nan_flag);
+        GVDB_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     char* p = (char*)tmp;
     const size_t al = align256((size_t)N * 4);
     uint32_t* k0 = (uint32_t*)p;

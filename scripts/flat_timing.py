@@ -53,8 +53,8 @@ for B in [int(b) for b in os.environ.get("BS", "256,64,1").split(",")]:
         L.gvdb_timing_read(6, C.byref(tm), C.byref(tn))
     e_ms = em.value / max(en.value, 1)
     kpad = (D + 127) // 128 * 128 if i8 else (D + 63) // 64 * 64
-    tf = 2.0 * N * kpad * 256 / (e_ms * 1e-3) / 1e12
-    gbs = N * kpad * (1 if i8 else 2) / (e_ms * 1e-3) / 1e9
+    tf = 2.0 * N * kpad * 256 / (e_ms * 1e-3) / 1e12 if e_ms > 0 else 0.0  # 0: the small-N path ran
+    gbs = N * kpad * (1 if i8 else 2) / (e_ms * 1e-3) / 1e9 if e_ms > 0 else 0.0
     print(f"        k_flat_mx emit {e_ms:.3f} ms ({tf:.0f} TOP/s incl. padding slots, {gbs:.0f} GB/s rows), "
           f"group total {tm.value / max(tn.value, 1):.3f} ms", flush=True)
     print(f"B={B:4d}  {ms:8.3f} ms/batch  {B / ms * 1e3:10.0f} QPS  fallbacks {L.gvdb_flat_fallback_count() - f0}"

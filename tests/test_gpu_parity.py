@@ -392,6 +392,36 @@ def test_flat_mfma_after_mutations(g, oracle_mod):
         assert list(ids[b, : n[b]]) == list(live[ri]) and same_f32(sc[b, : n[b]], rs)
 
 
+@pytest.mark.parametrize("N,k", [(4000, 1), (4000, 10), (4000, 1000), (4000, 1024), (4000, 1500), (4000, 5000),
+                                 (40000, 10), (40000, 1024)])
+def test_flat_small_n_topk_matches_oracle_and_sort_path(g, oracle_mod, monkeypatch, N, k):
+    """Small-N exact flat (the batched one-block-per-query top-k, limit <= 1024,
+    keys staged in LDS up to 16K rows; larger limits take the per-query radix
+    sort): heavy ties (3 distinct rows, zero-norm rows), both metrics, equal to
+    the oracle and to the sort path."""
+    D = 48
+    base = rng_rows(21, 3, D)
+    x = base[np.arange(N) % 3].copy()
+    x[5] = 0.0
+    x[123] = 0.0
+    Q = rng_rows(22, 6, D)
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    for metric, ref in ((0, oracle_mod.storage_vector_search), (2, oracle_mod.flat_cosine_distance_search)):
+        ids, sc, n = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=metric))
+        for b in range(len(Q)):
+            ri, rs = ref(Q[b], x, k)
+            assert list(ids[b, :n[b]]) == list(ri) and same_f32(sc[b, :n[b]], rs), (metric, b)
+        monkeypatch.setenv("GVDB_FLAT_SORT", "1")
+        ids2, sc2, n2 = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=metric))
+        monkeypatch.delenv("GVDB_FLAT_SORT")
+        assert (n2 == n).all() and (ids2 == ids).all() and sc2.tobytes() == sc.tobytes()
+    idx, sc, n = g.flat_search(Q, x, k, threshold=0.1)
+    for b in range(len(Q)):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], x, k, threshold=0.1)
+        assert list(idx[b, :n[b]]) == list(ri) and same_f32(sc[b, :n[b]], rs)
+
+
 def test_flat_search_threshold(g, oracle_mod):
     N, D = 2000, 32
     x = rng_rows(11, N, D)
