@@ -328,7 +328,8 @@ def main():
                                             f"VGPRs, {32 * MX4_QT[w4]} queries per launch, {scan_launches} launches "
                                             f"per batch; achieved over the batch's launches)")
         else:
-            peak, kname = PEAK_FP4_TFLOPS, "k_scan_mx3 (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4, rows in VGPRs)"
+            peak, kname = PEAK_FP4_TFLOPS, ("k_scan_mx5 ({0,1} x {+-1} e2m1 dot seeded with thr - |q|, "
+                                            "v_mfma_scale_f32_32x32x64_f8f6f4, rows in VGPRs)")
         roof = {
             "kernel": "stage-1 BQ Hamming filter: " + kname,
             "bound": "mfma",
@@ -348,7 +349,7 @@ def main():
         }
     roof.update({
         "frac": roof["achieved"] / peak,
-        "traffic": pmc_traffic("gvdb::k_scan_mx3<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
+        "traffic": pmc_traffic("gvdb::k_scan_mx5<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
         "hbm_bytes_per_launch": n_local * w4 * 16 * scan_launches,
@@ -515,17 +516,21 @@ def main():
 
 
 def pmc_traffic(kernel_prefix, n_local, D):
-    """HBM read bytes per launch of `kernel_prefix` from the committed PMC pass
-    (profiles/r01/pmc_10M.json: rocprofv3 --pmc FETCH_SIZE, x2 gfx950 streaming
-    correction), only when it was collected at this workload's shard size."""
-    path = os.path.join(ROOT, "profiles", "r01", "pmc_10M.json")
-    if n_local != 10_000_000 or D != 768 or not os.path.exists(path):
+    """HBM read bytes per launch of `kernel_prefix` from the committed PMC passes
+    (profiles/r02/pmc_10M_mx5.json, then profiles/r01/pmc_10M.json: rocprofv3 --pmc
+    FETCH_SIZE, x2 gfx950 streaming correction), only when collected at this
+    workload's shard size."""
+    if n_local != 10_000_000 or D != 768:
         return None
-    with open(path) as f:
-        kern = json.load(f)["kernels"]
-    for name, d in kern.items():
-        if name.startswith(kernel_prefix) and "hbm_read_bytes_per_launch" in d:
-            return d["hbm_read_bytes_per_launch"]
+    for rel in (("r02", "pmc_10M_mx5.json"), ("r01", "pmc_10M.json")):
+        path = os.path.join(ROOT, "profiles", *rel)
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            kern = json.load(f)["kernels"]
+        for name, d in kern.items():
+            if name.startswith(kernel_prefix) and "hbm_read_bytes_per_launch" in d:
+                return d["hbm_read_bytes_per_launch"]
     return None
 
 

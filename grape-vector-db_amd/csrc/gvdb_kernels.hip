@@ -953,6 +953,18 @@ __device__ __forceinline__ void mfma_fp4_first(v16f_t& d, const v4i_t& a, const 
                  : "=&v"(d)
                  : "v"(a), "v"(b), "v"(scale));
 }
+// an MFMA whose B operand may have just been written by VALU: the two wait
+// states of the VALU-write -> MFMA-operand hazard inside the string
+__device__ __forceinline__ void mfma_fp4_first_nop(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "=&v"(d)
+                 : "v"(a), "v"(b), "v"(scale));
+}
+__device__ __forceinline__ void mfma_fp4_acc_nop(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
+    asm volatile("s_nop 1\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "+v"(d)
+                 : "v"(a), "v"(b), "v"(scale));
+}
 __device__ __forceinline__ void mfma_fp4_acc(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
     asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
                  : "+v"(d)
@@ -1366,18 +1378,7 @@ __device__ __forceinline__ void flush_stage_block(const uint64_t (*st_key)[kStag
     }
 }
 
-// k_scan_mx3: the FP4 scan with the candidates in REGISTERS and the queries
-// resident in LDS.  The whole query batch (<= 256 queries) is expanded to fp4
-// MFMA fragments once per block (96 KiB at 768 bits), then every wave streams
-// its own 32-row sub-tiles of the code planes straight from HBM into VGPRs
-// (two register sets: the next sub-tile's planes are in flight while the
-// current one is consumed), expands one code word per lane per k-step and runs
-// it against all query tiles (one A fragment per MFMA from LDS, a 4-deep
-// register ring hides the LDS latency).  No LDS traffic for candidates and no
-// block barrier in the loop: waves run independently, so one wave's
-// expansion / threshold VALU fills the other wave's MFMA gaps on the SIMD.
-// Semantics are those of k_scan_mx2 (exact +/-1 dot = D_pad - 2 Hamming;
-// emits (d << 32 | row) for d <= thr[q], staged per wave in LDS).
+// geometry shared by k_scan_mx3 (VARIANTS build) and k_scan_mx4
 #ifndef MX3_PF
 #define MX3_PF 4
 #endif
@@ -1392,11 +1393,24 @@ constexpr int kMx3Threads = 512;
 #ifndef MX3_PASSES
 #define MX3_PASSES 1
 #endif
-constexpr int kMx3Passes = MX3_PASSES;
+[[maybe_unused]] constexpr int kMx3Passes = MX3_PASSES;
 #ifndef MX3_RING
 #define MX3_RING 2
 #endif
-constexpr int kMx3Ring = MX3_RING;
+[[maybe_unused]] constexpr int kMx3Ring = MX3_RING;
+#ifdef GVDB_SCAN_VARIANTS  // k_scan_mx3: the previous default (GVDB_SCAN=mx3 in a VARIANTS=1 build)
+// k_scan_mx3: the FP4 scan with the candidates in REGISTERS and the queries
+// resident in LDS.  The whole query batch (<= 256 queries) is expanded to fp4
+// MFMA fragments once per block (96 KiB at 768 bits), then every wave streams
+// its own 32-row sub-tiles of the code planes straight from HBM into VGPRs
+// (two register sets: the next sub-tile's planes are in flight while the
+// current one is consumed), expands one code word per lane per k-step and runs
+// it against all query tiles (one A fragment per MFMA from LDS, a 4-deep
+// register ring hides the LDS latency).  No LDS traffic for candidates and no
+// block barrier in the loop: waves run independently, so one wave's
+// expansion / threshold VALU fills the other wave's MFMA gaps on the SIMD.
+// Semantics are those of k_scan_mx2 (exact +/-1 dot = D_pad - 2 Hamming;
+// emits (d << 32 | row) for d <= thr[q], staged per wave in LDS).
 template <int W4>
 __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const uint32_t* __restrict__ qwords,
@@ -1601,6 +1615,282 @@ static void launch_scan_mx3_t(const Stage1Args& a, hipStream_t s) {
     for (uint32_t g = 0; g < a.B; g += 256) {
         const uint32_t bg = min(256u, a.B - g);
         hipLaunchKernelGGL((k_scan_mx3<W4>), dim3(grid), dim3(kMx3Threads), 0, s, a.codes, a.cap, a.N,
+                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
+                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+    }
+}
+
+#endif  // GVDB_SCAN_VARIANTS
+
+// ---------------------------------------------------------------------------
+// k_scan_mx5: the stage-1 FP4 scan for D <= 768 (the bench's 10M x 768, B=256).
+// Same contract as k_scan_mx3 (emit (d << 32 | row) for every row with Hamming
+// d <= thr[q]), three changes measured against it:
+//  * {0,1} x {+-1} operands: a row bit b becomes e2m1 {0, v_c} and a query bit
+//    e2m1 +-1/v_c, so dot = sum over the row's set bits of (q ? +1 : -1)
+//    = 2 pop(q & x) - |x| and Hamming = |q| - dot exactly (|q| per query in
+//    LDS).  The row expansion is then one AND per dword (class c = bit 4j+c of
+//    the word, v = 0.5 / 1 / 2 / 2; the last class needs one shift): 5 VALU per
+//    k-step instead of 12 (shift/and/or per dword plus the half select).
+//  * each lane half loads only its own words (uint2 per plane: half h takes
+//    components 2h, 2h+1, k-step s uses plane s/2, component 2h + (s&1); the
+//    query fragments use the same map), so a ring slot is 2*W4 VGPRs and there
+//    is no per-k-step word select.
+//  * the code loads are inline asm into a static 3-deep ring with hand-placed
+//    s_waitcnt vmcnt(2*W4): hipcc drained vmcnt to 0 at the top of every
+//    k_scan_mx3 sub-tile (register copies of the ring across the loop back
+//    edge), exposing a full HBM round trip per sub-tile.  Any younger or older
+//    vector-memory op (the rare overflow emit) only makes that wait stricter.
+// The next k-step's row fragment is expanded between the current k-step's
+// MFMAs, so a wave's own VALU runs under its MFMA pipe time.
+#ifndef MX5_ABL
+#define MX5_ABL 0  // timing ablations (results invalid): 1 no epilogue, 2 no code loads, 4 no LDS A reads
+#endif
+#ifndef MX5_PRIO
+#define MX5_PRIO 0
+#endif
+#ifndef MX5_PF
+#define MX5_PF 8
+#endif
+constexpr int kMx5Threads = 512;
+#ifndef MX5_RING
+#define MX5_RING 2
+#endif
+constexpr int kMx5Ring = MX5_RING;
+__device__ __forceinline__ v4i_t fp4_row01(uint32_t w) {
+    v4i_t r;
+    r.x = (int)(w & 0x11111111u);         // 0.5
+    r.y = (int)(w & 0x22222222u);         // 1.0
+    r.z = (int)(w & 0x44444444u);         // 2.0
+    r.w = (int)((w >> 1) & 0x44444444u);  // 2.0 (bit 4j+3)
+    return r;
+}
+__device__ __forceinline__ v4i_t fp4_query_pm(uint32_t w) {
+    // +-2 / +-1 / +-0.5 / +-0.5 against the row classes above (sign = query bit clear)
+    const uint32_t nw = ~w;
+    v4i_t r;
+    r.x = (int)(((nw & 0x11111111u) << 3) | 0x44444444u);
+    r.y = (int)(((nw & 0x22222222u) << 2) | 0x22222222u);
+    r.z = (int)(((nw & 0x44444444u) << 1) | 0x11111111u);
+    r.w = (int)((nw & 0x88888888u) | 0x11111111u);
+    return r;
+}
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float d;
+    asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+template <int W4>
+__global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                           const uint32_t* __restrict__ qwords,
+                                                           const uint32_t* __restrict__ thr, uint32_t B,
+                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                           uint32_t bufcap) {
+    constexpr int KW = 4 * W4;  // 32-bit code words per row
+    constexpr int KS = KW / 2;  // k-steps of 64 bits
+    constexpr int QT = 8;       // query tiles of 32
+    constexpr uint32_t kWaveStage = 512;
+    constexpr int NW = kMx5Threads / 64;
+    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
+    // accumulator seed per (tile, lane half, row r): thr - |q|, so acc = thr - Hamming
+    __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
+    __shared__ float thrc_lds[QT * 32];
+    __shared__ uint64_t st_key[NW][kWaveStage];
+    __shared__ uint8_t st_q[NW][kWaveStage];
+    __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t h = lane >> 5;
+#if MX5_PRIO == 1
+    // static priority for the second wave of each SIMD (waves 4-7): the pair
+    // then drifts out of phase, so one wave's epilogue runs under the other's MFMAs
+    if (wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#elif MX5_PRIO == 2
+    if (wv < NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+    // query fragments: (tile qt, k-step s, lane l) = query qt*32 + (l & 31), word 4(s/2) + 2(l/32) + (s&1)
+    // k-step-major (s, qt, lane): MFMA m = s*QT + qt reads fragment m, so the A
+    // reads of the loop need one base register per 64 KiB (tile-major needed one
+    // per read above 64 KiB: ~20 VGPRs of addresses)
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx5Threads) {
+        const uint32_t l = i & 63u, st = i >> 6, qt = st % QT, qs = st / QT;
+        const uint32_t q = qt * 32u + (l & 31u);
+        const uint32_t wi = 4u * (qs >> 1) + 2u * (l >> 5) + (qs & 1u);
+        qfrag[i] = fp4_query_pm(q < B ? qwords[(uint64_t)q * KW + wi] : 0u);
+    }
+    // thr is clamped to the padded width (every Hamming distance is <= it, so
+    // the hit set is unchanged) to keep thr - |q| exact in f32
+    constexpr uint32_t kPadBits = 32u * KW;
+    if (tid < QT * 32) {
+        const uint32_t q = tid;
+        uint32_t pc = 0;
+        if (q < B)
+            for (int w = 0; w < KW; ++w) pc += __popc(qwords[(uint64_t)q * KW + w]);
+        const float tc = q < B ? (float)min(thr[q], kPadBits) : 0.0f;
+        thrc_lds[q] = tc;
+        // query q sits in tile q/32, lane half ((q&31)>>2)&1, row r = (q&3) + 4*((q&31)>>3)
+        const uint32_t qt = q >> 5, j = q & 31u, hh = (j >> 2) & 1u, r = (j & 3u) + 4u * (j >> 3);
+        seed_lds[(qt * 2 + hh) * 16 + r] = q < B ? tc - (float)pc : -1.0e9f;
+        qcnt[q] = 0u;
+    }
+    __syncthreads();
+    const uint32_t nqt = (B + 31u) / 32u;
+    const uint32_t nsub = (N + 31u) / 32u;
+    const uint32_t W = gridDim.x * NW;  // waves in the grid
+    // ring slot: this lane's half of the W4 planes of one 32-row sub-tile
+    uint2 ring[kMx5Ring][W4];
+    auto load = [&](uint32_t sb, uint2 (&c)[W4]) __attribute__((always_inline)) {
+        const uint32_t n = min(sb * 32u + (lane & 31u), N - 1u);  // clamped: branch-free ring
+        const uint32_t voff = n * 16u + h * 8u;
+#pragma unroll
+        for (int p = 0; p < W4; ++p) {
+            const uint4* base = codes + (uint64_t)p * cap;
+            if constexpr (MX5_ABL & 2)  // timing ablation: no code loads
+                c[p] = make_uint2(voff * 2654435761u + p, voff ^ (0x9e3779b9u * p));
+            else
+                asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(c[p]) : "v"(voff), "s"(base));
+        }
+    };
+    auto wait_slot = [&](uint2 (&c)[W4]) __attribute__((always_inline)) {
+        // the slot's W4 loads are the oldest of kMx5Ring in-flight sets
+#pragma unroll
+        for (int p = 0; p < W4; ++p)
+            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(c[p]) : "n"((kMx5Ring - 1) * W4));
+    };
+    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
+    v16f_t acc[QT];
+    const int scale1 = 0x7f7f7f7f;
+    auto process = [&](uint32_t sb, uint2 (&c)[W4], bool reload, uint32_t sb_next) __attribute__((always_inline)) {
+        const uint32_t n = sb * 32u + (lane & 31u);
+        uint32_t* cnt = counts;
+        uint64_t* bf = buf;
+        uint32_t bcap = bufcap;
+        asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
+        wait_slot(c);
+        // seed the accumulators (LDS broadcast: all 32 lanes of a half read the same 64 B)
+#pragma unroll
+        for (int qt = 0; qt < QT && !(MX5_ABL & 8); ++qt) {
+            const float4* sp = (const float4*)(seed_lds + (qt * 2 + h) * 16);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 v = sp[g];
+                acc[qt][4 * g + 0] = v.x;
+                acc[qt][4 * g + 1] = v.y;
+                acc[qt][4 * g + 2] = v.z;
+                acc[qt][4 * g + 3] = v.w;
+            }
+        }
+        const v4i_t* qf = qfrag + lane;
+        constexpr int PF = MX5_PF;  // A-fragment LDS ring depth (in MFMAs)
+        v4i_t ar[PF];
+#pragma unroll
+        for (int m = 0; m < PF; ++m) ar[m] = qf[m * 64];
+        v4i_t bcur = fp4_row01(c[0].x);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            __builtin_amdgcn_sched_barrier(0);
+            v4i_t bnext = bcur;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const int m = s * QT + qt;
+                const v4i_t a = ar[m % PF];
+                if (!(MX5_ABL & 4) || s == 0)  // ablation 4: A fragments of k-step 0 only
+                    if (m + PF < KS * QT) ar[m % PF] = qf[(m + PF) * 64];
+                if (s == 0 && (MX5_ABL & 8))  // ablation 8: no seeds (no hits below)
+                    mfma_fp4_first_nop(acc[qt], a, bcur, scale1);
+                else if (s == 0 && qt == 0)
+                    mfma_fp4_acc_nop(acc[qt], a, bcur, scale1);
+                else
+                    mfma_fp4_acc(acc[qt], a, bcur, scale1);
+                if (qt == 1 && s + 1 < KS) {  // next k-step's row fragment under this one's MFMAs
+                    const uint2 v = c[(s + 1) >> 1];
+                    bnext = fp4_row01(((s + 1) & 1) ? v.y : v.x);
+                }
+            }
+            bcur = bnext;
+        }
+        mfma_fp4_drain();
+        if (reload) load(sb_next, c);  // the slot is free once the MFMAs have read it
+        // threshold epilogue: acc = thr - Hamming, a hit is acc >= 0; one max over
+        // the lane's 16 queries rejects a tile with no hit
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            if (qt >= (int)nqt) break;
+            const v16f_t& A = acc[qt];
+            if constexpr (MX5_ABL & 1) {  // ablation: results consumed, nothing emitted
+                float t = A[0];
+#pragma unroll
+                for (int r = 1; r < 16; ++r) t += A[r];
+                if (t == 12345.678f) wcnt += 1;
+                continue;
+            }
+            float amax = max3f(A[0], A[1], A[2]);
+#pragma unroll
+            for (int r = 3; r < 15; r += 2) amax = max3f(amax, A[r], A[r + 1]);
+            amax = fmaxf(amax, A[15]);
+            if (!__ballot(amax >= ((MX5_ABL & 8) ? 1e9f : 0.0f) && n < N)) continue;
+            uint32_t rb = qt * 32u + 4u * h;
+            asm volatile("" : "+v"(rb));  // keeps the 128 per-(tile, r) query indices from being hoisted
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const bool hit = A[r] >= 0.0f && n < N;
+                const uint64_t m = __ballot(hit);
+                if (m) {
+                    if (hit) {
+                        const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
+                        const uint32_t d = (uint32_t)(int)(thrc_lds[qi] - A[r]);
+                        const uint64_t key = ((uint64_t)d << 32) | n;
+                        if (sp < kWaveStage) {
+                            st_key[wv][sp] = key;
+                            st_q[wv][sp] = (uint8_t)qi;
+                        } else {
+                            const uint32_t pos = atomicAdd(&cnt[qi], 1u);
+                            if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = key;
+                        }
+                    }
+                    wcnt += (uint32_t)__popcll(m);
+                }
+            }
+        }
+    };
+    // static ring: trip t processes slots 0,1,2 (sub-tiles sb, sb+W, sb+2W) and
+    // refills each with the sub-tile three strides ahead
+    uint32_t sb = blockIdx.x * NW + wv;
+    constexpr uint32_t RW = kMx5Ring;
+    load(sb, ring[0]);
+    load(sb + W, ring[1]);
+    if constexpr (kMx5Ring == 3) load(sb + 2 * W, ring[kMx5Ring - 1]);
+    for (; sb < nsub; sb += RW * W) {  // explicit slots: the ring stays in fixed registers
+        process(sb, ring[0], true, sb + RW * W);
+        if (sb + W >= nsub) break;
+        process(sb + W, ring[1], true, sb + W + RW * W);
+        if constexpr (kMx5Ring == 3) {
+            if (sb + 2 * W >= nsub) break;
+            process(sb + 2 * W, ring[kMx5Ring - 1], true, sb + 2 * W + RW * W);
+        }
+    }
+    // drain the clamped prefetches before the LDS stage is flushed
+#pragma unroll
+    for (int k = 0; k < kMx5Ring; ++k)
+#pragma unroll
+        for (int p = 0; p < W4; ++p) asm volatile("s_waitcnt vmcnt(0)" : "+v"(ring[k][p]));
+    flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase, counts,
+                                      buf, bufcap);
+}
+
+template <int W4>
+static void launch_scan_mx5_t(const Stage1Args& a, hipStream_t s) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t nsub = (a.N + 31u) / 32u;
+    const uint32_t wpb = kMx5Threads / 64;
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus, (nsub + wpb - 1) / wpb));
+    for (uint32_t g = 0; g < a.B; g += 256) {
+        const uint32_t bg = min(256u, a.B - g);
+        hipLaunchKernelGGL((k_scan_mx5<W4>), dim3(grid), dim3(kMx5Threads), 0, s, a.codes, a.cap, a.N,
                            (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
                            a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
@@ -1866,6 +2156,13 @@ static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
                        a.cap, a.N, a.D, a.sample_stride, a.qcodes, a.B, QT, a.hist);
 }
 
+#ifdef GVDB_SCAN_VARIANTS
+static bool scan_selected(const char* v) {  // read per launch: tests switch it between calls
+    const char* e = getenv("GVDB_SCAN");
+    return e && strcmp(e, v) == 0;
+}
+#endif
+
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     const uint32_t W4 = code_w4(a.D);
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
@@ -1925,13 +2222,20 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 4: launch_scan_mx2_t<4>(a, s); break;
             default: launch_scan_mx2_t<6>(a, s); break;
         }
-#endif  // GVDB_SCAN_VARIANTS
-    } else if (mfma) {  // FP4 block-scaled MFMA, candidates in registers (default for large batches)
+    } else if (mfma && scan_selected("mx3")) {  // the previous default, +-1 operands (A/B)
         switch (W4) {
             case 2: launch_scan_mx3_t<2>(a, s); break;
             case 3: launch_scan_mx3_t<3>(a, s); break;
             case 4: launch_scan_mx3_t<4>(a, s); break;
             default: launch_scan_mx3_t<6>(a, s); break;
+        }
+#endif  // GVDB_SCAN_VARIANTS
+    } else if (mfma) {  // FP4 block-scaled MFMA, {0,1} x {+-1} operands (default for large batches)
+        switch (W4) {
+            case 2: launch_scan_mx5_t<2>(a, s); break;
+            case 3: launch_scan_mx5_t<3>(a, s); break;
+            case 4: launch_scan_mx5_t<4>(a, s); break;
+            default: launch_scan_mx5_t<6>(a, s); break;
         }
     } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \

@@ -11,7 +11,7 @@ for f in sorted(glob.glob(sys.argv[1] + "/counters_p*.csv")):
         d[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"]),
                                          int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
 for k, cs in d.items():
-    if len(sys.argv) > 2 and sys.argv[2] not in k:
+    if len(sys.argv) > 2 and not sys.argv[2].startswith("--") and sys.argv[2] not in k:
         continue
     print(k)
     for c, v in sorted(cs.items()):
@@ -21,3 +21,29 @@ for k, cs in d.items():
             dur[di] = du
         vals = list(per.values())
         print(f"   {c:32s} {sum(vals) / len(vals):14.4g}  n={len(vals)} dur_us={sum(dur.values()) / len(dur) / 1e3:.1f}")
+
+# --json <path>: the per-kernel averages in the profiles/ JSON layout used by bench.py's pmc_traffic
+if "--json" in sys.argv:
+    import json
+
+    outp = sys.argv[sys.argv.index("--json") + 1]
+    res = {"source": f"scripts/pmc_summary.py over {sys.argv[1]} (rocprofv3 --pmc, one counter set per run)",
+           "fetch_size_unit": "KiB; gfx950 FETCH_SIZE counts half of the bytes of a 16-B/lane streaming read "
+                              "(MI355X_MICROARCH.md, HBM) -> hbm_read_bytes = 2 * 1024 * FETCH_SIZE",
+           "kernels": {}}
+    for k, cs in d.items():
+        e = {}
+        for c, v in cs.items():
+            per = collections.defaultdict(float)
+            for di, val, du in v:
+                per[di] += val
+            e[c] = sum(per.values()) / len(per)
+            e["dispatches"] = len(per)
+            e["avg_dur_us"] = sum(du for _, _, du in v) / len(v) / 1e3
+        if "FETCH_SIZE" in e:
+            e["hbm_read_bytes_per_launch"] = 2 * 1024 * e["FETCH_SIZE"]
+        if "WRITE_SIZE" in e:
+            e["hbm_write_bytes_per_launch"] = 1024 * e["WRITE_SIZE"]
+        res["kernels"][k] = e
+    with open(outp, "w") as f:
+        json.dump(res, f, indent=1)

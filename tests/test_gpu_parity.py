@@ -133,10 +133,11 @@ def test_stage1_topr_matches_oracle(g, oracle_mod, N, D, B, R, dup):
 @pytest.mark.parametrize("N,D,B,R", [(200_000, 768, 160, 100), (100_000, 256, 96, 64), (120_000, 384, 128, 200),
                                      (90_000, 512, 300, 50), (80_000, 1024, 100, 100), (70_000, 768, 256, 1000),
                                      (50_000, 1536, 200, 100), (40_000, 2048, 200, 300), (60_000, 3072, 256, 100),
-                                     (50_000, 3000, 130, 100), (40_000, 4096, 100, 100)])
+                                     (50_000, 3000, 130, 100), (40_000, 4096, 100, 100),
+                                     (60_000, 200, 128, 100), (50_000, 700, 97, 100), (30_001, 330, 256, 40)])
 def test_stage1_mfma_batches_match_oracle(g, oracle_mod, N, D, B, R):
-    """Large batches (B >= 96) take the FP4-MFMA scan: k_scan_mx3 for W4 in
-    {2,3,4,6}, k_scan_mx4 (query tiles per launch bounded by LDS, partial
+    """Large batches (B >= 96) take the FP4-MFMA scan: k_scan_mx5 for W4 in
+    {2,3,4,6} (padded dims included: D = 200, 330, 700), k_scan_mx4 (query tiles per launch bounded by LDS, partial
     last launch) for W4 in {8,12,16,24,32}; distances must equal the popcount
     path (GVDB_SCAN=valu) and the oracle bit for bit.  (The A/B variants
     i8 / fp4u / fp4lds are compiled only by `make VARIANTS=1`.)"""
