@@ -235,21 +235,23 @@ def main():
         q1 = [q[i:i + 1].contiguous() for i in range(B)]
         o1i = torch.zeros((1, k), dtype=torch.int64, device=dev)
         o1s = torch.zeros((1, k), dtype=torch.float32, device=dev)
-        for i in range(3):
-            ix.search_device(q1[i], k, o1i, o1s, None, sp)
-        torch.cuda.synchronize()
+        # results (for recall and the batch comparison) and the scan's HIP-event
+        # average come from an untimed pass; the timed pass is the searches alone
+        # (no per-query result copies, no event records)
+        res1 = []
         L.gvdb_timing_reset()
         L.gvdb_timing_enable(1)
-        res1 = []
+        for i in range(min(B, args.b1_queries)):
+            ix.search_device(q1[i], k, o1i, o1s, None, sp)
+            res1.append(o1i.clone())
+        torch.cuda.synchronize()
+        L.gvdb_timing_enable(0)
+        b1_scan_ms, b1_scan_n = timing_slot(L, 1)
         tb = time.perf_counter()
         for i in range(args.b1_queries):
             ix.search_device(q1[i % B], k, o1i, o1s, None, sp)
-            if i < B:
-                res1.append(o1i.clone())
         torch.cuda.synchronize()
         tb = time.perf_counter() - tb
-        L.gvdb_timing_enable(0)
-        b1_scan_ms, b1_scan_n = timing_slot(L, 1)
         f1 = torch.cat(res1).cpu().numpy()
         b1_scan_avg = b1_scan_ms / max(b1_scan_n, 1)
         code_bytes = n_local * gvdb_code_w4(D) * 16
