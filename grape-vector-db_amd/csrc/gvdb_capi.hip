@@ -386,6 +386,26 @@ void timing_submit(EvSet* e) {
     if (timing().pending.size() > 512) timing_drain_locked(256);
 }
 
+// tests: the stage-1 thresholds of the last batch searched with GVDB_DEBUG_THR=1
+uint32_t*& debug_thr() {
+    static uint32_t* p = nullptr;
+    return p;
+}
+uint32_t& debug_thr_cap() {
+    static uint32_t n = 0;
+    return n;
+}
+static hipError_t debug_keep_thr(const uint32_t* thr, uint32_t B, hipStream_t s) {
+    if (!getenv_flag("GVDB_DEBUG_THR")) return hipSuccess;
+    uint32_t*& dt = debug_thr();
+    if (debug_thr_cap() < B) {
+        if (dt) (void)hipFree(dt);
+        hipError_t e = hipMalloc((void**)&dt, (size_t)B * 4);
+        if (e != hipSuccess) return e;
+        debug_thr_cap() = B;
+    }
+    return hipMemcpyAsync(dt, thr, (size_t)B * 4, hipMemcpyDeviceToDevice, s);
+}
 unsigned long long*& debug_b1_clk() {
     static unsigned long long* p = nullptr;
     return p;
@@ -549,6 +569,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             s1.R = R;
             s1.ev = ev ? ev->e : nullptr;
             HIP_TRY(launch_stage1_fast(s1, s), "stage1");
+            HIP_TRY(debug_keep_thr(s1.thr, B, s), "copy thresholds");
         } else {
             // R beyond the LDS select: every query on the exact all-rows path
             HIP_TRY(ws.slow.ensure(stage1_slow_bytes(v.N)), "alloc slow path");
@@ -1387,6 +1408,7 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
         s1.B = (uint32_t)B;
         s1.R = RR;
         HIP_TRY(launch_stage1_fast(s1, s), "stage1");
+        HIP_TRY(debug_keep_thr(s1.thr, (uint32_t)B, s), "copy thresholds");
     } else {
         HIP_TRY(ws.slow.ensure(stage1_slow_bytes((uint32_t)ix->n)), "alloc slow");
         for (uint64_t q = 0; q < B; ++q)
@@ -1883,6 +1905,12 @@ gvdb_status gvdb::report_status(gvdb_status s, const std::string& msg) { return 
 int gvdb::index_device(const gvdb_index* ix) { return ix->device; }
 
 // timing study: the last k_b1_tail phase clocks (GVDB_B1_CLK=1), 16 words
+// tests only (not part of include/gvdb.h): thresholds T[0..B) of the last GVDB_DEBUG_THR=1 batch
+extern "C" int gvdb_debug_stage1_thresholds(uint32_t* out, uint32_t B) {
+    if (!debug_thr() || B > debug_thr_cap()) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    return (int)hipMemcpy(out, debug_thr(), (size_t)B * 4, hipMemcpyDeviceToHost);
+}
 extern "C" int gvdb_debug_b1_clock(unsigned long long* out) {
     if (!debug_b1_clk()) return -1;
     return (int)hipMemcpy(out, debug_b1_clk(), 16 * 8, hipMemcpyDeviceToHost);

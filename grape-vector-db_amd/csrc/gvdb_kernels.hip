@@ -971,6 +971,14 @@ __device__ __forceinline__ void mfma_fp4_acc(v16f_t& d, const v4i_t& a, const v4
                  : "v"(a), "v"(b), "v"(scale));
 }
 __device__ __forceinline__ void mfma_fp4_drain() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); }
+// the same drain naming the accumulators as operands: no compiler read of them
+// can be scheduled above it (plain C++ reads of asm-MFMA results otherwise can)
+template <int NA>
+__device__ __forceinline__ void mfma_fp4_drain_acc(v16f_t (&acc)[NA]) {
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(acc[i]));
+}
 
 #ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
 template <int W4>
@@ -1809,7 +1817,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
             }
             bcur = bnext;
         }
-        mfma_fp4_drain();
+        mfma_fp4_drain_acc(acc);
         if (reload) load(sb_next, c);  // the slot is free once the MFMAs have read it
         // threshold epilogue: acc = thr - Hamming, a hit is acc >= 0; one max over
         // the lane's 16 queries rejects a tile with no hit
@@ -2129,6 +2137,176 @@ static void launch_scan_t(const Stage1Args& a, hipStream_t s) {
                        a.counts, a.buf, a.bufcap);
 }
 
+// k_sample_mx: the sample histogram of a large batch on the FP4 MFMA (the
+// k_scan_mx5 operands; accumulators seeded with -|q|, so acc = -Hamming).
+// The VALU form (k_sample_hist) re-reads the sample once per group of ~13
+// queries (LDS holds 13 full histograms) and spends ~48 VALU per pair: 0.10 ms
+// per 10M x 768 batch.  Here a block holds 128 queries' fragments (48 KiB) and
+// their histograms of d < cap = min(D+1, 384) as packed u16 pairs (96 KiB), so
+// the sample is read once per 128 queries.  Flush: each query's bins only up
+// to the block's own target-th smallest distance t_b (all bins below cap if the
+// block never reaches target).  The global threshold T = smallest t with
+// sum_b cnt_b(<= t) >= target satisfies T <= t_b for every block that reached
+// target, so the flushed histogram gives k_threshold exactly the T of the full
+// one (T >= cap reads as D: a looser, still valid threshold).  Only used for
+// sampled shards (N > kExactN, target << sample rows); correctness of the
+// search never depends on T (k_select certifies the top-R).
+constexpr int kSmxThreads = 512;
+constexpr uint32_t kSmxCap = 384;  // histogram bins per query (d < cap)
+constexpr uint32_t kSmxHW = kSmxCap / 2;
+template <int W4>
+__global__ __launch_bounds__(kSmxThreads, 1) void k_sample_mx(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                            uint32_t D, uint32_t stride, uint32_t nsub,
+                                                            const uint32_t* __restrict__ qwords, uint32_t B,
+                                                            uint32_t target, uint32_t* __restrict__ hist) {
+    constexpr int KW = 4 * W4;
+    constexpr int KS = KW / 2;
+    constexpr int QT = 4;  // query tiles per block (128 queries)
+    constexpr int NW = kSmxThreads / 64;
+    __shared__ __attribute__((aligned(16))) v4i_t qfrag[KS * QT * 64];
+    __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
+    __shared__ uint32_t hl[QT * 32 * kSmxHW];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t h = lane >> 5;
+    const uint32_t q0 = blockIdx.y * (QT * 32u);
+    const uint32_t binc = min(D + 1u, kSmxCap);
+    for (uint32_t i = tid; i < (uint32_t)(KS * QT * 64); i += kSmxThreads) {
+        const uint32_t l = i & 63u, st = i >> 6, qt = st % QT, qs = st / QT;
+        const uint32_t q = q0 + qt * 32u + (l & 31u);
+        const uint32_t wi = 4u * (qs >> 1) + 2u * (l >> 5) + (qs & 1u);
+        qfrag[i] = fp4_query_pm(q < B ? qwords[(uint64_t)q * KW + wi] : 0u);
+    }
+    for (uint32_t i = tid; i < (uint32_t)(QT * 32 * kSmxHW); i += kSmxThreads) hl[i] = 0u;
+    if (tid < QT * 32) {
+        const uint32_t q = q0 + tid;
+        uint32_t pc = 0;
+        if (q < B)
+            for (int w = 0; w < KW; ++w) pc += __popc(qwords[(uint64_t)q * KW + w]);
+        const uint32_t qt = tid >> 5, j = tid & 31u, hh = (j >> 2) & 1u, r = (j & 3u) + 4u * (j >> 3);
+        // padding queries: acc stays hugely negative -> d >= cap, never counted
+        seed_lds[(qt * 2 + hh) * 16 + r] = q < B ? -(float)pc : -1.0e6f;
+    }
+    __syncthreads();
+    const uint32_t W = gridDim.x * NW;
+    const int scale1 = 0x7f7f7f7f;
+    v16f_t acc[QT];
+    for (uint32_t sb = blockIdx.x * NW + wv; sb < nsub; sb += W) {
+        // sample sub-tile sb: chunk (32 sb) / 4096 at stride rows, 32 consecutive rows
+        const uint32_t s0 = sb * 32u;
+        const uint32_t n = (s0 >> 12) * stride + (s0 & 4095u) + (lane & 31u);
+        const uint32_t nc = min(n, N - 1u);
+        uint2 c[W4];
+#pragma unroll
+        for (int p = 0; p < W4; ++p) c[p] = ((const uint2*)(codes + (uint64_t)p * cap + nc))[h];
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+            const float4* sp = (const float4*)(seed_lds + (t * 2 + h) * 16);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 v = sp[g];
+                acc[t][4 * g + 0] = v.x;
+                acc[t][4 * g + 1] = v.y;
+                acc[t][4 * g + 2] = v.z;
+                acc[t][4 * g + 3] = v.w;
+            }
+        }
+        const v4i_t* qf = qfrag + lane;
+        constexpr int PF = 6;  // A-fragment LDS ring depth (in MFMAs)
+        v4i_t ar[PF];
+#pragma unroll
+        for (int m = 0; m < PF; ++m) ar[m] = qf[m * 64];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const uint2 v = c[s >> 1];
+            const v4i_t b = fp4_row01((s & 1) ? v.y : v.x);
+#pragma unroll
+            for (int t = 0; t < QT; ++t) {
+                const int m = s * QT + t;
+                const v4i_t a = ar[m % PF];
+                if (m + PF < KS * QT) ar[m % PF] = qf[(m + PF) * 64];
+                if (t == 0)
+                    mfma_fp4_acc_nop(acc[t], a, b, scale1);
+                else
+                    mfma_fp4_acc(acc[t], a, b, scale1);
+            }
+        }
+        mfma_fp4_drain_acc(acc);
+        const uint32_t lim = n < N ? binc : 0u;  // rows past N (defensive: sampled chunks lie inside the shard)
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+            uint32_t rb = t * 32u + 4u * h;
+            asm volatile("" : "+v"(rb));
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t d = (uint32_t)(int)(-acc[t][r]);
+                if (d < lim) {
+                    const uint32_t ql = rb + (r & 3) + 8 * (r >> 2);
+                    atomicAdd(&hl[ql * kSmxHW + (d >> 1)], 1u << ((d & 1u) << 4));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // flush: one wave per query; lane l holds bins [6l, 6l + 6)
+    const uint32_t nb = D + 1u;
+    for (uint32_t ql = wv; ql < QT * 32u; ql += NW) {
+        const uint32_t q = q0 + ql;
+        if (q >= B) break;
+        uint32_t cnt[6], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t wi = lane * 3u + i;
+            const uint32_t w = wi < kSmxHW ? hl[ql * kSmxHW + wi] : 0u;
+            cnt[2 * i] = w & 0xffffu;
+            cnt[2 * i + 1] = w >> 16;
+            sum += cnt[2 * i] + cnt[2 * i + 1];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(incl, off);
+            if ((int)lane >= off) incl += v;
+        }
+        const uint64_t m = __ballot(incl >= target);
+        uint32_t tb = binc - 1u;
+        if (m) {
+            const uint32_t first = __ffsll((long long)m) - 1;
+            uint32_t t = 0;
+            if (lane == first) {
+                uint32_t cum = incl - sum;
+                for (int i = 0; i < 6; ++i) {
+                    cum += cnt[i];
+                    if (cum >= target) {
+                        t = lane * 6u + i;
+                        break;
+                    }
+                }
+            }
+            tb = __shfl(t, first);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const uint32_t bin = lane * 6u + i;
+            if (bin <= tb && bin < binc && cnt[i]) atomicAdd(&hist[(uint64_t)q * nb + bin], cnt[i]);
+        }
+    }
+}
+
+template <int W4>
+static void launch_sample_mx_t(const Stage1Args& a, hipStream_t s) {
+    const uint32_t nsub = a.sample_chunks * (4096u / 32u);
+    const uint32_t gy = (a.B + 127u) / 128u;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    // about one block per CU over the query groups; >= 8 x-blocks keeps a
+    // block's per-bin count below 2^16 for any sample (<= 262144 rows)
+    const uint32_t gx = std::max<uint32_t>(8u, std::min<uint32_t>((uint32_t)cus / gy, (nsub + 7u) / 8u));
+    hipLaunchKernelGGL((k_sample_mx<W4>), dim3(gx, gy), dim3(kSmxThreads), 0, s, a.codes, a.cap, a.N, a.D,
+                       a.sample_stride, nsub, (const uint32_t*)a.qcodes, a.B, a.target, a.hist);
+}
+
 template <int W4>
 static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
     // GVDB_HIST_LDS_WORDS: LDS histogram words per block (timing knob; default 12288)
@@ -2156,6 +2334,10 @@ static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
                        a.cap, a.N, a.D, a.sample_stride, a.qcodes, a.B, QT, a.hist);
 }
 
+static bool getenv_flag_eq(const char* name, const char* v) {  // read per launch (tests switch it)
+    const char* e = getenv(name);
+    return e && strcmp(e, v) == 0;
+}
 #ifdef GVDB_SCAN_VARIANTS
 static bool scan_selected(const char* v) {  // read per launch: tests switch it between calls
     const char* e = getenv("GVDB_SCAN");
@@ -2166,7 +2348,21 @@ static bool scan_selected(const char* v) {  // read per launch: tests switch it 
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     const uint32_t W4 = code_w4(a.D);
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    switch (W4) {
+    // sampled shard + large batch + >= 32 sample chunks (128K rows): the FP4-MFMA sample
+    // histogram (10M x 768: 55 vs 91 us; at the 64K-row floor of the 1.25M shard the VALU
+    // one is 1 % faster per step).  GVDB_SAMPLE=valu / =mx force one (tests, A/B).
+    const bool force_mx = getenv_flag_eq("GVDB_SAMPLE", "mx");
+    const bool sample_mx = a.use_mfma == 1 && a.B >= kMfmaMinB && mfma_scan_supported(W4) &&
+                           a.target < a.sample_chunks * 4096u / 2u && a.N > a.sample_chunks * 4096u &&
+                           !getenv_flag_eq("GVDB_SAMPLE", "valu") && (a.sample_chunks >= 32u || force_mx);
+    if (sample_mx) {
+        switch (W4) {
+            case 2: launch_sample_mx_t<2>(a, s); break;
+            case 3: launch_sample_mx_t<3>(a, s); break;
+            case 4: launch_sample_mx_t<4>(a, s); break;
+            default: launch_sample_mx_t<6>(a, s); break;
+        }
+    } else switch (W4) {
 #define GVDB_CASE(w, cpl)            \
     case w:                          \
         launch_hist_t<w>(a, s);      \

@@ -635,3 +635,45 @@ def test_sharded_packed_world1_equals_single_device(g):
     torch.cuda.synchronize()
     assert torch.equal(pi, oi) and torch.equal(pn, on)
     assert same_f32(ps.cpu().numpy(), osc.cpu().numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,D,B,R", [(1_200_000, 768, 256, 100), (600_000, 256, 128, 1000), (400_000, 384, 200, 100),
+                                     (350_000, 512, 96, 4000)])
+def test_sample_histogram_mfma_thresholds_equal_valu(g, N, D, B, R):
+    """The FP4-MFMA sample histogram (k_sample_mx: 128 queries per block, bins
+    d < 384, each block flushes only up to its own target-th distance) must give
+    k_threshold exactly the thresholds of the VALU histogram (GVDB_SAMPLE=valu),
+    and the searches the same ids and distances (sampled shards: N > 262144)."""
+    import ctypes as C
+    import os
+
+    import torch
+
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(N + D)
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    for c0 in range(0, N, 1 << 19):
+        n = min(1 << 19, N - c0)
+        ix.add_device(torch.randn((n, D), generator=gen, device=dev), torch.arange(c0, c0 + n, device=dev))
+    q = torch.randn((B, D), generator=gen, device=dev)
+    L = g.lib()
+    L.gvdb_debug_stage1_thresholds.argtypes = [C.POINTER(C.c_uint32), C.c_uint32]
+    out = {}
+    os.environ["GVDB_DEBUG_THR"] = "1"
+    try:
+        for mode in ("mfma", "valu"):
+            os.environ["GVDB_SAMPLE"] = "mx" if mode == "mfma" else "valu"
+            rows = torch.zeros((B, R), dtype=torch.int64, device=dev)
+            dist = torch.zeros((B, R), dtype=torch.int32, device=dev)
+            ix.bq_topr_device(q, R, rows, dist)
+            torch.cuda.synchronize()
+            thr = (C.c_uint32 * B)()
+            assert L.gvdb_debug_stage1_thresholds(thr, B) == 0
+            out[mode] = (list(thr), rows.cpu().numpy(), dist.cpu().numpy())
+    finally:
+        os.environ.pop("GVDB_DEBUG_THR", None)
+        os.environ.pop("GVDB_SAMPLE", None)
+    assert out["mfma"][0] == out["valu"][0]
+    assert max(out["mfma"][0]) < D  # a real estimate, not the no-pruning fallback
+    assert (out["mfma"][1] == out["valu"][1]).all() and (out["mfma"][2] == out["valu"][2]).all()
