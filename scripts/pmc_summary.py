@@ -7,7 +7,7 @@ import sys
 d = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(sys.argv[1] + "/counters_p*.csv")):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].replace("void gvdb::(anonymous namespace)::", "")[:40]
+        k = r["Kernel_Name"].replace("void gvdb::(anonymous namespace)::", "").removeprefix("void ")[:40]
         d[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"]),
                                          int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
 for k, cs in d.items():
