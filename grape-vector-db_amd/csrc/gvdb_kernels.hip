@@ -1832,11 +1832,14 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
                 if (t == 12345.678f) wcnt += 1;
                 continue;
             }
-            float amax = max3f(A[0], A[1], A[2]);
+            // any acc >= 0 <=> some sign bit clear <=> the AND of the 16 words is
+            // non-negative as an int (acc is never -0.0: the seed thr - |q| is +0 when
+            // zero and an exact zero sum of nonzero terms rounds to +0); v_and3_b32, no
+            // canonicalising max
+            int aand = __float_as_int(A[0]);
 #pragma unroll
-            for (int r = 3; r < 15; r += 2) amax = max3f(amax, A[r], A[r + 1]);
-            amax = fmaxf(amax, A[15]);
-            if (!__ballot(amax >= ((MX5_ABL & 8) ? 1e9f : 0.0f) && n < N)) continue;
+            for (int r = 1; r < 16; ++r) aand &= __float_as_int(A[r]);
+            if (!__ballot(((MX5_ABL & 8) ? false : aand >= 0) && n < N)) continue;
             uint32_t rb = qt * 32u + 4u * h;
             asm volatile("" : "+v"(rb));  // keeps the 128 per-(tile, r) query indices from being hoisted
 #pragma unroll
