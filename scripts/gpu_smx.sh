@@ -8,15 +8,17 @@ mkdir -p gpurun_out
 rc=$?; [ -n "$SKIP_TESTS" ] || { tail -4 gpurun_out/smx_tests.log; [ $rc -eq 0 ] || exit $rc; }
 : > gpurun_out/smx_timing.log
 for v in mx valu mx valu; do
-  if [ $v = valu ]; then export GVDB_SAMPLE=valu; else unset GVDB_SAMPLE; fi
+  export GVDB_SAMPLE=$v
   TAG=sample_$v timeout -k 10 300 python -u scripts/b256_timing.py >> gpurun_out/smx_timing.log 2>&1 || exit 1
 done
-unset GVDB_SAMPLE
+export GVDB_SAMPLE=mx
+TAG=shard_mx SHARD_N=1250000 timeout -k 10 300 python -u scripts/b256_timing.py >> gpurun_out/smx_timing.log 2>&1 || exit 1
+GVDB_SAMPLE=valu TAG=shard_valu SHARD_N=1250000 timeout -k 10 300 python -u scripts/b256_timing.py >> gpurun_out/smx_timing.log 2>&1 || exit 1
 TAG=shard_mx SHARD_N=1250000 timeout -k 10 300 python -u scripts/b256_timing.py >> gpurun_out/smx_timing.log 2>&1 || exit 1
 GVDB_SAMPLE=valu TAG=shard_valu SHARD_N=1250000 timeout -k 10 300 python -u scripts/b256_timing.py >> gpurun_out/smx_timing.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/smx_timing.log
 unset GVDB_SAMPLE
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_smx -o run -- python3 scripts/b256_timing.py > gpurun_out/prof_smx.log 2>&1 || exit 1
+GVDB_SAMPLE=mx SHARD_N=${PROF_N:-1250000} timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_smx -o run -- python3 scripts/b256_timing.py > gpurun_out/prof_smx.log 2>&1 || exit 1
 python3 -c "
 import csv
 for r in csv.DictReader(open('gpurun_out/prof_smx/run_kernel_stats.csv')):
