@@ -1768,6 +1768,21 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
     uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
     v16f_t acc[QT];
     const int scale1 = 0x7f7f7f7f;
+    // accumulator seeds of tile qt (LDS broadcast: all 32 lanes of a half read the same
+    // 64 B); issued right after tile qt's epilogue, so the next sub-tile's seeds are in
+    // flight during the remaining tiles' epilogues
+    auto seed = [&](int qt) __attribute__((always_inline)) {
+        if constexpr (MX5_ABL & 8) return;
+        const float4* sp = (const float4*)(seed_lds + (qt * 2 + h) * 16);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 v = sp[g];
+            acc[qt][4 * g + 0] = v.x;
+            acc[qt][4 * g + 1] = v.y;
+            acc[qt][4 * g + 2] = v.z;
+            acc[qt][4 * g + 3] = v.w;
+        }
+    };
     auto process = [&](uint32_t sb, uint2 (&c)[W4], bool reload, uint32_t sb_next) __attribute__((always_inline)) {
         const uint32_t n = sb * 32u + (lane & 31u);
         uint32_t* cnt = counts;
@@ -1775,19 +1790,6 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
         uint32_t bcap = bufcap;
         asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
         wait_slot(c);
-        // seed the accumulators (LDS broadcast: all 32 lanes of a half read the same 64 B)
-#pragma unroll
-        for (int qt = 0; qt < QT && !(MX5_ABL & 8); ++qt) {
-            const float4* sp = (const float4*)(seed_lds + (qt * 2 + h) * 16);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 v = sp[g];
-                acc[qt][4 * g + 0] = v.x;
-                acc[qt][4 * g + 1] = v.y;
-                acc[qt][4 * g + 2] = v.z;
-                acc[qt][4 * g + 3] = v.w;
-            }
-        }
         const v4i_t* qf = qfrag + lane;
         constexpr int PF = MX5_PF;  // A-fragment LDS ring depth (in MFMAs)
         v4i_t ar[PF];
@@ -1823,7 +1825,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
         // the lane's 16 queries rejects a tile with no hit
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
-            if (qt >= (int)nqt) break;
+            if (qt < (int)nqt) do {  // (a `continue` below leaves this do-while)
             const v16f_t& A = acc[qt];
             if constexpr (MX5_ABL & 1) {  // ablation: results consumed, nothing emitted
                 float t = A[0];
@@ -1864,12 +1866,16 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
                     wcnt += (uint32_t)__popcll(m);
                 }
             }
+            } while (0);
+            seed(qt);  // the next sub-tile's seeds
         }
     };
     // static ring: trip t processes slots 0,1,2 (sub-tiles sb, sb+W, sb+2W) and
     // refills each with the sub-tile three strides ahead
     uint32_t sb = blockIdx.x * NW + wv;
     constexpr uint32_t RW = kMx5Ring;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) seed(qt);  // the first sub-tile's
     load(sb, ring[0]);
     load(sb + W, ring[1]);
     if constexpr (kMx5Ring == 3) load(sb + 2 * W, ring[kMx5Ring - 1]);
