@@ -147,7 +147,7 @@ struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
-        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids, flt_codes;
+        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids, flt_codes, s1_mx;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     // Searches return without a host sync: the workspace goes back to the pool
@@ -165,7 +165,7 @@ struct Workspace {
         if (done) (void)hipEventDestroy(done);
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
                         &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
-                        &fx_scores, &flt_rows, &flt_ids, &flt_codes, &b1})
+                        &fx_scores, &flt_rows, &flt_ids, &flt_codes, &s1_mx, &b1})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -278,8 +278,9 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t sample_div, uint32_t& chunks
 
 // Stage-1 workspace: ONE memset zeroes flags | counts | fail | hist, which
 // sit contiguously in ws.zero (flags[0] = any stage-1 failure, flags[1] = NaN).
+// fast: launch_stage1_fast will run (its first kernel may zero the state)
 gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D, uint32_t R, uint32_t N,
-                           hipStream_t s) {
+                           hipStream_t s, bool fast) {
     // GVDB_SCAN=valu forces the popcount scan for every batch size; default:
     // FP4 MFMA for large batches.  The A/B variants (=i8, =fp4u, =fp4lds)
     // exist only in a `make VARIANTS=1` build.
@@ -301,15 +302,38 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     }();
     plan_sampling(N, R, (s1.use_mfma && B >= kMfmaMinB) ? big_div : 32u, s1.sample_chunks, s1.sample_stride,
                   s1.target, s1.bufcap);
+    s1.B = B;
+    s1.D = D;
+    s1.N = N;
+    s1.R = R;
+    const size_t extra = stage1_plan(s1);
     const size_t nb = (size_t)D + 1u;
-    const size_t words = 4 + 2 * (size_t)B + (size_t)B * nb;
+    // the dense sample needs no histogram: only flags | counts | fail are zeroed
+    const size_t words = 4 + 2 * (size_t)B + (s1.sample_mode == kSampleDense ? 0 : (size_t)B * nb);
     HIP_TRY(ws.zero.ensure(words * 4 + 16), "alloc stage-1 state");
+    if (extra) {
+        HIP_TRY(ws.s1_mx.ensure(extra), "alloc stage-1 MFMA operands");
+        char* p = ws.s1_mx.as<char>();
+        if (s1.mfma_scan) {
+            const size_t ng = (B + 255u) / 256u;
+            s1.qfrag = (uint4*)p;
+            p += ng * 8u * 2u * code_w4(D) * 64u * 16u;
+            s1.qpc = (uint32_t*)p;
+            p += ng * 256u * 4u;
+        }
+        if (s1.sample_mode == kSampleDense) s1.smp = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+    }
     HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
     HIP_TRY(ws.buf.ensure((size_t)B * s1.bufcap * 8), "alloc candidate buffer");
     HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
     HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
-    HIP_TRY(hipMemsetAsync(ws.zero.p, 0, ((words * 4 + 15) / 16) * 16, s), "memset stage-1 state");
     uint32_t* z = ws.zero.as<uint32_t>();
+    if (fast && s1.mfma_scan && s1.sample_mode == kSampleDense) {  // k_qfrag, the first stage-1 kernel, zeroes them
+        s1.zero = z;
+        s1.nzero = (uint32_t)words;
+    } else {
+        HIP_TRY(hipMemsetAsync(ws.zero.p, 0, ((words * 4 + 15) / 16) * 16, s), "memset stage-1 state");
+    }
     s1.any_fail = z;
     s1.counts = z + 4;
     s1.fail = z + 4 + B;
@@ -511,6 +535,10 @@ gvdb_status bq_search_b1(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     hipError_t e = launch_b1_search(b, s);
     if (e != hipSuccess) {
         ws.b1_sig = 0;  // state unknown: zero it again next time
+        if (ev) {
+            std::lock_guard<std::mutex> lk(timing().mu);
+            timing().free_sets.push_back(ev);
+        }
         return dev_fail(e, "batch-1 search");
     }
     if (ev) {
@@ -540,7 +568,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
     HIP_TRY(ws.scores.ensure((size_t)B * R * 4), "alloc scores");
     Stage1Args s1{};
-    gvdb_status pst = prepare_stage1(ws, s1, B, v.D, R, v.N, s);
+    gvdb_status pst = prepare_stage1(ws, s1, B, v.D, R, v.N, s, a.dims_match && v.D > 0 && R <= kSelectLdsCap);
     if (pst != GVDB_OK) return pst;
     uint32_t* d_flags = s1.any_fail;  // [0] any stage-1 rescan, [1] NaN seen, [2] per-query NaN scratch
 
@@ -550,6 +578,14 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         timed = timing().on;
     }
     EvSet* ev = nullptr;
+    struct EvBack {  // an EvSet not submitted (error return) goes back to the pool
+        EvSet*& e;
+        ~EvBack() {
+            if (!e) return;
+            std::lock_guard<std::mutex> lk(timing().mu);
+            timing().free_sets.push_back(e);
+        }
+    } ev_back{ev};
     if (!a.dims_match || v.D == 0) {
         HIP_TRY(launch_iota_rows(ws.s1_rows.as<uint32_t>(), B, R, s), "iota");
     } else {
@@ -624,6 +660,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     if (ev) {
         HIP_TRY(hipEventRecord(ev->e[5], s), "event");
         timing_submit(ev);
+        ev = nullptr;
     }
     return GVDB_OK;
 }
@@ -670,6 +707,11 @@ struct gvdb_index {
     mutable bool rows_nonfinite = false;
     // adaptive flat tiers: batches left that skip the i8 tier after it failed
     mutable std::atomic<uint32_t> i8_skip{0};
+    // searches return before their kernels finish: each records an event on
+    // its stream after its last read of this index; a mutation waits for those
+    // events only (not for the whole device)
+    mutable std::mutex use_mu;
+    mutable std::vector<hipEvent_t> inflight, ev_free;
 
     uint32_t w4() const { return code_w4(dim); }
     size_t device_bytes() const {
@@ -702,15 +744,54 @@ gvdb_status set_device(int dev) {
 }
 
 // Mutations take the caller's exclusive lock, but searches return before
-// their kernels finish: drain the device before rows / codes / ids change
-// under an in-flight search.
+// their kernels finish: wait for the searches still reading this index (their
+// end events, index_track_use) before rows / codes / ids change under them.
 gvdb_status quiesce(const gvdb_index* ix) {
     gvdb_status st = set_device(ix->device);
     if (st != GVDB_OK) return st;
-    hipError_t e = hipDeviceSynchronize();
+    std::lock_guard<std::mutex> g(ix->use_mu);
+    hipError_t e = hipSuccess;
+    for (hipEvent_t ev : ix->inflight) {
+        const hipError_t e2 = hipEventSynchronize(ev);
+        if (e == hipSuccess) e = e2;
+        ix->ev_free.push_back(ev);
+    }
+    ix->inflight.clear();
+    if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
     if (e != hipSuccess) return dev_fail(e, "drain in-flight searches");
     return GVDB_OK;
 }
+
+// Record the end of this call's reads of ix on stream s (see quiesce).
+void track_use(const gvdb_index* ix, hipStream_t s) {
+    std::lock_guard<std::mutex> g(ix->use_mu);
+    // recycle the events of searches that have finished
+    size_t w = 0;
+    for (size_t i = 0; i < ix->inflight.size(); ++i) {
+        if (hipEventQuery(ix->inflight[i]) == hipSuccess)
+            ix->ev_free.push_back(ix->inflight[i]);
+        else
+            ix->inflight[w++] = ix->inflight[i];
+    }
+    ix->inflight.resize(w);
+    hipEvent_t ev = nullptr;
+    if (!ix->ev_free.empty()) {
+        ev = ix->ev_free.back();
+        ix->ev_free.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamSynchronize(s);  // no event: make this call synchronous instead
+        return;
+    }
+    if (hipEventRecord(ev, s) == hipSuccess)
+        ix->inflight.push_back(ev);
+    else
+        ix->ev_free.push_back(ev);
+}
+struct UseGuard {  // records the use when the entry point returns (any path)
+    const gvdb_index* ix;
+    hipStream_t s;
+    ~UseGuard() { track_use(ix, s); }
+};
 
 // Grow HBM storage to hold `need` rows (copies the live rows; planes are
 // re-strided because the SoA plane stride is the capacity).
@@ -866,6 +947,7 @@ gvdb_status gvdb_index_create(const gvdb_params* params, gvdb_index** out) {
 void gvdb_index_destroy(gvdb_index* ix) {
     if (!ix) return;
     (void)quiesce(ix);
+    for (hipEvent_t ev : ix->ev_free) (void)hipEventDestroy(ev);
     ix->free_all();
     (void)hipStreamDestroy(ix->stream);
     delete ix;
@@ -888,11 +970,12 @@ gvdb_status gvdb_index_add_device(gvdb_index* ix, const float* d_rows, uint64_t 
                                   void* stream) {
     if (!ix || (n && (!d_rows || !d_ids))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (n == 0) return GVDB_OK;
-    gvdb_status st = quiesce(ix);  // also waits for the caller's stream that produced the rows
+    gvdb_status st = quiesce(ix);
     if (st != GVDB_OK) return st;
+    // the rows / ids were produced on the caller's stream; the copies run on the index's own
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "sync the producing stream");
     if ((st = check_add_dim(ix, dim)) != GVDB_OK) return st;
     if ((st = ensure_capacity(ix, ix->n + n)) != GVDB_OK) return st;
-    (void)stream;
     HIP_TRY(hipMemcpyAsync(ix->rows + ix->n * dim, d_rows, n * dim * 4, hipMemcpyDeviceToDevice, ix->stream),
             "copy rows");
     HIP_TRY(hipMemcpyAsync(ix->ids + ix->n, d_ids, n * 8, hipMemcpyDeviceToDevice, ix->stream), "copy ids");
@@ -1285,9 +1368,11 @@ gvdb_status gvdb_index_search_filtered(const gvdb_index* ix, const float* querie
         memset(out_n, 0, B * 4);
         return GVDB_OK;
     }
+    // sp == NULL: the exact scan of the allowed rows (BQ with the default ratio
+    // would keep only R = 0.1 M candidates of a small allowed set)
     gvdb_search_params sp{};
     sp.metric = GVDB_METRIC_COSINE;
-    sp.mode = GVDB_SEARCH_BQ_RERANK;
+    sp.mode = GVDB_SEARCH_FLAT;
     sp.rescore_ratio = 0.1f;
     if (sp_in) sp = *sp_in;
     const int kind = sp.metric == GVDB_METRIC_L2 ? kScoreL2
@@ -1376,6 +1461,7 @@ gvdb_status gvdb_index_search_device(const gvdb_index* ix, const float* d_querie
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
     g.begin(s);
+    UseGuard ug{ix, s};
     return index_search_impl(ix, d_queries, B, dim, k, sp, d_out_ids, d_out_scores, d_out_n, *g.w, s);
 }
 
@@ -1392,11 +1478,12 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
     Workspace& ws = *g.w;
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream
     g.begin(s);
+    UseGuard ug{ix, s};
     const uint32_t W4 = code_w4(dim);
     const uint32_t RR = (uint32_t)R;
     HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc");
     Stage1Args s1{};
-    st = prepare_stage1(ws, s1, (uint32_t)B, dim, RR, (uint32_t)ix->n, s);
+    st = prepare_stage1(ws, s1, (uint32_t)B, dim, RR, (uint32_t)ix->n, s, RR <= kSelectLdsCap);
     if (st != GVDB_OK) return st;
     HIP_TRY(launch_pack(d_queries, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
     if (RR <= kSelectLdsCap) {
@@ -1742,6 +1829,7 @@ gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* ix, const float* d
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
     g.begin(s);
+    UseGuard ug{ix, s};
     BqSearchArgs a{};
     a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
     a.d_q = d_queries;
@@ -1916,36 +2004,65 @@ extern "C" int gvdb_debug_b1_clock(unsigned long long* out) {
     return (int)hipMemcpy(out, debug_b1_clk(), 16 * 8, hipMemcpyDeviceToHost);
 }
 
-// Sharded-search building block (gvdb_comm.hip): this shard's stage-1 top-R
-// (R clamped to its row count) with exact cosines, rows of the output at
-// stride `stride`, counts[q] = the clamped R.
-gvdb_status gvdb::shard_candidates(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
-                                   uint64_t stride, uint64_t* ids, uint32_t* dist, float* cosv, uint32_t* counts,
-                                   hipStream_t s) {
-    gvdb_status st = check_search(ix, dim, B, R);
+// Sharded-search building blocks (gvdb_shard.hip / gvdb_comm.hip).
+void gvdb::index_track_use(const gvdb_index* ix, hipStream_t s) { track_use(ix, s); }
+
+gvdb::ShardInfo gvdb::index_shard_info(const gvdb_index* ix) {
+    ShardInfo si{};
+    si.rows = ix->rows;
+    si.norms = ix->norms;
+    si.ids = ix->ids;
+    si.n = ix->n;
+    si.dim = ix->dim;
+    si.device = ix->device;
+    return si;
+}
+
+// This shard's exact stage-1 top-min(R, rows) by (Hamming asc, row asc) as
+// sorted keys (d << 32 | row) into keys[q*R + i] (the exchange-1 block of the
+// two-exchange sharded search).  An empty shard writes nothing (the caller
+// sends count 0).  R <= kSelectLdsCap.
+gvdb_status gvdb::shard_stage1_keys(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
+                                    uint64_t* keys, hipStream_t s) {
+    if (!ix) return fail(GVDB_ERR_INVALID_ARGUMENT, "null index");
+    if (ix->n == 0 || B == 0 || R == 0) return GVDB_OK;
+    if (dim != ix->dim) return dim_mismatch(ix->dim, dim);
+    if (ix->n > 0xFFFFFFFFull) return fail(GVDB_ERR_INDEX, "shard exceeds 2^32 rows");
+    const uint32_t Rl = (uint32_t)std::min<uint64_t>(R, ix->n);
+    if (Rl > kSelectLdsCap) return fail(GVDB_ERR_INVALID_ARGUMENT, "sharded search: R exceeds 8192");
+    gvdb_status st = set_device(ix->device);
     if (st != GVDB_OK) return st;
-    const uint64_t Rl = std::min<uint64_t>(R, ix->n);
-    if (B == 0) return GVDB_OK;
-    HIP_TRY(hipMemsetD32Async(counts, (int)Rl, B, s), "candidate counts");
-    if (Rl == 0) return GVDB_OK;
-    if ((st = set_device(ix->device)) != GVDB_OK) return st;
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
     g.begin(s);
-    BqSearchArgs a{};
-    a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
-    a.d_q = d_q;
-    a.qlen = dim;
-    a.B = (uint32_t)B;
-    a.thr = ix->thr;
-    a.dims_match = true;
-    a.R = (uint32_t)Rl;
-    a.kout = (uint32_t)Rl;
-    a.kind = kScoreCosine;
-    a.descending = 1;
-    a.d_out_ids = ids;
-    a.d_out_scores = cosv;
-    a.d_out_dist = dist;
-    a.out_stride = stride;
-    return bq_search(a, *g.w, s);
+    UseGuard ug{ix, s};
+    const uint32_t W4 = code_w4(dim);
+    HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc qcodes");
+    Stage1Args s1{};
+    st = prepare_stage1(ws, s1, (uint32_t)B, dim, Rl, (uint32_t)ix->n, s, true);
+    if (st != GVDB_OK) return st;
+    HIP_TRY(launch_pack(d_q, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
+    bool timed = false;
+    {
+        std::lock_guard<std::mutex> lk(timing().mu);
+        timed = timing().on;
+    }
+    EvSet* ev = timed ? timing_events() : nullptr;
+    s1.codes = ix->codes;
+    s1.cap = ix->cap;
+    s1.qcodes = ws.qcodes.as<uint4>();
+    s1.keys_out = keys;
+    s1.ev = ev ? ev->e : nullptr;
+    hipError_t e = launch_stage1_fast(s1, s);
+    if (e == hipSuccess && ev) {
+        // stage-2 slot of the timing: zero here (the sharded rerank is timed by the caller)
+        (void)hipEventRecord(ev->e[5], s);
+        timing_submit(ev);
+    } else if (ev) {
+        std::lock_guard<std::mutex> lk(timing().mu);
+        timing().free_sets.push_back(ev);
+    }
+    if (e != hipSuccess) return dev_fail(e, "sharded stage 1");
+    return GVDB_OK;
 }

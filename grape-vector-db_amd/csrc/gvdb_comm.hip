@@ -2,25 +2,24 @@
 //
 // Replaces ShardManager::search_vectors (src/distributed/shard.rs:760-786:
 // fan out to every shard, concat, sort by score, truncate) inside one node:
-// one process per GPU, each holding a contiguous row range of the corpus
-// whose ids are global row numbers.  One exchange per batch:
+// one process per GPU, each holding a contiguous row range of the corpus.
+// gvdb_index_search_sharded_device composes the two-exchange protocol of
+// gvdb_shard.hip with two ncclAllGather calls on the caller's stream:
 //
-//   rank g:  stage-1 local top-R + exact cosines (gvdb::shard_candidates)
-//            written straight into its send block
-//              [ids u64 B*R | dist u32 B*R | cos f32 B*R | counts u32 B | pad]
-//   all:     ncclAllGather of the blocks on the caller's stream (xGMI)
-//   all:     k_bq_shard_merge over the gathered blocks in place
+//   BQ:    local stage-1 keys -> AllGather -> global top-R merge + rerank of
+//          the owned rows + local top-k -> AllGather -> final merge
+//   FLAT:  local exact top-k -> AllGather -> merge
 //
-// The union of the local top-R lists holds the global top-R by
-// (Hamming, id), so the merge reproduces multi_stage_search over the whole
-// corpus bit for bit.  RCCL is dlopen'ed on first use so that a host that
-// never shards does not need it (and a process that already loaded
-// librccl.so.1, e.g. PyTorch, shares that copy).
+// Results are bit-identical to one search over the concatenated corpus.  RCCL
+// is dlopen'ed on first use so that a host that never shards does not need it
+// (and a process that already loaded librccl.so.1, e.g. PyTorch, shares that
+// copy).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -75,8 +74,13 @@ struct gvdb_comm {
     ncclComm_t comm = nullptr;
     int32_t world = 1, rank = 0, device = 0;
     std::mutex mu;                // one search at a time per communicator
-    uint32_t* buf = nullptr;      // [send block][world recv blocks]
-    size_t buf_words = 0;
+    void* buf = nullptr;          // exchange blocks + scratch (see search_sharded)
+    size_t buf_bytes = 0;
+    // the buffer is reused by the next call, possibly on another stream: the
+    // next call's stream waits for `done` (recorded after the final merge)
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+    bool pending = false;
 };
 
 extern "C" {
@@ -123,6 +127,7 @@ void gvdb_comm_destroy(gvdb_comm* c) {
     (void)hipDeviceSynchronize();
     if (c->comm) (void)rccl().comm_destroy(c->comm);
     if (c->buf) (void)hipFree(c->buf);
+    if (c->done) (void)hipEventDestroy(c->done);
     delete c;
 }
 
@@ -137,53 +142,91 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
                                              uint32_t dim, uint64_t k, const gvdb_search_params* sp,
                                              uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
                                              void* stream) {
+    // argument checks that are the same on every rank come first: a rank that
+    // returns here returns on every rank, so no collective is left waiting
     if (!shard || !c || !sp) return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (B == 0 || k == 0) return GVDB_OK;
     if (!d_q || !d_out_ids || !d_out_scores) return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
-    if (sp->mode != GVDB_SEARCH_BQ_RERANK || sp->metric != GVDB_METRIC_COSINE)
-        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: BQ + cosine rerank only");
-    if (sp->rescore_count == 0)
+    const bool flat = sp->mode == GVDB_SEARCH_FLAT;
+    if (!flat && (sp->mode != GVDB_SEARCH_BQ_RERANK || sp->metric != GVDB_METRIC_COSINE))
+        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: BQ + cosine rerank, or FLAT");
+    if (!flat && sp->rescore_count == 0)
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search needs rescore_count (global R)");
     if (index_device(shard) != c->device)
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "shard and communicator on different devices");
-    const uint64_t R = sp->rescore_count > k ? sp->rescore_count : k;
-    if ((uint64_t)c->world * R > kSortLdsCap || B > 0xFFFFFFFFull)
-        return report_status(GVDB_ERR_INVALID_ARGUMENT, "world * R exceeds the 4096-entry merge");
+    const uint64_t G = (uint64_t)c->world;
+    const uint64_t R = flat ? k : std::max<uint64_t>(sp->rescore_count, k);
+    if (R > kSelectLdsCap || G * k > kSelectLdsCap || B > 0xFFFFFFFFull || dim > 8192)
+        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: R <= 8192, world * k <= 8192, dim <= 8192");
     std::lock_guard<std::mutex> g(c->mu);
     hipError_t he = hipSetDevice(c->device);
     if (he != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(he));
     hipStream_t s = (hipStream_t)stream;
-    const uint64_t BR = B * R;
-    const uint64_t blk = (4 * BR + B + 1) & ~1ull;  // words per rank block, even (u64 ids stay aligned)
-    const size_t need = blk * (size_t)(c->world + 1);
-    if (need > c->buf_words) {
+    uint64_t w1 = 0, w2 = 0, scratch = 0;
+    gvdb_shard_sizes(B, R, k, &w1, &w2, &scratch);
+    const uint64_t wf = shard_words_flat(B, k);
+    // layout: send1 | recv1 [G] | send2 | recv2 [G] | scratch   (FLAT: sendF | recvF [G])
+    const size_t need = flat ? wf * 4 * (G + 1) : ((w1 + w2) * (G + 1)) * 4 + scratch;
+    if (c->pending && c->last != s) (void)hipStreamWaitEvent(s, c->done, 0);
+    if (need > c->buf_bytes) {
         if (c->buf) {
-            (void)hipStreamSynchronize(s);
+            (void)hipDeviceSynchronize();  // every earlier call's use of the old buffer
             (void)hipFree(c->buf);
         }
         c->buf = nullptr;
-        c->buf_words = 0;
-        he = hipMalloc((void**)&c->buf, need * 4);
+        c->buf_bytes = 0;
+        he = hipMalloc(&c->buf, need);
         if (he != hipSuccess)
             return report_status(he == hipErrorOutOfMemory ? GVDB_ERR_OUT_OF_MEMORY : GVDB_ERR_DEVICE,
                                  std::string("sharded search buffers: ") + hipGetErrorString(he));
-        c->buf_words = need;
+        c->buf_bytes = need;
     }
-    uint32_t* send = c->buf;
-    uint32_t* recv = c->world > 1 ? c->buf + blk : send;
-    gvdb_status st = shard_candidates(shard, d_q, B, dim, R, R, reinterpret_cast<uint64_t*>(send), send + 2 * BR,
-                                      reinterpret_cast<float*>(send + 3 * BR), send + 4 * BR, s);
-    if (st != GVDB_OK) return st;
-    if (c->world > 1) {
-        ncclResult_t e = rccl().all_gather(send, recv, blk, ncclUint32, c->comm, s);
-        if (e != ncclSuccess) return rccl_fail(e, "ncclAllGather");
+    auto all_gather = [&](const uint32_t* send, uint32_t* recv, uint64_t words) -> gvdb_status {
+        if (G == 1) return GVDB_OK;
+        ncclResult_t e = rccl().all_gather(send, recv, words, ncclUint32, c->comm, s);
+        return e == ncclSuccess ? GVDB_OK : rccl_fail(e, "ncclAllGather");
+    };
+    gvdb_status local = GVDB_OK, st = GVDB_OK;
+    uint32_t* base = (uint32_t*)c->buf;
+    if (flat) {
+        uint32_t* send = base;
+        uint32_t* recv = G > 1 ? base + wf : send;
+        const uint64_t BK = B * k;
+        // the rank's exact top-k (certified MFMA tiers / exact scan, storage.rs:296-339)
+        local = gvdb_index_search_device(shard, d_q, B, dim, k, sp, reinterpret_cast<uint64_t*>(send),
+                                         reinterpret_cast<float*>(send + 2 * BK), send + 3 * BK, stream);
+        if (local == GVDB_ERR_INDEX_NOT_BUILT) local = GVDB_OK;  // an empty shard contributes nothing
+        const bool ok = local == GVDB_OK && gvdb_index_len(shard) > 0;
+        if (!ok) (void)hipMemsetD32Async(send + 3 * BK, 0, B, s);
+        (void)hipMemsetD32Async(send + 3 * BK + B, local == GVDB_OK ? 0 : 1, 1, s);
+        if ((st = all_gather(send, recv, wf)) != GVDB_OK) return st;
+        if ((st = gvdb_shard_flat_final_device(recv, G, B, k, sp->metric, d_out_ids, d_out_scores, d_out_n, stream)) !=
+            GVDB_OK)
+            return st;
+    } else {
+        uint32_t* send1 = base;
+        uint32_t* recv1 = G > 1 ? send1 + w1 : send1;
+        uint32_t* send2 = base + w1 * (G + 1);
+        uint32_t* recv2 = G > 1 ? send2 + w2 : send2;
+        void* scr = base + (w1 + w2) * (G + 1);
+        // 1. local stage 1 (an empty or failing shard still joins with no entries)
+        local = gvdb_shard_stage1_device(shard, d_q, B, dim, R, send1, stream);
+        const std::string local_err = local != GVDB_OK ? std::string(gvdb_last_error()) : std::string();
+        if ((st = all_gather(send1, recv1, w1)) != GVDB_OK) return st;
+        // 2. global top-R, rerank of the owned rows, local top-k
+        st = gvdb_shard_rerank_device(shard, d_q, B, dim, R, k, recv1, G, (uint64_t)c->rank, scr, send2, stream);
+        if (st != GVDB_OK) return st;
+        if (local != GVDB_OK) (void)hipMemsetD32Async(send2 + 4 * B * k + 2 * B, 1, 1, s);  // poison the merge
+        if ((st = all_gather(send2, recv2, w2)) != GVDB_OK) return st;
+        // 3. the merged top-k on every rank
+        if ((st = gvdb_shard_final_device(recv2, G, B, k, d_out_ids, d_out_scores, d_out_n, stream)) != GVDB_OK)
+            return st;
+        if (local != GVDB_OK) report_status(local, local_err);
     }
-    he = launch_bq_shard_merge(reinterpret_cast<const uint64_t*>(recv), recv + 2 * BR,
-                               reinterpret_cast<const float*>(recv + 3 * BR), recv + 4 * BR, (uint32_t)c->world,
-                               (uint32_t)B, (uint32_t)R, (uint32_t)R, (uint32_t)k, d_out_ids, d_out_scores, d_out_n,
-                               nullptr, s, blk / 2, blk, blk, 1);
-    if (he != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard merge: ") + hipGetErrorString(he));
-    return GVDB_OK;
+    if (!c->done) (void)hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+    c->pending = c->done && hipEventRecord(c->done, s) == hipSuccess;
+    c->last = s;
+    return local;
 }
 
 }  // extern "C"

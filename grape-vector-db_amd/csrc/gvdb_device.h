@@ -39,10 +39,52 @@ __device__ inline void bitonic_sort_lds(uint64_t* s, uint32_t P) {
     }
 }
 
-__device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
+__host__ __device__ __forceinline__ uint32_t next_pow2(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;
     return p;
+}
+
+// Smallest t in [0, nb) with sum(h[0..t]) >= target (nb-1 if never), by one
+// full wave: each lane sums a contiguous segment, a shuffle scan finds the
+// segment that crosses the target, that lane walks its segment.
+__device__ inline uint32_t wave_find_cum(const uint32_t* h, uint32_t nb, uint32_t target) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t seg = (nb + 63u) / 64u;
+    const uint32_t b0 = lane * seg;
+    const uint32_t b1 = min(b0 + seg, nb);
+    uint32_t s = 0;
+    for (uint32_t i = b0; i < b1; ++i) s += h[i];
+    uint32_t incl = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off);
+        if ((int)lane >= off) incl += v;
+    }
+    const uint64_t m = __ballot(incl >= target);
+    if (m == 0) return nb - 1;
+    const uint32_t first = __ffsll((long long)m) - 1;
+    uint32_t t = nb - 1;
+    if (lane == first) {
+        uint32_t cum = incl - s;
+        for (uint32_t i = b0; i < b1; ++i) {
+            cum += h[i];
+            if (cum >= target) {
+                t = i;
+                break;
+            }
+        }
+    }
+    return __shfl(t, first);
+}
+
+// Sum of h[0..t) by one full wave.
+__device__ inline uint32_t wave_sum_below(const uint32_t* h, uint32_t t) {
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x & 63u; i < t; i += 64) s += h[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    return s;
 }
 
 }  // namespace gvdb

@@ -81,8 +81,23 @@ struct Stage1Args {
     int use_mfma;            // large batches: 0 popcount only, 1 FP4 MFMA scan, 2 i8 MFMA scan
     int dbg;                 // ablation switches for timing studies (GVDB_SCAN_DBG); 0 in production
     int force_rescan;        // tests: every query takes k_select's exact all-rows rescan (GVDB_FORCE_RESCAN)
+    // FP4-MFMA paths (stage1_plan): query fragments built once per batch by k_qfrag
+    int sample_mode;         // kSampleValu / kSampleMxHist / kSampleDense
+    bool mfma_scan;          // k_scan_mx5 runs (needs qfrag / qpc)
+    uint4* qfrag;            // [ceil(B/256)][8 * 2*W4 * 64] FP4 query fragments
+    uint32_t* qpc;           // [ceil(B/256) * 256] |q|
+    uint16_t* smp;           // kSampleDense: [B][sample rows] sampled distances
+    uint64_t* keys_out;      // optional [B][R]: the sorted top-R keys (d << 32 | row) (sharded search),
+                             // followed by u32 counts [B] (= R)
+    uint32_t* zero;          // mfma_scan: words k_qfrag zeroes before stage 1 (else the caller memsets)
+    uint32_t nzero;
 };
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
+enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
+// Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
+// sample_chunks, target set) and return the workspace bytes of qfrag + qpc +
+// smp it needs (0 = none).
+size_t stage1_plan(Stage1Args& a);
 // code widths with an MFMA scan instantiation (D <= 768; wider codes would
 // not fit the query fragments + prefetch in 256 VGPRs at 2 waves/SIMD)
 __host__ __device__ inline bool mfma_scan_supported(uint32_t W4) { return W4 == 2 || W4 == 3 || W4 == 4 || W4 == 6; }
@@ -293,13 +308,49 @@ hipError_t launch_gather(const float* rows, float* nrows, const uint4* codes, ui
                          float* nnorms, const uint64_t* ids, uint64_t* nids, const uint64_t* map, uint64_t m,
                          uint64_t cap, uint32_t D, hipStream_t s);
 
-// ---- sharded search (gvdb_comm.hip) ----------------------------------------------
+// ---- sharded search (gvdb_shard.hip, gvdb_comm.hip) -------------------------------
 int index_device(const gvdb_index* ix);
-// this shard's stage-1 top-min(R, rows) + exact cosines, output rows at `stride`,
-// counts[q] = min(R, rows) (gvdb_capi.hip)
-gvdb_status shard_candidates(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
-                             uint64_t stride, uint64_t* ids, uint32_t* dist, float* cosv, uint32_t* counts,
-                             hipStream_t s);
+struct ShardInfo {
+    const float* rows;
+    const float* norms;
+    const uint64_t* ids;
+    uint64_t n;
+    uint32_t dim;
+    int device;
+};
+ShardInfo index_shard_info(const gvdb_index* ix);
+// a _device call read ix on stream s (mutations wait for it; gvdb_capi.hip)
+void index_track_use(const gvdb_index* ix, hipStream_t s);
+// this shard's exact stage-1 top-min(R, rows) as sorted keys (d << 32 | row) at
+// keys[q*R + i] (gvdb_capi.hip); nothing for an empty shard
+gvdb_status shard_stage1_keys(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
+                              uint64_t* keys, hipStream_t s);
+// Two-exchange block layouts (u32 words; even, so u64 fields stay aligned):
+//   block 1 (rank -> all): keys u64 [B][R] | counts u32 [B] | err u32 | pad
+//   block 2 (rank -> all): entries [B][k] x {cos bits, global stage-1 position,
+//                          id lo, id hi} | meta u32 [B] (count | nan << 31) |
+//                          reff u32 [B] | err u32 | pad
+inline uint64_t shard_words1(uint64_t B, uint64_t R) { return (2 * B * R + B + 1 + 1) & ~1ull; }
+inline uint64_t shard_words2(uint64_t B, uint64_t k) { return (4 * B * k + 2 * B + 1 + 1) & ~1ull; }
+// merge of the gathered exchange-1 blocks -> this rank's owned entries of the
+// global top-R: own_rows / own_pos [B][R], own_cnt [B], reff [B] (= min(R, total))
+hipError_t launch_shard_merge(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
+                              uint32_t R, uint32_t D, uint32_t* own_rows, uint32_t* own_pos, uint32_t* own_cnt,
+                              uint32_t* reff, hipStream_t s);
+// owned entries' exact cosines -> this rank's exchange-2 block (local top-k by
+// (cos desc, position asc))
+hipError_t launch_shard_local_topk(const float* scores, const uint32_t* own_rows, const uint32_t* own_pos,
+                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t R, uint32_t k,
+                                   const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s);
+// sharded FLAT: gathered blocks of the ranks' exact top-k -> merged top-k
+//   block F (sharded FLAT): ids u64 [B][k] | scores f32 [B][k] | counts [B] | err | pad
+inline uint64_t shard_words_flat(uint64_t B, uint64_t k) { return (3 * B * k + B + 1 + 1) & ~1ull; }
+hipError_t launch_shard_flat_final(const uint32_t* gathered, uint64_t words, uint32_t G, uint32_t B, uint32_t k,
+                                   int descending, uint64_t* out_ids, float* out_scores, uint32_t* out_n,
+                                   hipStream_t s);
+// gathered exchange-2 blocks -> top-k on every rank
+hipError_t launch_shard_final(const uint32_t* gathered2, uint64_t words2, uint32_t G, uint32_t B, uint32_t k,
+                              uint64_t* out_ids, float* out_scores, uint32_t* out_n, hipStream_t s);
 
 // ---- error reporting shared by the C-ABI translation units ---------------------
 // sets the thread-local gvdb_last_error() text and returns s

@@ -323,39 +323,6 @@ __global__ __launch_bounds__(256) void k_sample_hist(const uint4* __restrict__ c
     }
 }
 
-// Smallest t in [0, nb) with sum(h[0..t]) >= target (nb-1 if never), by one
-// full wave: each lane sums a contiguous segment, a shuffle scan finds the
-// segment that crosses the target, that lane walks its segment.
-__device__ uint32_t wave_find_cum(const uint32_t* h, uint32_t nb, uint32_t target) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t seg = (nb + 63u) / 64u;
-    const uint32_t b0 = lane * seg;
-    const uint32_t b1 = min(b0 + seg, nb);
-    uint32_t s = 0;
-    for (uint32_t i = b0; i < b1; ++i) s += h[i];
-    uint32_t incl = s;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t v = __shfl_up(incl, off);
-        if ((int)lane >= off) incl += v;
-    }
-    const uint64_t m = __ballot(incl >= target);
-    if (m == 0) return nb - 1;
-    const uint32_t first = __ffsll((long long)m) - 1;
-    uint32_t t = nb - 1;
-    if (lane == first) {
-        uint32_t cum = incl - s;
-        for (uint32_t i = b0; i < b1; ++i) {
-            cum += h[i];
-            if (cum >= target) {
-                t = i;
-                break;
-            }
-        }
-    }
-    return __shfl(t, first);
-}
-
 // T[q] = smallest t with (sample count of d <= t) >= target; D if never.
 // One wave per query.
 __global__ __launch_bounds__(256) void k_threshold(const uint32_t* __restrict__ hist, uint32_t B, uint32_t D,
@@ -492,15 +459,6 @@ __device__ __forceinline__ uint32_t block_prefix_flag(bool f, uint32_t* wcnt, ui
     __syncthreads();  // wcnt is rewritten by the next call
     *total = tot;
     return pre;
-}
-
-// Sum of h[0..t) by one full wave.
-__device__ uint32_t wave_sum_below(const uint32_t* h, uint32_t t) {
-    uint32_t s = 0;
-    for (uint32_t i = threadIdx.x & 63u; i < t; i += 64) s += h[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    return s;
 }
 
 __device__ __forceinline__ uint32_t code_dist(const uint4* __restrict__ codes, uint64_t cap, uint32_t W4,
@@ -724,7 +682,7 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
                                                 uint32_t W4, const uint4* __restrict__ qcodes,
                                                 uint32_t* __restrict__ fail, uint32_t* __restrict__ any_fail,
                                                 uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist,
-                                                int force_rescan) {
+                                                int force_rescan, uint64_t* __restrict__ keys_out) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist, then radix bins
     uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
     uint32_t* bins = hist + ((D + 4u) & ~3u);
@@ -739,7 +697,10 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
         const uint64_t key = sk[i];
         s1_rows[(uint64_t)q * R + i] = (uint32_t)key;
         s1_dist[(uint64_t)q * R + i] = (uint32_t)(key >> 32);
+        if (keys_out) keys_out[(uint64_t)q * R + i] = key;  // sharded search: the exchange-1 block
     }
+    // ... whose per-query counts follow the B x R keys
+    if (keys_out && threadIdx.x == 0) ((uint32_t*)(keys_out + (uint64_t)gridDim.x * R))[q] = R;
 }
 
 // ----------------------------------------------------------------------------
@@ -1688,9 +1649,38 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
     asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
 }
+// Query operands of the FP4-MFMA stage-1 kernels (k_sample_dense, k_scan_mx5),
+// expanded ONCE per batch instead of once per block: for query group g (256
+// queries), qfrag[g][(s*8 + qt)*64 + l] = fp4_query_pm(word 4(s/2) + 2(l/32) +
+// (s&1) of query 256g + 32qt + (l&31)), zero words past B; qpc[256g + j] = |q|.
+// The kernels' prologue is then a straight 16-B copy of the group's fragments
+// (L2-resident, 96 KiB at D = 768) into LDS.
+template <int W4>
+__global__ __launch_bounds__(256) void k_qfrag(const uint32_t* __restrict__ qwords, uint32_t B, uint32_t ngroups,
+                                               v4i_t* __restrict__ qfrag, uint32_t* __restrict__ qpc,
+                                               uint32_t* __restrict__ zero, uint32_t nzero) {
+    constexpr int KW = 4 * W4, KS = KW / 2, QT = 8;
+    constexpr uint32_t kPer = QT * KS * 64;
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < nzero) zero[i] = 0u;  // the stage-1 flags / counts (instead of a memset launch)
+    if (i < ngroups * kPer) {
+        const uint32_t g = i / kPer, f = i % kPer, l = f & 63u, st = f >> 6, qt = st % QT, qs = st / QT;
+        const uint32_t q = g * 256u + qt * 32u + (l & 31u);
+        const uint32_t wi = 4u * (qs >> 1) + 2u * (l >> 5) + (qs & 1u);
+        qfrag[i] = fp4_query_pm(q < B ? qwords[(uint64_t)q * KW + wi] : 0u);
+    }
+    if (i < ngroups * 256u) {
+        uint32_t pc = 0;
+        if (i < B)
+            for (int w = 0; w < KW; ++w) pc += __popc(qwords[(uint64_t)i * KW + w]);
+        qpc[i] = pc;
+    }
+}
+
 template <int W4>
 __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
-                                                           const uint32_t* __restrict__ qwords,
+                                                           const v4i_t* __restrict__ qfrag_g,
+                                                           const uint32_t* __restrict__ qpc,
                                                            const uint32_t* __restrict__ thr, uint32_t B,
                                                            uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
                                                            uint32_t bufcap) {
@@ -1716,24 +1706,17 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
 #elif MX5_PRIO == 2
     if (wv < NW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-    // query fragments: (tile qt, k-step s, lane l) = query qt*32 + (l & 31), word 4(s/2) + 2(l/32) + (s&1)
-    // k-step-major (s, qt, lane): MFMA m = s*QT + qt reads fragment m, so the A
-    // reads of the loop need one base register per 64 KiB (tile-major needed one
-    // per read above 64 KiB: ~20 VGPRs of addresses)
-    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx5Threads) {
-        const uint32_t l = i & 63u, st = i >> 6, qt = st % QT, qs = st / QT;
-        const uint32_t q = qt * 32u + (l & 31u);
-        const uint32_t wi = 4u * (qs >> 1) + 2u * (l >> 5) + (qs & 1u);
-        qfrag[i] = fp4_query_pm(q < B ? qwords[(uint64_t)q * KW + wi] : 0u);
-    }
+    // query fragments (k_qfrag): k-step-major (s, qt, lane), so MFMA m = s*QT + qt
+    // reads fragment m and the A reads of the loop need one base register per
+    // 64 KiB (tile-major needed one per read above 64 KiB: ~20 VGPRs of addresses)
+#pragma unroll 4
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx5Threads) qfrag[i] = qfrag_g[i];
     // thr is clamped to the padded width (every Hamming distance is <= it, so
     // the hit set is unchanged) to keep thr - |q| exact in f32
     constexpr uint32_t kPadBits = 32u * KW;
     if (tid < QT * 32) {
         const uint32_t q = tid;
-        uint32_t pc = 0;
-        if (q < B)
-            for (int w = 0; w < KW; ++w) pc += __popc(qwords[(uint64_t)q * KW + w]);
+        const uint32_t pc = qpc[q];
         const float tc = q < B ? (float)min(thr[q], kPadBits) : 0.0f;
         thrc_lds[q] = tc;
         // query q sits in tile q/32, lane half ((q&31)>>2)&1, row r = (q&3) + 4*((q&31)>>3)
@@ -1897,18 +1880,39 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
                                       buf, bufcap);
 }
 
+// CUs of the current device (cached per device: read on every launch)
+static uint32_t cu_count() {
+    static int cached[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (!cached[dev]) {
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        cached[dev] = cus > 0 ? cus : 256;
+    }
+    return (uint32_t)cached[dev];
+}
+
+template <int W4>
+static void launch_qfrag_t(const Stage1Args& a, hipStream_t s) {
+    constexpr uint32_t kPer = 8u * (2u * W4) * 64u;
+    const uint32_t ng = (a.B + 255u) / 256u;
+    const uint32_t n = std::max<uint32_t>(ng * kPer, a.nzero);
+    hipLaunchKernelGGL((k_qfrag<W4>), dim3((n + 255u) / 256u), dim3(256), 0, s, (const uint32_t*)a.qcodes, a.B, ng,
+                       (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero);
+}
+
 template <int W4>
 static void launch_scan_mx5_t(const Stage1Args& a, hipStream_t s) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint32_t nsub = (a.N + 31u) / 32u;
     const uint32_t wpb = kMx5Threads / 64;
-    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus, (nsub + wpb - 1) / wpb));
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(cu_count(), (nsub + wpb - 1) / wpb));
+    constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
     for (uint32_t g = 0; g < a.B; g += 256) {
         const uint32_t bg = min(256u, a.B - g);
         hipLaunchKernelGGL((k_scan_mx5<W4>), dim3(grid), dim3(kMx5Threads), 0, s, a.codes, a.cap, a.N,
-                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
+                           (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
                            a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
 }
@@ -2316,6 +2320,236 @@ static void launch_sample_mx_t(const Stage1Args& a, hipStream_t s) {
                        a.sample_stride, nsub, (const uint32_t*)a.qcodes, a.B, a.target, a.hist);
 }
 
+// k_sample_dense + k_sample_select: the stage-1 threshold estimate of a large
+// batch without histogram atomics.  k_sample_mx spends most of its time in
+// the per-pair LDS-atomic histogram epilogue (~1 atomic per 2 pairs on i.i.d.
+// codes); here the FP4 MFMA (k_scan_mx5's operands, accumulators seeded with
+// -|q|, so acc = -Hamming) writes every sampled distance as a u16 into a dense
+// [B][S] block, and one block per query then finds the target-th smallest
+// distance: a min pass, then histograms of narrow windows above the min (only
+// the low tail does LDS atomics; the window doubles while the target is not
+// reached).  T[q] = smallest t with count(d <= t) >= target over the same
+// sample rows as k_sample_hist, so the thresholds equal the VALU form's.
+template <int W4>
+__global__ __launch_bounds__(kMx5Threads, 1) void k_sample_dense(const uint4* __restrict__ codes, uint64_t cap,
+                                                               uint32_t N, uint32_t stride, uint32_t nsub,
+                                                               const v4i_t* __restrict__ qfrag_g,
+                                                               const uint32_t* __restrict__ qpc, uint32_t B,
+                                                               uint16_t* __restrict__ dsm, uint32_t S) {
+    constexpr int KW = 4 * W4;
+    constexpr int KS = KW / 2;
+    constexpr int QT = 8;
+    constexpr int NW = kMx5Threads / 64;
+    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
+    __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t h = lane >> 5;
+#pragma unroll 4
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx5Threads) qfrag[i] = qfrag_g[i];
+    if (tid < QT * 32) {
+        const uint32_t q = tid;
+        const uint32_t qt = q >> 5, j = q & 31u, hh = (j >> 2) & 1u, r = (j & 3u) + 4u * (j >> 3);
+        seed_lds[(qt * 2 + hh) * 16 + r] = q < B ? -(float)qpc[q] : -1.0e6f;
+    }
+    __syncthreads();
+    const uint32_t nqt = (B + 31u) / 32u;
+    const uint32_t W = gridDim.x * NW;
+    const int scale1 = 0x7f7f7f7f;
+    v16f_t acc[QT];
+    for (uint32_t sb = blockIdx.x * NW + wv; sb < nsub; sb += W) {
+        // sample sub-tile sb: chunk (32 sb) / 4096 at `stride` rows, 32 consecutive rows
+        const uint32_t s0 = sb * 32u;
+        const uint32_t n = (s0 >> 12) * stride + (s0 & 4095u) + (lane & 31u);
+        const uint32_t nc = min(n, N - 1u);
+        uint2 c[W4];
+#pragma unroll
+        for (int p = 0; p < W4; ++p) c[p] = ((const uint2*)(codes + (uint64_t)p * cap + nc))[h];
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+            const float4* sp = (const float4*)(seed_lds + (t * 2 + h) * 16);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 v = sp[g];
+                acc[t][4 * g + 0] = v.x;
+                acc[t][4 * g + 1] = v.y;
+                acc[t][4 * g + 2] = v.z;
+                acc[t][4 * g + 3] = v.w;
+            }
+        }
+        const v4i_t* qf = qfrag + lane;
+        constexpr int PF = 8;  // A-fragment LDS ring depth (in MFMAs)
+        v4i_t ar[PF];
+#pragma unroll
+        for (int m = 0; m < PF; ++m) ar[m] = qf[m * 64];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const uint2 v = c[s >> 1];
+            const v4i_t b = fp4_row01((s & 1) ? v.y : v.x);
+#pragma unroll
+            for (int t = 0; t < QT; ++t) {
+                const int m = s * QT + t;
+                const v4i_t a = ar[m % PF];
+                if (m + PF < KS * QT) ar[m % PF] = qf[(m + PF) * 64];
+                if (t == 0)
+                    mfma_fp4_acc_nop(acc[t], a, b, scale1);
+                else
+                    mfma_fp4_acc(acc[t], a, b, scale1);
+            }
+        }
+        mfma_fp4_drain_acc(acc);
+        // lane (h, j) holds row s0 + j of queries qt*32 + 8(r/4) + 4h + (r%4):
+        // per register, 32 lanes write one query's 64 contiguous bytes.  Rows
+        // past N (the last chunk of an unsampled small shard) read as 0xffff.
+        const float lim = n < N ? 65535.0f : -1.0f;
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+            if (t < (int)nqt) {
+                // opaque per sub-tile: otherwise the 128 per-(tile, r) row
+                // addresses are hoisted out of the loop and spill
+                uint32_t qb = t * 32u + 4u * h;
+                asm volatile("" : "+v"(qb));
+                uint16_t* dq = dsm + (uint64_t)qb * S + s0 + (lane & 31u);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t qo = 8u * (r >> 2) + (r & 3);
+                    const float dv = -acc[t][r];
+                    if (qb + qo < B) dq[(uint64_t)qo * S] = lim < 0.0f ? (uint16_t)0xffffu : (uint16_t)min(dv, lim);
+                }
+            }
+        }
+    }
+}
+
+// One block per query over its S dense sample distances (S % 8 == 0): the
+// query's values are loaded once into registers (kSsPer uint4 = 8 u16 each per
+// thread, all loads in flight together), then a min pass and windowed
+// histograms run on the registers.  Larger samples stream from memory.
+constexpr int kSsThreads = 512;
+constexpr int kSsPer = 40;  // uint4 per thread: S <= 512 * 40 * 8 = 163840 in registers
+__device__ __forceinline__ void ss_count(uint32_t w, uint32_t base, uint32_t win, uint32_t* hist) {
+    const uint32_t o0 = (w & 0xffffu) - base, o1 = (w >> 16) - base;  // wrap below base: outside
+    if (o0 < win) atomicAdd(&hist[o0], 1u);
+    if (o1 < win) atomicAdd(&hist[o1], 1u);
+}
+__global__ __launch_bounds__(kSsThreads) void k_sample_select(const uint16_t* __restrict__ dsm, uint32_t S, uint32_t D,
+                                                              uint32_t target, uint32_t* __restrict__ thr) {
+    constexpr uint32_t kMaxWin = 1024;
+    __shared__ uint32_t hist[kMaxWin];
+    __shared__ uint32_t red[kSsThreads / 64];
+    __shared__ uint32_t s_T, s_cum;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
+    const uint4* v = (const uint4*)(dsm + (uint64_t)q * S);
+    const uint32_t nv = S / 8u;
+    const bool inreg = nv <= (uint32_t)kSsThreads * kSsPer;
+    uint4 x[kSsPer];
+    uint32_t mn = 0xffffu;
+    if (inreg) {
+#pragma unroll
+        for (int j = 0; j < kSsPer; ++j) {
+            const uint32_t i = tid + (uint32_t)j * kSsThreads;
+            x[j] = i < nv ? v[i] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+#pragma unroll
+        for (int j = 0; j < kSsPer; ++j) {
+            const uint32_t a = min(min(x[j].x & 0xffffu, x[j].x >> 16), min(x[j].y & 0xffffu, x[j].y >> 16));
+            const uint32_t b = min(min(x[j].z & 0xffffu, x[j].z >> 16), min(x[j].w & 0xffffu, x[j].w >> 16));
+            mn = min(mn, min(a, b));
+        }
+    } else {
+        for (uint32_t i = tid; i < nv; i += kSsThreads) {
+            const uint4 y = v[i];
+            const uint32_t a = min(min(y.x & 0xffffu, y.x >> 16), min(y.y & 0xffffu, y.y >> 16));
+            const uint32_t b = min(min(y.z & 0xffffu, y.z >> 16), min(y.w & 0xffffu, y.w >> 16));
+            mn = min(mn, min(a, b));
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off));
+    if (lane == 0) red[tid >> 6] = mn;
+    if (tid == 0) {
+        s_T = ~0u;
+        s_cum = 0u;
+    }
+    __syncthreads();
+    uint32_t base = red[0];
+#pragma unroll
+    for (int w = 1; w < kSsThreads / 64; ++w) base = min(base, red[w]);
+    uint32_t win = 16;
+    while (true) {
+        for (uint32_t i = tid; i < win; i += kSsThreads) hist[i] = 0u;
+        __syncthreads();
+        if (inreg) {
+#pragma unroll
+            for (int j = 0; j < kSsPer; ++j) {
+                ss_count(x[j].x, base, win, hist);
+                ss_count(x[j].y, base, win, hist);
+                ss_count(x[j].z, base, win, hist);
+                ss_count(x[j].w, base, win, hist);
+            }
+        } else {
+            for (uint32_t i = tid; i < nv; i += kSsThreads) {
+                const uint4 y = v[i];
+                ss_count(y.x, base, win, hist);
+                ss_count(y.y, base, win, hist);
+                ss_count(y.z, base, win, hist);
+                ss_count(y.w, base, win, hist);
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {  // first bin whose running count reaches the target
+            const uint32_t seg = (win + 63u) / 64u, b0 = lane * seg, b1 = min(b0 + seg, win);
+            uint32_t sum = 0;
+            for (uint32_t i = b0; i < b1; ++i) sum += hist[i];
+            uint32_t incl = sum;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t t = __shfl_up(incl, off);
+                if ((int)lane >= off) incl += t;
+            }
+            const uint32_t cum0 = s_cum;
+            const uint64_t m = __ballot(cum0 + incl >= target);
+            if (m) {
+                const uint32_t first = __ffsll((long long)m) - 1;
+                if (lane == first) {
+                    uint32_t cum = cum0 + incl - sum;
+                    for (uint32_t i = b0; i < b1; ++i) {
+                        cum += hist[i];
+                        if (cum >= target) {
+                            s_T = base + i;
+                            break;
+                        }
+                    }
+                }
+            } else if (lane == 63) {
+                s_cum = cum0 + incl;
+            }
+        }
+        __syncthreads();
+        if (s_T != ~0u || base + win > D) break;
+        base += win;
+        win = min(win * 2u, kMaxWin);
+        __syncthreads();
+    }
+    if (tid == 0) thr[q] = min(s_T, D);
+}
+
+template <int W4>
+static void launch_sample_dense_t(const Stage1Args& a, hipStream_t s) {
+    const uint32_t S = a.sample_chunks * 4096u;
+    const uint32_t nsub = S / 32u;
+    const uint32_t wpb = kMx5Threads / 64;
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(cu_count(), (nsub + wpb - 1) / wpb));
+    constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
+    for (uint32_t g = 0; g < a.B; g += 256) {
+        const uint32_t bg = min(256u, a.B - g);
+        hipLaunchKernelGGL((k_sample_dense<W4>), dim3(grid), dim3(kMx5Threads), 0, s, a.codes, a.cap, a.N,
+                           a.sample_stride, nsub, (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, bg,
+                           a.smp + (uint64_t)g * S, S);
+    }
+    hipLaunchKernelGGL(k_sample_select, dim3(a.B), dim3(kSsThreads), 0, s, a.smp, S, a.D, a.target, a.thr);
+}
+
 template <int W4>
 static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
     // GVDB_HIST_LDS_WORDS: LDS histogram words per block (timing knob; default 12288)
@@ -2354,17 +2588,55 @@ static bool scan_selected(const char* v) {  // read per launch: tests switch it 
 }
 #endif
 
+size_t stage1_plan(Stage1Args& a) {
+    const uint32_t W4 = code_w4(a.D);
+    const uint64_t S = (uint64_t)a.sample_chunks * 4096u;
+    const bool big = a.use_mfma == 1 && a.B >= kMfmaMinB && mfma_scan_supported(W4);
+    a.mfma_scan = big;
+    a.sample_mode = kSampleValu;
+    // GVDB_SAMPLE=valu / =mx / =dense force a sample form (tests, A/B).  Default
+    // for large batches: the dense FP4 sample (any shard size: for N <= kExactN
+    // the "sample" is the whole shard and T is the exact R-th distance); the
+    // FP4 histogram only when the dense block would exceed 1 GiB.
+    if (big && !getenv_flag_eq("GVDB_SAMPLE", "valu")) {
+        const bool sampled = a.target < S / 2u && a.N > S;
+        if (getenv_flag_eq("GVDB_SAMPLE", "mx")) {
+            if (sampled) a.sample_mode = kSampleMxHist;
+        } else if ((uint64_t)a.B * S * 2u <= (1ull << 30)) {
+            a.sample_mode = kSampleDense;
+        } else if (sampled) {
+            a.sample_mode = kSampleMxHist;
+        }
+    }
+    size_t bytes = 0;
+    if (big) {
+        const uint64_t ng = (a.B + 255u) / 256u;
+        bytes += ng * (8u * 2u * W4 * 64u * 16u + 256u * 4u);
+    }
+    if (a.sample_mode == kSampleDense) bytes += (size_t)a.B * S * 2u + 256u;
+    return bytes;
+}
+
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     const uint32_t W4 = code_w4(a.D);
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    // sampled shard + large batch + >= 32 sample chunks (128K rows): the FP4-MFMA sample
-    // histogram (10M x 768: 55 vs 91 us; at the 64K-row floor of the 1.25M shard the VALU
-    // one is 1 % faster per step).  GVDB_SAMPLE=valu / =mx force one (tests, A/B).
-    const bool force_mx = getenv_flag_eq("GVDB_SAMPLE", "mx");
-    const bool sample_mx = a.use_mfma == 1 && a.B >= kMfmaMinB && mfma_scan_supported(W4) &&
-                           a.target < a.sample_chunks * 4096u / 2u && a.N > a.sample_chunks * 4096u &&
-                           !getenv_flag_eq("GVDB_SAMPLE", "valu") && (a.sample_chunks >= 32u || force_mx);
-    if (sample_mx) {
+    if (a.mfma_scan) {
+        switch (W4) {
+            case 2: launch_qfrag_t<2>(a, s); break;
+            case 3: launch_qfrag_t<3>(a, s); break;
+            case 4: launch_qfrag_t<4>(a, s); break;
+            default: launch_qfrag_t<6>(a, s); break;
+        }
+        GVDB_LAUNCH_CHECK();
+    }
+    if (a.sample_mode == kSampleDense) {
+        switch (W4) {
+            case 2: launch_sample_dense_t<2>(a, s); break;
+            case 3: launch_sample_dense_t<3>(a, s); break;
+            case 4: launch_sample_dense_t<4>(a, s); break;
+            default: launch_sample_dense_t<6>(a, s); break;
+        }
+    } else if (a.sample_mode == kSampleMxHist) {
         switch (W4) {
             case 2: launch_sample_mx_t<2>(a, s); break;
             case 3: launch_sample_mx_t<3>(a, s); break;
@@ -2392,8 +2664,10 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
                                a.N, a.D, W4, a.sample_stride, a.qcodes, a.B, a.hist);
     }
     GVDB_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_threshold, dim3((a.B + 3) / 4), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
-    GVDB_LAUNCH_CHECK();
+    if (a.sample_mode != kSampleDense) {
+        hipLaunchKernelGGL(k_threshold, dim3((a.B + 3) / 4), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
+        GVDB_LAUNCH_CHECK();
+    }
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
     const bool mfma = a.use_mfma && a.B >= kMfmaMinB && mfma_scan_supported(W4);
     const bool wide = a.use_mfma == 1 && a.B >= kMfmaMinB && mx4_scan_supported(W4);
@@ -2466,7 +2740,7 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
     const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
     hipLaunchKernelGGL(k_select, dim3(a.B), dim3(256), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R, a.codes, a.cap,
-                       a.N, W4, a.qcodes, a.fail, a.any_fail, a.s1_rows, a.s1_dist, a.force_rescan);
+                       a.N, W4, a.qcodes, a.fail, a.any_fail, a.s1_rows, a.s1_dist, a.force_rescan, a.keys_out);
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[3], s);
     return hipSuccess;

@@ -390,12 +390,16 @@ class GpuVectorIndex:
         """Vector search restricted to the ids a FilterEngine::execute_filter
         (filtering.rs:374) returned; ids the index does not hold are ignored.
         ``params.mode`` BQ: multi_stage_search over those rows (R from their
-        count); FLAT: exact scan of those rows (metric of ``params``)."""
+        count); FLAT: exact scan of those rows (metric of ``params``).  Without
+        ``params`` the search is the exact scan (an approximate BQ pass over a
+        small allowed set would keep only R = 0.1 M candidates)."""
         q = _f32(queries)
         if q.ndim == 1:
             q = q.reshape(1, -1)
         B, D = q.shape
-        sp = (params or self.params).to_c()
+        if params is None:
+            params = SearchParams(mode=_ffi.GVDB_SEARCH_FLAT, metric=self.params.metric)
+        sp = params.to_c()
         al = np.array([self._id_of[s] for s in allowed if s in self._id_of], np.uint64)
         ids = np.zeros((B, max(k, 1)), np.uint64)
         sc = np.zeros((B, max(k, 1)), np.float32)

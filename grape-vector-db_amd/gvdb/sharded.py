@@ -1,4 +1,15 @@
-"""Exact sharded BQ multi-stage search over torch.distributed.
+"""Exact sharded search over torch.distributed.
+
+:class:`TwoExchangeSearch` is the production protocol (the same one
+``gvdb_index_search_sharded_device`` runs with RCCL inside libgvdb, see
+``csrc/gvdb_shard.hip``) driven over ANY torch.distributed transport:
+local stage-1 keys -> all-gather -> global top-R + rerank of the rows this rank
+owns + local top-k -> all-gather -> merged top-k.  On a GPU it calls the
+device phases; on a CPU transport (gloo) it takes the local stage 1 and the
+cosines from callables and runs the merges' host forms.
+
+:class:`ShardedBQSearch` below is the earlier one-exchange variant (every rank
+reranks its whole local top-R and ships (id, Hamming, cosine) triplets).
 
 Replaces ``ShardManager::search_vectors`` (src/distributed/shard.rs:760-786:
 scatter to shards, concat, sort, truncate) inside one node.  Each rank owns a
@@ -31,6 +42,100 @@ CandidatesFn = Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor, t
 
 def shard_bounds(n: int, world: int) -> List[int]:
     return [n * g // world for g in range(world + 1)]
+
+
+class TwoExchangeSearch:
+    """Two-exchange exact sharded search for B queries, global depth R, k results.
+
+    device mode (``index`` given): the rank's shard is a GpuVectorIndex whose
+    rows are the rank's contiguous range of the corpus (ranks in corpus order);
+    the phases run on the GPU and the all-gathers move device tensors.
+    host mode (``stage1_fn`` / ``cosine_fn`` given, CPU tensors): stage1_fn(q, R)
+    -> (local rows int [B, Rl], Hamming int [B, Rl]) sorted by (d, row) with
+    Rl = min(R, shard rows); cosine_fn(q_index, local_rows) -> f32 cosines;
+    ``id_offset`` turns local rows into the ids reported (global row numbers).
+    """
+
+    def __init__(self, B: int, R: int, k: int, device: torch.device, group=None, index=None, stage1_fn=None,
+                 cosine_fn=None, id_offset: int = 0):
+        import ctypes as C
+
+        self.B, self.R, self.k = B, R, k
+        self.dev, self.group = device, group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.index, self.stage1_fn, self.cosine_fn, self.id_offset = index, stage1_fn, cosine_fn, id_offset
+        w1, w2, scr = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        lib().gvdb_shard_sizes(B, R, k, C.byref(w1), C.byref(w2), C.byref(scr))
+        self.w1, self.w2 = w1.value, w2.value
+        self.send1 = torch.zeros(self.w1, dtype=torch.int32, device=device)
+        self.recv1 = torch.zeros((self.world, self.w1), dtype=torch.int32, device=device)
+        self.send2 = torch.zeros(self.w2, dtype=torch.int32, device=device)
+        self.recv2 = torch.zeros((self.world, self.w2), dtype=torch.int32, device=device)
+        self.scratch = torch.zeros(scr.value, dtype=torch.uint8, device=device) if index is not None else None
+        self.out_ids = torch.zeros((B, k), dtype=torch.int64, device=device)
+        self.out_scores = torch.zeros((B, k), dtype=torch.float32, device=device)
+        self.out_n = torch.zeros(B, dtype=torch.int32, device=device)
+
+    def _gather(self, send, recv):
+        if self.world == 1:
+            recv[0].copy_(send)
+        elif send.is_cuda:
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+        else:
+            parts = list(recv.unbind(0))
+            dist.all_gather(parts, send, group=self.group)
+
+    def search(self, q: torch.Tensor):
+        B, R, k = self.B, self.R, self.k
+        L = lib()
+        if self.index is not None:
+            st = torch.cuda.current_stream(q.device).cuda_stream or None
+            D = q.shape[1]
+            check(L.gvdb_shard_stage1_device(self.index._h, q.data_ptr(), B, D, R, self.send1.data_ptr(), st))
+            self._gather(self.send1, self.recv1)
+            check(L.gvdb_shard_rerank_device(self.index._h, q.data_ptr(), B, D, R, k, self.recv1.data_ptr(), self.world,
+                                             self.rank, self.scratch.data_ptr(), self.send2.data_ptr(), st))
+            self._gather(self.send2, self.recv2)
+            check(L.gvdb_shard_final_device(self.recv2.data_ptr(), self.world, B, k, self.out_ids.data_ptr(),
+                                            self.out_scores.data_ptr(), self.out_n.data_ptr(), st))
+            return self.out_ids, self.out_scores, self.out_n
+        # host transport: the same blocks, host merges
+        rows, dd = self.stage1_fn(q, R)
+        rows, dd = np.asarray(rows, np.uint64), np.asarray(dd, np.uint64)
+        s1 = self.send1.numpy().view(np.uint32)
+        s1[:] = 0
+        keys = s1[:2 * B * R].view(np.uint64).reshape(B, R)
+        rl = rows.shape[1]
+        keys[:, :rl] = (dd << np.uint64(32)) | rows
+        s1[2 * B * R:2 * B * R + B] = rl
+        self._gather(self.send1, self.recv1)
+        g1 = np.ascontiguousarray(self.recv1.numpy().view(np.uint32))
+        own_rows = np.zeros((B, R), np.uint32)
+        own_pos = np.zeros((B, R), np.uint32)
+        own_cnt = np.zeros(B, np.uint32)
+        reff = np.zeros(B, np.uint32)
+        check(L.gvdb_shard_merge_host(g1.ctypes.data, self.world, self.rank, B, R, own_rows.ctypes.data,
+                                      own_pos.ctypes.data, own_cnt.ctypes.data, reff.ctypes.data))
+        scores = np.zeros((B, R), np.float32)
+        ids = np.zeros((B, R), np.uint64)
+        for i in range(B):
+            c = int(own_cnt[i])
+            if c:
+                scores[i, :c] = self.cosine_fn(i, own_rows[i, :c])
+                ids[i, :c] = own_rows[i, :c].astype(np.uint64) + np.uint64(self.id_offset)
+        s2 = self.send2.numpy().view(np.uint32)
+        s2[:] = 0
+        check(L.gvdb_shard_local_topk_host(scores.ctypes.data, own_pos.ctypes.data, ids.ctypes.data,
+                                           own_cnt.ctypes.data, reff.ctypes.data, B, R, k, 0, s2.ctypes.data))
+        self._gather(self.send2, self.recv2)
+        g2 = np.ascontiguousarray(self.recv2.numpy().view(np.uint32))
+        oi = np.zeros((B, k), np.uint64)
+        osc = np.zeros((B, k), np.float32)
+        on = np.zeros(B, np.uint32)
+        check(L.gvdb_shard_final_host(g2.ctypes.data, self.world, B, k, oi.ctypes.data, osc.ctypes.data,
+                                      on.ctypes.data))
+        return torch.from_numpy(oi.view(np.int64)), torch.from_numpy(osc), torch.from_numpy(on.view(np.int32))
 
 
 class ShardedBQSearch:
@@ -135,13 +240,14 @@ def gpu_candidates_fn(index) -> CandidatesFn:
 
 
 class RcclShardedSearch:
-    """The same exact sharded search with the collective inside libgvdb
-    (``gvdb_index_search_sharded_device``): local candidates -> ncclAllGather
-    on the caller's stream -> merge, all behind the C ABI, so a host without
-    torch (the Rust FFI of INTEGRATION.md) shards the same way.  torch.distributed
-    is used here only to hand rank 0's RCCL unique id to the other ranks."""
+    """The two-exchange search with the collectives inside libgvdb
+    (``gvdb_index_search_sharded_device``: two ncclAllGather calls on the
+    caller's stream), all behind the C ABI, so a host without torch (the Rust
+    FFI of INTEGRATION.md) shards the same way.  ``params`` may select FLAT
+    (the ranks' exact top-k merged).  torch.distributed is used here only to
+    hand rank 0's RCCL unique id to the other ranks."""
 
-    def __init__(self, index, R: int, k: int, group=None):
+    def __init__(self, index, R: int, k: int, group=None, params=None):
         import ctypes as C
 
         self.index, self.R, self.k = index, R, k
@@ -160,7 +266,7 @@ class RcclShardedSearch:
         self._h = h
         from . import SearchParams
 
-        self.sp = SearchParams(rescore_count=R).to_c()
+        self.sp = (params or SearchParams(rescore_count=R)).to_c()
 
     def search_into(self, q: torch.Tensor, out_ids: torch.Tensor, out_scores: torch.Tensor, out_n=None) -> None:
         import ctypes as C

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GVDB_ABI_VERSION 2
+#define GVDB_ABI_VERSION 3
 
 /* out_n[q] of a _device search whose query hit a NaN score (the reference's
  * partial_cmp().unwrap() sort would panic): that query has no results.  The
@@ -179,8 +179,14 @@ gvdb_status gvdb_index_build(gvdb_index* index);
 gvdb_status gvdb_index_search(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
                               uint64_t k, const gvdb_search_params* sp, uint64_t* out_ids,
                               float* out_scores, uint32_t* out_n);
-/* Same with queries and outputs in HBM.  out_n may be NULL.  Synchronises
- * the stream before returning (the fallback decision reads a device flag). */
+/* Same with queries and outputs in HBM.  out_n may be NULL.  The work is
+ * enqueued on `stream`: results are ready once the caller synchronises that
+ * stream (BQ mode returns without any host sync; FLAT mode synchronises
+ * internally because its tier decision reads a device flag).  A query whose
+ * top-R holds a NaN score (the reference's partial_cmp().unwrap() sort would
+ * panic) is reported ONLY through out_n[q] = GVDB_N_POISONED: callers that need
+ * the reference's failure must pass out_n (with out_n == NULL such a query's
+ * order is unspecified). */
 gvdb_status gvdb_index_search_device(const gvdb_index* index, const float* d_queries, uint64_t B,
                                      uint32_t dim, uint64_t k, const gvdb_search_params* sp,
                                      uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
@@ -208,7 +214,7 @@ gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* index, const float
  * (quantization.rs:151-193) over those rows, R = rescore_count or
  * (M as f32 * rescore_ratio) as usize for M allowed rows (the allowed rows'
  * codes are compacted on the device: O(M) extra memory); FLAT: the exact scan
- * of those rows.  Host buffers. */
+ * of those rows; sp == NULL: FLAT, cosine.  Host buffers. */
 gvdb_status gvdb_index_search_filtered(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
                                        uint64_t k, const gvdb_search_params* sp, const uint64_t* allowed,
                                        uint64_t n_allowed, uint64_t* out_ids, float* out_scores, uint32_t* out_n);
@@ -301,21 +307,70 @@ gvdb_status gvdb_comm_create(const uint8_t id[GVDB_COMM_ID_BYTES], int32_t world
                              gvdb_comm** out);
 void gvdb_comm_destroy(gvdb_comm* comm);
 gvdb_status gvdb_comm_info(const gvdb_comm* comm, int32_t* world, int32_t* rank);
-/* Exact sharded BQ search (collective; every rank passes the same queries and
- * its own shard).  Per rank: stage 1 local top-R (Hamming asc, id asc) with the
- * exact cosine of each candidate (quantization.rs:165-187), written straight
- * into the rank's all-gather block; ONE ncclAllGather on `stream` moves the
- * blocks over xGMI; every rank merges: union by (Hamming, id) -> first R ->
- * stable by cosine desc -> first k.  Bit-identical to one multi_stage_search
- * over the union of the shards.  R = sp->rescore_count (> 0; the global
- * rescore_ratio form needs the global row count: pass the count), R >= k,
- * world * R <= 4096.  Results land on every rank, on `stream`; no host sync
- * (a NaN-poisoned query gets out_n = GVDB_N_POISONED).  Calls on one comm
- * are serialised. */
+/* Exact sharded search (collective; every rank passes the same queries and its
+ * own shard = a contiguous row range of the corpus, ranks in corpus order).
+ * sp->mode BQ_RERANK (cosine), the two-exchange protocol of gvdb_shard_*:
+ * local stage-1 top-R keys -> ncclAllGather (B*R*8 B per rank) -> every rank
+ * takes the global top-R by (Hamming, corpus row), reranks only the rows it
+ * owns (~R/world per query) and keeps its local top-k -> ncclAllGather
+ * (B*k*16 B per rank) -> merged top-k.  sp->mode FLAT: the rank's exact top-k
+ * -> ncclAllGather -> merge by (score, corpus row).  Bit-identical to one
+ * search over the concatenated shards.  R = max(sp->rescore_count, k) (> 0;
+ * the global rescore_ratio form needs the global row count: pass the count),
+ * R <= 8192, world * k <= 8192, dim <= 8192.  Results land on every rank, on
+ * `stream`; no host sync in BQ mode.  An empty shard contributes nothing; a
+ * rank whose local part fails still joins both collectives (no deadlock),
+ * returns its error, and poisons every query of the merge (out_n =
+ * GVDB_N_POISONED on every rank), as does a NaN score.  Calls on one comm are
+ * serialised; a call on a different stream than the previous one waits for
+ * it on the device. */
 gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm* comm, const float* d_queries,
                                              uint64_t B, uint32_t dim, uint64_t k, const gvdb_search_params* sp,
                                              uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
                                              void* stream);
+
+/* ---- the two-exchange protocol as phases (for hosts with their own transport:
+ * MPI, torch.distributed, a CPU fabric).  Block layouts in u32 words:
+ *   exchange 1 (per rank, words1): keys u64 [B][R] (Hamming << 32 | local row,
+ *     sorted) | counts u32 [B] | err u32 | pad;
+ *   exchange 2 (per rank, words2): [B][k] x {cosine bits, global stage-1
+ *     position, id lo, id hi} | meta u32 [B] (count | NaN << 31) | reff [B] |
+ *     err | pad.
+ * Gathered buffers hold rank g's block at word g * words. ------------------- */
+void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint64_t* words1, uint64_t* words2,
+                      uint64_t* scratch_bytes);
+uint64_t gvdb_shard_flat_words(uint64_t B, uint64_t k);
+/* Phase 1: this rank's exchange-1 block (an empty shard: count 0). */
+gvdb_status gvdb_shard_stage1_device(const gvdb_index* shard, const float* d_queries, uint64_t B, uint32_t dim,
+                                     uint64_t R, uint32_t* d_block1, void* stream);
+/* Phase 2: from the gathered exchange-1 blocks, this rank's exchange-2 block
+ * (global top-R, exact cosine of the owned rows, local top-k).  d_scratch:
+ * scratch_bytes of device memory. */
+gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_queries, uint64_t B, uint32_t dim,
+                                     uint64_t R, uint64_t k, const uint32_t* d_gathered1, uint64_t G, uint64_t rank,
+                                     void* d_scratch, uint32_t* d_block2, void* stream);
+/* Phase 3: the merged top-k from the gathered exchange-2 blocks. */
+gvdb_status gvdb_shard_final_device(const uint32_t* d_gathered2, uint64_t G, uint64_t B, uint64_t k,
+                                    uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n, void* stream);
+/* Sharded FLAT: rank g's block (gvdb_shard_flat_words u32 words) holds its
+ * exact top-k as gvdb_index_search_device writes it: ids u64 [B][k] at word 0,
+ * scores f32 [B][k] at word 2*B*k, out_n u32 [B] at word 3*B*k, then an err
+ * word (nonzero poisons every query); the merge orders by
+ * (score per `metric`, rank, list position) = (score, corpus row). */
+gvdb_status gvdb_shard_flat_final_device(const uint32_t* d_gathered, uint64_t G, uint64_t B, uint64_t k,
+                                         uint32_t metric, uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
+                                         void* stream);
+/* Host forms of the merges (host memory, same layouts): phase 2's merge gives
+ * this rank's owned rows / global positions [B][R], their count and the global
+ * list length per query; local_topk builds the exchange-2 block from the owned
+ * entries' cosines and ids (in own_pos order); final = phase 3. */
+gvdb_status gvdb_shard_merge_host(const uint32_t* gathered1, uint64_t G, uint64_t rank, uint64_t B, uint64_t R,
+                                  uint32_t* own_rows, uint32_t* own_pos, uint32_t* own_cnt, uint32_t* reff);
+gvdb_status gvdb_shard_local_topk_host(const float* scores, const uint32_t* own_pos, const uint64_t* own_ids,
+                                       const uint32_t* own_cnt, const uint32_t* reff, uint64_t B, uint64_t R,
+                                       uint64_t k, uint32_t err, uint32_t* block2);
+gvdb_status gvdb_shard_final_host(const uint32_t* gathered2, uint64_t G, uint64_t B, uint64_t k, uint64_t* out_ids,
+                                  float* out_scores, uint32_t* out_n);
 
 /* ---- BM25 sparse index (src/sparse.rs:29-222) ---------------------------- */
 /* SparseIndex: documents are (term id, term frequency) lists with a

@@ -46,7 +46,7 @@ def test_status_codes_consistent(gvdb_mod):
     for k, v in codes.items():
         assert getattr(_ffi, k) == v, k
     L = gvdb_mod.lib()
-    assert L.gvdb_abi_version() == 2
+    assert L.gvdb_abi_version() == 3
     assert L.gvdb_status_string(1) == b"IndexNotBuilt"
     assert L.gvdb_status_string(2) == b"DimensionMismatch"
 

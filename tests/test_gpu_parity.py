@@ -639,12 +639,17 @@ def test_sharded_packed_world1_equals_single_device(g):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,D,B,R", [(1_200_000, 768, 256, 100), (600_000, 256, 128, 1000), (400_000, 384, 200, 100),
-                                     (350_000, 512, 96, 4000)])
+                                     (350_000, 512, 96, 4000), (1_250_000, 768, 300, 100), (200_000, 768, 256, 100),
+                                     (70_000, 700, 128, 1000)])
 def test_sample_histogram_mfma_thresholds_equal_valu(g, N, D, B, R):
-    """The FP4-MFMA sample histogram (k_sample_mx: 128 queries per block, bins
-    d < 384, each block flushes only up to its own target-th distance) must give
-    k_threshold exactly the thresholds of the VALU histogram (GVDB_SAMPLE=valu),
-    and the searches the same ids and distances (sampled shards: N > 262144)."""
+    """The FP4-MFMA sample forms must give exactly the thresholds of the VALU
+    histogram (GVDB_SAMPLE=valu), and the searches the same ids and distances:
+    k_sample_mx (128 queries per block, bins d < 384, each block flushes only up
+    to its own target-th distance; sampled shards N > 262144 only) and the
+    default dense form (k_sample_dense + k_sample_select: every sampled distance
+    as u16, per-query windowed select; also N <= 262144, where the "sample" is
+    the whole shard and T is the exact R-th distance; B = 300 spans two
+    256-query groups)."""
     import ctypes as C
     import os
 
@@ -662,8 +667,8 @@ def test_sample_histogram_mfma_thresholds_equal_valu(g, N, D, B, R):
     out = {}
     os.environ["GVDB_DEBUG_THR"] = "1"
     try:
-        for mode in ("mfma", "valu"):
-            os.environ["GVDB_SAMPLE"] = "mx" if mode == "mfma" else "valu"
+        for mode in ("mfma", "dense", "valu"):
+            os.environ["GVDB_SAMPLE"] = {"mfma": "mx", "dense": "dense", "valu": "valu"}[mode]
             rows = torch.zeros((B, R), dtype=torch.int64, device=dev)
             dist = torch.zeros((B, R), dtype=torch.int32, device=dev)
             ix.bq_topr_device(q, R, rows, dist)
@@ -674,6 +679,7 @@ def test_sample_histogram_mfma_thresholds_equal_valu(g, N, D, B, R):
     finally:
         os.environ.pop("GVDB_DEBUG_THR", None)
         os.environ.pop("GVDB_SAMPLE", None)
-    assert out["mfma"][0] == out["valu"][0]
-    assert max(out["mfma"][0]) < D  # a real estimate, not the no-pruning fallback
-    assert (out["mfma"][1] == out["valu"][1]).all() and (out["mfma"][2] == out["valu"][2]).all()
+    for mode in ("mfma", "dense"):
+        assert out[mode][0] == out["valu"][0], mode
+        assert max(out[mode][0]) < D  # a real estimate, not the no-pruning fallback
+        assert (out[mode][1] == out["valu"][1]).all() and (out[mode][2] == out["valu"][2]).all(), mode

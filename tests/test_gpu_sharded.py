@@ -1,6 +1,17 @@
 """GPU: the sharded search path (ShardManager::search_vectors, shard.rs:760-786,
 within one node) through the C ABI.
 
+* The two-exchange protocol (gvdb_shard_stage1_device -> gather ->
+  gvdb_shard_rerank_device -> gather -> gvdb_shard_final_device) with G = 8
+  ranks emulated on ONE GPU (each rank's blocks written where an all-gather
+  would put them): equal to one index over the concatenated corpus and to the
+  oracle, for R = 100 and R = 1000 (G*R = 8000 > the old 4096 merge cap),
+  batch 256 (FP4-MFMA stage 1), uneven shards and an EMPTY shard, D = 768 and
+  the config-4 width D = 3072.
+* Sharded FLAT with G = 8 at D = 3072: the ranks' exact top-k merged by
+  gvdb_shard_flat_final_device == the single index's exact flat search ==
+  the oracle.
+
 * G = 8 shard indices on ONE GPU (config 4's split at reduced N, D = 3072):
   per-shard candidates written into the blocks one all-gather would deliver,
   then the packed merge with G = 8 -- equal to one index over the whole
@@ -88,6 +99,118 @@ def test_g8_packed_merge_d3072_equals_single_index_and_oracle(g, oracle_mod):
     assert got_i[3, 0] == 12_345 and got_i[9, 0] == N - 1
 
 
+def emulate_two_exchange(g, shards, q, D, R, k):
+    """Run the three phases for every rank on one GPU; returns the merged
+    results of every rank (they must all agree)."""
+    import ctypes as C
+
+    import torch
+
+    L = g.lib()
+    G, B = len(shards), q.shape[0]
+    w1, w2, scr = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    L.gvdb_shard_sizes(B, R, k, C.byref(w1), C.byref(w2), C.byref(scr))
+    g1 = torch.zeros((G, w1.value), dtype=torch.int32, device="cuda")
+    g2 = torch.zeros((G, w2.value), dtype=torch.int32, device="cuda")
+    scratch = torch.zeros(scr.value, dtype=torch.uint8, device="cuda")
+    for r, ix in enumerate(shards):
+        g.check(L.gvdb_shard_stage1_device(ix._h, q.data_ptr(), B, D, R, g1[r].data_ptr(), None))
+    for r, ix in enumerate(shards):
+        g.check(L.gvdb_shard_rerank_device(ix._h, q.data_ptr(), B, D, R, k, g1.data_ptr(), G, r, scratch.data_ptr(),
+                                           g2[r].data_ptr(), None))
+    outs = []
+    for _ in range(2):  # every rank runs the same final merge
+        oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+        osc = torch.zeros((B, k), dtype=torch.float32, device="cuda")
+        on = torch.zeros(B, dtype=torch.int32, device="cuda")
+        g.check(L.gvdb_shard_final_device(g2.data_ptr(), G, B, k, oi.data_ptr(), osc.data_ptr(), on.data_ptr(), None))
+        outs.append((oi, osc, on))
+    torch.cuda.synchronize()
+    (a, b, c), (a2, b2, c2) = outs
+    assert torch.equal(a, a2) and torch.equal(b, b2) and torch.equal(c, c2)
+    return a.cpu().numpy().view(np.uint64), b.cpu().numpy(), c.cpu().numpy()
+
+
+@pytest.mark.parametrize("sizes,D,B,R", [
+    ((9000, 11000, 0, 10000, 12500, 7000, 10000, 10500), 768, 256, 100),
+    ((9000, 11000, 0, 10000, 12500, 7000, 10000, 10500), 768, 96, 1000),
+    ((5000,) * 8, 3072, 32, 100),
+    ((2000, 3, 2000, 2000, 1, 2000, 2000, 2000), 256, 20, 50),
+])
+def test_two_exchange_g8_equals_single_index_and_oracle(g, oracle_mod, sizes, D, B, R):
+    import torch
+
+    k = 10
+    N = sum(sizes)
+    x = rows(500 + D + R, N, D, dup=80)
+    bounds = np.cumsum((0,) + sizes)
+    # ties across shard boundaries: equal rows in different shards
+    for j in range(1, 8):
+        if sizes[j] and bounds[j] > 0:
+            x[bounds[j]] = x[0]
+    Q = rows(501 + D, B, D)
+    Q[0] = x[0]
+    Q[1] = x[N - 1]
+    Q[2] = x[bounds[4]]
+    q = torch.from_numpy(Q).cuda()
+    shards = []
+    for r in range(8):
+        ix = g.GpuVectorIndex(dimension=D)
+        if sizes[r]:
+            ix.add_batch(np.arange(bounds[r], bounds[r + 1], dtype=np.uint64), x[bounds[r]:bounds[r + 1]])
+        shards.append(ix)
+    got_i, got_s, got_n = emulate_two_exchange(g, shards, q, D, R, k)
+    si, ss, sn = single_device(g, x, Q, R, k)
+    assert (got_n == sn).all() and (got_i == si).all() and same_f32(got_s, ss)
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R, kind=0)
+    assert (got_i == ri[:, :k]).all() and same_f32(got_s, rs[:, :k])
+
+
+def test_sharded_flat_g8_d3072_equals_single_index_and_oracle(g, oracle_mod):
+    """Sharded FLAT (the recall-1.0 mode) at the config-4 width: 8 shards of
+    9K rows (> the 65536-row MFMA floor on no shard: exact scans) and 2 shards
+    of 70K (MFMA-certified tiers), ranks' exact top-k merged on the device."""
+    import ctypes as C
+
+    import torch
+
+    D, B, k = 3072, 12, 10
+    sizes = (9000, 70000, 9000, 9000, 70000, 9000, 9000, 9000)
+    N = sum(sizes)
+    bounds = np.cumsum((0,) + sizes)
+    x = rows(601, N, D, dup=20)
+    x[bounds[3]] = x[5]  # a tie across shards
+    Q = rows(602, B, D)
+    Q[0] = x[5]
+    q = torch.from_numpy(Q).cuda()
+    L = g.lib()
+    wf = L.gvdb_shard_flat_words(B, k)
+    gathered = torch.zeros((8, wf), dtype=torch.int32, device="cuda")
+    sp = g.SearchParams(mode=1, metric=0).to_c()
+    shards = []
+    for r in range(8):
+        ix = g.GpuVectorIndex(dimension=D)
+        ix.add_batch(np.arange(bounds[r], bounds[r + 1], dtype=np.uint64), x[bounds[r]:bounds[r + 1]])
+        p = gathered[r].data_ptr()
+        g.check(L.gvdb_index_search_device(ix._h, q.data_ptr(), B, D, k, C.byref(sp), p, p + 8 * B * k,
+                                           p + 12 * B * k, None))
+        shards.append(ix)
+    oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+    osc = torch.zeros((B, k), dtype=torch.float32, device="cuda")
+    on = torch.zeros(B, dtype=torch.int32, device="cuda")
+    g.check(L.gvdb_shard_flat_final_device(gathered.data_ptr(), 8, B, k, 0, oi.data_ptr(), osc.data_ptr(),
+                                           on.data_ptr(), None))
+    torch.cuda.synchronize()
+    got_i, got_s, got_n = oi.cpu().numpy().view(np.uint64), osc.cpu().numpy(), on.cpu().numpy()
+    full = g.GpuVectorIndex(dimension=D)
+    full.add_batch(np.arange(N, dtype=np.uint64), x)
+    si, ss, sn = full.search_batch(Q, k, g.SearchParams(mode=1, metric=0))
+    assert (got_n == sn).all() and (got_i == si).all() and same_f32(got_s, ss)
+    for b in range(B):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], x, k)
+        assert list(got_i[b]) == list(ri) and same_f32(got_s[b], rs)
+
+
 @pytest.mark.parametrize("N,B", [(120_000, 64), (50, 5)])
 def test_rccl_world1_equals_single_device(g, N, B):
     """gvdb_index_search_sharded_device over a 1-rank RCCL communicator (the
@@ -109,13 +232,47 @@ def test_rccl_world1_equals_single_device(g, N, B):
     oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
     osc = torch.zeros((B, k), dtype=torch.float32, device="cuda")
     on = torch.zeros(B, dtype=torch.int32, device="cuda")
-    for _ in range(2):  # the second call reuses the communicator's buffers
-        sh.search_into(q, oi, osc, on)
+    side = torch.cuda.Stream()
+    for it in range(3):  # later calls reuse the communicator's buffers; the last on another stream
+        if it == 2:
+            with torch.cuda.stream(side):
+                sh.search_into(q, oi, osc, on)
+            side.synchronize()
+        else:
+            sh.search_into(q, oi, osc, on)
     torch.cuda.synchronize()
     si, ss, sn = single_device(g, x, Q, R, k)
     assert (oi.cpu().numpy().view(np.uint64) == si).all()
     assert same_f32(osc.cpu().numpy(), ss)
     assert (on.cpu().numpy() == sn).all()
+    sh.close()
+    # FLAT through the same communicator path: the exact top-k
+    shf = RcclShardedSearch(ix, R, k, params=g.SearchParams(mode=1, metric=0))
+    shf.search_into(q, oi, osc, on)
+    torch.cuda.synchronize()
+    fi, fs, fn = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=0))
+    assert (oi.cpu().numpy().view(np.uint64) == fi).all() and same_f32(osc.cpu().numpy(), fs)
+    assert (on.cpu().numpy() == fn.astype(np.int32)).all()
+    shf.close()
+
+
+def test_rccl_world1_empty_shard_joins_and_returns_nothing(g):
+    """An empty shard still runs the protocol (no early return that would
+    leave other ranks in the collective): every query gets 0 results."""
+    import torch
+
+    from gvdb.sharded import RcclShardedSearch
+
+    D, B, k = 64, 4, 10
+    ix = g.GpuVectorIndex(dimension=D)
+    sh = RcclShardedSearch(ix, 100, k)
+    q = torch.from_numpy(rows(406, B, D)).cuda()
+    oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+    osc = torch.zeros((B, k), dtype=torch.float32, device="cuda")
+    on = torch.full((B,), 7, dtype=torch.int32, device="cuda")
+    sh.search_into(q, oi, osc, on)
+    torch.cuda.synchronize()
+    assert (on.cpu().numpy() == 0).all()
     sh.close()
 
 
@@ -134,8 +291,8 @@ def test_rccl_sharded_argument_checks(g):
     oi = torch.zeros((2, 10), dtype=torch.int64, device="cuda")
     osc = torch.zeros((2, 10), dtype=torch.float32, device="cuda")
     L = g.lib()
-    for sp in (g.SearchParams(rescore_count=0), g.SearchParams(rescore_count=5000),
-               g.SearchParams(rescore_count=100, mode=1)):
+    for sp in (g.SearchParams(rescore_count=0), g.SearchParams(rescore_count=9000),
+               g.SearchParams(rescore_count=100, metric=1)):
         c = sp.to_c()
         st = L.gvdb_index_search_sharded_device(ix._h, sh._h, q.data_ptr(), 2, D, 10, C.byref(c), oi.data_ptr(),
                                                 osc.data_ptr(), None, None)

@@ -1,9 +1,14 @@
-"""CPU, world_size 2 (gloo): the sharded orchestration (gvdb.sharded) —
-contiguous row shards with global ids, one all-gather of (id, Hamming,
-cosine) triplets, exact merge (the product's host merge in libgvdb) — equals
-one multi_stage_search over the whole corpus.  Per-shard candidates come from
-the oracle here (no GPU on this host); on the GPU box the same class runs
-with gpu_candidates_fn and the device merge (bench.py)."""
+"""CPU, world_size 2 and 3 (gloo): the sharded orchestrations (gvdb.sharded)
+equal one multi_stage_search over the whole corpus.
+
+* TwoExchangeSearch -- the production protocol: local stage-1
+  keys -> all-gather -> global top-R by (Hamming, corpus row) + rerank of the
+  rows this rank owns + local top-k -> all-gather -> merged top-k, through the
+  host forms of libgvdb's merges (gvdb_shard_merge_host / _local_topk_host /
+  _final_host; the device forms run the same blocks on the GPU).  Includes
+  uneven shards and an EMPTY shard (it joins both exchanges with no entries).
+* ShardedBQSearch -- the earlier one-exchange variant.
+Per-shard stage 1 and cosines come from the oracle here (no GPU on this host)."""
 import os
 import socket
 
@@ -66,6 +71,52 @@ def _worker(rank, world, port, ret):
               and sc.numpy().tobytes() == rs[:, :K].tobytes())
     ret[rank] = int(ok)
     dist.destroy_process_group()
+
+
+def _worker2(rank, world, port, ret, bounds, R):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "grape-vector-db_amd")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import oracle
+    from gvdb.sharded import TwoExchangeSearch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, q = _data()
+    lo, hi = bounds[rank], bounds[rank + 1]
+    xs = x[lo:hi]
+
+    def stage1(qt, r):
+        if hi == lo:
+            return np.zeros((B, 0), np.uint64), np.zeros((B, 0), np.uint64)
+        idx, dd = oracle.bq_topr_batch(oracle.quantize(qt.numpy()), oracle.quantize(xs), D, min(r, hi - lo))
+        return idx, dd
+
+    def cosine(i, local_rows):
+        return np.array([oracle.cosine_manual(q[i], xs[int(j)]) for j in local_rows], np.float32)
+
+    s = TwoExchangeSearch(B, R, K, torch.device("cpu"), stage1_fn=stage1, cosine_fn=cosine, id_offset=lo)
+    ids, sc, n = s.search(torch.from_numpy(q))
+    ri, rs = oracle.multi_stage_search_batch_r(oracle.quantize(q), oracle.quantize(x), q, x, R)
+    ok = bool((n.numpy() == K).all() and (ids.numpy().astype(np.uint64) == ri[:, :K]).all()
+              and sc.numpy().tobytes() == rs[:, :K].tobytes())
+    ret[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bounds,R", [(2, (0, 1500, N), 40), (3, (0, 900, 900, N), 40),
+                                            (3, (0, 1000, 2000, N), 300)])
+def test_two_exchange_equals_single_corpus(world, bounds, R, oracle_mod, gvdb_lib_path):
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker2, args=(world, _free_port(), ret, bounds, R), nprocs=world, join=True)
+    assert dict(ret) == {r: 1 for r in range(world)}
 
 
 @pytest.mark.parametrize("world", [2])
