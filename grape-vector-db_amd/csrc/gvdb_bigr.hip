@@ -1,0 +1,362 @@
+// gvdb_bigr.hip — multi_stage_search at the reference's DEFAULT rescore depth.
+//
+// BinaryQuantizationConfig::default() sets rescore_ratio = 0.1
+// (src/quantization.rs:27), so multi_stage_search reranks R = (N as f32 * 0.1)
+// as usize candidates (quantization.rs:178-179): 100K per query at 1M rows,
+// far beyond the LDS select (<= 8192 keys) of the regular stage 1.  Batched
+// here, for every query of the batch at once:
+//
+//   stage 1   the regular sample -> threshold -> scan (k_scan_mx5 / k_scan)
+//             into a candidate buffer sized for R, then k_select_big per
+//             query: exact top-R MEMBERSHIP by (Hamming, row) -- histogram of
+//             the buffered distances -> T_R, every key below T_R, and the
+//             first R - count(< T_R) rows tied at T_R in row order (radix
+//             select over the row index).  No sort: the order among the R is
+//             restored exactly by the final step.  A query whose buffer cannot
+//             certify (fewer than R keys passed the estimate, or overflow)
+//             is recomputed by the same block over all rows.
+//   stage 2   k_rerank over the R members (exact cosine, reference fold order)
+//   final     k_topk_big per query: the first k of the reference's stable
+//             cosine sort of the stage-1 list = the k smallest keys
+//             (~order(cos), Hamming, row); radix select on the 32-bit cosine
+//             order, ties resolved by (Hamming, row); take(k), then orphan rows
+//             are dropped, as in k_final_sort.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gvdb_device.h"
+#include "gvdb_internal.h"
+
+namespace gvdb {
+
+constexpr int kBigThreads = 1024;
+
+__device__ __forceinline__ uint32_t big_dist(const uint4* __restrict__ codes, uint64_t cap, uint32_t W4,
+                                             const uint4* __restrict__ qc, uint64_t n) {
+    uint32_t d = 0;
+    for (uint32_t w = 0; w < W4; ++w) {
+        const uint4 c = codes[(uint64_t)w * cap + n], q = qc[w];
+        d += __popc(c.x ^ q.x) + __popc(c.y ^ q.y) + __popc(c.z ^ q.z) + __popc(c.w ^ q.w);
+    }
+    return d;
+}
+
+// Block-wide exclusive prefix of a flag in thread order; *total = block count.
+__device__ __forceinline__ uint32_t big_prefix(bool f, uint32_t* wcnt, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wcnt[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), tot = 0;
+    for (uint32_t i = 0; i < nw; ++i) {
+        const uint32_t c = wcnt[i];
+        if (i < w) pre += c;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre;
+}
+
+// Wave-aggregated append of (row, d) to the query's member list.
+__device__ __forceinline__ void big_append(bool keep, uint32_t row, uint32_t d, uint32_t* s_n, uint32_t* rows,
+                                           uint32_t* dist, uint32_t R) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t m = __ballot(keep);
+    if (!m) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(s_n, (uint32_t)__popcll(m));
+    base = __shfl(base, 0);
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (keep && pos < R) {
+        rows[pos] = row;
+        dist[pos] = d;
+    }
+}
+
+// LDS: hist [(D + 4) & ~3] u32, then bins [2048] u32.
+__global__ __launch_bounds__(kBigThreads) void k_select_big(const uint32_t* __restrict__ counts,
+                                                            const uint64_t* __restrict__ buf, uint32_t bufcap,
+                                                            uint32_t D, uint32_t R, const uint4* __restrict__ codes,
+                                                            uint64_t cap, uint32_t N, uint32_t W4,
+                                                            const uint4* __restrict__ qcodes,
+                                                            uint32_t* __restrict__ fail, uint32_t* __restrict__ any_fail,
+                                                            uint32_t* __restrict__ s1_rows,
+                                                            uint32_t* __restrict__ s1_dist, int force_rescan) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    uint32_t* bins = hist + ((D + 4u) & ~3u);
+    __shared__ uint32_t s_T, s_lt, s_n, s_cut, s_below, s_tie, wcnt[kBigThreads / 64];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t cnt = counts[q];
+    const uint64_t* b = buf + (uint64_t)q * bufcap;
+    const uint4* qc = qcodes + (uint64_t)q * W4;
+    uint32_t* orow = s1_rows + (uint64_t)q * R;
+    uint32_t* odist = s1_dist + (uint64_t)q * R;
+    const bool rescan = cnt < R || cnt > bufcap || force_rescan;
+    for (uint32_t i = tid; i <= D; i += nt) hist[i] = 0u;
+    if (tid == 0) s_n = 0u;
+    __syncthreads();
+    if (rescan) {
+        for (uint64_t n = tid; n < N; n += nt) atomicAdd(&hist[big_dist(codes, cap, W4, qc, n)], 1u);
+    } else {
+        for (uint32_t i = tid; i < cnt; i += nt) atomicAdd(&hist[(uint32_t)(b[i] >> 32)], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t t = wave_find_cum(hist, D + 1u, R);
+        const uint32_t lt = wave_sum_below(hist, t);
+        if (tid == 0) {
+            s_T = t;
+            s_lt = lt;
+        }
+    }
+    __syncthreads();
+    const uint32_t T = s_T, need = R - s_lt;
+    if (rescan) {
+        // every row in order: d < T, then the first `need` rows tied at T
+        if (tid == 0) s_tie = 0u;
+        __syncthreads();
+        for (uint64_t base = 0; base < N; base += nt) {
+            const uint64_t n = base + tid;
+            const uint32_t d = n < N ? big_dist(codes, cap, W4, qc, n) : ~0u;
+            uint32_t tot;
+            const uint32_t rank = s_tie + big_prefix(d == T, wcnt, &tot);
+            big_append(d < T || (d == T && rank < need), (uint32_t)n, d, &s_n, orow, odist, R);
+            __syncthreads();
+            if (tid == 0) s_tie += tot;
+            __syncthreads();
+        }
+        if (tid == 0) {
+            fail[q] = 1u;
+            atomicOr(any_fail, 1u);
+        }
+        return;
+    }
+    uint32_t cut = ~0u;  // tied rows with row <= cut are kept
+    if (hist[T] > need) {
+        // the need-th smallest row among the keys with d == T: 11 + 11 + 10 bits
+        uint32_t left = need, prefix = 0u, pmask = 0u;
+        for (int pass = 0; pass < 3; ++pass) {
+            const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+            const uint32_t nb = pass == 2 ? 1024u : 2048u, dm = nb - 1u;
+            for (uint32_t i = tid; i < nb; i += nt) bins[i] = 0u;
+            __syncthreads();
+            for (uint32_t i = tid; i < cnt; i += nt) {
+                const uint64_t key = b[i];
+                const uint32_t row = (uint32_t)key;
+                if ((uint32_t)(key >> 32) == T && (row & pmask) == prefix) atomicAdd(&bins[(row >> shift) & dm], 1u);
+            }
+            __syncthreads();
+            if (tid < 64) {
+                const uint32_t bin = wave_find_cum(bins, nb, left);
+                const uint32_t below = wave_sum_below(bins, bin);
+                if (tid == 0) {
+                    s_cut = bin;
+                    s_below = below;
+                }
+            }
+            __syncthreads();
+            left -= s_below;
+            prefix |= s_cut << shift;
+            pmask |= dm << shift;
+            __syncthreads();
+        }
+        cut = prefix;
+    }
+    for (uint32_t i0 = 0; i0 < cnt; i0 += nt) {
+        const uint32_t i = i0 + tid;
+        uint64_t key = ~0ull;
+        if (i < cnt) key = b[i];
+        const uint32_t d = (uint32_t)(key >> 32), row = (uint32_t)key;
+        big_append(i < cnt && (d < T || (d == T && row <= cut)), row, d, &s_n, orow, odist, R);
+    }
+}
+
+hipError_t launch_select_big(const Stage1Args& a, hipStream_t s) {
+    const uint32_t W4 = code_w4(a.D);
+    const size_t lds = (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
+    hipLaunchKernelGGL(k_select_big, dim3(a.B), dim3(kBigThreads), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R,
+                       a.codes, a.cap, a.N, W4, a.qcodes, a.fail, a.any_fail, a.s1_rows, a.s1_dist, a.force_rescan);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ---- final: the first k of the stable cosine sort of an unordered stage-1 list
+constexpr uint32_t kTopkBigMax = 1024;  // k
+constexpr uint32_t kTieLds = 4096;      // tied entries sorted in LDS (more: radix select)
+
+__global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restrict__ scores,
+                                                          const uint32_t* __restrict__ s1_rows,
+                                                          const uint32_t* __restrict__ s1_dist, uint32_t R,
+                                                          uint32_t kout, int descending,
+                                                          const uint64_t* __restrict__ ids, uint64_t row_offset,
+                                                          uint64_t* __restrict__ out_ids,
+                                                          float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
+                                                          uint32_t* __restrict__ nan_flag) {
+    __shared__ uint32_t bins[256];
+    __shared__ uint64_t tk[kTieLds];          // ties: (d << 32 | row)
+    __shared__ uint32_t sel[kTopkBigMax];     // selected entry indices
+    __shared__ uint32_t srt[kTopkBigMax];     // sorted order
+    __shared__ uint32_t su[kTopkBigMax];      // selected: ukey
+    __shared__ uint64_t sdr[kTopkBigMax];     // selected: (d << 32 | row)
+    __shared__ uint32_t s_nan, s_cut, s_below, s_nsel, s_ntie;
+    __shared__ uint64_t s_tcut;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const float* sc = scores + (uint64_t)q * R;
+    const uint32_t* rw = s1_rows + (uint64_t)q * R;
+    const uint32_t* dd = s1_dist + (uint64_t)q * R;
+    const uint32_t k = min(kout, R);
+    auto ukey = [&](uint32_t i) {
+        const uint32_t o = f32_order(sc[i]);
+        return descending ? ~o : o;  // ascending = better first
+    };
+    if (tid == 0) {
+        s_nan = 0u;
+        s_nsel = 0u;
+        s_ntie = 0u;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < R; i += nt)
+        if (sc[i] != sc[i]) s_nan = 1u;
+    // U = the k-th smallest ukey: 4 radix passes of 8 bits
+    uint32_t left = k, prefix = 0u, pmask = 0u;
+    for (int pass = 0; pass < 4 && k > 0; ++pass) {
+        const int shift = 24 - 8 * pass;
+        for (uint32_t i = tid; i < 256; i += nt) bins[i] = 0u;
+        __syncthreads();
+        for (uint32_t i = tid; i < R; i += nt) {
+            const uint32_t u = ukey(i);
+            if ((u & pmask) == prefix) atomicAdd(&bins[(u >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const uint32_t bin = wave_find_cum(bins, 256, left);
+            const uint32_t below = wave_sum_below(bins, bin);
+            if (tid == 0) {
+                s_cut = bin;
+                s_below = below;
+            }
+        }
+        __syncthreads();
+        left -= s_below;
+        prefix |= s_cut << shift;
+        pmask |= 255u << shift;
+        __syncthreads();
+    }
+    const uint32_t U = prefix, need = left;  // `need` entries tied at U complete the top k
+    // entries strictly better than U (fewer than k), and the ties at U
+    for (uint32_t i = tid; i < R && k > 0; i += nt) {
+        const uint32_t u = ukey(i);
+        if (u < U) {
+            sel[atomicAdd(&s_nsel, 1u)] = i;
+        } else if (u == U) {
+            const uint32_t t = atomicAdd(&s_ntie, 1u);
+            if (t < kTieLds) tk[t] = ((uint64_t)dd[i] << 32) | i;  // stage-1 order (d, row) resolved below
+        }
+    }
+    __syncthreads();
+    const uint32_t nties = s_ntie;
+    if (k > 0 && nties <= kTieLds) {
+        // order the ties by (d, row): re-key with the row, sort, take `need`
+        for (uint32_t t = tid; t < nties; t += nt) {
+            const uint32_t i = (uint32_t)tk[t];
+            tk[t] = ((uint64_t)dd[i] << 52) | ((uint64_t)rw[i] << 20) | i;  // d < 2^12, row < 2^32, i < 2^20
+        }
+        __syncthreads();
+        const uint32_t P = next_pow2(max(nties, 1u));
+        for (uint32_t t = nties + tid; t < P; t += nt) tk[t] = ~0ull;
+        __syncthreads();
+        bitonic_sort_lds(tk, P);
+        for (uint32_t t = tid; t < need; t += nt) sel[s_nsel + t] = (uint32_t)tk[t] & 0xfffffu;
+        __syncthreads();
+    } else if (k > 0) {
+        // massive tie (more than kTieLds equal scores): radix select the need-th
+        // smallest (d, row) among them, 64-bit key in 8 passes of 8 bits
+        uint64_t tpre = 0, tmask = 0;
+        uint32_t tl = need;
+        for (int pass = 0; pass < 8; ++pass) {
+            const int shift = 56 - 8 * pass;
+            for (uint32_t i = tid; i < 256; i += nt) bins[i] = 0u;
+            __syncthreads();
+            for (uint32_t i = tid; i < R; i += nt) {
+                if (ukey(i) != U) continue;
+                const uint64_t key = ((uint64_t)dd[i] << 32) | rw[i];
+                if ((key & tmask) == tpre) atomicAdd(&bins[(uint32_t)(key >> shift) & 255u], 1u);
+            }
+            __syncthreads();
+            if (tid < 64) {
+                const uint32_t bin = wave_find_cum(bins, 256, tl);
+                const uint32_t below = wave_sum_below(bins, bin);
+                if (tid == 0) {
+                    s_cut = bin;
+                    s_below = below;
+                }
+            }
+            __syncthreads();
+            tl -= s_below;
+            tpre |= (uint64_t)s_cut << shift;
+            tmask |= 255ull << shift;
+            __syncthreads();
+        }
+        if (tid == 0) s_tcut = tpre;
+        __syncthreads();
+        for (uint32_t i = tid; i < R; i += nt) {
+            if (ukey(i) != U) continue;
+            const uint64_t key = ((uint64_t)dd[i] << 32) | rw[i];
+            if (key <= s_tcut) sel[atomicAdd(&s_nsel, 1u)] = i;  // distinct rows: exactly `need` keys
+        }
+        __syncthreads();
+    }
+    // sort the k selected by (ukey, d, row): rank counting over LDS copies
+    for (uint32_t a = tid; a < k; a += nt) {
+        const uint32_t ia = sel[a];
+        su[a] = ukey(ia);
+        sdr[a] = ((uint64_t)dd[ia] << 32) | rw[ia];
+    }
+    __syncthreads();
+    for (uint32_t a = tid; a < k; a += nt) {
+        const uint32_t ua = su[a];
+        const uint64_t da = sdr[a];
+        uint32_t rank = 0;
+        for (uint32_t c = 0; c < k; ++c) rank += su[c] < ua || (su[c] == ua && sdr[c] < da);
+        srt[rank] = sel[a];
+    }
+    __syncthreads();
+    if (tid < 64) {  // take(k), then drop orphan rows (index.rs:217-228)
+        uint32_t o = 0;
+        for (uint32_t i0 = 0; i0 < k; i0 += 64) {
+            const uint32_t i = i0 + tid;
+            uint64_t id = kOrphan;
+            uint32_t e = 0;
+            if (i < k) {
+                e = srt[i];
+                id = ids ? ids[rw[e]] : (uint64_t)rw[e] + row_offset;
+            }
+            const bool keep = i < k && id != kOrphan;
+            const uint64_t m = __ballot(keep);
+            const uint32_t before = __popcll(m & ((1ull << tid) - 1ull));
+            if (keep) {
+                out_ids[(uint64_t)q * kout + o + before] = id;
+                out_scores[(uint64_t)q * kout + o + before] = sc[e];
+            }
+            o += __popcll(m);
+        }
+        const bool poisoned = s_nan && R >= 2;
+        if (tid == 0) {
+            if (poisoned) atomicOr(nan_flag, 1u);
+            if (out_n) out_n[q] = poisoned ? GVDB_N_POISONED : o;
+        }
+    }
+}
+
+hipError_t launch_topk_big(const FinalArgs& a, const uint32_t* s1_dist, hipStream_t s) {
+    if (a.B == 0) return hipSuccess;
+    if (a.kout > kTopkBigMax) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_topk_big, dim3(a.B), dim3(kBigThreads), 0, s, a.scores, a.s1_rows, s1_dist, a.R, a.kout,
+                       a.descending, a.ids, a.row_offset, a.out_ids, a.out_scores, a.out_n, a.nan_flag);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+}  // namespace gvdb

@@ -302,6 +302,14 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     }();
     plan_sampling(N, R, (s1.use_mfma && B >= kMfmaMinB) ? big_div : 32u, s1.sample_chunks, s1.sample_stride,
                   s1.target, s1.bufcap);
+    if (R > kSelectLdsCap) {
+        // k_select_big: R candidates or more per query -- twice the expected
+        // emission (one Hamming bin of ties can add a few % of N), not 8x
+        const uint64_t S = (uint64_t)s1.sample_chunks * 4096u;
+        const double expect = N <= kExactN ? (double)N : (double)s1.target * (double)N / (double)S;
+        s1.bufcap = (uint32_t)std::min<double>((double)N, 2.0 * expect + 4096.0);
+        s1.big_select = 1;
+    }
     s1.B = B;
     s1.D = D;
     s1.N = N;
@@ -567,8 +575,12 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     HIP_TRY(ws.qnorm.ensure((size_t)B * 4), "alloc qnorm");
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
     HIP_TRY(ws.scores.ensure((size_t)B * R * 4), "alloc scores");
+    // the batched large-R path (gvdb_bigr.hip): unordered exact top-R + k_topk_big
+    const bool big = R > kSelectLdsCap && a.dims_match && v.D > 0 && v.D < 4096 && R <= kBigRMax && a.kout <= 1024 &&
+                     !a.d_out_dist && !getenv_flag("GVDB_BIGR_OFF");
     Stage1Args s1{};
-    gvdb_status pst = prepare_stage1(ws, s1, B, v.D, R, v.N, s, a.dims_match && v.D > 0 && R <= kSelectLdsCap);
+    gvdb_status pst =
+        prepare_stage1(ws, s1, B, v.D, R, v.N, s, a.dims_match && v.D > 0 && (R <= kSelectLdsCap || big));
     if (pst != GVDB_OK) return pst;
     uint32_t* d_flags = s1.any_fail;  // [0] any stage-1 rescan, [1] NaN seen, [2] per-query NaN scratch
 
@@ -606,6 +618,19 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             s1.ev = ev ? ev->e : nullptr;
             HIP_TRY(launch_stage1_fast(s1, s), "stage1");
             HIP_TRY(debug_keep_thr(s1.thr, B, s), "copy thresholds");
+        } else if (big) {
+            // R beyond the LDS select (the reference's default ratio 0.1): the
+            // batched stage 1 with k_select_big (exact top-R membership)
+            if (timed) ev = timing_events();
+            s1.codes = v.codes;
+            s1.cap = v.cap;
+            s1.N = v.N;
+            s1.D = v.D;
+            s1.qcodes = ws.qcodes.as<uint4>();
+            s1.B = B;
+            s1.R = R;
+            s1.ev = ev ? ev->e : nullptr;
+            HIP_TRY(launch_stage1_fast(s1, s), "stage1 (large R)");
         } else {
             // R beyond the LDS select: every query on the exact all-rows path
             HIP_TRY(ws.slow.ensure(stage1_slow_bytes(v.N)), "alloc slow path");
@@ -650,7 +675,9 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         fa.out_scores = a.d_out_scores;
         fa.out_n = a.d_out_n;
         fa.nan_flag = d_flags + 1;
-        if (R <= kSortLdsCap) {
+        if (big) {
+            HIP_TRY(launch_topk_big(fa, ws.s1_dist.as<uint32_t>(), s), "final top-k (large R)");
+        } else if (R <= kSortLdsCap) {
             HIP_TRY(launch_final_sort(fa, s), "final sort");
         } else {
             HIP_TRY(ws.sort_tmp.ensure(final_sort_global_bytes(R)), "alloc sort tmp");
@@ -2053,6 +2080,7 @@ gvdb_status gvdb::shard_stage1_keys(const gvdb_index* ix, const float* d_q, uint
     s1.cap = ix->cap;
     s1.qcodes = ws.qcodes.as<uint4>();
     s1.keys_out = keys;
+    s1.keys_stride = (uint32_t)R;  // the block's row stride is the global R (this shard may hold fewer rows)
     s1.ev = ev ? ev->e : nullptr;
     hipError_t e = launch_stage1_fast(s1, s);
     if (e == hipSuccess && ev) {

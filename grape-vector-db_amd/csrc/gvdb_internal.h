@@ -87,11 +87,16 @@ struct Stage1Args {
     uint4* qfrag;            // [ceil(B/256)][8 * 2*W4 * 64] FP4 query fragments
     uint32_t* qpc;           // [ceil(B/256) * 256] |q|
     uint16_t* smp;           // kSampleDense: [B][sample rows] sampled distances
-    uint64_t* keys_out;      // optional [B][R]: the sorted top-R keys (d << 32 | row) (sharded search),
-                             // followed by u32 counts [B] (= R)
+    uint64_t* keys_out;      // optional [B][keys_stride]: the sorted top-R keys (d << 32 | row) (sharded
+                             // search), followed by u32 counts [B] (= R)
+    uint32_t keys_stride;
     uint32_t* zero;          // mfma_scan: words k_qfrag zeroes before stage 1 (else the caller memsets)
     uint32_t nzero;
+    int big_select;          // R > kSelectLdsCap: k_select_big (unordered exact top-R membership)
 };
+// ---- large rescore depth (gvdb_bigr.hip): R up to 2^20, D < 4096, k <= 1024 --------
+constexpr uint32_t kBigRMax = 1u << 20;
+hipError_t launch_select_big(const Stage1Args& a, hipStream_t s);
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
@@ -168,6 +173,7 @@ struct RerankArgs {
     int kind;                // ScoreKind
     float* scores;           // [B][R]
     const uint32_t* counts;  // optional [B]: only the first counts[q] entries are valid
+    int short_lists;         // counts are mostly <= 16 (sharded owned rows): k_rerank_small
 };
 hipError_t launch_rerank(const RerankArgs& a, hipStream_t s);
 
@@ -190,6 +196,9 @@ struct FinalArgs {
 hipError_t launch_final_sort(const FinalArgs& a, hipStream_t s);
 size_t final_sort_global_bytes(uint32_t R);
 hipError_t launch_final_sort_global(const FinalArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s);
+// the first kout (<= 1024) of the stable order of an UNORDERED stage-1 list
+// (k_select_big's): keys (score order, Hamming, row) (gvdb_bigr.hip)
+hipError_t launch_topk_big(const FinalArgs& a, const uint32_t* s1_dist, hipStream_t s);
 
 // ---- flat exact scan (storage.rs:296-339, index.rs:620-640) --------------------
 // list (optional, [N]): scan the shard rows list[0..N) instead of rows 0..N-1

@@ -682,7 +682,8 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
                                                 uint32_t W4, const uint4* __restrict__ qcodes,
                                                 uint32_t* __restrict__ fail, uint32_t* __restrict__ any_fail,
                                                 uint32_t* __restrict__ s1_rows, uint32_t* __restrict__ s1_dist,
-                                                int force_rescan, uint64_t* __restrict__ keys_out) {
+                                                int force_rescan, uint64_t* __restrict__ keys_out,
+                                                uint32_t keys_stride) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // kSelectLdsCap keys, then hist, then radix bins
     uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);
     uint32_t* bins = hist + ((D + 4u) & ~3u);
@@ -697,10 +698,10 @@ __global__ __launch_bounds__(256) void k_select(const uint32_t* __restrict__ cou
         const uint64_t key = sk[i];
         s1_rows[(uint64_t)q * R + i] = (uint32_t)key;
         s1_dist[(uint64_t)q * R + i] = (uint32_t)(key >> 32);
-        if (keys_out) keys_out[(uint64_t)q * R + i] = key;  // sharded search: the exchange-1 block
+        if (keys_out) keys_out[(uint64_t)q * keys_stride + i] = key;  // sharded search: the exchange-1 block
     }
-    // ... whose per-query counts follow the B x R keys
-    if (keys_out && threadIdx.x == 0) ((uint32_t*)(keys_out + (uint64_t)gridDim.x * R))[q] = R;
+    // ... whose per-query counts follow the B x keys_stride keys
+    if (keys_out && threadIdx.x == 0) ((uint32_t*)(keys_out + (uint64_t)gridDim.x * keys_stride))[q] = R;
 }
 
 // ----------------------------------------------------------------------------
@@ -746,128 +747,6 @@ __device__ __forceinline__ v4i_t pm1_x16(uint32_t h16) {
     return r;
 }
 
-#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
-constexpr int kMfThreads = 512;
-constexpr int kMxDepth = 4;
-constexpr int kMxLdsDepth = 3;  // k-steps of B-fragment LDS prefetch in k_scan_mx2
-constexpr uint32_t kStampTiles = 64;
-__device__ unsigned long long g_stamps[2][kStampTiles][8];   // register tile-ring depth of k_scan_mx2
-constexpr int kMfCand = 64;  // candidates per tile (2 MFMA sub-tiles of 32)
-
-template <int W4>
-__global__ __launch_bounds__(kMfThreads, 2) void k_scan_mfma(const uint4* __restrict__ codes, uint64_t cap,
-                                                            uint32_t N, const uint32_t* __restrict__ qwords,
-                                                            const uint32_t* __restrict__ thr, uint32_t B,
-                                                            uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
-                                                            uint32_t bufcap) {
-    constexpr int KS = 4 * W4;                    // k-steps = 32-bit code words
-    constexpr int kTileBytes = 2 * KS * 64 * 16;  // [sub-tile][k-step][half][col][16 B]
-    constexpr int U = KS / 4;                     // expansion units per thread per tile (= W4)
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2][kTileBytes];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
-    const uint32_t q0 = wv * 32u;
-    const bool active = q0 < B;  // scalar branch: whole waves compute or only expand
-    // query fragments (A operand): lane holds query (q0 + lane&31), half (lane>>5)
-    v4i_t qa[KS];
-    int32_t T[16];  // per accumulator row: threshold of that query, -1 = padding row (never emits)
-    {
-        const uint32_t qr = min(q0 + (lane & 31u), B - 1u);
-        const uint32_t* qw = qwords + (uint64_t)qr * (4u * W4);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) qa[s] = pm1_x16(qw[s] >> (16u * (lane >> 5)));
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            T[r] = qi < B ? (int32_t)thr[qi] : -1;
-        }
-    }
-    constexpr uint32_t kPad = 32u * KS;
-    const uint32_t ntiles = (N + kMfCand - 1) / kMfCand;
-    // Expansion unit g = u*512 + tid  <->  (sub-tile st, word s, half h, col):
-    //   g = ((st*KS + s)*2 + h)*32 + col, LDS byte offset g*16 (one wave writes 1 KiB contiguously).
-    // Codes are prefetched TWO tiles ahead (nw: tile t+1, expanded during tile
-    // t's MFMAs; nw2: tile t+2, in flight), so no expansion waits on HBM.
-    uint32_t nw[U], nw2[U];
-    auto load = [&](uint32_t t, uint32_t (&dst)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = u * kMfThreads + tid;
-            const uint32_t col = g & 31u, s = (g >> 6) % KS, st = (g >> 6) / KS;
-            const uint32_t n = min(t * kMfCand + st * 32u + col, N - 1u);
-            dst[u] = ((const uint32_t*)codes)[(((uint64_t)(s >> 2) * cap) + n) * 4u + (s & 3u)];
-        }
-    };
-    auto expand_unit = [&](int u, int b) {
-        const uint32_t g = u * kMfThreads + tid;
-        const uint32_t h = (g >> 5) & 1u;
-        *(v4i_t*)(&lds[b][g * 16u]) = pm1_x16(nw[u] >> (16u * h));
-    };
-    uint32_t t = blockIdx.x;
-    if (t < ntiles) {
-        load(t, nw);
-#pragma unroll
-        for (int u = 0; u < U; ++u) expand_unit(u, 0);
-        if (t + gridDim.x < ntiles) load(t + gridDim.x, nw);
-    }
-    __syncthreads();
-    for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
-        const int b = it & 1;
-        const uint32_t tn = t + gridDim.x;
-        const bool more = tn < ntiles;
-        const bool more2 = tn + gridDim.x < ntiles;
-        if (more2) load(tn + gridDim.x, nw2);
-        if (active) {
-            // B fragments are read one k-step ahead of the MFMAs that use them;
-            // the next tile's expansion (other buffer) rides in the MFMA gaps.
-            const v4i_t* bf = (const v4i_t*)lds[b];
-            v16i_t acc0 = {0}, acc1 = {0};
-            v4i_t b0 = bf[(0 * KS) * 64 + lane], b1 = bf[(1 * KS) * 64 + lane];
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                v4i_t n0 = b0, n1 = b1;
-                if (s + 1 < KS) {
-                    n0 = bf[(0 * KS + s + 1) * 64 + lane];
-                    n1 = bf[(1 * KS + s + 1) * 64 + lane];
-                }
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], b0, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], b1, acc1, 0, 0, 0);
-                if ((s & 3) == 3 && more) expand_unit(s >> 2, b ^ 1);
-                b0 = n0;
-                b1 = n1;
-            }
-#pragma unroll
-            for (int st = 0; st < 2; ++st) {
-                const v16i_t& acc = st ? acc1 : acc0;
-                const uint32_t n = t * kMfCand + st * 32u + (lane & 31u);
-                bool any = false;
-                uint32_t d[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    d[r] = (kPad - (uint32_t)acc[r]) >> 1;
-                    any |= (int32_t)d[r] <= T[r];
-                }
-                if (any && n < N) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        if ((int32_t)d[r] <= T[r]) {
-                            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                            const uint32_t pos = atomicAdd(&counts[qi], 1u);
-                            if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = ((uint64_t)d[r] << 32) | n;
-                        }
-                    }
-                }
-            }
-        } else if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) expand_unit(u, b ^ 1);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) nw[u] = nw2[u];
-        __syncthreads();
-    }
-}
-#endif  // GVDB_SCAN_VARIANTS
 
 // ----------------------------------------------------------------------------
 // k_scan_mx — the large-batch stage-1 filter on block-scaled FP4 MFMA.
@@ -941,114 +820,6 @@ __device__ __forceinline__ void mfma_fp4_drain_acc(v16f_t (&acc)[NA]) {
     for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(acc[i]));
 }
 
-#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
-template <int W4>
-__global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
-                                                          const uint32_t* __restrict__ qwords,
-                                                          const uint32_t* __restrict__ thr, uint32_t B,
-                                                          uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
-                                                          uint32_t bufcap) {
-    constexpr int KW = 4 * W4;                 // 32-bit code words per row
-    constexpr int KS = KW / 2;                 // K=64 steps (two words each)
-    constexpr int kUnits = kMfCand * KW;       // (candidate, word) expansion units per tile
-    constexpr int U = (kUnits + kMfThreads - 1) / kMfThreads;
-    constexpr int kTileBytes = kUnits * 16;    // [sub-tile][k-step][half][col][16 B]
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2][kTileBytes];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t q0 = wv * 32u;
-    const bool active = q0 < B;
-    v4i_t qa[KS];
-    int32_t T[16];
-    {
-        const uint32_t qr = min(q0 + (lane & 31u), B - 1u);
-        const uint32_t* qw = qwords + (uint64_t)qr * KW;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) qa[s] = fp4_x32(qw[2 * s + (lane >> 5)]);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            T[r] = qi < B ? (int32_t)thr[qi] : -1;
-        }
-    }
-    constexpr int32_t kPad = 32 * KW;
-    const uint32_t ntiles = (N + kMfCand - 1) / kMfCand;
-    // unit g = ((st*KS + s)*2 + h)*32 + col  <->  word (2s+h) of candidate st*32+col
-    uint32_t nw[U];
-    auto load = [&](uint32_t t) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = u * kMfThreads + tid;
-            if (g < (uint32_t)kUnits) {
-                const uint32_t col = g & 31u, h = (g >> 5) & 1u, s = (g >> 6) % KS, st = (g >> 6) / KS;
-                const uint32_t w = 2u * s + h;
-                const uint32_t n = min(t * kMfCand + st * 32u + col, N - 1u);
-                nw[u] = ((const uint32_t*)codes)[(((uint64_t)(w >> 2) * cap) + n) * 4u + (w & 3u)];
-            }
-        }
-    };
-    auto expand = [&](int b) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = u * kMfThreads + tid;
-            if (g < (uint32_t)kUnits) *(v4i_t*)(&lds[b][g * 16u]) = fp4_x32(nw[u]);
-        }
-    };
-    uint32_t t = blockIdx.x;
-    if (t < ntiles) {
-        load(t);
-        expand(0);
-    }
-    __syncthreads();
-    for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
-        const int b = it & 1;
-        const uint32_t tn = t + gridDim.x;
-        const bool more = tn < ntiles;
-        if (more) load(tn);  // lands during this tile's MFMAs
-        if (active) {
-            const v4i_t* bf = (const v4i_t*)lds[b];
-            v16f_t acc0 = {0}, acc1 = {0};
-            v4i_t b0 = bf[(0 * KS) * 64 + lane], b1 = bf[(1 * KS) * 64 + lane];
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                v4i_t n0 = b0, n1 = b1;
-                if (s + 1 < KS) {
-                    n0 = bf[(0 * KS + s + 1) * 64 + lane];
-                    n1 = bf[(1 * KS + s + 1) * 64 + lane];
-                }
-                acc0 = mfma_fp4(qa[s], b0, acc0);
-                acc1 = mfma_fp4(qa[s], b1, acc1);
-                b0 = n0;
-                b1 = n1;
-            }
-#pragma unroll
-            for (int st = 0; st < 2; ++st) {
-                const v16f_t& acc = st ? acc1 : acc0;
-                const uint32_t n = t * kMfCand + st * 32u + (lane & 31u);
-                bool any = false;
-                int32_t d[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    d[r] = (kPad - (int32_t)acc[r]) >> 1;
-                    any |= d[r] <= T[r];
-                }
-                if (any && n < N) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        if (d[r] <= T[r]) {
-                            const uint32_t qi = q0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                            const uint32_t pos = atomicAdd(&counts[qi], 1u);
-                            if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = ((uint64_t)(uint32_t)d[r] << 32) | n;
-                        }
-                    }
-                }
-            }
-        }
-        if (more) expand(b ^ 1);
-        __syncthreads();
-    }
-}
-#endif  // GVDB_SCAN_VARIANTS
 
 // k_scan_mx2: the FP4 scan with staggered wave halves.  8 waves per CU, one
 // 32-query tile each; waves w and w+4 share a SIMD.  Every tile both halves
@@ -1060,253 +831,6 @@ __global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx(const uint4* __restri
 // MFMAs instead of all waves alternating between the two phases together.
 // Each half keeps ONE register set for its codes (expanded, then reloaded:
 // no register moves, which would wait on the loads).  One barrier per tile.
-#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
-template <int W4>
-__global__ __launch_bounds__(kMfThreads, 2) void k_scan_mx2(const uint4* __restrict__ codes, uint64_t cap,
-                                                           uint32_t N, const uint32_t* __restrict__ qwords,
-                                                           const uint32_t* __restrict__ thr, uint32_t B,
-                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
-                                                           uint32_t bufcap, int dbg) {
-    constexpr int KW = 4 * W4;
-    constexpr int KS = KW / 2;
-    constexpr int kUnits = kMfCand * KW;       // (candidate, word) units per tile
-    constexpr int kHalf = kUnits / 2;          // per wave half
-    constexpr int U = (kHalf + 255) / 256;     // units per thread
-    constexpr int kTileBytes = kUnits * 16;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2][kTileBytes];
-    __shared__ __attribute__((aligned(16))) float tf_lds[256];
-    // Candidate staging: a returning global atomic per emit would stall the
-    // emitting wave ~2 us and, through the per-tile barrier, the whole block.
-    // Each wave appends its emits to a private LDS slice (its fill count is a
-    // wave-uniform scalar: no atomics) and the slices are flushed to the
-    // per-query global buffers once, after the last tile; a full slice falls
-    // back to direct global emits.
-    constexpr uint32_t kWaveStage = 512;
-    __shared__ uint64_t st_key[kMfThreads / 64][kWaveStage];
-    __shared__ uint8_t st_q[kMfThreads / 64][kWaveStage];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool late = wv >= 4;                 // second half: expand first, then MFMA
-    const uint32_t q0 = wv * 32u;
-    const bool active = q0 < B;
-    const uint32_t ntiles = (N + kMfCand - 1) / kMfCand;
-    const uint32_t G = gridDim.x;
-    constexpr float kPadF = (float)(32 * KW);
-    const int scale1 = 0x7f7f7f7f;
-    if (tid < 256) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
-
-    // expansion units of this thread: g = (late ? kHalf : 0) + u*256 + (tid & 255)
-    // unit g = ((st*KS + s)*2 + h)*32 + col  <->  word (2s+h) of candidate st*32+col
-    uint64_t woff[U];   // u32-element offset of the unit's word in row 0
-    uint32_t rofs[U];   // unit's row within a tile
-    bool uok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t g = (late ? kHalf : 0) + u * 256u + (tid & 255u);
-        uok[u] = u * 256u + (tid & 255u) < (uint32_t)kHalf;
-        const uint32_t col = g & 31u, h = (g >> 5) & 1u, s = (g >> 6) % KS, st = (g >> 6) / KS;
-        const uint32_t w = 2u * s + h;
-        woff[u] = uok[u] ? ((uint64_t)(w >> 2) * cap) * 4u + (w & 3u) : 0;
-        rofs[u] = uok[u] ? st * 32u + col : 0;
-    }
-    const uint32_t* cw = (const uint32_t*)codes;
-    // D register sets of raw code words: tile j of this block lives in set j % D,
-    // so every load is issued D-1..D tiles (>= the HBM latency) before its expand.
-    // Loads are unconditional and branch-free (rows clamped to N-1, also past the
-    // last tile): a conditional load makes the compiler merge register sets with
-    // copies that wait for the load, serialising the ring.
-    constexpr int D = kMxDepth;
-    uint32_t nw[D][U];
-    auto load = [&](uint32_t t, uint32_t (&w)[U]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t n = min(t * kMfCand + rofs[u], N - 1u);
-            w[u] = cw[woff[u] + (uint64_t)n * 4u];
-        }
-    };
-    auto expand = [&](int b, const uint32_t (&w)[U]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t g = (late ? kHalf : 0) + u * 256u + (tid & 255u);
-            if (uok[u]) *(v4i_t*)(&lds[b][g * 16u]) = fp4_x32(w[u]);
-        }
-    };
-    v4i_t qa[KS];
-    if (active) {
-        const uint32_t qr = min(q0 + (lane & 31u), B - 1u);
-        const uint32_t* qw = qwords + (uint64_t)qr * KW;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) qa[s] = fp4_x32(qw[2 * s + (lane >> 5)]);
-    }
-    // dbg & 16 in a -DGVDB_SCAN_STAMPS build: shader-clock stamps of waves 0 and
-    // 4 of block 0 (dev aid; compiled out by default)
-    auto mark = [&](uint32_t j, int p) __attribute__((always_inline)) {
-#ifdef GVDB_SCAN_STAMPS
-        if ((dbg & 16) && blockIdx.x == 0 && (wv & 3u) == 0 && lane == 0 && j < kStampTiles)
-            g_stamps[wv >> 2][j][p] = __builtin_amdgcn_s_memtime();
-#else
-        (void)j;
-        (void)p;
-#endif
-    };
-    // MFMA phase of a tile: 2 x KS block-scaled FP4 MFMAs into one accumulator pair.
-    // B fragments ride a PF-deep register ring: the LDS read for k-step s is
-    // issued PF steps (2*PF MFMAs) before its use, covering LDS latency.
-    auto mma = [&](int b, v16f_t& acc0, v16f_t& acc1) __attribute__((always_inline)) {
-        const v4i_t* bf = (const v4i_t*)lds[b];
-        constexpr int PF = kMxLdsDepth < KS ? kMxLdsDepth : KS;
-        v4i_t r0[PF], r1[PF];
-#pragma unroll
-        for (int s = 0; s < PF; ++s) {
-            r0[s] = bf[(0 * KS + s) * 64 + lane];
-            r1[s] = bf[(1 * KS + s) * 64 + lane];
-        }
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const v4i_t b0 = r0[s % PF], b1 = r1[s % PF];
-            if (s == 0) {
-                mfma_fp4_first(acc0, qa[s], b0, scale1);
-                mfma_fp4_first(acc1, qa[s], b1, scale1);
-            } else {
-                mfma_fp4_acc(acc0, qa[s], b0, scale1);
-                mfma_fp4_acc(acc1, qa[s], b1, scale1);
-            }
-            if (s + PF < KS) {
-                r0[s % PF] = bf[(0 * KS + s + PF) * 64 + lane];
-                r1[s % PF] = bf[(1 * KS + s + PF) * 64 + lane];
-            }
-        }
-    };
-    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
-    // Threshold epilogue of a tile whose MFMAs were issued one step earlier (its
-    // results are complete by then: the wave does not wait on the MFMA pipe).
-    auto epi = [&](uint32_t t, const v16f_t& acc0, const v16f_t& acc1) __attribute__((always_inline)) {
-        if (dbg & 4) return;
-        float Tf[16];
-        const float* tq = tf_lds + q0 + 4u * (lane >> 5);
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            const float4 v = *(const float4*)(tq + 8 * g4);
-            Tf[4 * g4 + 0] = v.x;
-            Tf[4 * g4 + 1] = v.y;
-            Tf[4 * g4 + 2] = v.z;
-            Tf[4 * g4 + 3] = v.w;
-        }
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            const v16f_t& acc = st ? acc1 : acc0;
-            // fast reject: one max-reduction per lane, one ballot per wave
-            float mx = acc[0] - Tf[0];
-#pragma unroll
-            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r] - Tf[r]);
-            if (!__ballot(mx >= 0.0f) || (dbg & 8)) continue;
-            const uint32_t n = t * kMfCand + st * 32u + (lane & 31u);
-            uint32_t rb = q0 + 4u * (lane >> 5);
-            asm volatile("" : "+v"(rb));  // keep row addresses out of the tile loop
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const bool hit = acc[r] >= Tf[r] && n < N;
-                const uint64_t m = __ballot(hit);
-                if (m) {
-                    if (hit) {
-                        const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
-                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
-                        const uint32_t d = (uint32_t)(kPadF - acc[r]) >> 1;
-                        const uint64_t key = ((uint64_t)d << 32) | n;
-                        if (sp < kWaveStage) {
-                            st_key[wv][sp] = key;
-                            st_q[wv][sp] = (uint8_t)qi;
-                        } else {
-                            const uint32_t pos = atomicAdd(&counts[qi], 1u);
-                            if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = key;
-                        }
-                    }
-                    wcnt += (uint32_t)__popcll(m);
-                }
-            }
-        }
-    };
-    // block-local tile j is global tile blockIdx.x + j*G
-    const uint32_t nt = blockIdx.x < ntiles ? (ntiles - blockIdx.x + G - 1) / G : 0;
-    auto tile = [&](uint32_t j) { return blockIdx.x + j * G; };
-#pragma unroll
-    for (int s = 0; s < D; ++s) load(tile(s), nw[s]);
-    if (nt) expand(0, nw[0]);
-    load(tile(D), nw[0]);
-    __syncthreads();
-    // Step j: MFMAs of tile j (lds[j&1]) into accumulator pair j&1; threshold
-    // epilogue of tile j-1 from the other pair (software-pipelined, so no wave
-    // waits on its own MFMA results); expand tile j+1 (set (j+1)%D) into
-    // lds[(j+1)&1] and refill that set with tile j+1+D.  The early half (waves
-    // 0-3) issues its MFMAs first, the late half (waves 4-7) expands first, so
-    // the halves' VALU and MFMA phases interleave on each SIMD.  Separate loops
-    // per half keep the register ring static.
-    v16f_t accA0, accA1, accB0, accB1;
-    auto step = [&](uint32_t j, auto S, auto LATE) __attribute__((always_inline)) {
-        constexpr int s1 = (decltype(S)::value + 1) % D;
-        constexpr int b = decltype(S)::value & 1;
-        v16f_t& c0 = b ? accB0 : accA0;
-        v16f_t& c1 = b ? accB1 : accA1;
-        const v16f_t& p0 = b ? accA0 : accB0;
-        const v16f_t& p1 = b ? accA1 : accB1;
-        const bool more = j + 1 < nt;
-        const bool work = active && !(dbg & 1);
-        mark(j, 0);
-        if constexpr (!decltype(LATE)::value) {
-            if (work) mma(b, c0, c1);
-            mark(j, 1);
-            if (work && j > 0) epi(tile(j - 1), p0, p1);
-            mark(j, 2);
-            if (more && !(dbg & 2)) expand(b ^ 1, nw[s1]);
-            load(tile(j + 1 + D), nw[s1]);
-        } else {
-            if (more && !(dbg & 2)) expand(b ^ 1, nw[s1]);
-            load(tile(j + 1 + D), nw[s1]);
-            mark(j, 1);
-            if (work) mma(b, c0, c1);
-            mark(j, 2);
-            if (work && j > 0) epi(tile(j - 1), p0, p1);
-        }
-        mark(j, 3);
-        __syncthreads();
-        mark(j, 4);
-    };
-    static_assert(D == 4, "the unrolled ring below has four steps");
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    auto run = [&](auto LATE) __attribute__((always_inline)) {
-        for (uint32_t j = 0; j < nt; j += D) {
-            step(j, I0{}, LATE);
-            if (j + 1 < nt) step(j + 1, I1{}, LATE);
-            if (j + 2 < nt) step(j + 2, I2{}, LATE);
-            if (j + 3 < nt) step(j + 3, I3{}, LATE);
-        }
-    };
-    if (late)
-        run(std::true_type{});
-    else
-        run(std::false_type{});
-    // epilogue of the block's last tile
-    if (nt && active && !(dbg & 1)) {
-        mfma_fp4_drain();
-        if ((nt - 1) & 1)
-            epi(tile(nt - 1), accB0, accB1);
-        else
-            epi(tile(nt - 1), accA0, accA1);
-    }
-    __syncthreads();
-    // flush the staged candidates: all global atomics of the wave in flight at once
-    const uint32_t ns = min(wcnt, kWaveStage);
-    for (uint32_t e = lane; e < ns; e += 64u) {
-        const uint32_t qi = st_q[wv][e];
-        const uint32_t pos = atomicAdd(&counts[qi], 1u);
-        if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = st_key[wv][e];
-    }
-}
-#endif  // GVDB_SCAN_VARIANTS
 
 // Block-aggregated flush of the per-wave staged emits (k_scan_mx3/mx4): one
 // LDS atomic per entry gives its rank within (block, query), then ONE global
@@ -1367,229 +891,6 @@ constexpr int kMx3Threads = 512;
 #define MX3_RING 2
 #endif
 [[maybe_unused]] constexpr int kMx3Ring = MX3_RING;
-#ifdef GVDB_SCAN_VARIANTS  // k_scan_mx3: the previous default (GVDB_SCAN=mx3 in a VARIANTS=1 build)
-// k_scan_mx3: the FP4 scan with the candidates in REGISTERS and the queries
-// resident in LDS.  The whole query batch (<= 256 queries) is expanded to fp4
-// MFMA fragments once per block (96 KiB at 768 bits), then every wave streams
-// its own 32-row sub-tiles of the code planes straight from HBM into VGPRs
-// (two register sets: the next sub-tile's planes are in flight while the
-// current one is consumed), expands one code word per lane per k-step and runs
-// it against all query tiles (one A fragment per MFMA from LDS, a 4-deep
-// register ring hides the LDS latency).  No LDS traffic for candidates and no
-// block barrier in the loop: waves run independently, so one wave's
-// expansion / threshold VALU fills the other wave's MFMA gaps on the SIMD.
-// Semantics are those of k_scan_mx2 (exact +/-1 dot = D_pad - 2 Hamming;
-// emits (d << 32 | row) for d <= thr[q], staged per wave in LDS).
-template <int W4>
-__global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx3(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
-                                                           const uint32_t* __restrict__ qwords,
-                                                           const uint32_t* __restrict__ thr, uint32_t B,
-                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
-                                                           uint32_t bufcap) {
-    constexpr int KW = 4 * W4;  // 32-bit code words per row
-    constexpr int KS = KW / 2;  // k-steps of 64 bits
-    constexpr int QT = 8;       // query tiles of 32 (256 queries per launch)
-    constexpr uint32_t kWaveStage = 512;
-    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
-    __shared__ __attribute__((aligned(16))) float tf_lds[QT * 32];
-    __shared__ uint64_t st_key[kMx3Threads / 64][kWaveStage];
-    __shared__ uint8_t st_q[kMx3Threads / 64][kWaveStage];
-    __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-#if defined(MX3_PRIO) && MX3_PRIO == 1
-    // static priority for the younger half (waves 4-7): they lose VALU
-    // arbitration to the older half otherwise (MI355X_MICROARCH.md, two waves per SIMD)
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
-    constexpr float kPadF = (float)(32 * KW);
-    const int scale1 = 0x7f7f7f7f;
-    // query fragments: (tile qt, k-step s, lane l) = query qt*32 + (l & 31), code word 2s + (l >> 5)
-    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx3Threads) {
-        const uint32_t l = i & 63u, st = i >> 6, qs = st % KS, qt = st / KS;
-        const uint32_t q = qt * 32u + (l & 31u);
-        qfrag[i] = fp4_x32(q < B ? qwords[(uint64_t)q * KW + 2u * qs + (l >> 5)] : 0u);
-    }
-    if (tid < QT * 32) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
-    if (tid < QT * 32) qcnt[tid] = 0u;
-    __syncthreads();
-    // per (query tile, lane half): the smallest threshold among the 16 queries a
-    // lane's accumulator rows hold, so a sub-tile with no hit is rejected with a
-    // max over the accumulator and one compare per query tile
-    __shared__ float tmin_lds[QT * 2];
-    if (tid < QT * 2) {
-        const float* tq = tf_lds + (tid >> 1) * 32 + 4u * (tid & 1u);
-        float m = tq[0];
-        for (int r = 1; r < 16; ++r) m = fminf(m, tq[(r & 3) + 8 * (r >> 2)]);
-        tmin_lds[tid] = m;
-    }
-    __syncthreads();
-    const uint32_t nqt = (B + 31u) / 32u;
-    const uint32_t nsub = (N + kMx3Rows - 1) / kMx3Rows;
-    const uint32_t W = gridDim.x * (kMx3Threads / 64);  // waves in the grid
-    const uint32_t h = lane >> 5;                      // lane half: code word 2s + h
-    // code planes of one sub-tile: lane holds plane p of row (lane & 31) (both halves the same row)
-    uint4 ca[W4], cb[W4];
-    auto load = [&](uint32_t sb, uint4 (&c)[W4]) __attribute__((always_inline)) {
-        const uint32_t n = min(sb * (uint32_t)kMx3Rows + (lane & 31u), N - 1u);  // clamped: branch-free ring
-#pragma unroll
-        for (int p = 0; p < W4; ++p) c[p] = codes[(uint64_t)p * cap + n];
-    };
-    auto word = [&](const uint4 (&c)[W4], int s) __attribute__((always_inline)) {
-        // code word 2s + h = component (2s & 3) + h of plane (2s >> 2)
-        const uint4 v = c[(2 * s) >> 2];
-        return (2 * s) & 3 ? (h ? v.w : v.z) : (h ? v.y : v.x);
-    };
-    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
-    // MX3_PASSES passes of QH query tiles per sub-tile: 1 = every query tile's
-    // accumulator live (128 VGPRs), 2 = half of them (the row fragment is then
-    // re-expanded per pass: 8 VALU per k-step).
-    constexpr int QH = QT / kMx3Passes;
-    v16f_t acc[QH];
-
-    auto process = [&](uint32_t sb, const uint4 (&c)[W4]) __attribute__((always_inline)) {
-        const uint32_t n = sb * (uint32_t)kMx3Rows + (lane & 31u);
-        // opaque copies of the emit pointers (see k_scan_mx4): keeps the per-(tile, row)
-        // overflow addresses from being hoisted out of the loop
-        uint32_t* cnt = counts;
-        uint64_t* bf = buf;
-        uint32_t bcap = bufcap;
-        asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
-#pragma unroll 1
-        for (int pass = 0; pass < kMx3Passes; ++pass) {
-            if (pass * QH >= (int)nqt) break;
-            // k-loop: one expanded row fragment per k-step, reused by QH query tiles
-            const v4i_t* qf = qfrag + lane;
-            constexpr int PF = MX3_PF;  // A-fragment LDS ring depth (in MFMAs)
-            v4i_t ar[PF];
-            auto aidx = [&](int m) { return ((pass * QH + m % QH) * KS + (m / QH)) * 64; };  // MFMA m = s*QH + qt
-#pragma unroll
-            for (int m = 0; m < PF; ++m) ar[m] = qf[aidx(m)];
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                // keep the scheduler from hoisting later k-steps' LDS reads and
-                // expansions (their registers would spill)
-                __builtin_amdgcn_sched_barrier(0);
-                const v4i_t b = fp4_x32(word(c, s));
-#if defined(MX3_PRIO) && MX3_PRIO == 2
-                __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-                for (int qt = 0; qt < QH; ++qt) {
-                    const int m = s * QH + qt;
-                    const v4i_t a = ar[m % PF];
-                    if (m + PF < KS * QH) ar[m % PF] = qf[aidx(m + PF)];
-                    if (s == 0)
-                        mfma_fp4_first(acc[qt], a, b, scale1);
-                    else
-                        mfma_fp4_acc(acc[qt], a, b, scale1);
-                }
-#if defined(MX3_PRIO) && MX3_PRIO == 2
-                __builtin_amdgcn_s_setprio(0);
-#endif
-            }
-            mfma_fp4_drain();
-            // threshold epilogue of these QH query tiles
-#pragma unroll
-            for (int qh = 0; qh < QH; ++qh) {
-                const int qt = pass * QH + qh;
-                if (qt >= (int)nqt) break;
-                float amax = acc[qh][0];
-#pragma unroll
-                for (int r = 1; r < 16; ++r) amax = fmaxf(amax, acc[qh][r]);
-                if (!__ballot(amax >= tmin_lds[qt * 2 + h] && n < N)) continue;
-                float Tf[16];
-                const float* tq = tf_lds + qt * 32 + 4u * h;
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const float4 v = *(const float4*)(tq + 8 * g4);
-                    Tf[4 * g4 + 0] = v.x;
-                    Tf[4 * g4 + 1] = v.y;
-                    Tf[4 * g4 + 2] = v.z;
-                    Tf[4 * g4 + 3] = v.w;
-                }
-                float mx = acc[qh][0] - Tf[0];
-#pragma unroll
-                for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[qh][r] - Tf[r]);
-                if (!__ballot(mx >= 0.0f && n < N)) continue;
-#if defined(MX3_ABL) && MX3_ABL == 2  // timing ablation: no emission (results invalid)
-                if (mx < 1e30f) continue;
-#endif
-                const uint32_t rb = qt * 32u + 4u * h;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const bool hit = acc[qh][r] >= Tf[r] && n < N;
-                    const uint64_t m = __ballot(hit);
-                    if (m) {
-                        if (hit) {
-                            const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
-                                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
-                            const uint32_t d = (uint32_t)(kPadF - acc[qh][r]) >> 1;
-                            const uint64_t key = ((uint64_t)d << 32) | n;
-                            if (sp < kWaveStage) {
-                                st_key[wv][sp] = key;
-                                st_q[wv][sp] = (uint8_t)qi;
-                            } else {
-                                const uint32_t pos = atomicAdd(&cnt[qi], 1u);
-                                if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = key;
-                            }
-                        }
-                        wcnt += (uint32_t)__popcll(m);
-                    }
-                }
-            }
-        }
-    };
-    uint32_t sb = blockIdx.x * (kMx3Threads / 64) + wv;
-    if constexpr (kMx3Ring == 2) {
-        load(sb, ca);
-        load(sb + W, cb);
-        for (; sb < nsub; sb += 2 * W) {
-            process(sb, ca);
-            load(sb + 2 * W, ca);
-            if (sb + W < nsub) process(sb + W, cb);
-            load(sb + 3 * W, cb);
-        }
-    } else {
-        uint4 cc[W4];
-        load(sb, ca);
-        load(sb + W, cb);
-        load(sb + 2 * W, cc);
-        for (; sb < nsub; sb += 3 * W) {
-            process(sb, ca);
-            load(sb + 3 * W, ca);
-            if (sb + W < nsub) process(sb + W, cb);
-            load(sb + 4 * W, cb);
-            if (sb + 2 * W < nsub) process(sb + 2 * W, cc);
-            load(sb + 5 * W, cc);
-        }
-    }
-    // drain the clamped prefetches, then flush the staged candidates
-#if defined(MX3_ABL) && MX3_ABL == 1  // timing ablation: no flush (results invalid)
-    wcnt = 0;
-#endif
-    flush_stage_block<kMx3Threads / 64, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt,
-                                                     qbase, counts, buf, bufcap);
-}
-
-template <int W4>
-static void launch_scan_mx3_t(const Stage1Args& a, hipStream_t s) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t nsub = (a.N + kMx3Rows - 1) / kMx3Rows;
-    const uint32_t wpb = kMx3Threads / 64;
-    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus, (nsub + wpb - 1) / wpb));
-    for (uint32_t g = 0; g < a.B; g += 256) {
-        const uint32_t bg = min(256u, a.B - g);
-        hipLaunchKernelGGL((k_scan_mx3<W4>), dim3(grid), dim3(kMx3Threads), 0, s, a.codes, a.cap, a.N,
-                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
-                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
-    }
-}
-
-#endif  // GVDB_SCAN_VARIANTS
 
 // ---------------------------------------------------------------------------
 // k_scan_mx5: the stage-1 FP4 scan for D <= 768 (the bench's 10M x 768, B=256).
@@ -1613,7 +914,7 @@ static void launch_scan_mx3_t(const Stage1Args& a, hipStream_t s) {
 // The next k-step's row fragment is expanded between the current k-step's
 // MFMAs, so a wave's own VALU runs under its MFMA pipe time.
 #ifndef MX5_ABL
-#define MX5_ABL 0  // timing ablations (results invalid): 1 no epilogue, 2 no code loads, 4 no LDS A reads
+#define MX5_ABL 0  // timing ablations (results invalid): 1 no epilogue, 2 no code loads, 4 no LDS A reads, 16 no flush
 #endif
 #ifndef MX5_PRIO
 #define MX5_PRIO 0
@@ -1876,6 +1177,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
     for (int k = 0; k < kMx5Ring; ++k)
 #pragma unroll
         for (int p = 0; p < W4; ++p) asm volatile("s_waitcnt vmcnt(0)" : "+v"(ring[k][p]));
+    if constexpr (MX5_ABL & 16) return;  // timing ablation: no flush (results invalid)
     flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase, counts,
                                       buf, bufcap);
 }
@@ -2090,57 +1392,8 @@ static void launch_scan_mx4_t(const Stage1Args& a, hipStream_t s) {
     }
 }
 
-#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
-template <int W4>
-static void launch_scan_mx2_t(const Stage1Args& a, hipStream_t s) {
-    const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t grid = min(ntiles, (uint32_t)cus);
-    for (uint32_t g = 0; g < a.B; g += 256) {
-        const uint32_t bg = min(256u, a.B - g);
-        hipLaunchKernelGGL((k_scan_mx2<W4>), dim3(grid), dim3(kMfThreads), 0, s, a.codes, a.cap, a.N,
-                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
-                           a.buf + (uint64_t)g * a.bufcap, a.bufcap, a.dbg);
-    }
-}
-#endif  // GVDB_SCAN_VARIANTS
 
-#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
-template <int W4>
-static void launch_scan_mx_t(const Stage1Args& a, hipStream_t s) {
-    const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t grid = min(ntiles, (uint32_t)cus);
-    for (uint32_t g = 0; g < a.B; g += 256) {
-        const uint32_t bg = min(256u, a.B - g);
-        hipLaunchKernelGGL((k_scan_mx<W4>), dim3(grid), dim3(kMfThreads), 0, s, a.codes, a.cap, a.N,
-                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
-                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
-    }
-}
-#endif  // GVDB_SCAN_VARIANTS
 
-#ifdef GVDB_SCAN_VARIANTS  // A/B variants, not in the product build (make VARIANTS=1)
-template <int W4>
-static void launch_scan_mfma_t(const Stage1Args& a, hipStream_t s) {
-    const uint32_t ntiles = (a.N + kMfCand - 1) / kMfCand;
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t grid = min(ntiles, (uint32_t)cus);
-    // 256 queries per launch (8 waves x 32); larger batches loop over query groups
-    for (uint32_t g = 0; g < a.B; g += 256) {
-        const uint32_t bg = min(256u, a.B - g);
-        hipLaunchKernelGGL((k_scan_mfma<W4>), dim3(grid), dim3(kMfThreads), 0, s, a.codes, a.cap, a.N,
-                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
-                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
-    }
-}
-#endif  // GVDB_SCAN_VARIANTS
 
 template <int W4, int CPL>
 static void launch_scan_t(const Stage1Args& a, hipStream_t s) {
@@ -2482,6 +1735,10 @@ __global__ __launch_bounds__(kSsThreads) void k_sample_select(const uint16_t* __
         if (inreg) {
 #pragma unroll
             for (int j = 0; j < kSsPer; ++j) {
+                // the bulk of the values lies above the window: one test per 8
+                const uint32_t a = min(min(x[j].x & 0xffffu, x[j].x >> 16), min(x[j].y & 0xffffu, x[j].y >> 16));
+                const uint32_t b = min(min(x[j].z & 0xffffu, x[j].z >> 16), min(x[j].w & 0xffffu, x[j].w >> 16));
+                if (min(a, b) - base >= win && min(a, b) >= base) continue;
                 ss_count(x[j].x, base, win, hist);
                 ss_count(x[j].y, base, win, hist);
                 ss_count(x[j].z, base, win, hist);
@@ -2576,6 +1833,10 @@ static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
     hipLaunchKernelGGL((k_sample_hist<W4>), dim3(a.sample_chunks, (a.B + QT - 1) / QT), dim3(256), lds, s, a.codes,
                        a.cap, a.N, a.D, a.sample_stride, a.qcodes, a.B, QT, a.hist);
 }
+
+#ifdef GVDB_SCAN_VARIANTS  // the A/B stage-1 scans (make VARIANTS=1), kept out of the product source
+#include "gvdb_scan_variants.inc"
+#endif
 
 static bool getenv_flag_eq(const char* name, const char* v) {  // read per launch (tests switch it)
     const char* e = getenv(name);
@@ -2738,10 +1999,16 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     }
     GVDB_LAUNCH_CHECK();
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
-    const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
-    hipLaunchKernelGGL(k_select, dim3(a.B), dim3(256), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R, a.codes, a.cap,
-                       a.N, W4, a.qcodes, a.fail, a.any_fail, a.s1_rows, a.s1_dist, a.force_rescan, a.keys_out);
-    GVDB_LAUNCH_CHECK();
+    if (a.big_select) {
+        hipError_t e = launch_select_big(a, s);
+        if (e != hipSuccess) return e;
+    } else {
+        const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
+        hipLaunchKernelGGL(k_select, dim3(a.B), dim3(256), lds, s, a.counts, a.buf, a.bufcap, a.D, a.R, a.codes,
+                           a.cap, a.N, W4, a.qcodes, a.fail, a.any_fail, a.s1_rows, a.s1_dist, a.force_rescan,
+                           a.keys_out, a.keys_stride);
+        GVDB_LAUNCH_CHECK();
+    }
     if (a.ev) (void)hipEventRecord(a.ev[3], s);
     return hipSuccess;
 }
@@ -3270,7 +2537,8 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t small_slots = (uint64_t)a.B * ((a.R + kRsRows - 1) / kRsRows);
-    if (small_slots <= rerank_small_max() && std::min(a.qlen, a.clen) <= kRsMaxLen && small_slots < (1ull << 31)) {
+    if ((small_slots <= rerank_small_max() || (a.short_lists && a.counts)) && std::min(a.qlen, a.clen) <= kRsMaxLen &&
+        small_slots < (1ull << 31)) {
         hipLaunchKernelGGL(k_rerank_small, dim3((uint32_t)small_slots), dim3(kRsThreads), 0, s, a.rows, a.clen,
                            a.norms, a.q, a.qlen, a.s1_rows, a.B, a.R, a.counts, a.kind, a.scores);
         GVDB_LAUNCH_CHECK();

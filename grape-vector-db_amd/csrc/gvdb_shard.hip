@@ -228,12 +228,9 @@ __global__ __launch_bounds__(256) void k_shard_final(const uint32_t* __restrict_
                                                      uint32_t G, uint32_t B, uint32_t k, uint64_t* __restrict__ out_ids,
                                                      float* __restrict__ out_scores, uint32_t* __restrict__ out_n) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // [next_pow2(G * k)]
-    __shared__ uint32_t s_bad, s_n;
+    __shared__ uint32_t s_bad;
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
-    if (tid == 0) {
-        s_bad = 0u;
-        s_n = 0u;
-    }
+    if (tid == 0) s_bad = 0u;
     __syncthreads();
     for (uint32_t g = tid; g < G; g += 256) {
         const uint32_t* meta = gathered + (uint64_t)g * words2 + 4ull * B * k;
@@ -441,6 +438,7 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
         rr.kind = kScoreCosine;
         rr.scores = scores;
         rr.counts = own_cnt;
+        rr.short_lists = R <= 64u * G;  // ~R/G owned rows per query: 16-row blocks, loads all in flight
         e = launch_rerank(rr, s);
         if (e != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard rerank: ") + hipGetErrorString(e));
     } else if (hipMemsetAsync(own_cnt, 0, B * 4, s) != hipSuccess) {

@@ -53,6 +53,8 @@ _SIG = {
     "bm25o_search_batch": (None, [C.c_void_p, P, P, P, u64, u64, P, P, P, C.c_int]),
     "bm25o_add_csr": (None, [C.c_void_p, P, P, P, P, P, u64]),
     "hnsw_free": (None, [C.c_void_p]),
+    "hnsw_build2": (C.c_void_p, [P, u64, u32, u32, u32, u64, C.c_int, C.c_int]),
+    "hnsw_set_fast": (None, [C.c_void_p, C.c_int]),
     "hnsw_search": (C.c_int, [C.c_void_p, P, u64, u32, u32, C.c_int, P, P, P]),
 }
 
@@ -269,15 +271,18 @@ class Hnsw:
     baseline of HnswVectorIndex (index.rs:140-154, 212-231).  Distances are L2
     (index.rs:64-79).  Recall-only parity; the rows array must stay alive."""
 
-    def __init__(self, rows, M=32, ef_construction=100, seed=0x6772617065, threads=0):
+    def __init__(self, rows, M=32, ef_construction=100, seed=0x6772617065, threads=0, fast=False):
+        """fast=True builds with re-associated (AVX2) L2 sums instead of the
+        reference's strict fold (hnsw_oracle.cpp, l2_fast)."""
         self.rows = _f32(rows)
         n, d = self.rows.shape
         self.d = d
-        self.h = lib().hnsw_build(_p(self.rows), n, d, M, ef_construction, seed, threads)
+        self.h = lib().hnsw_build2(_p(self.rows), n, d, M, ef_construction, seed, threads, int(fast))
         if not self.h:
             raise ValueError("hnsw_build failed")
 
-    def search(self, q, k=10, ef_search=100, threads=0):
+    def search(self, q, k=10, ef_search=100, threads=0, fast=False):
+        lib().hnsw_set_fast(self.h, int(fast))
         q = _f32(q).reshape(-1, self.d)
         B = q.shape[0]
         ids = np.zeros((B, k), dtype=np.uint64)

@@ -77,6 +77,44 @@ void l2x4(const float* q, const float* const* r, uint32_t d, float* out) {
     out[3] = std::sqrt(s3);
 }
 
+// "fast" distances (opt-in, hnsw_build2 / hnsw_set_fast): the same L2 with the
+// sum split over 32 partial sums (AVX2 lanes), i.e. re-associated -- results
+// differ from the strict fold in the last bits.  Used to BUILD the 10M-row
+// graph in reasonable time (the graph is random anyway: the crate builds it in
+// parallel from an OS seed) and as the optimised-CPU point of the baseline;
+// the reference-faithful strict fold stays the default.
+typedef float v8f __attribute__((vector_size(32)));
+__attribute__((target("avx2"))) float l2_fast(const float* a, const float* b, uint32_t d) {
+    v8f s0 = {0, 0, 0, 0, 0, 0, 0, 0}, s1 = s0, s2 = s0, s3 = s0;
+    uint32_t i = 0;
+    for (; i + 32 <= d; i += 32) {
+        v8f x0, x1, x2, x3, y0, y1, y2, y3;
+        std::memcpy(&x0, a + i, 32);
+        std::memcpy(&x1, a + i + 8, 32);
+        std::memcpy(&x2, a + i + 16, 32);
+        std::memcpy(&x3, a + i + 24, 32);
+        std::memcpy(&y0, b + i, 32);
+        std::memcpy(&y1, b + i + 8, 32);
+        std::memcpy(&y2, b + i + 16, 32);
+        std::memcpy(&y3, b + i + 24, 32);
+        x0 -= y0;
+        x1 -= y1;
+        x2 -= y2;
+        x3 -= y3;
+        s0 += x0 * x0;
+        s1 += x1 * x1;
+        s2 += x2 * x2;
+        s3 += x3 * x3;
+    }
+    const v8f t = (s0 + s1) + (s2 + s3);
+    float s = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+    for (; i < d; ++i) {
+        const float u = a[i] - b[i];
+        s = s + u * u;
+    }
+    return std::sqrt(s);
+}
+
 uint64_t splitmix(uint64_t& s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -106,6 +144,16 @@ struct Hnsw {
     std::vector<std::vector<float>> upd;
     std::vector<uint32_t> upslot;               // point -> slot in upper layers (or ~0)
     std::vector<std::mutex> locks;
+    bool fast = false;  // l2_fast instead of the strict fold
+
+    void dist4(const float* q, const float* const* r4, float* out) const {
+        if (fast) {
+            for (int t = 0; t < 4; ++t) out[t] = l2_fast(q, r4[t], d);
+        } else {
+            l2x4(q, r4, d, out);
+        }
+    }
+    float dist_rows(const float* a, const float* b) const { return fast ? l2_fast(a, b, d) : l2(a, b, d); }
 
     uint32_t cap(uint32_t layer) const { return layer == 0 ? 2 * M : M; }
     uint32_t* links(uint32_t p, uint32_t layer, uint32_t*& cnt, float** ds = nullptr) {
@@ -119,7 +167,7 @@ struct Hnsw {
         if (ds) *ds = &upd[layer - 1][(uint64_t)s * M];
         return &up[layer - 1][(uint64_t)s * M];
     }
-    float dist(const float* q, uint32_t p) const { return l2(q, rows + (uint64_t)p * d, d); }
+    float dist(const float* q, uint32_t p) const { return dist_rows(q, rows + (uint64_t)p * d); }
 
     // ef-beam on one layer from the given entry set; returns ascending results
     std::vector<Cand> beam(const float* q, const std::vector<Cand>& eps, uint32_t ef, uint32_t layer,
@@ -165,7 +213,7 @@ struct Hnsw {
             for (; j + 4 <= todo.size(); j += 4) {
                 const float* r4[4];
                 for (int t = 0; t < 4; ++t) r4[t] = rows + (uint64_t)todo[j + t] * d;
-                l2x4(q, r4, d, &dv4[j]);
+                dist4(q, r4, &dv4[j]);
             }
             for (; j < todo.size(); ++j) dv4[j] = dist(q, todo[j]);
             for (size_t t = 0; t < todo.size(); ++t) {
@@ -198,11 +246,11 @@ struct Hnsw {
                 const float* r4[4];
                 float d4[4];
                 for (int t = 0; t < 4; ++t) r4[t] = rows + (uint64_t)keep[j + t].id * d;
-                l2x4(x, r4, d, d4);
+                dist4(x, r4, d4);
                 for (int t = 0; t < 4; ++t) good = good && !(d4[t] < c.d);
             }
             for (; good && j < keep.size(); ++j)
-                if (l2(x, rows + (uint64_t)keep[j].id * d, d) < c.d) good = false;
+                if (dist_rows(x, rows + (uint64_t)keep[j].id * d) < c.d) good = false;
             (good ? keep : pruned).push_back(c);
         }
         for (size_t i = 0; i < pruned.size() && keep.size() < m; ++i) keep.push_back(pruned[i]);
@@ -262,11 +310,22 @@ struct Hnsw {
 
 extern "C" {
 
+void* hnsw_build2(const float* rows, uint64_t n, uint32_t d, uint32_t M, uint32_t ef_construction, uint64_t seed,
+                  int threads, int fast);
 // Build over caller-owned rows (must outlive the handle).  threads<=0 -> all cores.
 void* hnsw_build(const float* rows, uint64_t n, uint32_t d, uint32_t M, uint32_t ef_construction, uint64_t seed,
                  int threads) {
+    return hnsw_build2(rows, n, d, M, ef_construction, seed, threads, 0);
+}
+// fast = 1: build with l2_fast (see above)
+void hnsw_set_fast(void* p, int fast) {
+    if (p) ((Hnsw*)p)->fast = fast != 0;
+}
+void* hnsw_build2(const float* rows, uint64_t n, uint32_t d, uint32_t M, uint32_t ef_construction, uint64_t seed,
+                  int threads, int fast) {
     if (!rows || n == 0 || d == 0 || n > 0xFFFFFFFFull) return nullptr;
     Hnsw* h = new Hnsw;
+    h->fast = fast != 0;
     h->rows = rows;
     h->n = n;
     h->d = d;

@@ -1,0 +1,94 @@
+#!/bin/bash
+# One entry point for the GPU-box runs (gpurun -- 'bash scripts/gpu.sh TASK[+TASK...] [ARGS]').
+# Every step runs under its own time limit; the first failing step ends the run.
+#
+#   tests        pytest -m gpu (all GPU tests, one process)            -> gpurun_out/pytest_gpu.log
+#   tests:EXPR   pytest -m gpu -k EXPR
+#   smoke        __graft_entry__.smoke()                                -> gpurun_out/smoke.log
+#   bench        python bench.py (the driver's default command)         -> gpurun_out/bench.json / .log
+#   benchprof    the same command under rocprofv3 --kernel-trace --stats -> gpurun_out/prof_bench/
+#   b256         scripts/b256_timing.py at 10M (SHARD_N / RCCL env pass through)
+#   c3           scripts/c3_emulate.py (config 3, 8 shards on one GPU)  -> gpurun_out/c3.json / .log
+#   c3prof       c3_emulate (no single index, no oracle) under rocprofv3 -> gpurun_out/prof_c3/
+#   c4           scripts/c4_emulate.py (config 4, 8 shards of 1.25M x 3072)
+#   hybrid       scripts/bench_hybrid.py (config 5)                     -> gpurun_out/hybrid.json / .log
+#   hnsw10m      scripts/hnsw10m_gpu.py (GPU side of the 10M equal-recall experiment)
+#   pmc:NAME:REGEX:CMD   rocprofv3 --pmc passes (one counter set per run) over python3 CMD (spaces as ','),
+#                        rows whose kernel name matches REGEX -> gpurun_out/pmc_NAME/pmc.json
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+
+run() {  # run LIMIT_S LOG cmd...
+    local lim=$1 log=$2
+    shift 2
+    echo "[gpu.sh] $(date +%T) $*" >&2
+    timeout -k 10 "$lim" "$@" > "$log" 2>&1
+    local rc=$?
+    if [ $rc -ne 0 ]; then
+        echo "[gpu.sh] FAILED rc=$rc: $*" >&2
+        tail -30 "$log" >&2
+        exit $rc
+    fi
+}
+
+PMC_SETS=("GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU"
+          "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT"
+          "FETCH_SIZE" "WRITE_SIZE")
+
+IFS='+' read -ra TASKS <<< "$1"
+for t in "${TASKS[@]}"; do
+    case "$t" in
+        tests)
+            run 1500 gpurun_out/pytest_gpu.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+            grep -E "passed|failed" gpurun_out/pytest_gpu.log | tail -2 ;;
+        tests:*)
+            run 1500 gpurun_out/pytest_gpu_k.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${t#tests:}"
+            grep -E "passed|failed" gpurun_out/pytest_gpu_k.log | tail -2 ;;
+        smoke)
+            run 300 gpurun_out/smoke.log python -u -c "import __graft_entry__ as g; g.smoke()"
+            tail -3 gpurun_out/smoke.log ;;
+        bench)
+            run 900 gpurun_out/bench.log python -u bench.py
+            grep '^{' gpurun_out/bench.log > gpurun_out/bench.json; tail -c 600 gpurun_out/bench.json; echo ;;
+        benchprof)
+            run 900 gpurun_out/benchprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py
+            grep '^{' gpurun_out/benchprof.log > gpurun_out/benchprof.json || true ;;
+        b256)
+            run 600 gpurun_out/b256.log python3 -u scripts/b256_timing.py
+            grep -v amdgpu.ids gpurun_out/b256.log | tail -4 ;;
+        c3)
+            run 900 gpurun_out/c3.log python -u scripts/c3_emulate.py
+            grep '^{' gpurun_out/c3.log > gpurun_out/c3.json; grep '^\[c3\]' gpurun_out/c3.log | tail -4 ;;
+        c3prof)
+            run 600 gpurun_out/c3prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10 ;;
+        c4)
+            run 1100 gpurun_out/c4.log python -u scripts/c4_emulate.py
+            grep '^{' gpurun_out/c4.log > gpurun_out/c4.json; tail -3 gpurun_out/c4.log ;;
+        hybrid)
+            run 900 gpurun_out/hybrid.log python -u scripts/bench_hybrid.py
+            grep '^{' gpurun_out/hybrid.log > gpurun_out/hybrid.json; tail -3 gpurun_out/hybrid.log ;;
+        hnsw10m)
+            run 1100 gpurun_out/hnsw10m_gpu.log python -u scripts/hnsw10m_gpu.py
+            tail -5 gpurun_out/hnsw10m_gpu.log ;;
+        pmc:*)
+            IFS=':' read -r _ name regex cmd <<< "$t"
+            cmd=${cmd//,/ }
+            out=gpurun_out/pmc_$name
+            mkdir -p "$out"
+            i=0
+            for set in "${PMC_SETS[@]}"; do
+                i=$((i + 1))
+                # shellcheck disable=SC2086
+                run 300 "$out/p$i.log" rocprofv3 --pmc $set --output-format csv -d "$out/p$i" -o run -- python3 $cmd
+                f=$(find "$out/p$i" -name "*counter_collection.csv" | head -1)
+                if [ -n "$f" ]; then head -1 "$f" > "$out/counters_p$i.csv"; grep -E "$regex" "$f" >> "$out/counters_p$i.csv" || true; fi
+                rm -rf "${out:?}/p$i"
+            done
+            python3 scripts/pmc_summary.py "$out" --json "$out/pmc.json" | tail -40 ;;
+        *)
+            echo "[gpu.sh] unknown task $t" >&2
+            exit 2 ;;
+    esac
+done

@@ -203,6 +203,33 @@ def test_index_search_matches_oracle(g, oracle_mod, N, D, B, R, k, metric):
     assert same_f32(sc[:, :kk], rs[:, :kk])
 
 
+@pytest.mark.parametrize("N,D,B,ratio,k,force", [(200_000, 768, 8, 0.1, 10, False), (200_000, 768, 128, 0.1, 10, False),
+                                                  (400_000, 256, 96, 0.05, 25, False), (60_000, 200, 4, 0.3, 300, False),
+                                                  (50_000, 128, 3, 0.2, 10, True)])
+def test_default_rescore_ratio_large_r_matches_oracle(g, oracle_mod, monkeypatch, N, D, B, ratio, k, force):
+    """The reference's DEFAULT depth R = (N as f32 * 0.1) as usize
+    (quantization.rs:27,178) -- R = 20K at 200K rows, beyond the LDS select --
+    on the batched large-R path (gvdb_bigr.hip: k_select_big's exact top-R
+    membership, rerank, k_topk_big): ids and cosine bits equal the oracle's
+    multi_stage_search; B = 128 / 96 take the FP4-MFMA scan, 400K rows a
+    sampled threshold, k = 300 > the tie LDS window's usual size, and a forced
+    device-side rescan (GVDB_FORCE_RESCAN) the all-rows fallback."""
+    if force:
+        monkeypatch.setenv("GVDB_FORCE_RESCAN", "1")
+    x = rng_rows(N + D, N, D, dup=200)
+    Q = rng_rows(D + 17, B, D)
+    Q[0] = x[123]
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=ratio))
+    R = int(np.float32(N) * np.float32(ratio))
+    assert R > 8192
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (n == k).all()
+    assert (ids == ri[:, :k]).all()
+    assert same_f32(sc, rs[:, :k])
+
+
 def test_index_semantics(g):
     ix = g.GpuVectorIndex()
     with pytest.raises(g.IndexNotBuilt):  # index.rs:213
