@@ -9,10 +9,12 @@ reported beside it.  A "step" = one search call over one 256-query batch
 with the corpus already resident in HBM.
 
 N GPUs (torchrun, one process per GPU): the corpus is sharded by contiguous
-row ranges (the same 10M rows in total: strong scaling); every step each
-rank computes its local stage-1 top-R with exact cosines, ONE RCCL all-gather
-moves the (id, Hamming, cosine) triplets, and every rank merges them with the
-exact sharded merge (bit-identical to the single-GPU result).
+row ranges (the same 10M rows in total: strong scaling); every step runs the
+two-exchange protocol inside libgvdb (gvdb_index_search_sharded_device): local
+stage-1 keys -> ncclAllGather -> global top-R, rerank of the rows each rank
+owns, local top-k -> ncclAllGather -> merged top-k, bit-identical to the
+single-GPU result.  The exact flat search (recall 1.0) is reported beside it
+through the same communicator.
 
 Prints ONE JSON line on rank 0.
 """
@@ -109,7 +111,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
         assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
         comm_info = {"world_size": dist.get_world_size(), "torch_backend": dist.get_backend(),
-                     "merge_collective": "ncclAllGather inside libgvdb (gvdb_index_search_sharded_device)"}
+                     "merge_collective": "two ncclAllGather inside libgvdb (gvdb_index_search_sharded_device: "
+                                         "stage-1 keys B*R*8 B, then local top-k B*k*16 B per rank)"}
         log(f"[bench] world={dist.get_world_size()} backend={dist.get_backend()} rank={rank} device={local_rank}")
     elif args.gpus != 1:
         raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes (WORLD_SIZE=1)")
@@ -261,15 +264,17 @@ def main():
             "recall_at_10": recall_at(f1, truth[: len(f1)]),
             "same_results_as_batch": bool((f1 == found[: len(f1)]).all()),
             "roofline": {
-                "kernel": "k_scan (stage-1 BQ Hamming filter), batch 1",
+                "kernel": "k_b1_scan (stage-1 BQ Hamming filter, batch 1: v_xor + v_bcnt, non-temporal code loads)",
                 "bound": "hbm",
                 "achieved": code_bytes / (b1_scan_avg * 1e-3) / 1e9,
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": code_bytes / (b1_scan_avg * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                "traffic": pmc_traffic("gvdb::k_scan<", n_local, D),
+                "traffic": pmc_traffic("gvdb::k_b1_scan<", n_local, D),
                 "avg_launch_ms": b1_scan_avg,
                 "algorithmic_bytes_per_launch": code_bytes,
+                "source": "avg_launch_ms: HIP events around each k_b1_scan launch on its stream; traffic: "
+                          "rocprofv3 --pmc FETCH_SIZE x 2 (gfx950 streaming correction), " + PMC_FILE,
             },
         }
 
@@ -311,6 +316,33 @@ def main():
                 run_point(f"bq R={r}", gvdb.SearchParams(rescore_count=r), qp, ptruth, "planted (x_j + 0.1 n, |n| = 1)")
             run_point("exact flat (i8/bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1),
                       qp, ptruth, "planted (x_j + 0.1 n, |n| = 1)")
+
+    # ---------------- N GPUs: the exact flat operating point (recall 1.0) through the
+    # same communicator path (each rank's exact top-k, one ncclAllGather, merge)
+    if world > 1 and args.points:
+        import torch.distributed as dist
+        from gvdb.sharded import RcclShardedSearch
+
+        points = [{"search": f"bq R={R} (two-exchange)", "queries": "iid", "qps": qps,
+                   "ms_per_step": 1e3 * t_max / args.steps, "recall_at_10": rec, "steps": args.steps}]
+        shf = RcclShardedSearch(ix, R, k, params=gvdb.SearchParams(mode=1))
+        fi = torch.zeros((B, k), dtype=torch.int64, device=dev)
+        fs = torch.zeros((B, k), dtype=torch.float32, device=dev)
+        shf.search_into(q, fi, fs, None)
+        op_steps = max(2, args.steps // 4)
+        barrier()
+        tp = time.perf_counter()
+        for _ in range(op_steps):
+            shf.search_into(q, fi, fs, None)
+        torch.cuda.synchronize()
+        tp = time.perf_counter() - tp
+        tt = torch.tensor([tp], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tp = float(tt.item())
+        points.append({"search": "exact flat (sharded: each rank's certified exact top-k, ncclAllGather, merge)",
+                       "queries": "iid", "qps": B * op_steps / tp, "ms_per_step": 1e3 * tp / op_steps,
+                       "recall_at_10": recall_at(fi.cpu().numpy(), truth), "steps": op_steps})
+        shf.close()
 
     # ---------------- roofline of the dominant kernel (stage-1 scan at batch B)
     scan_avg = scan_ms / max(scan_n, 1)
@@ -355,6 +387,9 @@ def main():
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
         "hbm_bytes_per_launch": n_local * w4 * 16 * scan_launches,
+        "source": f"avg_launch_ms: HIP events around each scan launch of the {args.steps} timed steps, on the "
+                  f"search stream; the rocprofv3 kernel trace of this command gives the same launches' average "
+                  f"(scripts/roofline_from_trace.py); traffic: rocprofv3 --pmc FETCH_SIZE x 2, {PMC_FILE}",
         "note": "batch-256 stage 1 is compute-bound (96 B of codes per row read once per batch); "
                 "the HBM-bound batch-1 scan is in batch1.roofline",
     })
@@ -365,7 +400,7 @@ def main():
     if want_cpu:
         import oracle
 
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads = cpu_share()
         qn = q.cpu().numpy()
         qbits = oracle.quantize(qn)
         ratio = np.float32(R) / np.float32(N)
@@ -409,7 +444,7 @@ def main():
     if want_cpu and args.hnsw_rows > 0:
         import oracle
 
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads = cpu_share()
         ns = min(args.hnsw_rows, N)
         xs = np.ascontiguousarray(host_rows[:ns])
         qn = q.cpu().numpy()
@@ -517,14 +552,17 @@ def main():
         dist.destroy_process_group()
 
 
+PMC_FILE = "profiles/r03/pmc_bench_10M.json"
+
+
 def pmc_traffic(kernel_prefix, n_local, D):
-    """HBM read bytes per launch of `kernel_prefix` from the committed PMC passes
-    (profiles/r02/pmc_10M_mx5.json, then profiles/r01/pmc_10M.json: rocprofv3 --pmc
-    FETCH_SIZE, x2 gfx950 streaming correction), only when collected at this
-    workload's shard size."""
+    """HBM read bytes per launch of `kernel_prefix` from the committed PMC pass of
+    this round (PMC_FILE: rocprofv3 --pmc FETCH_SIZE over bench.py's own command,
+    x2 gfx950 streaming correction), only when collected at this workload's
+    shard size."""
     if n_local != 10_000_000 or D != 768:
         return None
-    for rel in (("r02", "pmc_10M_mx5.json"), ("r01", "pmc_10M.json")):
+    for rel in (PMC_FILE.split("/")[1:],):
         path = os.path.join(ROOT, "profiles", *rel)
         if not os.path.exists(path):
             continue
@@ -534,6 +572,15 @@ def pmc_traffic(kernel_prefix, n_local, D):
             if name.startswith(kernel_prefix) and "hbm_read_bytes_per_launch" in d:
                 return d["hbm_read_bytes_per_launch"]
     return None
+
+
+def cpu_share():
+    """Host cores this process may use: the job's CPU share (OMP_NUM_THREADS,
+    16 per GPU on the GPU box, where nproc reports the whole machine), else
+    the affinity mask."""
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    aff = len(os.sched_getaffinity(0))
+    return max(1, min(aff, int(omp))) if omp.isdigit() and int(omp) > 0 else aff
 
 
 def config_label(n, d):
