@@ -603,6 +603,9 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     } else {
         if (a.d_qwords) {
             HIP_TRY(hipMemcpyAsync(ws.qcodes.p, a.d_qwords, (size_t)B * W4 * 16, hipMemcpyDeviceToDevice, s), "qcopy");
+        } else if (s1.mfma_scan && (R <= kSelectLdsCap || big) && a.qlen == v.D) {
+            s1.qf32 = a.d_q;  // k_qprep packs the queries with the operand build (one launch)
+            s1.qthr = a.thr;
         } else {
             HIP_TRY(launch_pack(a.d_q, B, v.D, a.thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
         }
@@ -2069,7 +2072,12 @@ gvdb_status gvdb::shard_stage1_keys(const gvdb_index* ix, const float* d_q, uint
     Stage1Args s1{};
     st = prepare_stage1(ws, s1, (uint32_t)B, dim, Rl, (uint32_t)ix->n, s, true);
     if (st != GVDB_OK) return st;
-    HIP_TRY(launch_pack(d_q, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
+    if (s1.mfma_scan) {
+        s1.qf32 = d_q;  // packed by k_qprep
+        s1.qthr = ix->thr;
+    } else {
+        HIP_TRY(launch_pack(d_q, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
+    }
     bool timed = false;
     {
         std::lock_guard<std::mutex> lk(timing().mu);

@@ -93,6 +93,8 @@ struct Stage1Args {
     uint32_t* zero;          // mfma_scan: words k_qfrag zeroes before stage 1 (else the caller memsets)
     uint32_t nzero;
     int big_select;          // R > kSelectLdsCap: k_select_big (unordered exact top-R membership)
+    const float* qf32;       // mfma_scan: the f32 queries [B][D] -- k_qprep packs qcodes itself
+    float qthr;              //   (packing threshold)
 };
 // ---- large rescore depth (gvdb_bigr.hip): R up to 2^20, D < 4096, k <= 1024 --------
 constexpr uint32_t kBigRMax = 1u << 20;
@@ -341,16 +343,13 @@ gvdb_status shard_stage1_keys(const gvdb_index* ix, const float* d_q, uint64_t B
 //                          reff u32 [B] | err u32 | pad
 inline uint64_t shard_words1(uint64_t B, uint64_t R) { return (2 * B * R + B + 1 + 1) & ~1ull; }
 inline uint64_t shard_words2(uint64_t B, uint64_t k) { return (4 * B * k + 2 * B + 1 + 1) & ~1ull; }
-// merge of the gathered exchange-1 blocks -> this rank's owned entries of the
-// global top-R: own_rows / own_pos [B][R], own_cnt [B], reff [B] (= min(R, total))
-hipError_t launch_shard_merge(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
-                              uint32_t R, uint32_t D, uint32_t* own_rows, uint32_t* own_pos, uint32_t* own_cnt,
-                              uint32_t* reff, hipStream_t s);
-// owned entries' exact cosines -> this rank's exchange-2 block (local top-k by
-// (cos desc, position asc))
-hipError_t launch_shard_local_topk(const float* scores, const uint32_t* own_rows, const uint32_t* own_pos,
-                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t R, uint32_t k,
-                                   const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s);
+// gathered exchange-1 blocks -> this rank's exchange-2 block: global top-R, exact
+// cosine of the owned rows, local top-k (one kernel per query; gvdb_shard.hip).
+// rows / norms / ids may be null for a shard that owns nothing; opos / orow: [B][R]
+hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
+                               uint32_t R, uint32_t D, const float* rows, const float* norms, const uint64_t* ids,
+                               const float* queries, uint32_t k, uint32_t err, uint32_t* block2, uint32_t* opos,
+                               uint32_t* orow, hipStream_t s);
 // sharded FLAT: gathered blocks of the ranks' exact top-k -> merged top-k
 //   block F (sharded FLAT): ids u64 [B][k] | scores f32 [B][k] | counts [B] | err | pad
 inline uint64_t shard_words_flat(uint64_t B, uint64_t k) { return (3 * B * k + B + 1 + 1) & ~1ull; }

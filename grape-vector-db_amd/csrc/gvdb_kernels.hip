@@ -1122,14 +1122,23 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
             // non-negative as an int (acc is never -0.0: the seed thr - |q| is +0 when
             // zero and an exact zero sum of nonzero terms rounds to +0); v_and3_b32, no
             // canonicalising max
-            int aand = __float_as_int(A[0]);
+            // four partial ANDs (same 15 v_and as one chain): a tile with a hit
+            // then tests its 16 accumulators only in the groups of 4 that hold one
+            int pa[4];
 #pragma unroll
-            for (int r = 1; r < 16; ++r) aand &= __float_as_int(A[r]);
+            for (int g = 0; g < 4; ++g)
+                pa[g] = __float_as_int(A[4 * g]) & __float_as_int(A[4 * g + 1]) & __float_as_int(A[4 * g + 2]) &
+                        __float_as_int(A[4 * g + 3]);
+            const int aand = (pa[0] & pa[1]) & (pa[2] & pa[3]);
             if (!__ballot(((MX5_ABL & 8) ? false : aand >= 0) && n < N)) continue;
             uint32_t rb = qt * 32u + 4u * h;
             asm volatile("" : "+v"(rb));  // keeps the 128 per-(tile, r) query indices from being hoisted
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
+                if ((r & 3) == 0 && !__ballot(pa[r >> 2] >= 0 && n < N)) {
+                    r += 3;  // no hit in this group of 4
+                    continue;
+                }
                 const bool hit = A[r] >= 0.0f && n < N;
                 const uint64_t m = __ballot(hit);
                 if (m) {
@@ -1196,8 +1205,56 @@ static uint32_t cu_count() {
     return (uint32_t)cached[dev];
 }
 
+// k_qfrag with the query packing fused in: one wave per query slot of the
+// groups (ceil(B/256)*256 slots).  The wave packs its query like k_pack (a
+// ballot per 64 dims: bit = x > thr, Msb0 words, pad bits 0), writes the words
+// [B][4*W4] (the VALU rescan / k_select read them), |q|, and the query's 2*KS
+// FP4 fragments (slots past B: zero words) -- one launch instead of two.
+template <int W4>
+__global__ __launch_bounds__(64) void k_qprep(const float* __restrict__ qf, uint32_t D, float thr, uint32_t B,
+                                              uint32_t* __restrict__ qwords, v4i_t* __restrict__ qfrag,
+                                              uint32_t* __restrict__ qpc, uint32_t* __restrict__ zero,
+                                              uint32_t nzero) {
+    constexpr int KW = 4 * W4, KS = KW / 2, QT = 8;
+    constexpr uint32_t kPer = QT * KS * 64;
+    __shared__ uint32_t w[KW];
+    const uint32_t slot = blockIdx.x, lane = threadIdx.x;
+    for (uint32_t i = slot * 64u + lane; i < nzero; i += gridDim.x * 64u) zero[i] = 0u;
+    const bool live = slot < B;
+    for (uint32_t c = 0; c < (uint32_t)KW / 2; ++c) {  // 64 dims per ballot = 2 words
+        const uint32_t d = 64u * c + lane;
+        const bool bit = live && d < D && qf[(uint64_t)slot * D + d] > thr;
+        const uint64_t m = __ballot(bit);
+        if (lane == 0) {
+            w[2 * c] = msb0_word((uint32_t)m);
+            w[2 * c + 1] = msb0_word((uint32_t)(m >> 32));
+        }
+    }
+    __syncthreads();
+    if (live && lane < (uint32_t)KW) qwords[(uint64_t)slot * KW + lane] = w[lane];
+    if (lane == 0) {
+        uint32_t pc = 0;
+#pragma unroll
+        for (int i = 0; i < KW; ++i) pc += __popc(w[i]);
+        qpc[slot] = live ? pc : 0u;
+    }
+    // fragment (s, qt, l) with l = 32 h + j holds word 4(s/2) + 2h + (s&1) of query 32 qt + j
+    const uint32_t g = slot / 256u, qt = (slot % 256u) / 32u, j = slot % 32u;
+    for (uint32_t t = lane; t < (uint32_t)(2 * KS); t += 64u) {
+        const uint32_t s = t >> 1, h = t & 1u;
+        const uint32_t wi = 4u * (s >> 1) + 2u * h + (s & 1u);
+        qfrag[(uint64_t)g * kPer + (s * QT + qt) * 64u + h * 32u + j] = fp4_query_pm(w[wi]);
+    }
+}
+
 template <int W4>
 static void launch_qfrag_t(const Stage1Args& a, hipStream_t s) {
+    if (a.qf32) {
+        const uint32_t ng = (a.B + 255u) / 256u;
+        hipLaunchKernelGGL((k_qprep<W4>), dim3(ng * 256u), dim3(64), 0, s, a.qf32, a.D, a.qthr, a.B,
+                           (uint32_t*)a.qcodes, (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero);
+        return;
+    }
     constexpr uint32_t kPer = 8u * (2u * W4) * 64u;
     const uint32_t ng = (a.B + 255u) / 256u;
     const uint32_t n = std::max<uint32_t>(ng * kPer, a.nzero);
@@ -1577,12 +1634,16 @@ static void launch_sample_mx_t(const Stage1Args& a, hipStream_t s) {
 // batch without histogram atomics.  k_sample_mx spends most of its time in
 // the per-pair LDS-atomic histogram epilogue (~1 atomic per 2 pairs on i.i.d.
 // codes); here the FP4 MFMA (k_scan_mx5's operands, accumulators seeded with
-// -|q|, so acc = -Hamming) writes every sampled distance as a u16 into a dense
-// [B][S] block, and one block per query then finds the target-th smallest
-// distance: a min pass, then histograms of narrow windows above the min (only
-// the low tail does LDS atomics; the window doubles while the target is not
-// reached).  T[q] = smallest t with count(d <= t) >= target over the same
-// sample rows as k_sample_hist, so the thresholds equal the VALU form's.
+// -|q|, so acc = -Hamming) computes every sampled distance and keeps, per
+// query and group of 16 consecutive sample rows, their MINIMUM (u16, via a
+// per-wave LDS transpose): a dense [B][S/16] block, 1/16 of the distances.
+// One block per query then takes the target-th smallest group minimum: a min
+// pass, then histograms of narrow windows above the min (only the low tail
+// does LDS atomics; the window doubles while the target is not reached).
+// Every group whose minimum is <= T holds a row with d <= T, so at least
+// `target` sample rows lie at or below T: T is never below the VALU form's
+// threshold (equal unless two of the target smallest distances share a
+// group), and k_select certifies the top-R whatever T is.
 template <int W4>
 __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_dense(const uint4* __restrict__ codes, uint64_t cap,
                                                                uint32_t N, uint32_t stride, uint32_t nsub,
@@ -1595,6 +1656,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_dense(const uint4* __
     constexpr int NW = kMx5Threads / 64;
     __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
     __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
+    __shared__ __attribute__((aligned(16))) uint16_t tr_lds[NW][32 * 32];  // per wave: [query][row] of one tile
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t h = lane >> 5;
@@ -1605,6 +1667,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_dense(const uint4* __
         const uint32_t qt = q >> 5, j = q & 31u, hh = (j >> 2) & 1u, r = (j & 3u) + 4u * (j >> 3);
         seed_lds[(qt * 2 + hh) * 16 + r] = q < B ? -(float)qpc[q] : -1.0e6f;
     }
+    uint16_t* tw = tr_lds[wv];
     __syncthreads();
     const uint32_t nqt = (B + 31u) / 32u;
     const uint32_t W = gridDim.x * NW;
@@ -1651,30 +1714,44 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_dense(const uint4* __
             }
         }
         mfma_fp4_drain_acc(acc);
-        // lane (h, j) holds row s0 + j of queries qt*32 + 8(r/4) + 4h + (r%4):
-        // per register, 32 lanes write one query's 64 contiguous bytes.  Rows
-        // past N (the last chunk of an unsampled small shard) read as 0xffff.
+        // lane (h, j) holds row s0 + j of queries qt*32 + 8(r/4) + 4h + (r%4).
+        // Transposed through the wave's LDS tile so that each lane stores 32
+        // contiguous bytes (16 rows of one query) instead of 16 scattered u16.
+        // Rows past N (the last chunk of an unsampled small shard) read as 0xffff.
         const float lim = n < N ? 65535.0f : -1.0f;
+        const uint32_t jj = lane & 31u;
 #pragma unroll
         for (int t = 0; t < QT; ++t) {
             if (t < (int)nqt) {
-                // opaque per sub-tile: otherwise the 128 per-(tile, r) row
-                // addresses are hoisted out of the loop and spill
-                uint32_t qb = t * 32u + 4u * h;
-                asm volatile("" : "+v"(qb));
-                uint16_t* dq = dsm + (uint64_t)qb * S + s0 + (lane & 31u);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const uint32_t qo = 8u * (r >> 2) + (r & 3);
+                    const uint32_t qo = 8u * (r >> 2) + 4u * h + (r & 3);
                     const float dv = -acc[t][r];
-                    if (qb + qo < B) dq[(uint64_t)qo * S] = lim < 0.0f ? (uint16_t)0xffffu : (uint16_t)min(dv, lim);
+                    tw[qo * 32u + jj] = lim < 0.0f ? (uint16_t)0xffffu : (uint16_t)min(dv, lim);
                 }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                // lane L: query L/2 of the tile, rows 16 (L%2) .. +15 -> their minimum
+                const uint32_t qo = lane >> 1, rh = lane & 1u;
+                const uint4 v0 = *(const uint4*)(tw + qo * 32u + rh * 16u);
+                const uint4 v1 = *(const uint4*)(tw + qo * 32u + rh * 16u + 8u);
+                uint32_t mn = 0xffffu;
+                {
+                    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) mn = min(mn, min(w[e] & 0xffffu, w[e] >> 16));
+                }
+                uint32_t qg = t * 32u + qo;
+                asm volatile("" : "+v"(qg));  // keeps the per-tile row addresses from being hoisted
+                if (qg < B) dsm[(uint64_t)qg * (S >> 4) + (s0 >> 4) + rh] = (uint16_t)mn;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
         }
     }
 }
 
-// One block per query over its S dense sample distances (S % 8 == 0): the
+// One block per query over its S dense values (S % 8 == 0; here the group minima): the
 // query's values are loaded once into registers (kSsPer uint4 = 8 u16 each per
 // thread, all loads in flight together), then a min pass and windowed
 // histograms run on the registers.  Larger samples stream from memory.
@@ -1802,9 +1879,9 @@ static void launch_sample_dense_t(const Stage1Args& a, hipStream_t s) {
         const uint32_t bg = min(256u, a.B - g);
         hipLaunchKernelGGL((k_sample_dense<W4>), dim3(grid), dim3(kMx5Threads), 0, s, a.codes, a.cap, a.N,
                            a.sample_stride, nsub, (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, bg,
-                           a.smp + (uint64_t)g * S, S);
+                           a.smp + (uint64_t)g * (S / 16u), S);
     }
-    hipLaunchKernelGGL(k_sample_select, dim3(a.B), dim3(kSsThreads), 0, s, a.smp, S, a.D, a.target, a.thr);
+    hipLaunchKernelGGL(k_sample_select, dim3(a.B), dim3(kSsThreads), 0, s, a.smp, S / 16u, a.D, a.target, a.thr);
 }
 
 template <int W4>
@@ -1863,7 +1940,7 @@ size_t stage1_plan(Stage1Args& a) {
         const bool sampled = a.target < S / 2u && a.N > S;
         if (getenv_flag_eq("GVDB_SAMPLE", "mx")) {
             if (sampled) a.sample_mode = kSampleMxHist;
-        } else if ((uint64_t)a.B * S * 2u <= (1ull << 30)) {
+        } else if ((uint64_t)a.B * (S / 16u) * 2u <= (1ull << 30)) {
             a.sample_mode = kSampleDense;
         } else if (sampled) {
             a.sample_mode = kSampleMxHist;
@@ -1874,7 +1951,7 @@ size_t stage1_plan(Stage1Args& a) {
         const uint64_t ng = (a.B + 255u) / 256u;
         bytes += ng * (8u * 2u * W4 * 64u * 16u + 256u * 4u);
     }
-    if (a.sample_mode == kSampleDense) bytes += (size_t)a.B * S * 2u + 256u;
+    if (a.sample_mode == kSampleDense) bytes += (size_t)a.B * (S / 16u) * 2u + 256u;
     return bytes;
 }
 

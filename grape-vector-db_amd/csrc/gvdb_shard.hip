@@ -40,45 +40,85 @@ namespace gvdb {
 constexpr uint32_t kShardMaxG = 1024;   // ranks (the merge key holds 16 bits of rank)
 constexpr uint32_t kShardMaxD = 8192;   // distance histogram of the merge in LDS (key field: 16 bits)
 
-// ---- step 3a: merge of the gathered exchange-1 blocks ---------------------------
-// One block per query.  Every list is sorted by (d, row), so after the R-th
-// smallest distance T of the union is known (LDS histogram), list g contributes
-// its a_g entries with d < T and then, in rank order, ties at T until R
-// entries are taken -- exactly the first R of the union in (d, rank, row)
-// order.  Those R keys (d << 48 | rank << 32 | row) are sorted in LDS to get
-// each one's global position.  LDS: keys [8192] u64, hist [D + 1], per-list
-// [3 * G].
-__global__ __launch_bounds__(256) void k_shard_merge(const uint32_t* __restrict__ gathered, uint64_t words1,
-                                                     uint32_t G, uint32_t me, uint32_t B, uint32_t R, uint32_t D,
-                                                     uint32_t* __restrict__ own_rows, uint32_t* __restrict__ own_pos,
-                                                     uint32_t* __restrict__ own_cnt, uint32_t* __restrict__ reff) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // [kSelectLdsCap]
-    uint32_t* hist = (uint32_t*)(sk + kSelectLdsCap);               // [D + 1]
-    uint32_t* lg = hist + ((D + 4u) & ~3u);                          // [G] count of d < T
-    uint32_t* eg = lg + G;                                           // [G] count of d == T
-    uint32_t* bg = eg + G;                                           // [G] first slot in sk
-    __shared__ uint32_t s_total, s_own, s_T, s_lt;
+// ---- step 3: one kernel per query -- global top-R, rerank of the owned rows, local top-k
+// Every list is sorted by (d, row).  (i) A histogram of the distances of all
+// G lists gives the R-th smallest distance T of the union; list g contributes
+// its a_g entries with d < T and then, in rank order, ties at T until R are
+// taken -- exactly the first R of the union in (d, rank, row) order, and a
+// PREFIX of every list.  (ii) This rank's owned entries are the prefix of its
+// own list; the global position of each is its index plus, for every other
+// list, the count of its selected keys below it (binary searches in LDS).
+// (iii) Exact cosine of the owned rows, 16 at a time: the rows stream through
+// LDS in 256-dimension chunks, lane r < 16 folds row r in the reference's
+// order (acc = acc + q_j * x_j from -0.0), lane 16 folds q_j * q_j.  (iv) The
+// owned entries sorted by (cosine desc, position) -> the first k go to the
+// exchange-2 block.
+// LDS (dynamic): hist [(D+4)&~3] | lg, eg, bg, cg [G] | sel u64 [R] | tile; the owned
+// positions / rows go to global scratch (opos, orow [B][R]).
+constexpr uint32_t kP2Threads = 256;
+constexpr uint32_t kP2Rows = 16;    // rows re-scored together
+constexpr uint32_t kP2Ch = 256;     // dimensions per LDS chunk
+constexpr uint32_t kP2Ld = kP2Ch + 4;
+constexpr uint32_t kP2AllCap = 4096;  // keys of all lists staged in LDS up to this many
+__global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __restrict__ gathered, uint64_t words1,
+                                                             uint32_t G, uint32_t me, uint32_t B, uint32_t R,
+                                                             uint32_t D, const float* __restrict__ rows,
+                                                             const float* __restrict__ norms,
+                                                             const uint64_t* __restrict__ ids,
+                                                             const float* __restrict__ queries, uint32_t k,
+                                                             uint32_t err, uint32_t* __restrict__ block2,
+                                                             uint32_t* __restrict__ opos_g,
+                                                             uint32_t* __restrict__ orow_g) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* hist = lds;
+    uint32_t* lg = hist + ((D + 4u) & ~3u);
+    uint32_t* eg = lg + G;
+    uint32_t* bg = eg + G;
+    uint32_t* cg = bg + G;
+    uint64_t* sel = (uint64_t*)(((uintptr_t)(cg + G) + 15) & ~(uintptr_t)15);
+    float* tile = (float*)(((uintptr_t)(sel + R) + 15) & ~(uintptr_t)15);  // [kP2Rows][kP2Ld]
+    float* qs = tile + kP2Rows * kP2Ld;                                       // [kP2Ch]
+    uint64_t* allk = (uint64_t*)(qs + kP2Ch);  // [G*R] every list's keys, when G*R <= kP2AllCap
+    const bool staged = G * R <= kP2AllCap;
+    __shared__ uint32_t s_total, s_T, s_lt, s_nan, s_rows[kP2Rows];
+    __shared__ float s_cos[kP2Rows], s_qq;
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
-    auto list = [&](uint32_t g) { return (const uint64_t*)(gathered + (uint64_t)g * words1) + (uint64_t)q * R; };
-    auto count = [&](uint32_t g) { return min(gathered[(uint64_t)g * words1 + 2ull * B * R + q], R); };
-    for (uint32_t i = tid; i <= D; i += 256) hist[i] = 0u;
+    uint32_t* opos = opos_g + (uint64_t)q * R;
+    uint32_t* orow = orow_g + (uint64_t)q * R;
+    auto glist = [&](uint32_t g) { return (const uint64_t*)(gathered + (uint64_t)g * words1) + (uint64_t)q * R; };
+    auto key_at = [&](uint32_t g, uint32_t i) { return staged ? allk[g * R + i] : glist(g)[i]; };
+    for (uint32_t i = tid; i <= D; i += kP2Threads) hist[i] = 0u;
     if (tid == 0) {
         s_total = 0u;
-        s_own = 0u;
+        s_nan = 0u;
     }
     __syncthreads();
-    for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t c = count(g);
-        const uint64_t* L = list(g);
-        for (uint32_t i = tid; i < c; i += 256) atomicAdd(&hist[min((uint32_t)(L[i] >> 32), D)], 1u);
-        if (tid == 0) s_total += c;
+    for (uint32_t g = tid; g < G; g += kP2Threads) {
+        const uint32_t c = min(gathered[(uint64_t)g * words1 + 2ull * B * R + q], R);
+        cg[g] = c;
+        lg[g] = 0u;
+        eg[g] = 0u;
+        atomicAdd(&s_total, c);
+    }
+    __syncthreads();
+    // (i) histogram of every list's distances: one flat pass (all loads in flight),
+    //     the keys staged in LDS for the passes below
+    for (uint32_t x = tid; x < G * R; x += kP2Threads) {
+        const uint32_t g = x / R, i = x - g * R;
+        if (i < cg[g]) {
+            const uint64_t key = glist(g)[i];
+            if (staged) allk[x] = key;
+            atomicAdd(&hist[min((uint32_t)(key >> 32), D)], 1u);
+        }
     }
     __syncthreads();
     const uint32_t Re = min(R, s_total);
+    uint32_t* meta = block2 + 4ull * B * k;
     if (Re == 0) {
         if (tid == 0) {
-            own_cnt[q] = 0u;
-            reff[q] = 0u;
+            meta[q] = 0u;
+            meta[B + q] = 0u;
+            if (q == 0) meta[2 * B] = err;
         }
         return;
     }
@@ -92,23 +132,13 @@ __global__ __launch_bounds__(256) void k_shard_merge(const uint32_t* __restrict_
     }
     __syncthreads();
     const uint32_t T = s_T;
-    // per list: entries below T and tied at T (binary searches on the sorted d field)
-    for (uint32_t g = tid; g < G; g += 256) {
-        const uint32_t c = count(g);
-        const uint64_t* L = list(g);
-        uint32_t lo = 0, hi = c;  // first index with d >= T
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if ((uint32_t)(L[mid] >> 32) < T) lo = mid + 1; else hi = mid;
+    for (uint32_t x = tid; x < G * R; x += kP2Threads) {
+        const uint32_t g = x / R, i = x - g * R;
+        if (i < cg[g]) {
+            const uint32_t d = (uint32_t)(key_at(g, i) >> 32);
+            if (d < T) atomicAdd(&lg[g], 1u);
+            else if (d == T) atomicAdd(&eg[g], 1u);
         }
-        const uint32_t a = lo;
-        hi = c;  // first index with d > T
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if ((uint32_t)(L[mid] >> 32) <= T) lo = mid + 1; else hi = mid;
-        }
-        lg[g] = a;
-        eg[g] = lo - a;
     }
     __syncthreads();
     if (tid == 0) {  // ties at T go to the lowest ranks first (rank order = corpus order)
@@ -116,105 +146,165 @@ __global__ __launch_bounds__(256) void k_shard_merge(const uint32_t* __restrict_
         for (uint32_t g = 0; g < G; ++g) {
             const uint32_t t = min(eg[g], need);
             need -= t;
+            eg[g] = lg[g] + t;  // the selected prefix of list g
             bg[g] = base;
-            eg[g] = lg[g] + t;  // entries taken from list g
             base += eg[g];
         }
     }
     __syncthreads();
-    for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t take = eg[g], b0 = bg[g];
-        const uint64_t* L = list(g);
-        for (uint32_t i = tid; i < take; i += 256) {
-            const uint64_t k = L[i];
-            sk[b0 + i] = ((k >> 32) << 48) | ((uint64_t)g << 32) | (k & 0xffffffffull);
-        }
-    }
-    const uint32_t P = next_pow2(Re);
-    for (uint32_t i = Re + tid; i < P; i += 256) sk[i] = ~0ull;
-    __syncthreads();
-    bitonic_sort_lds(sk, P);
-    for (uint32_t p = tid; p < Re; p += 256) {
-        const uint64_t k = sk[p];
-        if (((uint32_t)(k >> 32) & 0xffffu) == me) {
-            const uint32_t c = atomicAdd(&s_own, 1u);
-            own_rows[(uint64_t)q * R + c] = (uint32_t)k;
-            own_pos[(uint64_t)q * R + c] = p;
+    for (uint32_t x = tid; x < G * R; x += kP2Threads) {
+        const uint32_t g = x / R, i = x - g * R;
+        if (i < eg[g]) {
+            const uint64_t key = key_at(g, i);
+            sel[bg[g] + i] = ((key >> 32) << 48) | ((uint64_t)g << 32) | (key & 0xffffffffull);
         }
     }
     __syncthreads();
-    if (tid == 0) {
-        own_cnt[q] = s_own;
-        reff[q] = Re;
+    // (ii) global positions of the owned entries (the prefix of this rank's list)
+    const uint32_t c = eg[me];
+    for (uint32_t i = tid; i < c; i += kP2Threads) {
+        const uint64_t key = sel[bg[me] + i];
+        uint32_t pos = i;
+        for (uint32_t g = 0; g < G; ++g) {
+            if (g == me) continue;
+            uint32_t lo = 0, hi = eg[g];
+            const uint64_t* L = sel + bg[g];
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L[mid] < key) lo = mid + 1; else hi = mid;
+            }
+            pos += lo;
+        }
+        opos[i] = pos;
+        orow[i] = (uint32_t)key;
     }
-}
-
-hipError_t launch_shard_merge(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
-                              uint32_t R, uint32_t D, uint32_t* own_rows, uint32_t* own_pos, uint32_t* own_cnt,
-                              uint32_t* reff, hipStream_t s) {
-    if (B == 0) return hipSuccess;
-    const size_t lds = (size_t)kSelectLdsCap * 8u + (size_t)((D + 4u) & ~3u) * 4u + 3u * (size_t)G * 4u;
-    hipLaunchKernelGGL(k_shard_merge, dim3(B), dim3(256), lds, s, gathered1, words1, G, me, B, R, D, own_rows, own_pos,
-                       own_cnt, reff);
-    GVDB_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-// ---- step 3b: this rank's local top-k of its owned entries --------------------
-// Keys (~order(cos) << 32 | position): cosine descending, ties by global
-// stage-1 position (the reference's stable sort).  A NaN among the owned
-// scores poisons the query when the global list has >= 2 entries (the
-// reference's partial_cmp().unwrap() sort panics).
-__global__ __launch_bounds__(256) void k_shard_local_topk(const float* __restrict__ scores,
-                                                          const uint32_t* __restrict__ own_rows,
-                                                          const uint32_t* __restrict__ own_pos,
-                                                          const uint32_t* __restrict__ own_cnt,
-                                                          const uint32_t* __restrict__ reff, uint32_t B, uint32_t R,
-                                                          uint32_t k, const uint64_t* __restrict__ ids, uint32_t err,
-                                                          uint32_t* __restrict__ block2) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];  // [next_pow2(R)]
-    __shared__ uint32_t s_nan;
-    const uint32_t q = blockIdx.x, tid = threadIdx.x;
-    const uint32_t c = min(own_cnt[q], R);
-    if (tid == 0) s_nan = 0u;
     __syncthreads();
-    for (uint32_t i = tid; i < c; i += 256) {
-        const float f = scores[(uint64_t)q * R + i];
-        if (f != f) s_nan = 1u;
-        // (position, owned index) in the low bits: positions are distinct (< 2^13)
-        sk[i] = ((uint64_t)~f32_order(f) << 32) | ((uint64_t)own_pos[(uint64_t)q * R + i] << 13) | i;
+    // (iii) exact cosine of the owned rows, kP2Rows at a time (scores into the sel area)
+    float* cosv = (float*)sel;
+    const float* qv = queries + (uint64_t)q * D;
+    const uint32_t nch = (D + kP2Ch - 1) / kP2Ch;
+    constexpr uint32_t kPer = kP2Rows * kP2Ch / kP2Threads;  // floats per thread per chunk (16)
+    for (uint32_t r0 = 0; r0 < c; r0 += kP2Rows) {
+        const uint32_t nr = min(kP2Rows, c - r0);
+        float acc = -0.0f;
+        float x[kPer];
+        if (tid < kP2Rows) s_rows[tid] = tid < nr ? (uint32_t)sel[bg[me] + r0 + tid] : 0u;
+        __syncthreads();
+        auto load = [&](uint32_t ch) {
+#pragma unroll
+            for (uint32_t e = 0; e < kPer; ++e) {
+                const uint32_t f = tid + e * kP2Threads, r = f / kP2Ch, j = ch * kP2Ch + (f % kP2Ch);
+                x[e] = (r < nr && j < D) ? rows[(uint64_t)s_rows[r] * D + j] : 0.0f;
+            }
+        };
+        load(0);
+        for (uint32_t ch = 0; ch < nch; ++ch) {
+#pragma unroll
+            for (uint32_t e = 0; e < kPer; ++e) {
+                const uint32_t f = tid + e * kP2Threads;
+                tile[(f / kP2Ch) * kP2Ld + (f % kP2Ch)] = x[e];
+            }
+            qs[tid] = ch * kP2Ch + tid < D ? qv[ch * kP2Ch + tid] : 0.0f;  // kP2Threads == kP2Ch
+            __syncthreads();
+            if (ch + 1 < nch) load(ch + 1);  // next chunk in flight during the folds
+            const uint32_t m = min(kP2Ch, D - ch * kP2Ch);
+            // lanes < 16 fold their row, lane 16 the query norm (group 0): the
+            // reference's left-to-right order; float4 LDS reads, 8 in flight
+            const bool fold_q = tid == kP2Rows && r0 == 0;
+            if (tid < nr || fold_q) {
+                const float* tr = fold_q ? qs : tile + tid * kP2Ld;
+                float a2 = fold_q ? (ch == 0 ? -0.0f : s_qq) : acc;
+                uint32_t j = 0;
+                if (m == kP2Ch) {
+#pragma unroll 8
+                    for (; j < kP2Ch; j += 4) {
+                        const float4 x4 = *(const float4*)(tr + j);
+                        const float4 w4 = *(const float4*)(qs + j);
+                        a2 = a2 + w4.x * x4.x;
+                        a2 = a2 + w4.y * x4.y;
+                        a2 = a2 + w4.z * x4.z;
+                        a2 = a2 + w4.w * x4.w;
+                    }
+                }
+                for (; j < m; ++j) a2 = a2 + qs[j] * tr[j];
+                if (fold_q) s_qq = a2; else acc = a2;
+            }
+            __syncthreads();
+        }
+        if (tid < nr) {
+            const float na = sqrtf(s_qq), nb = norms[orow[r0 + tid]];
+            const float sc = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
+            s_cos[tid] = sc;
+        }
+        __syncthreads();
+        if (tid < nr) {
+            cosv[r0 + tid] = s_cos[tid];  // bytes below every sel entry a later group reads
+            if (s_cos[tid] != s_cos[tid]) s_nan = 1u;
+        }
+        __syncthreads();
     }
+    // (iv) local top-k by (cosine desc, global position): keys (~order(cos), pos, owned
+    //      index) sorted in the tile area (up to 2080 keys; more owned entries: scans)
     const uint32_t P = next_pow2(max(c, 1u));
-    for (uint32_t i = c + tid; i < P; i += 256) sk[i] = ~0ull;
-    __syncthreads();
-    if (c > 1) bitonic_sort_lds(sk, P);
+    const uint32_t* rows_keep = orow;
+    uint64_t* keys = (uint64_t*)tile;
+    const bool keys_fit = P <= kP2Rows * kP2Ld / 2;
+    if (keys_fit) {
+        for (uint32_t i = tid; i < P; i += kP2Threads)
+            keys[i] = i < c ? ((uint64_t)~f32_order(cosv[i]) << 32) | ((uint64_t)opos[i] << 13) | i : ~0ull;
+        __syncthreads();
+        if (c > 1) bitonic_sort_lds(keys, P);
+    }
     const uint32_t take = min(k, c);
     uint32_t* ent = block2 + (uint64_t)q * k * 4u;
-    for (uint32_t i = tid; i < take; i += 256) {
-        const uint64_t key = sk[i];
-        const uint32_t pos = ((uint32_t)key >> 13) & 0x1fffu, j = (uint32_t)key & 0x1fffu;
-        const uint32_t row = own_rows[(uint64_t)q * R + j];
-        const uint64_t id = ids ? ids[row] : (uint64_t)row;
-        ent[4 * i + 0] = __float_as_uint(scores[(uint64_t)q * R + j]);
-        ent[4 * i + 1] = pos;
-        ent[4 * i + 2] = (uint32_t)id;
-        ent[4 * i + 3] = (uint32_t)(id >> 32);
+    if (keys_fit) {
+        for (uint32_t t = tid; t < take; t += kP2Threads) {
+            const uint32_t j = (uint32_t)keys[t] & 0x1fffu;
+            const uint32_t row = rows_keep[j];
+            const uint64_t id = ids ? ids[row] : (uint64_t)row;
+            ent[4 * t + 0] = __float_as_uint(cosv[j]);
+            ent[4 * t + 1] = opos[j];
+            ent[4 * t + 2] = (uint32_t)id;
+            ent[4 * t + 3] = (uint32_t)(id >> 32);
+        }
+    } else if (tid == 0) {
+        // many owned entries (a skewed shard): selection of the k best by repeated scans
+        uint64_t prev = 0;
+        for (uint32_t t = 0; t < take; ++t) {
+            uint64_t best = ~0ull;
+            for (uint32_t i = 0; i < c; ++i) {
+                const uint64_t key = ((uint64_t)~f32_order(cosv[i]) << 32) | ((uint64_t)opos[i] << 13) | i;
+                if ((t == 0 || key > prev) && key < best) best = key;
+            }
+            prev = best;
+            const uint32_t j = (uint32_t)best & 0x1fffu;
+            const uint32_t row = rows_keep[j];
+            const uint64_t id = ids ? ids[row] : (uint64_t)row;
+            ent[4 * t + 0] = __float_as_uint(cosv[j]);
+            ent[4 * t + 1] = opos[j];
+            ent[4 * t + 2] = (uint32_t)id;
+            ent[4 * t + 3] = (uint32_t)(id >> 32);
+        }
     }
     if (tid == 0) {
-        uint32_t* meta = block2 + 4ull * B * k;
-        meta[q] = take | ((s_nan && reff[q] >= 2u) ? 0x80000000u : 0u);
-        meta[B + q] = reff[q];
+        meta[q] = take | ((s_nan && Re >= 2u) ? 0x80000000u : 0u);
+        meta[B + q] = Re;
         if (q == 0) meta[2 * B] = err;
     }
 }
 
-hipError_t launch_shard_local_topk(const float* scores, const uint32_t* own_rows, const uint32_t* own_pos,
-                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t R, uint32_t k,
-                                   const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s) {
+size_t shard_phase2_lds(uint32_t G, uint32_t R, uint32_t D) {
+    return (size_t)((D + 4u) & ~3u) * 4u + 4u * (size_t)G * 4u + 16u + (size_t)R * 8u + 16u +
+           (size_t)(kP2Rows * kP2Ld + kP2Ch) * 4u + (G * R <= kP2AllCap ? (size_t)G * R * 8u : 0u);
+}
+
+hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
+                               uint32_t R, uint32_t D, const float* rows, const float* norms, const uint64_t* ids,
+                               const float* queries, uint32_t k, uint32_t err, uint32_t* block2, uint32_t* opos,
+                               uint32_t* orow, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    const size_t lds = (size_t)next_pow2(std::max<uint32_t>(R, 1u)) * 8u;
-    hipLaunchKernelGGL(k_shard_local_topk, dim3(B), dim3(256), lds, s, scores, own_rows, own_pos, own_cnt, reff, B, R,
-                       k, ids, err, block2);
+    hipLaunchKernelGGL(k_shard_phase2, dim3(B), dim3(kP2Threads), shard_phase2_lds(G, R, D), s, gathered1, words1, G,
+                       me, B, R, D, rows, norms, ids, queries, k, err, block2, opos, orow);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -369,8 +459,8 @@ void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint64_t* words1, uint
                       uint64_t* scratch_bytes) {
     if (words1) *words1 = shard_words1(B, R);
     if (words2) *words2 = shard_words2(B, k);
-    // own_rows | own_pos | scores [B][R] + own_cnt | reff [B]
-    if (scratch_bytes) *scratch_bytes = 12 * B * R + 8 * B + 256;
+    // the owned positions and rows [B][R] of phase 2
+    if (scratch_bytes) *scratch_bytes = 8 * B * R + 256;
 }
 
 uint64_t gvdb_shard_flat_words(uint64_t B, uint64_t k) { return shard_words_flat(B, k); }
@@ -407,47 +497,23 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (B == 0) return GVDB_OK;
     if (R == 0 || R > kSelectLdsCap || k == 0 || G == 0 || G > kShardMaxG || rank >= G || G * k > kSelectLdsCap ||
-        B > 0xFFFFFFFFull)
-        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: bad R / k / G / rank");
+        B > 0xFFFFFFFFull || dim == 0 || dim > kShardMaxD)
+        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: bad R / k / G / rank / dim");
     hipStream_t s = (hipStream_t)stream;
     const ShardInfo si = index_shard_info(shard);
     if (hipSetDevice(si.device) != hipSuccess) return report_status(GVDB_ERR_DEVICE, "hipSetDevice");
     const uint64_t BR = B * R;
-    uint32_t* own_rows = (uint32_t*)d_scratch;
-    uint32_t* own_pos = own_rows + BR;
-    float* scores = (float*)(own_pos + BR);
-    uint32_t* own_cnt = (uint32_t*)(scores + BR);
-    uint32_t* reff = own_cnt + B;
-    // the distance histogram spans [0, D]: use the widest distance any rank can send
-    const uint32_t D = std::max<uint32_t>(dim, 1u);
-    hipError_t e = launch_shard_merge(d_gathered1, shard_words1(B, R), (uint32_t)G, (uint32_t)rank, (uint32_t)B,
-                                      (uint32_t)R, std::min<uint32_t>(D, kShardMaxD), own_rows, own_pos, own_cnt, reff,
-                                      s);
-    if (e != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard merge: ") + hipGetErrorString(e));
+    uint32_t* opos = (uint32_t*)d_scratch;
+    uint32_t* orow = opos + BR;
+    // a shard that cannot rerank (empty, or a dimension mismatch already reported by
+    // phase 1) sent no entries, so it owns none: its rows are never read
     const bool usable = si.n > 0 && si.dim == dim;
-    if (usable) {
-        RerankArgs rr{};
-        rr.rows = si.rows;
-        rr.clen = dim;
-        rr.norms = si.norms;
-        rr.q = d_queries;
-        rr.qlen = dim;
-        rr.s1_rows = own_rows;
-        rr.B = (uint32_t)B;
-        rr.R = (uint32_t)R;
-        rr.kind = kScoreCosine;
-        rr.scores = scores;
-        rr.counts = own_cnt;
-        rr.short_lists = R <= 64u * G;  // ~R/G owned rows per query: 16-row blocks, loads all in flight
-        e = launch_rerank(rr, s);
-        if (e != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard rerank: ") + hipGetErrorString(e));
-    } else if (hipMemsetAsync(own_cnt, 0, B * 4, s) != hipSuccess) {
-        return report_status(GVDB_ERR_DEVICE, "shard rerank: memset");
-    }
-    e = launch_shard_local_topk(scores, own_rows, own_pos, own_cnt, reff, (uint32_t)B, (uint32_t)R, (uint32_t)k,
-                                si.ids, 0u, d_block2, s);
+    const hipError_t e = launch_shard_phase2(d_gathered1, shard_words1(B, R), (uint32_t)G, (uint32_t)rank, (uint32_t)B,
+                                             (uint32_t)R, dim, usable ? si.rows : nullptr,
+                                             usable ? si.norms : nullptr, usable ? si.ids : nullptr, d_queries,
+                                             (uint32_t)k, 0u, d_block2, opos, orow, s);
+    if (e != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard phase 2: ") + hipGetErrorString(e));
     if (usable) index_track_use(shard, s);
-    if (e != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard top-k: ") + hipGetErrorString(e));
     return GVDB_OK;
 }
 

@@ -669,14 +669,14 @@ def test_sharded_packed_world1_equals_single_device(g):
                                      (350_000, 512, 96, 4000), (1_250_000, 768, 300, 100), (200_000, 768, 256, 100),
                                      (70_000, 700, 128, 1000)])
 def test_sample_histogram_mfma_thresholds_equal_valu(g, N, D, B, R):
-    """The FP4-MFMA sample forms must give exactly the thresholds of the VALU
-    histogram (GVDB_SAMPLE=valu), and the searches the same ids and distances:
+    """The FP4-MFMA sample forms against the VALU histogram (GVDB_SAMPLE=valu):
     k_sample_mx (128 queries per block, bins d < 384, each block flushes only up
-    to its own target-th distance; sampled shards N > 262144 only) and the
-    default dense form (k_sample_dense + k_sample_select: every sampled distance
-    as u16, per-query windowed select; also N <= 262144, where the "sample" is
-    the whole shard and T is the exact R-th distance; B = 300 spans two
-    256-query groups)."""
+    to its own target-th distance; sampled shards N > 262144 only) gives exactly
+    its thresholds; the default dense form (k_sample_dense + k_sample_select:
+    per query the minimum of every 16 sample rows, windowed select of the
+    target-th smallest minimum; also N <= 262144, where the "sample" is the
+    whole shard) gives thresholds never below them.  The searches return the
+    same ids and distances in every case (B = 300 spans two 256-query groups)."""
     import ctypes as C
     import os
 
@@ -706,7 +706,12 @@ def test_sample_histogram_mfma_thresholds_equal_valu(g, N, D, B, R):
     finally:
         os.environ.pop("GVDB_DEBUG_THR", None)
         os.environ.pop("GVDB_SAMPLE", None)
+    # k_sample_mx: exactly the VALU thresholds; dense (16-row group minima): never
+    # below them, equal unless two of the target smallest share a group
+    assert out["mfma"][0] == out["valu"][0]
+    assert all(a >= b for a, b in zip(out["dense"][0], out["valu"][0]))
+    if N > 262_144:  # a sampled shard (small target): group collisions are rare
+        assert np.mean([a == b for a, b in zip(out["dense"][0], out["valu"][0])]) > 0.5
     for mode in ("mfma", "dense"):
-        assert out[mode][0] == out["valu"][0], mode
         assert max(out[mode][0]) < D  # a real estimate, not the no-pruning fallback
         assert (out[mode][1] == out["valu"][1]).all() and (out[mode][2] == out["valu"][2]).all(), mode
