@@ -13,8 +13,9 @@
 #   c4           scripts/c4_emulate.py (config 4, 8 shards of 1.25M x 3072)
 #   hybrid       scripts/bench_hybrid.py (config 5)                     -> gpurun_out/hybrid.json / .log
 #   hnsw10m      scripts/hnsw10m_gpu.py (GPU side of the 10M equal-recall experiment)
-#   pmc:NAME:REGEX:CMD   rocprofv3 --pmc passes (one counter set per run) over python3 CMD (spaces as ','),
-#                        rows whose kernel name matches REGEX -> gpurun_out/pmc_NAME/pmc.json
+#   pmc:NAME:REGEX:CMD[:FIRST]   rocprofv3 --pmc passes (one counter set per run) over python3 CMD (spaces as ','),
+#                        rows whose kernel name matches REGEX -> gpurun_out/pmc_NAME/pmc.json; FIRST = the
+#                        pmc_summary.py --first filter (kernel=N/...: only each kernel's first N dispatches)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -73,7 +74,7 @@ for t in "${TASKS[@]}"; do
             run 1100 gpurun_out/hnsw10m_gpu.log python -u scripts/hnsw10m_gpu.py
             tail -5 gpurun_out/hnsw10m_gpu.log ;;
         pmc:*)
-            IFS=':' read -r _ name regex cmd <<< "$t"
+            IFS=':' read -r _ name regex cmd first <<< "$t"
             cmd=${cmd//,/ }
             out=gpurun_out/pmc_$name
             mkdir -p "$out"
@@ -86,7 +87,11 @@ for t in "${TASKS[@]}"; do
                 if [ -n "$f" ]; then head -1 "$f" > "$out/counters_p$i.csv"; grep -E "$regex" "$f" >> "$out/counters_p$i.csv" || true; fi
                 rm -rf "${out:?}/p$i"
             done
-            python3 scripts/pmc_summary.py "$out" --json "$out/pmc.json" | tail -40 ;;
+            if [ -n "$first" ]; then
+                python3 scripts/pmc_summary.py "$out" --first "${first//\//,}" --json "$out/pmc.json" | tail -40
+            else
+                python3 scripts/pmc_summary.py "$out" --json "$out/pmc.json" | tail -40
+            fi ;;
         *)
             echo "[gpu.sh] unknown task $t" >&2
             exit 2 ;;

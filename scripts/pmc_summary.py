@@ -1,8 +1,18 @@
-"""Average per-dispatch PMC counters per kernel from gpu_pmc*.sh outputs."""
+"""Average per-dispatch PMC counters per kernel from scripts/gpu.sh pmc:* outputs.
+
+--first NAME=N[,NAME=N...]: keep only the first N dispatches (in dispatch order,
+per counter pass) of kernels whose short name contains NAME -- e.g. the
+warmup + timed launches of bench.py, before its smaller-N legs run."""
 import collections
 import csv
 import glob
 import sys
+
+first = {}
+if "--first" in sys.argv:
+    for kv in sys.argv[sys.argv.index("--first") + 1].split(","):
+        name, n = kv.split("=")
+        first[name] = int(n)
 
 d = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(sys.argv[1] + "/counters_p*.csv")):
@@ -10,6 +20,13 @@ for f in sorted(glob.glob(sys.argv[1] + "/counters_p*.csv")):
         k = r["Kernel_Name"].replace("void gvdb::(anonymous namespace)::", "").removeprefix("void ")[:40]
         d[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"]),
                                          int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+for k, cs in d.items():
+    lim = next((n for name, n in first.items() if name in k), None)
+    if lim is None:
+        continue
+    for c, v in cs.items():
+        keep = sorted({di for di, _, _ in v})[:lim]
+        cs[c] = [x for x in v if x[0] in set(keep)]
 for k, cs in d.items():
     if len(sys.argv) > 2 and not sys.argv[2].startswith("--") and sys.argv[2] not in k:
         continue
@@ -27,7 +44,8 @@ if "--json" in sys.argv:
     import json
 
     outp = sys.argv[sys.argv.index("--json") + 1]
-    res = {"source": f"scripts/pmc_summary.py over {sys.argv[1]} (rocprofv3 --pmc, one counter set per run)",
+    res = {"source": f"scripts/pmc_summary.py over {sys.argv[1]} (rocprofv3 --pmc, one counter set per run)"
+                     + (f"; first dispatches only: {first}" if first else ""),
            "fetch_size_unit": "KiB; gfx950 FETCH_SIZE counts half of the bytes of a 16-B/lane streaming read "
                               "(MI355X_MICROARCH.md, HBM) -> hbm_read_bytes = 2 * 1024 * FETCH_SIZE",
            "kernels": {}}
