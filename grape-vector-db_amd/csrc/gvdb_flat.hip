@@ -793,6 +793,180 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
     return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------
+// k_flat_i8q: the i8 EMIT pass with the QUERY operands in registers (KC = 6, i.e.
+// D in (640, 768]).  k_flat_mx streams a 32 KiB query chunk through LDS per
+// step and holds the rows in VGPRs; here the roles swap.  Wave w owns query
+// tile w (32 of the 256 slots): its A fragments for all 4*KC k-steps live in
+// 96 VGPRs for the whole launch, as do its 16 slots' epilogue operands.  The
+// rows stream HBM -> LDS by DMA (global_load_lds_dwordx4, no staging registers)
+// in sub-tiles of two 32-row groups (48 KiB, the fragment-major mirror's own
+// 1 KiB pieces), three LDS buffers deep: sub-tiles i+1 and i+2 are in flight
+// while every wave reads sub-tile i's B fragments from LDS (48 ds_read_b128,
+// 256 B/clk) for its 2 x 24 MFMAs (v_mfma_i32_32x32x32_i8).  One barrier per
+// sub-tile; the mirror is read from HBM exactly once.  Epilogue, candidate rule
+// (U = approx + qa*rho_x + qd >= tau) and the block nomination list are
+// k_flat_mx's; all vector-memory ops of the loop are inline asm with counted vmcnt.
+constexpr uint32_t kI8qSub = 2;    // 32-row groups per LDS sub-tile
+constexpr uint32_t kI8qBufs = 3;   // LDS sub-tile buffers
+constexpr uint32_t kI8qCl = 1792;  // block nomination list, u32 entries (flushed at a barrier once half full)
+template <int KC>
+__global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
+    constexpr int KS = 4 * KC;                          // k-steps of 32 per row group
+    constexpr uint32_t kPieces = kI8qSub * KC * 4;      // 1 KiB pieces per sub-tile
+    constexpr uint32_t kPerWave = kPieces / 8;          // DMA instructions per wave per sub-tile
+    constexpr uint32_t kSubBytes = kPieces * 1024u;
+    static_assert(kPieces % 8 == 0, "pieces split evenly over the waves");
+    __shared__ __attribute__((aligned(16))) char Bs[kI8qBufs][kSubBytes];
+    // nomination (slot q, block step i, row group gi, row j) as q << 24 | i << 6 | gi << 5 | j
+    __shared__ uint32_t cl[kI8qCl];
+    __shared__ uint32_t cl_n;
+    __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[kFxQ];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t N = a.N, G = gridDim.x;
+    const uint32_t nsub_all = ((N + kFxRows - 1) / kFxRows) * (kFxRows / 32u / kI8qSub);
+    const uint32_t ns = blockIdx.x < nsub_all ? (nsub_all - blockIdx.x + G - 1) / G : 0u;  // sub-tiles b, b+G, ...
+    const char* rowsx = (const char*)a.rowsx;
+    constexpr uint32_t kSubPerTile = kFxRows / 32u / kI8qSub;
+    // piece p = (gi*KC + c)*4 + s4 of sub-tile v: row group 2*(v % 4) + gi of tile v / 4
+    auto dma = [&](uint32_t i) __attribute__((always_inline)) {  // the block's i-th sub-tile -> buffer i % 3
+        const uint32_t ii = i < ns ? i : (ns ? ns - 1 : 0);  // clamped: a valid read, never used
+        const uint32_t v = blockIdx.x + ii * G, t = v / kSubPerTile, u = v % kSubPerTile;
+        const uint32_t l0 = (uint32_t)(uintptr_t)Bs[i % kI8qBufs];
+#pragma unroll
+        for (uint32_t k = 0; k < kPerWave; ++k) {
+            const uint32_t p = wv * kPerWave + k, s4 = p & 3u, c = (p >> 2) % KC, gi = (p >> 2) / KC;
+            const char* ga = rowsx + ((((uint64_t)t * KC + c) * 8u + kI8qSub * u + gi) * 4u + s4) * 1024u + lane * 16u;
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(ga), "s"(l0 + p * 1024u)
+                         : "memory");
+        }
+    };
+    // this wave's query fragments (A) and per-slot epilogue operands
+    fx_v4i A[KS];
+    {
+        const char* qx = (const char*)a.qx;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            A[s] = *(const fx_v4i*)(qx + (((uint32_t)(s >> 2) * 8u + wv) * 4u + (uint32_t)(s & 3)) * 1024u + lane * 16u);
+        // landed here, once: otherwise the waitcnt pass defers these waits into the
+        // loop, where its counts (blind to the asm DMAs) drain the row prefetch
+#pragma unroll
+        for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(A[s]));
+    }
+    if (tid < kFxQ) {
+        qinv_l[tid] = a.qinv[tid];
+        thr_l[tid] = a.thr[tid];
+        qa_l[tid] = a.qa[tid];
+    }
+    if (tid == 0) cl_n = 0;
+    __syncthreads();  // the compiler-visible loads above are complete from here on
+    if (ns) {
+        dma(0);
+        dma(1);
+    }
+    fx_v16i acc[kI8qSub];
+    float rsc[kI8qSub], rrh[kI8qSub];
+    auto row_of = [&](uint32_t e) {  // a list entry's row
+        const uint32_t v = blockIdx.x + ((e >> 6) & 0x3ffffu) * G;
+        return (v / kSubPerTile) * kFxRows + (kI8qSub * (v % kSubPerTile) + ((e >> 5) & 1u)) * 32u + (e & 31u);
+    };
+    auto flush = [&](uint32_t m) {  // the block's list -> the per-query global lists
+        for (uint32_t x = tid; x < m; x += kFxThreads) {
+            const uint32_t e = cl[x], q = e >> 24;
+            const uint32_t pos = atomicAdd(&a.counts[q], 1u);
+            if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = row_of(e);
+        }
+    };
+    for (uint32_t i = 0; i < ns; ++i) {
+        // sub-tile i landed (this wave's part: sub-tile i+1's kPerWave DMAs are younger), then all waves'
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
+        __syncthreads();
+        if (cl_n >= kI8qCl / 2) {  // (block-uniform) rare: empty the list before it can overflow
+            flush(min(cl_n, kI8qCl));
+            __syncthreads();
+            if (tid == 0) cl_n = 0;
+            __syncthreads();
+        }
+        const uint32_t v = blockIdx.x + i * G, t = v / kSubPerTile, u = v % kSubPerTile;
+        // the sub-tile's row operands, then sub-tile i+2 into the buffer read in step i-1
+#pragma unroll
+        for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
+            const uint32_t n = min(t * kFxRows + (kI8qSub * u + gi) * 32u + (lane & 31u), N - 1u);
+            asm volatile("global_load_dword %0, %1, off" : "=v"(rsc[gi]) : "v"(a.rscale + n) : "memory");
+            asm volatile("global_load_dword %0, %1, off" : "=v"(rrh[gi]) : "v"(a.rrho + n) : "memory");
+        }
+        dma(i + 2);
+        const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
+#pragma unroll
+        for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[gi][e] = 0;
+        fx_v4i bf[2][kI8qSub];
+#pragma unroll
+        for (uint32_t gi = 0; gi < kI8qSub; ++gi) bf[0][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u) * 1024u);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            if (s + 1 < KS) {
+#pragma unroll
+                for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+                    bf[(s + 1) & 1][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)(s + 1)) * 1024u);
+            }
+#pragma unroll
+            for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+                acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s & 1][gi], acc[gi], 0, 0, 0);
+        }
+        // the row operands (sub-tile i+2's DMAs are younger)
+#pragma unroll
+        for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(rsc[gi]), "+v"(rrh[gi]) : "n"(kPerWave));
+#pragma unroll
+        for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
+            const uint32_t n = t * kFxRows + (kI8qSub * u + gi) * 32u + (lane & 31u);
+            const float rinv = n < N ? rsc[gi] : 0.0f, rho = n < N ? rrh[gi] : 0.0f;
+            // this lane's 16 slots: qb0 + (e & 3) + 8 (e >> 2)
+            uint32_t qb0 = wv * 32u + 4u * (lane >> 5);
+            asm volatile("" : "+v"(qb0));  // keep the per-slot addresses out of the loop
+            float qs[16], ts[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 qv = *(const float4*)(qinv_l + qb0 + 8 * g);
+                const float4 tv = *(const float4*)(thr_l + qb0 + 8 * g);
+                const float4 av = *(const float4*)(qa_l + qb0 + 8 * g);
+                qs[4 * g + 0] = qv.x * rinv;
+                qs[4 * g + 1] = qv.y * rinv;
+                qs[4 * g + 2] = qv.z * rinv;
+                qs[4 * g + 3] = qv.w * rinv;
+                ts[4 * g + 0] = tv.x - av.x * rho;
+                ts[4 * g + 1] = tv.y - av.y * rho;
+                ts[4 * g + 2] = tv.z - av.z * rho;
+                ts[4 * g + 3] = tv.w - av.w * rho;
+            }
+            float mx = -__builtin_inff();
+#pragma unroll
+            for (int e = 0; e < 16; ++e) mx = fmaxf(mx, (float)acc[gi][e] * qs[e] - ts[e]);
+            if (!__ballot(mx >= 0.0f && n < N)) continue;
+            // rare: a candidate in this fragment (thr = +inf for slots >= B)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const uint32_t q = qb0 + (e & 3) + 8u * (e >> 2);
+                if (n < N && (float)acc[gi][e] * qs[e] >= ts[e]) {
+                    const uint32_t li = atomicAdd(&cl_n, 1u);
+                    if (li < kI8qCl) {
+                        cl[li] = (q << 24) | (i << 6) | (gi << 5) | (lane & 31u);
+                    } else {  // block list full (a burst within one sub-tile): straight to the global list
+                        const uint32_t pos = atomicAdd(&a.counts[q], 1u);
+                        if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = n;
+                    }
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped prefetches land before exit
+    __syncthreads();
+    flush(min(cl_n, kI8qCl));
+}
+
 static uint32_t fx_grid(uint32_t tiles) {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
@@ -814,7 +988,15 @@ hipError_t launch_flat_mx_sample(const FlatMxArgs& a, hipStream_t s) {
 hipError_t launch_flat_mx_emit(const FlatMxArgs& a, hipStream_t s) {
     const uint32_t tiles = (a.N + kFxRows - 1) / kFxRows;
     if (tiles == 0) return hipSuccess;
-    if (a.i8)
+    static const bool i8r = [] {  // GVDB_FLAT_I8R=0: k_flat_mx, the streamed-query kernel (A/B)
+        const char* e = getenv("GVDB_FLAT_I8R");
+        return !(e && e[0] == '0');
+    }();
+    const uint64_t nsub = (uint64_t)tiles * (kFxRows / 32u / kI8qSub);
+    const uint32_t g = fx_grid((uint32_t)std::min<uint64_t>(nsub, 0xffffffffull));
+    if (a.i8 && a.KC == 6 && i8r && nsub < (uint64_t)g << 18) {  // one block per CU over the 64-row sub-tiles
+        hipLaunchKernelGGL((k_flat_i8q<6>), dim3(g), dim3(kFxThreads), 0, s, a);
+    } else if (a.i8)
         hipLaunchKernelGGL((k_flat_mx<false, true>), dim3(fx_grid(tiles)), dim3(kFxThreads), 0, s, a);
     else
         hipLaunchKernelGGL((k_flat_mx<false, false>), dim3(fx_grid(tiles)), dim3(kFxThreads), 0, s, a);

@@ -345,11 +345,12 @@ inline uint64_t shard_words1(uint64_t B, uint64_t R) { return (2 * B * R + B + 1
 inline uint64_t shard_words2(uint64_t B, uint64_t k) { return (4 * B * k + 2 * B + 1 + 1) & ~1ull; }
 // gathered exchange-1 blocks -> this rank's exchange-2 block: global top-R, exact
 // cosine of the owned rows, local top-k (one kernel per query; gvdb_shard.hip).
-// rows / norms / ids may be null for a shard that owns nothing; opos / orow: [B][R]
+// rows / norms / ids may be null for a shard that owns nothing; opos / orow / ocos:
+// [B][R] scratch (used when R exceeds the kernel's LDS arrays)
 hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
                                uint32_t R, uint32_t D, const float* rows, const float* norms, const uint64_t* ids,
                                const float* queries, uint32_t k, uint32_t err, uint32_t* block2, uint32_t* opos,
-                               uint32_t* orow, hipStream_t s);
+                               uint32_t* orow, float* ocos, hipStream_t s);
 // sharded FLAT: gathered blocks of the ranks' exact top-k -> merged top-k
 //   block F (sharded FLAT): ids u64 [B][k] | scores f32 [B][k] | counts [B] | err | pad
 inline uint64_t shard_words_flat(uint64_t B, uint64_t k) { return (3 * B * k + B + 1 + 1) & ~1ull; }

@@ -236,8 +236,37 @@ __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ row
     if (myrow < n) out[myrow] = sqrtf(s);
 }
 
+// The same norms for FEW rows (a query batch): k_row_norms runs them in one
+// block whose per-chunk staging round trips serialise (~120 us for 256 x 768).
+// Here a block of 256 threads stages RB whole rows in LDS with one round trip
+// (all loads in flight), then lane r < RB folds row r from -0.0 in order.
+constexpr uint32_t kRnSmallFloats = 16384;  // LDS floats per block (64 KiB)
+__global__ __launch_bounds__(256) void k_row_norms_few(const float* __restrict__ rows, uint64_t n, uint32_t D,
+                                                       uint32_t RB, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float stage[];  // [RB][D + 1]
+    const uint64_t r0 = (uint64_t)blockIdx.x * RB;
+    const uint32_t nr = (uint32_t)min((uint64_t)RB, n - r0), ld = D + 1u;
+    const float* src = rows + r0 * D;
+    for (uint32_t i = threadIdx.x; i < nr * D; i += 256u) stage[(i / D) * ld + i % D] = src[i];
+    __syncthreads();
+    if (threadIdx.x < nr) {
+        const float* tr = stage + threadIdx.x * ld;
+        float s = -0.0f;
+        for (uint32_t j = 0; j < D; ++j) s = s + tr[j] * tr[j];
+        out[r0 + threadIdx.x] = sqrtf(s);
+    }
+}
+
 hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t D, float* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    const uint32_t rb = kRnSmallFloats / (D + 1u);
+    if (n <= 4096 && rb >= 1) {  // few rows: one staging round trip per block
+        const uint32_t RB = std::min<uint32_t>(rb, 16u);
+        hipLaunchKernelGGL(k_row_norms_few, dim3((uint32_t)((n + RB - 1) / RB)), dim3(256),
+                           (size_t)RB * (D + 1u) * 4u, s, rows, n, D, RB, out);
+        GVDB_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     const uint64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(k_row_norms, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, D, out);
     GVDB_LAUNCH_CHECK();
@@ -566,6 +595,16 @@ __device__ __forceinline__ bool select_topr(uint32_t cnt, const uint64_t* __rest
     // order, plus where the row's exact score was published.  A rescan's keys
     // carry idx = kNoIdx.
     __shared__ uint32_t s_T, s_lt, s_n, s_cut;
+    const uint32_t nt = blockDim.x;
+    // small buffers (the common case) stay in registers: one global read, issued
+    // with the count's (slots past the count are masked below)
+    constexpr int KPT = 8;
+    uint64_t kk[KPT];
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+        const uint32_t i = threadIdx.x + u * nt;
+        kk[u] = i < bufcap ? b[i] : ~0ull;
+    }
     if (cnt < R || cnt > bufcap || force_rescan) {
         select_rescan(codes, cap, N, D, W4, qc, R, sk, hist);
         if (with_idx) {
@@ -575,17 +614,11 @@ __device__ __forceinline__ bool select_topr(uint32_t cnt, const uint64_t* __rest
         }
         return true;
     }
-    const uint32_t nt = blockDim.x;
-    // small buffers (the common case) stay in registers: one global read
-    constexpr int KPT = 8;
     const bool inreg = cnt <= KPT * nt;
-    uint64_t kk[KPT];
     if (inreg) {
 #pragma unroll
-        for (int u = 0; u < KPT; ++u) {
-            const uint32_t i = threadIdx.x + u * nt;
-            kk[u] = i < cnt ? b[i] : ~0ull;
-        }
+        for (int u = 0; u < KPT; ++u)
+            if (threadIdx.x + u * nt >= cnt) kk[u] = ~0ull;
     }
     for (uint32_t i = threadIdx.x; i <= D; i += nt) hist[i] = 0u;
     if (threadIdx.x == 0) s_n = 0u;
@@ -1756,7 +1789,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_dense(const uint4* __
 // thread, all loads in flight together), then a min pass and windowed
 // histograms run on the registers.  Larger samples stream from memory.
 constexpr int kSsThreads = 512;
-constexpr int kSsPer = 40;  // uint4 per thread: S <= 512 * 40 * 8 = 163840 in registers
+constexpr int kSsPer = 8;  // uint4 per thread: S <= 512 * 8 * 8 = 32768 values in registers (more stream)
 __device__ __forceinline__ void ss_count(uint32_t w, uint32_t base, uint32_t win, uint32_t* hist) {
     const uint32_t o0 = (w & 0xffffu) - base, o1 = (w >> 16) - base;  // wrap below base: outside
     if (o0 < win) atomicAdd(&hist[o0], 1u);
@@ -1774,14 +1807,19 @@ __global__ __launch_bounds__(kSsThreads) void k_sample_select(const uint16_t* __
     const bool inreg = nv <= (uint32_t)kSsThreads * kSsPer;
     uint4 x[kSsPer];
     uint32_t mn = 0xffffu;
+    // register slots in use (block-uniform): the loops over x stop there -- a
+    // 1.25M-row shard's sample fills one slot of 40, 10M rows three
+    const int jn = (int)((nv + kSsThreads - 1) / kSsThreads);
     if (inreg) {
 #pragma unroll
         for (int j = 0; j < kSsPer; ++j) {
+            if (j >= jn) continue;
             const uint32_t i = tid + (uint32_t)j * kSsThreads;
             x[j] = i < nv ? v[i] : make_uint4(~0u, ~0u, ~0u, ~0u);
         }
 #pragma unroll
         for (int j = 0; j < kSsPer; ++j) {
+            if (j >= jn) continue;
             const uint32_t a = min(min(x[j].x & 0xffffu, x[j].x >> 16), min(x[j].y & 0xffffu, x[j].y >> 16));
             const uint32_t b = min(min(x[j].z & 0xffffu, x[j].z >> 16), min(x[j].w & 0xffffu, x[j].w >> 16));
             mn = min(mn, min(a, b));
@@ -1812,6 +1850,7 @@ __global__ __launch_bounds__(kSsThreads) void k_sample_select(const uint16_t* __
         if (inreg) {
 #pragma unroll
             for (int j = 0; j < kSsPer; ++j) {
+                if (j >= jn) continue;
                 // the bulk of the values lies above the window: one test per 8
                 const uint32_t a = min(min(x[j].x & 0xffffu, x[j].x >> 16), min(x[j].y & 0xffffu, x[j].y >> 16));
                 const uint32_t b = min(min(x[j].z & 0xffffu, x[j].z >> 16), min(x[j].w & 0xffffu, x[j].w >> 16));

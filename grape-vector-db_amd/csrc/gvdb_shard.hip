@@ -41,25 +41,48 @@ constexpr uint32_t kShardMaxG = 1024;   // ranks (the merge key holds 16 bits of
 constexpr uint32_t kShardMaxD = 8192;   // distance histogram of the merge in LDS (key field: 16 bits)
 
 // ---- step 3: one kernel per query -- global top-R, rerank of the owned rows, local top-k
-// Every list is sorted by (d, row).  (i) A histogram of the distances of all
-// G lists gives the R-th smallest distance T of the union; list g contributes
-// its a_g entries with d < T and then, in rank order, ties at T until R are
-// taken -- exactly the first R of the union in (d, rank, row) order, and a
-// PREFIX of every list.  (ii) This rank's owned entries are the prefix of its
-// own list; the global position of each is its index plus, for every other
-// list, the count of its selected keys below it (binary searches in LDS).
-// (iii) Exact cosine of the owned rows, 16 at a time: the rows stream through
-// LDS in 256-dimension chunks, lane r < 16 folds row r in the reference's
-// order (acc = acc + q_j * x_j from -0.0), lane 16 folds q_j * q_j.  (iv) The
-// owned entries sorted by (cosine desc, position) -> the first k go to the
+// Every list is sorted by (d, row), and the global order is (d, rank, row)
+// (the reference's stable order by candidate index over the concatenated
+// corpus).  (i) The global position of this rank's i-th entry is
+//     i + sum_{g < me} #{list g: d <= d_i} + sum_{g > me} #{list g: d < d_i}
+// (binary searches over the other lists' distances, staged in LDS); the
+// entry is in the global top-R iff that position is < Re = min(R, total), so
+// the owned entries are a prefix of the own list and their positions are
+// exactly their ranks in the global top-R.  (ii) Exact cosine of the owned
+// rows, kP2Rows at a time: the rows of the first group are loaded
+// speculatively (the first kP2Rows own-list entries) while (i) runs, through
+// LDS in chunks of kP2Ch dimensions; lane r < kP2Rows of wave 0 folds row r in
+// the reference's order (acc = acc + q_j * x_j from -0.0), wave 1's lane 0
+// folds q_j * q_j.  (iii) The owned entries ranked by (cosine desc, position)
+// (rank counting; a bitonic sort beyond kP2RankMax) -> the first k go to the
 // exchange-2 block.
-// LDS (dynamic): hist [(D+4)&~3] | lg, eg, bg, cg [G] | sel u64 [R] | tile; the owned
-// positions / rows go to global scratch (opos, orow [B][R]).
+// LDS (dynamic): qv [D] | cg [G] | dist [G*R] when G*R <= kP2DistLds |
+// own pos / row / cos [R] when R <= kP2OwnLds (else the global scratch) | tile.
 constexpr uint32_t kP2Threads = 256;
-constexpr uint32_t kP2Rows = 16;    // rows re-scored together
-constexpr uint32_t kP2Ch = 256;     // dimensions per LDS chunk
-constexpr uint32_t kP2Ld = kP2Ch + 4;
-constexpr uint32_t kP2AllCap = 4096;  // keys of all lists staged in LDS up to this many
+constexpr uint32_t kP2Rows = 24;    // rows re-scored together (one lane each)
+constexpr uint32_t kP2Ch = 768;     // dimensions per LDS chunk
+constexpr uint32_t kP2Ld = kP2Ch + 4;  // padded row stride: conflict-free ds_read_b128 across lanes
+constexpr uint32_t kP2F4 = kP2Rows * (kP2Ch / 4) / kP2Threads;  // float4 per thread per chunk (18)
+constexpr uint32_t kP2DistLds = 4096;  // other lists' distances staged in LDS up to this many
+constexpr uint32_t kP2OwnLds = 2048;   // own-entry arrays in LDS up to this R
+constexpr uint32_t kP2RankMax = 1024;  // rank counting up to this many owned entries
+static_assert(kP2Rows * (kP2Ch / 4) % kP2Threads == 0, "chunk tiling");
+static_assert(kP2Rows <= 64, "one wave folds the group");
+
+__device__ __forceinline__ uint32_t p2_count(const uint32_t* dl, uint32_t n, uint32_t d, bool le) {
+    // #{j < n: dl[j] <= d} (le) or < d; dl ascending
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (le ? dl[mid] <= d : dl[mid] < d) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// OWN_LDS: the own-entry arrays in LDS (R <= kP2OwnLds) -- a compile-time choice, so
+// every access is a plain LDS op (a runtime LDS-or-global pointer makes them FLAT ops,
+// whose vmcnt waits stall the ranking behind the in-flight row loads)
+template <bool OWN_LDS, bool VEC>
 __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __restrict__ gathered, uint64_t words1,
                                                              uint32_t G, uint32_t me, uint32_t B, uint32_t R,
                                                              uint32_t D, const float* __restrict__ rows,
@@ -68,50 +91,68 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
                                                              const float* __restrict__ queries, uint32_t k,
                                                              uint32_t err, uint32_t* __restrict__ block2,
                                                              uint32_t* __restrict__ opos_g,
-                                                             uint32_t* __restrict__ orow_g) {
+                                                             uint32_t* __restrict__ orow_g,
+                                                             float* __restrict__ ocos_g,
+                                                             unsigned long long* __restrict__ clk) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* hist = lds;
-    uint32_t* lg = hist + ((D + 4u) & ~3u);
-    uint32_t* eg = lg + G;
-    uint32_t* bg = eg + G;
-    uint32_t* cg = bg + G;
-    uint64_t* sel = (uint64_t*)(((uintptr_t)(cg + G) + 15) & ~(uintptr_t)15);
-    float* tile = (float*)(((uintptr_t)(sel + R) + 15) & ~(uintptr_t)15);  // [kP2Rows][kP2Ld]
-    float* qs = tile + kP2Rows * kP2Ld;                                       // [kP2Ch]
-    uint64_t* allk = (uint64_t*)(qs + kP2Ch);  // [G*R] every list's keys, when G*R <= kP2AllCap
-    const bool staged = G * R <= kP2AllCap;
-    __shared__ uint32_t s_total, s_T, s_lt, s_nan, s_rows[kP2Rows];
-    __shared__ float s_cos[kP2Rows], s_qq;
+    // GVDB_P2_CLK timing study: thread 0's shader clock at each phase boundary
+    const unsigned long long c0 = clk ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    auto mark = [&](int i) {
+        if (clk && threadIdx.x == 0) clk[blockIdx.x * 8u + i] = __builtin_amdgcn_s_memrealtime() - c0;
+    };
+    const bool dstaged = G * R <= kP2DistLds;
+    constexpr bool own_lds = OWN_LDS;
+    float* qv = (float*)lds;                                   // [D]
+    uint32_t* cg = lds + ((D + 3u) & ~3u);                     // [G]
+    uint32_t* dist = cg + ((G + 3u) & ~3u);                    // [G*R] (dstaged)
+    uint32_t* own = dist + (dstaged ? ((G * R + 3u) & ~3u) : 0u);
+    float* tile = (float*)(own + (own_lds ? ((3u * R + 3u) & ~3u) : 0u));  // [kP2Rows][kP2Ld]
+    __shared__ uint32_t s_total, s_c, s_nan;
+    __shared__ float s_qq;
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
-    uint32_t* opos = opos_g + (uint64_t)q * R;
-    uint32_t* orow = orow_g + (uint64_t)q * R;
+    uint32_t* opos;
+    uint32_t* orow;
+    float* ocos;
+    if constexpr (OWN_LDS) {
+        opos = own;
+        orow = own + R;
+        ocos = (float*)(own + 2 * R);
+    } else {
+        opos = opos_g + (uint64_t)q * R;
+        orow = orow_g + (uint64_t)q * R;
+        ocos = ocos_g + (uint64_t)q * R;
+    }
     auto glist = [&](uint32_t g) { return (const uint64_t*)(gathered + (uint64_t)g * words1) + (uint64_t)q * R; };
-    auto key_at = [&](uint32_t g, uint32_t i) { return staged ? allk[g * R + i] : glist(g)[i]; };
-    for (uint32_t i = tid; i <= D; i += kP2Threads) hist[i] = 0u;
+    const uint64_t* mine = glist(me);
+    // round A: every read that depends on nothing else, issued together -- the
+    // counts, this rank's keys (d parked in opos), the other lists' distances,
+    // the query row
     if (tid == 0) {
         s_total = 0u;
+        s_c = 0u;
         s_nan = 0u;
     }
     __syncthreads();
     for (uint32_t g = tid; g < G; g += kP2Threads) {
         const uint32_t c = min(gathered[(uint64_t)g * words1 + 2ull * B * R + q], R);
-        cg[g] = c;
-        lg[g] = 0u;
-        eg[g] = 0u;
+        cg[g] = g == me && !rows ? 0u : c;  // a shard that cannot rerank sent nothing
         atomicAdd(&s_total, c);
     }
-    __syncthreads();
-    // (i) histogram of every list's distances: one flat pass (all loads in flight),
-    //     the keys staged in LDS for the passes below
-    for (uint32_t x = tid; x < G * R; x += kP2Threads) {
-        const uint32_t g = x / R, i = x - g * R;
-        if (i < cg[g]) {
-            const uint64_t key = glist(g)[i];
-            if (staged) allk[x] = key;
-            atomicAdd(&hist[min((uint32_t)(key >> 32), D)], 1u);
-        }
+    for (uint32_t i = tid; i < R; i += kP2Threads) {  // the block holds R key slots per query
+        const uint64_t key = mine[i];
+        opos[i] = (uint32_t)(key >> 32);
+        orow[i] = (uint32_t)key;
     }
+    if (dstaged)
+        for (uint32_t x = tid; x < G * R; x += kP2Threads) {
+            const uint32_t g = x / R, i = x - g * R;
+            if (g != me) dist[x] = (uint32_t)(glist(g)[i] >> 32);
+        }
+    const float* qg = queries + (uint64_t)q * D;
+    for (uint32_t j = tid; j < D; j += kP2Threads) qv[j] = qg[j];
     __syncthreads();
+    mark(0);
+    const uint32_t cnt_me = cg[me];
     const uint32_t Re = min(R, s_total);
     uint32_t* meta = block2 + 4ull * B * k;
     if (Re == 0) {
@@ -122,189 +163,194 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
         }
         return;
     }
-    if (tid < 64) {
-        const uint32_t t = wave_find_cum(hist, D + 1u, Re);
-        const uint32_t lt = wave_sum_below(hist, t);
-        if (tid == 0) {
-            s_T = t;
-            s_lt = lt;
-        }
-    }
-    __syncthreads();
-    const uint32_t T = s_T;
-    for (uint32_t x = tid; x < G * R; x += kP2Threads) {
-        const uint32_t g = x / R, i = x - g * R;
-        if (i < cg[g]) {
-            const uint32_t d = (uint32_t)(key_at(g, i) >> 32);
-            if (d < T) atomicAdd(&lg[g], 1u);
-            else if (d == T) atomicAdd(&eg[g], 1u);
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {  // ties at T go to the lowest ranks first (rank order = corpus order)
-        uint32_t need = Re - s_lt, base = 0;
-        for (uint32_t g = 0; g < G; ++g) {
-            const uint32_t t = min(eg[g], need);
-            need -= t;
-            eg[g] = lg[g] + t;  // the selected prefix of list g
-            bg[g] = base;
-            base += eg[g];
-        }
-    }
-    __syncthreads();
-    for (uint32_t x = tid; x < G * R; x += kP2Threads) {
-        const uint32_t g = x / R, i = x - g * R;
-        if (i < eg[g]) {
-            const uint64_t key = key_at(g, i);
-            sel[bg[g] + i] = ((key >> 32) << 48) | ((uint64_t)g << 32) | (key & 0xffffffffull);
-        }
-    }
-    __syncthreads();
-    // (ii) global positions of the owned entries (the prefix of this rank's list)
-    const uint32_t c = eg[me];
-    for (uint32_t i = tid; i < c; i += kP2Threads) {
-        const uint64_t key = sel[bg[me] + i];
-        uint32_t pos = i;
-        for (uint32_t g = 0; g < G; ++g) {
-            if (g == me) continue;
-            uint32_t lo = 0, hi = eg[g];
-            const uint64_t* L = sel + bg[g];
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (L[mid] < key) lo = mid + 1; else hi = mid;
+    // round B: the first kP2Rows own-list rows (speculative: the owned entries are a
+    // prefix of the list), their norms and ids, in flight during the ranking
+    float4 xr[kP2F4];
+    constexpr bool vec = VEC;  // D % 4 == 0: 16-B row loads and LDS folds (a compile-time choice: clean loads)
+    auto load = [&](uint32_t r0, uint32_t nr, uint32_t ch) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t e = 0; e < kP2F4; ++e) {
+            const uint32_t L = tid + e * kP2Threads, r = L / (kP2Ch / 4), j = ch * kP2Ch + 4u * (L % (kP2Ch / 4));
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (r < nr && j < D) {
+                const float* src = rows + (uint64_t)orow[r0 + r] * D + j;
+                if constexpr (VEC) {
+                    v = *(const float4*)src;
+                } else {
+                    v.x = src[0];
+                    if (j + 1 < D) v.y = src[1];
+                    if (j + 2 < D) v.z = src[2];
+                    if (j + 3 < D) v.w = src[3];
+                }
             }
-            pos += lo;
+            xr[e] = v;
         }
-        opos[i] = pos;
-        orow[i] = (uint32_t)key;
+    };
+    const uint32_t nr0 = min(cnt_me, kP2Rows);
+    load(0, nr0, 0);
+    const float nb0 = tid < nr0 ? norms[orow[tid]] : 0.0f;
+    const uint64_t id0 = tid < nr0 ? (ids ? ids[orow[tid]] : (uint64_t)orow[tid]) : 0ull;
+    // (i) global positions of the own entries: pos_i = i + the other lists' counts
+    //     below d_i, one (entry, list) pair per thread (binary searches over the
+    //     staged distances), summed into posacc (the cosine slots, free until (ii))
+    uint32_t* posacc = (uint32_t*)ocos;
+    for (uint32_t i = tid; i < cnt_me; i += kP2Threads) posacc[i] = i;
+    __syncthreads();
+    for (uint32_t x = tid; x < cnt_me * G; x += kP2Threads) {
+        const uint32_t i = x / G, g = x - i * G;
+        if (g == me) continue;
+        const uint32_t d = opos[i];
+        uint32_t cnt;
+        if (dstaged) {
+            cnt = p2_count(dist + g * R, cg[g], d, g < me);
+        } else {  // large G * R: the same search over the gathered keys
+            const uint64_t* L = glist(g);
+            uint32_t lo = 0, hi = cg[g];
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1, dm = (uint32_t)(L[mid] >> 32);
+                if (g < me ? dm <= d : dm < d) lo = mid + 1; else hi = mid;
+            }
+            cnt = lo;
+        }
+        if (cnt) atomicAdd(&posacc[i], cnt);
     }
     __syncthreads();
-    // (iii) exact cosine of the owned rows, kP2Rows at a time (scores into the sel area)
-    float* cosv = (float*)sel;
-    const float* qv = queries + (uint64_t)q * D;
+    // the owned entries are those below Re (a prefix of the own list)
+    for (uint32_t i = tid; i < cnt_me; i += kP2Threads) {
+        const uint32_t pos = posacc[i];
+        opos[i] = pos;
+        if (pos < Re) atomicAdd(&s_c, 1u);
+    }
+    __syncthreads();
+    mark(1);
+    const uint32_t c = s_c;  // the owned entries: own-list prefix [0, c)
+    // (ii) exact cosine of the owned rows, kP2Rows at a time
     const uint32_t nch = (D + kP2Ch - 1) / kP2Ch;
-    constexpr uint32_t kPer = kP2Rows * kP2Ch / kP2Threads;  // floats per thread per chunk (16)
     for (uint32_t r0 = 0; r0 < c; r0 += kP2Rows) {
         const uint32_t nr = min(kP2Rows, c - r0);
+        if (r0 > 0) load(r0, nr, 0);  // groups past the speculative one (> kP2Rows owned)
         float acc = -0.0f;
-        float x[kPer];
-        if (tid < kP2Rows) s_rows[tid] = tid < nr ? (uint32_t)sel[bg[me] + r0 + tid] : 0u;
-        __syncthreads();
-        auto load = [&](uint32_t ch) {
-#pragma unroll
-            for (uint32_t e = 0; e < kPer; ++e) {
-                const uint32_t f = tid + e * kP2Threads, r = f / kP2Ch, j = ch * kP2Ch + (f % kP2Ch);
-                x[e] = (r < nr && j < D) ? rows[(uint64_t)s_rows[r] * D + j] : 0.0f;
-            }
-        };
-        load(0);
+        const bool fold_q = r0 == 0 && tid == 64;
+        float qq = -0.0f;
+        const float nb = r0 == 0 ? nb0 : tid < nr ? norms[orow[r0 + tid]] : 0.0f;
         for (uint32_t ch = 0; ch < nch; ++ch) {
 #pragma unroll
-            for (uint32_t e = 0; e < kPer; ++e) {
-                const uint32_t f = tid + e * kP2Threads;
-                tile[(f / kP2Ch) * kP2Ld + (f % kP2Ch)] = x[e];
+            for (uint32_t e = 0; e < kP2F4; ++e) {
+                const uint32_t L = tid + e * kP2Threads;
+                *(float4*)(tile + (L / (kP2Ch / 4)) * kP2Ld + 4u * (L % (kP2Ch / 4))) = xr[e];
             }
-            qs[tid] = ch * kP2Ch + tid < D ? qv[ch * kP2Ch + tid] : 0.0f;  // kP2Threads == kP2Ch
             __syncthreads();
-            if (ch + 1 < nch) load(ch + 1);  // next chunk in flight during the folds
-            const uint32_t m = min(kP2Ch, D - ch * kP2Ch);
-            // lanes < 16 fold their row, lane 16 the query norm (group 0): the
-            // reference's left-to-right order; float4 LDS reads, 8 in flight
-            const bool fold_q = tid == kP2Rows && r0 == 0;
+            if (ch + 1 < nch) load(r0, nr, ch + 1);  // next chunk in flight during the folds
+            const uint32_t j0 = ch * kP2Ch, m = min(kP2Ch, D - j0);
             if (tid < nr || fold_q) {
-                const float* tr = fold_q ? qs : tile + tid * kP2Ld;
-                float a2 = fold_q ? (ch == 0 ? -0.0f : s_qq) : acc;
+                const float* tr = fold_q ? qv + j0 : tile + tid * kP2Ld;
+                const float* qc = qv + j0;
+                float a2 = fold_q ? qq : acc;
                 uint32_t j = 0;
-                if (m == kP2Ch) {
+                if (vec) {
 #pragma unroll 8
-                    for (; j < kP2Ch; j += 4) {
+                    for (; j + 4 <= m; j += 4) {
                         const float4 x4 = *(const float4*)(tr + j);
-                        const float4 w4 = *(const float4*)(qs + j);
+                        const float4 w4 = *(const float4*)(qc + j);
                         a2 = a2 + w4.x * x4.x;
                         a2 = a2 + w4.y * x4.y;
                         a2 = a2 + w4.z * x4.z;
                         a2 = a2 + w4.w * x4.w;
                     }
                 }
-                for (; j < m; ++j) a2 = a2 + qs[j] * tr[j];
-                if (fold_q) s_qq = a2; else acc = a2;
+                for (; j < m; ++j) a2 = a2 + qc[j] * tr[j];
+                if (fold_q) qq = a2; else acc = a2;
             }
+            if (fold_q && ch + 1 == nch) s_qq = qq;
             __syncthreads();
         }
         if (tid < nr) {
-            const float na = sqrtf(s_qq), nb = norms[orow[r0 + tid]];
+            const float na = sqrtf(s_qq);
             const float sc = (na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb);
-            s_cos[tid] = sc;
+            ocos[r0 + tid] = sc;
+            if (sc != sc) s_nan = 1u;
         }
-        __syncthreads();
-        if (tid < nr) {
-            cosv[r0 + tid] = s_cos[tid];  // bytes below every sel entry a later group reads
-            if (s_cos[tid] != s_cos[tid]) s_nan = 1u;
-        }
-        __syncthreads();
     }
-    // (iv) local top-k by (cosine desc, global position): keys (~order(cos), pos, owned
-    //      index) sorted in the tile area (up to 2080 keys; more owned entries: scans)
-    const uint32_t P = next_pow2(max(c, 1u));
-    const uint32_t* rows_keep = orow;
-    uint64_t* keys = (uint64_t*)tile;
-    const bool keys_fit = P <= kP2Rows * kP2Ld / 2;
-    if (keys_fit) {
-        for (uint32_t i = tid; i < P; i += kP2Threads)
-            keys[i] = i < c ? ((uint64_t)~f32_order(cosv[i]) << 32) | ((uint64_t)opos[i] << 13) | i : ~0ull;
-        __syncthreads();
-        if (c > 1) bitonic_sort_lds(keys, P);
-    }
+    __syncthreads();
+    mark(2);
+    // (iii) local top-k by (cosine desc, global position): key (~order(cos), pos)
     const uint32_t take = min(k, c);
     uint32_t* ent = block2 + (uint64_t)q * k * 4u;
-    if (keys_fit) {
-        for (uint32_t t = tid; t < take; t += kP2Threads) {
-            const uint32_t j = (uint32_t)keys[t] & 0x1fffu;
-            const uint32_t row = rows_keep[j];
-            const uint64_t id = ids ? ids[row] : (uint64_t)row;
-            ent[4 * t + 0] = __float_as_uint(cosv[j]);
-            ent[4 * t + 1] = opos[j];
-            ent[4 * t + 2] = (uint32_t)id;
-            ent[4 * t + 3] = (uint32_t)(id >> 32);
+    uint64_t* keys = (uint64_t*)tile;
+    auto emit = [&](uint32_t t, uint32_t j) {  // j == tid for the rank-counted entries
+        const uint32_t row = orow[j];
+        const uint64_t id = j == tid && j < nr0 ? id0 : ids ? ids[row] : (uint64_t)row;
+        ent[4 * t + 0] = __float_as_uint(ocos[j]);
+        ent[4 * t + 1] = opos[j];
+        ent[4 * t + 2] = (uint32_t)id;
+        ent[4 * t + 3] = (uint32_t)(id >> 32);
+    };
+    if (c <= kP2RankMax) {
+        for (uint32_t i = tid; i < c; i += kP2Threads)
+            keys[i] = ((uint64_t)~f32_order(ocos[i]) << 32) | opos[i];
+        __syncthreads();
+        for (uint32_t i = tid; i < c; i += kP2Threads) {
+            const uint64_t ki = keys[i];
+            uint32_t rk = 0;
+            for (uint32_t j = 0; j < c; ++j) rk += keys[j] < ki;  // positions are distinct
+            if (rk < take) emit(rk, i);
         }
-    } else if (tid == 0) {
-        // many owned entries (a skewed shard): selection of the k best by repeated scans
-        uint64_t prev = 0;
-        for (uint32_t t = 0; t < take; ++t) {
-            uint64_t best = ~0ull;
-            for (uint32_t i = 0; i < c; ++i) {
-                const uint64_t key = ((uint64_t)~f32_order(cosv[i]) << 32) | ((uint64_t)opos[i] << 13) | i;
-                if ((t == 0 || key > prev) && key < best) best = key;
-            }
-            prev = best;
-            const uint32_t j = (uint32_t)best & 0x1fffu;
-            const uint32_t row = rows_keep[j];
-            const uint64_t id = ids ? ids[row] : (uint64_t)row;
-            ent[4 * t + 0] = __float_as_uint(cosv[j]);
-            ent[4 * t + 1] = opos[j];
-            ent[4 * t + 2] = (uint32_t)id;
-            ent[4 * t + 3] = (uint32_t)(id >> 32);
-        }
+    } else {  // P <= next_pow2(8192) keys of 8 B fit the tile (148 KiB)
+        const uint32_t P = next_pow2(c);
+        for (uint32_t i = tid; i < P; i += kP2Threads)
+            keys[i] = i < c ? ((uint64_t)~f32_order(ocos[i]) << 32) | ((uint64_t)opos[i] << 13) | i : ~0ull;
+        __syncthreads();
+        bitonic_sort_lds(keys, P);
+        for (uint32_t t = tid; t < take; t += kP2Threads) emit(t, (uint32_t)keys[t] & 0x1fffu);
     }
     if (tid == 0) {
         meta[q] = take | ((s_nan && Re >= 2u) ? 0x80000000u : 0u);
         meta[B + q] = Re;
         if (q == 0) meta[2 * B] = err;
     }
+    mark(3);
 }
 
 size_t shard_phase2_lds(uint32_t G, uint32_t R, uint32_t D) {
-    return (size_t)((D + 4u) & ~3u) * 4u + 4u * (size_t)G * 4u + 16u + (size_t)R * 8u + 16u +
-           (size_t)(kP2Rows * kP2Ld + kP2Ch) * 4u + (G * R <= kP2AllCap ? (size_t)G * R * 8u : 0u);
+    const size_t dist = G * R <= kP2DistLds ? (size_t)((G * R + 3u) & ~3u) * 4u : 0u;
+    const size_t own = R <= kP2OwnLds ? (size_t)((3u * R + 3u) & ~3u) * 4u : 0u;
+    const size_t tile = std::max<size_t>((size_t)kP2Rows * kP2Ld * 4u,
+                                         R > kP2RankMax ? (size_t)next_pow2(R) * 8u : 0u);
+    return (size_t)((D + 3u) & ~3u) * 4u + (size_t)((G + 3u) & ~3u) * 4u + dist + own + tile;
+}
+
+struct ShardClk {
+    unsigned long long* p;
+    uint32_t B;
+};
+static ShardClk& shard_clk() {
+    static ShardClk c{nullptr, 0};
+    return c;
 }
 
 hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
                                uint32_t R, uint32_t D, const float* rows, const float* norms, const uint64_t* ids,
                                const float* queries, uint32_t k, uint32_t err, uint32_t* block2, uint32_t* opos,
-                               uint32_t* orow, hipStream_t s) {
+                               uint32_t* orow, float* ocos, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_shard_phase2, dim3(B), dim3(kP2Threads), shard_phase2_lds(G, R, D), s, gathered1, words1, G,
-                       me, B, R, D, rows, norms, ids, queries, k, err, block2, opos, orow);
+    const size_t lds = shard_phase2_lds(G, R, D);
+    if (lds > 160u * 1024u) return hipErrorInvalidValue;
+    unsigned long long* clk = nullptr;
+    if (getenv("GVDB_P2_CLK")) {  // timing study (gvdb_debug_shard_clock)
+        static unsigned long long* buf = nullptr;
+        static uint32_t cap = 0;
+        if (cap < B) {
+            if (buf) (void)hipFree(buf);
+            if (hipMalloc((void**)&buf, (size_t)B * 64) != hipSuccess) buf = nullptr;
+            cap = buf ? B : 0;
+        }
+        clk = buf;
+        shard_clk() = {buf, B};
+    }
+    auto kern = R <= kP2OwnLds ? ((D & 3u) == 0 ? k_shard_phase2<true, true> : k_shard_phase2<true, false>)
+                               : ((D & 3u) == 0 ? k_shard_phase2<false, true> : k_shard_phase2<false, false>);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kP2Threads), lds, s, gathered1, words1, G, me, B, R, D, rows, norms, ids,
+                       queries, k, err, block2, opos, orow, ocos, clk);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -327,6 +373,7 @@ __global__ __launch_bounds__(256) void k_shard_final(const uint32_t* __restrict_
         if ((meta[q] >> 31) || meta[2 * B]) atomicOr(&s_bad, 1u);
     }
     const uint32_t n = G * k;
+    const bool by_rank = n <= kP2RankMax;  // rank counting (sk[n..n+k): the k smallest keys), else a sort
     for (uint32_t x = tid; x < n; x += 256) {
         const uint32_t g = x / k, i = x % k;
         const uint32_t* blk = gathered + (uint64_t)g * words2;
@@ -337,16 +384,30 @@ __global__ __launch_bounds__(256) void k_shard_final(const uint32_t* __restrict_
             key = ((uint64_t)~f32_order(__uint_as_float(e[0])) << 32) | ((uint64_t)e[1] << 18) | x;
         }
         sk[x] = key;
+        if (by_rank && x < k) sk[n + x] = ~0ull;
     }
-    const uint32_t P = next_pow2(max(n, 1u));
-    for (uint32_t i = n + tid; i < P; i += 256) sk[i] = ~0ull;
+    if (by_rank) {
+        __syncthreads();
+        for (uint32_t x = tid; x < n; x += 256) {
+            const uint64_t kx = sk[x];
+            if (kx == ~0ull) continue;
+            uint32_t rk = 0;
+            for (uint32_t j = 0; j < n; ++j) rk += sk[j] < kx;  // keys are distinct (x)
+            if (rk < k) sk[n + rk] = kx;
+        }
+    } else {
+        const uint32_t P = next_pow2(max(n, 1u));
+        for (uint32_t i = n + tid; i < P; i += 256) sk[i] = ~0ull;
+        __syncthreads();
+        bitonic_sort_lds(sk, P);
+    }
     __syncthreads();
-    bitonic_sort_lds(sk, P);
+    const uint64_t* top = by_rank ? sk + n : sk;
     if (tid < 64) {  // take(k), then drop orphans (order-preserving ballot compaction)
         uint32_t o = 0;
         for (uint32_t i0 = 0; i0 < k; i0 += 64) {
             const uint32_t i = i0 + tid;
-            const uint64_t key = i < k ? sk[i] : ~0ull;
+            const uint64_t key = i < k ? top[i] : ~0ull;
             uint64_t id = kOrphan;
             float sc = 0.0f;
             if (key != ~0ull) {
@@ -371,7 +432,8 @@ __global__ __launch_bounds__(256) void k_shard_final(const uint32_t* __restrict_
 hipError_t launch_shard_final(const uint32_t* gathered2, uint64_t words2, uint32_t G, uint32_t B, uint32_t k,
                               uint64_t* out_ids, float* out_scores, uint32_t* out_n, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    const size_t lds = (size_t)next_pow2(std::max<uint32_t>(G * k, 1u)) * 8u;
+    const uint32_t n = std::max<uint32_t>(G * k, 1u);
+    const size_t lds = (size_t)std::max<uint32_t>(next_pow2(n), n <= kP2RankMax ? n + k : 0u) * 8u;
     hipLaunchKernelGGL(k_shard_final, dim3(B), dim3(256), lds, s, gathered2, words2, G, B, k, out_ids, out_scores,
                        out_n);
     GVDB_LAUNCH_CHECK();
@@ -459,8 +521,8 @@ void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint64_t* words1, uint
                       uint64_t* scratch_bytes) {
     if (words1) *words1 = shard_words1(B, R);
     if (words2) *words2 = shard_words2(B, k);
-    // the owned positions and rows [B][R] of phase 2
-    if (scratch_bytes) *scratch_bytes = 8 * B * R + 256;
+    // the owned positions, rows and cosines [B][R] of phase 2 (used when R > 2048)
+    if (scratch_bytes) *scratch_bytes = 12 * B * R + 256;
 }
 
 uint64_t gvdb_shard_flat_words(uint64_t B, uint64_t k) { return shard_words_flat(B, k); }
@@ -511,7 +573,7 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
     const hipError_t e = launch_shard_phase2(d_gathered1, shard_words1(B, R), (uint32_t)G, (uint32_t)rank, (uint32_t)B,
                                              (uint32_t)R, dim, usable ? si.rows : nullptr,
                                              usable ? si.norms : nullptr, usable ? si.ids : nullptr, d_queries,
-                                             (uint32_t)k, 0u, d_block2, opos, orow, s);
+                                             (uint32_t)k, 0u, d_block2, opos, orow, (float*)(orow + BR), s);
     if (e != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard phase 2: ") + hipGetErrorString(e));
     if (usable) index_track_use(shard, s);
     return GVDB_OK;
@@ -539,6 +601,23 @@ gvdb_status gvdb_shard_flat_final_device(const uint32_t* d_gathered, uint64_t G,
                                            (hipStream_t)stream);
     if (e != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("shard flat merge: ") + hipGetErrorString(e));
     return GVDB_OK;
+}
+
+// GVDB_P2_CLK=1 timing study: average phase-boundary clocks (s_memrealtime, 100 MHz ticks, from
+// the block start) of the last phase-2 launch: out[0..3] = round A, ranking, folds, end.
+int gvdb_debug_shard_clock(double* out) {
+    const ShardClk c = shard_clk();
+    if (!c.p || !out) return -1;
+    std::vector<unsigned long long> h((size_t)c.B * 8);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h.data(), c.p, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -2;
+    for (int i = 0; i < 4; ++i) {
+        double s = 0;
+        for (uint32_t q = 0; q < c.B; ++q) s += (double)h[(size_t)q * 8 + i];
+        out[i] = s / c.B;
+    }
+    return 0;
 }
 
 // Host form of k_shard_merge: this rank's owned entries of the global top-R.

@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--oracle-queries", type=int, default=32)
     ap.add_argument("--no-single", action="store_true", help="skip the single-index comparison")
+    ap.add_argument("--p2clk", action="store_true", help="print phase-2 phase clocks (timing study)")
     a = ap.parse_args()
     N, D, G, B, R, k = a.n, a.dim, a.shards, a.batch, a.R, a.k
     dev = torch.device("cuda", 0)
@@ -131,6 +132,15 @@ def main():
         per_rank.append({"rank": r, "rows": bounds[r + 1] - bounds[r], "step_ms": 1e3 * step,
                          "stage1_ms": 1e3 * t1, "merge_rerank_topk_ms": 1e3 * t2})
     t3 = timed(p3, a.steps)
+    if a.p2clk:  # phase clocks of one rank's phase 2 (GVDB_P2_CLK timing study)
+        os.environ["GVDB_P2_CLK"] = "1"
+        p2(0)
+        torch.cuda.synchronize()
+        del os.environ["GVDB_P2_CLK"]
+        ck = (C.c_double * 4)()
+        if L.gvdb_debug_shard_clock(ck) == 0:
+            log("[c3] phase-2 clocks (us from block start, mean over blocks): round A %.2f, ranking %.2f, "
+                "folds %.2f, end %.2f" % tuple(v / 100.0 for v in ck))
     worst = max(p["step_ms"] for p in per_rank)
     log(f"[c3] per-rank step (no collectives): max {worst:.4f} ms, "
         f"mean {np.mean([p['step_ms'] for p in per_rank]):.4f} ms; final merge {1e3 * t3:.4f} ms")

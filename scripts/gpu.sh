@@ -63,7 +63,22 @@ for t in "${TASKS[@]}"; do
             run 900 gpurun_out/c3.log python -u scripts/c3_emulate.py
             grep '^{' gpurun_out/c3.log > gpurun_out/c3.json; grep '^\[c3\]' gpurun_out/c3.log | tail -4 ;;
         c3prof)
-            run 600 gpurun_out/c3prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10 ;;
+            run 600 gpurun_out/c3prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10
+            python3 scripts/trace_summary.py gpurun_out/prof_c3/run_kernel_trace.csv | grep gvdb | head -12 ;;
+        c3clk)
+            run 600 gpurun_out/c3clk.log python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10 --p2clk
+            grep '^\[c3\]' gpurun_out/c3clk.log ;;
+        flatab)  # exact flat at 10M x 768, one box: k_flat_i8q (default) | k_flat_mx (GVDB_FLAT_I8R=0)
+            for v in i8q old; do
+                case $v in
+                    i8q) BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
+                    old) GVDB_FLAT_I8R=0 BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
+                esac
+                echo "== $v"; grep -E "B=|emit" gpurun_out/flatab_$v.log | tail -2
+            done ;;
+        flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
+            BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
+            grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;
         c4)
             run 1100 gpurun_out/c4.log python -u scripts/c4_emulate.py
             grep '^{' gpurun_out/c4.log > gpurun_out/c4.json; tail -3 gpurun_out/c4.log ;;

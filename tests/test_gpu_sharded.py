@@ -136,6 +136,10 @@ def emulate_two_exchange(g, shards, q, D, R, k):
     ((9000, 11000, 0, 10000, 12500, 7000, 10000, 10500), 768, 96, 1000),
     ((5000,) * 8, 3072, 32, 100),
     ((2000, 3, 2000, 2000, 1, 2000, 2000, 2000), 256, 20, 50),
+    # a skewed split: rank 0 owns most of the global top-3000 (> 1024 owned
+    # entries: the sorted local top-k; R > 2048: the own arrays in scratch),
+    # D % 4 != 0 (the scalar row loads and folds of the rerank)
+    ((30000, 500, 500, 0, 500, 500, 500, 500), 130, 8, 3000),
 ])
 def test_two_exchange_g8_equals_single_index_and_oracle(g, oracle_mod, sizes, D, B, R):
     import torch
