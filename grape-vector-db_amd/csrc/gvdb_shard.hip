@@ -82,7 +82,7 @@ __device__ __forceinline__ uint32_t p2_count(const uint32_t* dl, uint32_t n, uin
 // OWN_LDS: the own-entry arrays in LDS (R <= kP2OwnLds) -- a compile-time choice, so
 // every access is a plain LDS op (a runtime LDS-or-global pointer makes them FLAT ops,
 // whose vmcnt waits stall the ranking behind the in-flight row loads)
-template <bool OWN_LDS, bool VEC>
+template <bool OWN_LDS, bool VEC, bool DSTAGED>
 __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __restrict__ gathered, uint64_t words1,
                                                              uint32_t G, uint32_t me, uint32_t B, uint32_t R,
                                                              uint32_t D, const float* __restrict__ rows,
@@ -100,7 +100,19 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
     auto mark = [&](int i) {
         if (clk && threadIdx.x == 0) clk[blockIdx.x * 8u + i] = __builtin_amdgcn_s_memrealtime() - c0;
     };
-    const bool dstaged = G * R <= kP2DistLds;
+    // a barrier for LDS traffic only, while the speculative row loads are in flight
+    // (__syncthreads' fence would wait for them: vmcnt(0)); the global-scratch form
+    // (OWN_LDS false) shares global words across the block and keeps the fence
+    auto sync_lds = [&]() __attribute__((always_inline)) {
+        if constexpr (OWN_LDS)
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            __syncthreads();
+    };
+    // DSTAGED: the other lists' distances fit LDS (G*R <= kP2DistLds); compile-time, so
+    // the LDS search loop carries no merged global-load waits that would drain the
+    // speculative row loads
+    constexpr bool dstaged = DSTAGED;
     constexpr bool own_lds = OWN_LDS;
     float* qv = (float*)lds;                                   // [D]
     uint32_t* cg = lds + ((D + 3u) & ~3u);                     // [G]
@@ -143,7 +155,7 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
         opos[i] = (uint32_t)(key >> 32);
         orow[i] = (uint32_t)key;
     }
-    if (dstaged)
+    if constexpr (DSTAGED)
         for (uint32_t x = tid; x < G * R; x += kP2Threads) {
             const uint32_t g = x / R, i = x - g * R;
             if (g != me) dist[x] = (uint32_t)(glist(g)[i] >> 32);
@@ -195,13 +207,13 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
     //     staged distances), summed into posacc (the cosine slots, free until (ii))
     uint32_t* posacc = (uint32_t*)ocos;
     for (uint32_t i = tid; i < cnt_me; i += kP2Threads) posacc[i] = i;
-    __syncthreads();
+    sync_lds();
     for (uint32_t x = tid; x < cnt_me * G; x += kP2Threads) {
         const uint32_t i = x / G, g = x - i * G;
         if (g == me) continue;
         const uint32_t d = opos[i];
         uint32_t cnt;
-        if (dstaged) {
+        if constexpr (DSTAGED) {
             cnt = p2_count(dist + g * R, cg[g], d, g < me);
         } else {  // large G * R: the same search over the gathered keys
             const uint64_t* L = glist(g);
@@ -214,14 +226,14 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
         }
         if (cnt) atomicAdd(&posacc[i], cnt);
     }
-    __syncthreads();
+    sync_lds();
     // the owned entries are those below Re (a prefix of the own list)
     for (uint32_t i = tid; i < cnt_me; i += kP2Threads) {
         const uint32_t pos = posacc[i];
         opos[i] = pos;
         if (pos < Re) atomicAdd(&s_c, 1u);
     }
-    __syncthreads();
+    sync_lds();
     mark(1);
     const uint32_t c = s_c;  // the owned entries: own-list prefix [0, c)
     // (ii) exact cosine of the owned rows, kP2Rows at a time
@@ -347,8 +359,11 @@ hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint3
         clk = buf;
         shard_clk() = {buf, B};
     }
-    auto kern = R <= kP2OwnLds ? ((D & 3u) == 0 ? k_shard_phase2<true, true> : k_shard_phase2<true, false>)
-                               : ((D & 3u) == 0 ? k_shard_phase2<false, true> : k_shard_phase2<false, false>);
+    const bool own = R <= kP2OwnLds, vec = (D & 3u) == 0, dst = G * R <= kP2DistLds;
+    auto kern = own ? (vec ? (dst ? k_shard_phase2<true, true, true> : k_shard_phase2<true, true, false>)
+                           : (dst ? k_shard_phase2<true, false, true> : k_shard_phase2<true, false, false>))
+                    : (vec ? (dst ? k_shard_phase2<false, true, true> : k_shard_phase2<false, true, false>)
+                           : (dst ? k_shard_phase2<false, false, true> : k_shard_phase2<false, false, false>));
     hipLaunchKernelGGL(kern, dim3(B), dim3(kP2Threads), lds, s, gathered1, words1, G, me, B, R, D, rows, norms, ids,
                        queries, k, err, block2, opos, orow, ocos, clk);
     GVDB_LAUNCH_CHECK();
