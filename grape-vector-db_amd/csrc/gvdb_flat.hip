@@ -807,6 +807,13 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
 // sub-tile; the mirror is read from HBM exactly once.  Epilogue, candidate rule
 // (U = approx + qa*rho_x + qd >= tau) and the block nomination list are
 // k_flat_mx's; all vector-memory ops of the loop are inline asm with counted vmcnt.
+#ifndef I8Q_PF
+#define I8Q_PF 2  // sub-tiles between a line's L2 prefetch and its DMA (A/B knob)
+#endif
+#ifndef I8Q_BR
+#define I8Q_BR 4  // B-fragment ring depth in k-steps (A/B knob)
+#endif
+constexpr int kI8qBr = I8Q_BR;
 constexpr uint32_t kI8qSub = 2;    // 32-row groups per LDS sub-tile
 constexpr uint32_t kI8qBufs = 3;   // LDS sub-tile buffers
 constexpr uint32_t kI8qCl = 1792;  // block nomination list, u32 entries (flushed at a barrier once half full)
@@ -814,14 +821,19 @@ template <int KC>
 __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     constexpr int KS = 4 * KC;                          // k-steps of 32 per row group
     constexpr uint32_t kPieces = kI8qSub * KC * 4;      // 1 KiB pieces per sub-tile
-    constexpr uint32_t kPerWave = kPieces / 8;          // DMA instructions per wave per sub-tile
+    constexpr uint32_t kPerWave = kPieces / 8;          // row DMAs per wave per sub-tile
     constexpr uint32_t kSubBytes = kPieces * 1024u;
+    constexpr uint32_t kRows = kI8qSub * 32u;           // rows per sub-tile (one per lane)
+    constexpr uint32_t kBufBytes = kSubBytes + 2u * kRows * 4u;  // + the rows' s_x/|x| and rho_x
+    constexpr uint32_t kOps = kPerWave + 1u;            // vector-memory ops per wave per stage
     static_assert(kPieces % 8 == 0, "pieces split evenly over the waves");
-    __shared__ __attribute__((aligned(16))) char Bs[kI8qBufs][kSubBytes];
+    static_assert(kRows == 64, "one operand word per lane");
+    __shared__ __attribute__((aligned(16))) char Bs[kI8qBufs][kBufBytes];
     // nomination (slot q, block step i, row group gi, row j) as q << 24 | i << 6 | gi << 5 | j
     __shared__ uint32_t cl[kI8qCl];
     __shared__ uint32_t cl_n;
     __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[kFxQ];
+    __shared__ __attribute__((aligned(16))) uint32_t pf_sink[64];  // the prefetches' landing words (never read)
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t N = a.N, G = gridDim.x;
@@ -829,16 +841,45 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     const uint32_t ns = blockIdx.x < nsub_all ? (nsub_all - blockIdx.x + G - 1) / G : 0u;  // sub-tiles b, b+G, ...
     const char* rowsx = (const char*)a.rowsx;
     constexpr uint32_t kSubPerTile = kFxRows / 32u / kI8qSub;
-    // piece p = (gi*KC + c)*4 + s4 of sub-tile v: row group 2*(v % 4) + gi of tile v / 4
-    auto dma = [&](uint32_t i) __attribute__((always_inline)) {  // the block's i-th sub-tile -> buffer i % 3
+    auto sub_of = [&](uint32_t i, uint32_t& t, uint32_t& u) __attribute__((always_inline)) {
         const uint32_t ii = i < ns ? i : (ns ? ns - 1 : 0);  // clamped: a valid read, never used
-        const uint32_t v = blockIdx.x + ii * G, t = v / kSubPerTile, u = v % kSubPerTile;
+        const uint32_t v = blockIdx.x + ii * G;
+        t = v / kSubPerTile;
+        u = v % kSubPerTile;
+    };
+    // stage i: the block's i-th sub-tile -> buffer i % 3, as kOps vector-memory ops per
+    // wave: kPerWave 1 KiB row pieces (piece p = (gi*KC + c)*4 + s4: row group
+    // kI8qSub*u + gi of tile t), then one more op -- waves 0 / 1 DMA the 64 rows' s_x/|x|
+    // / rho_x, waves 2..7 prefetch one 128-B line each (384 lines = one whole sub-tile)
+    // of sub-tile i + I8Q_PF into L2 / MALL ahead of its DMA
+    auto stage = [&](uint32_t i) __attribute__((always_inline)) {
+        uint32_t t, u;
+        sub_of(i, t, u);
         const uint32_t l0 = (uint32_t)(uintptr_t)Bs[i % kI8qBufs];
 #pragma unroll
         for (uint32_t k = 0; k < kPerWave; ++k) {
             const uint32_t p = wv * kPerWave + k, s4 = p & 3u, c = (p >> 2) % KC, gi = (p >> 2) / KC;
             const char* ga = rowsx + ((((uint64_t)t * KC + c) * 8u + kI8qSub * u + gi) * 4u + s4) * 1024u + lane * 16u;
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(ga), "s"(l0 + p * 1024u)
+                         : "memory");
+        }
+        if (wv < 2) {
+            const uint32_t n = min(t * kFxRows + u * kRows + lane, N - 1u);
+            const float* src = (wv == 0 ? a.rscale : a.rrho) + n;
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src),
+                         "s"(l0 + kSubBytes + wv * kRows * 4u)
+                         : "memory");
+        } else {
+            uint32_t tp, up;
+            sub_of(i + I8Q_PF, tp, up);
+            const uint32_t L = (wv - 2u) * 64u + lane, p = L >> 3, s4 = p & 3u, c = (p >> 2) % KC,
+                           gi = (p >> 2) / KC;
+            const char* ga = rowsx + ((((uint64_t)tp * KC + c) * 8u + kI8qSub * up + gi) * 4u + s4) * 1024u +
+                             (L & 7u) * 128u;
+            // into a scratch LDS word per lane (no VGPR destination: a register written
+            // when the load returns could already hold another value)
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(ga),
+                         "s"((uint32_t)(uintptr_t)pf_sink)
                          : "memory");
         }
     };
@@ -862,11 +903,10 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     if (tid == 0) cl_n = 0;
     __syncthreads();  // the compiler-visible loads above are complete from here on
     if (ns) {
-        dma(0);
-        dma(1);
+        stage(0);
+        stage(1);
     }
     fx_v16i acc[kI8qSub];
-    float rsc[kI8qSub], rrh[kI8qSub];
     auto row_of = [&](uint32_t e) {  // a list entry's row
         const uint32_t v = blockIdx.x + ((e >> 6) & 0x3ffffu) * G;
         return (v / kSubPerTile) * kFxRows + (kI8qSub * (v % kSubPerTile) + ((e >> 5) & 1u)) * 32u + (e & 31u);
@@ -879,8 +919,8 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         }
     };
     for (uint32_t i = 0; i < ns; ++i) {
-        // sub-tile i landed (this wave's part: sub-tile i+1's kPerWave DMAs are younger), then all waves'
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPerWave) : "memory");
+        // stage i landed (stage i+1's kOps ops are the younger ones), then every wave's part
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps) : "memory");
         __syncthreads();
         if (cl_n >= kI8qCl / 2) {  // (block-uniform) rare: empty the list before it can overflow
             flush(min(cl_n, kI8qCl));
@@ -888,42 +928,42 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             if (tid == 0) cl_n = 0;
             __syncthreads();
         }
-        const uint32_t v = blockIdx.x + i * G, t = v / kSubPerTile, u = v % kSubPerTile;
-        // the sub-tile's row operands, then sub-tile i+2 into the buffer read in step i-1
-#pragma unroll
-        for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
-            const uint32_t n = min(t * kFxRows + (kI8qSub * u + gi) * 32u + (lane & 31u), N - 1u);
-            asm volatile("global_load_dword %0, %1, off" : "=v"(rsc[gi]) : "v"(a.rscale + n) : "memory");
-            asm volatile("global_load_dword %0, %1, off" : "=v"(rrh[gi]) : "v"(a.rrho + n) : "memory");
-        }
-        dma(i + 2);
+        stage(i + 2);  // into the buffer read in step i-1
+        uint32_t t, u;
+        sub_of(i, t, u);
         const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
+        const float* ops = (const float*)(Bs[i % kI8qBufs] + kSubBytes);
 #pragma unroll
         for (uint32_t gi = 0; gi < kI8qSub; ++gi)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[gi][e] = 0;
-        fx_v4i bf[2][kI8qSub];
+        // B fragments from LDS, kI8qBr k-steps ahead of their MFMAs (LDS latency > the
+        // ~64 cycles of one k-step's two MFMAs)
+        constexpr int BR = kI8qBr;
+        fx_v4i bf[BR][kI8qSub];
 #pragma unroll
-        for (uint32_t gi = 0; gi < kI8qSub; ++gi) bf[0][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u) * 1024u);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            if (s + 1 < KS) {
-#pragma unroll
-                for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-                    bf[(s + 1) & 1][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)(s + 1)) * 1024u);
-            }
+        for (int s = 0; s < BR - 1; ++s)
 #pragma unroll
             for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-                acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s & 1][gi], acc[gi], 0, 0, 0);
-        }
-        // the row operands (sub-tile i+2's DMAs are younger)
+                bf[s][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)s) * 1024u);
 #pragma unroll
-        for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(rsc[gi]), "+v"(rrh[gi]) : "n"(kPerWave));
+        for (int s = 0; s < KS; ++s) {
+            if (s + BR - 1 < KS) {
+#pragma unroll
+                for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+                    bf[(s + BR - 1) % BR][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)(s + BR - 1)) * 1024u);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // the reads stay BR - 1 k-steps ahead (no sinking)
+#pragma unroll
+            for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+                acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
             const uint32_t n = t * kFxRows + (kI8qSub * u + gi) * 32u + (lane & 31u);
-            const float rinv = n < N ? rsc[gi] : 0.0f, rho = n < N ? rrh[gi] : 0.0f;
+            const uint32_t rl = gi * 32u + (lane & 31u);
+            const float rinv = n < N ? ops[rl] : 0.0f, rho = n < N ? ops[kRows + rl] : 0.0f;
             // this lane's 16 slots: qb0 + (e & 3) + 8 (e >> 2)
             uint32_t qb0 = wv * 32u + 4u * (lane >> 5);
             asm volatile("" : "+v"(qb0));  // keep the per-slot addresses out of the loop

@@ -124,6 +124,14 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t) / steps
 
+    # steady state before any rank is timed (the first-timed rank otherwise carries
+    # the clock ramp of the idle GPU)
+    for _ in range(10):
+        for r in range(G):
+            p1(r)
+            p2(r)
+            p3()
+    torch.cuda.synchronize()
     per_rank = []
     for r in range(G):
         step = timed(lambda: (p1(r), p2(r), p3()), a.steps)

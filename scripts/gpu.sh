@@ -69,10 +69,11 @@ for t in "${TASKS[@]}"; do
             run 600 gpurun_out/c3clk.log python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10 --p2clk
             grep '^\[c3\]' gpurun_out/c3clk.log ;;
         flatab)  # exact flat at 10M x 768, one box: k_flat_i8q (default) | k_flat_mx (GVDB_FLAT_I8R=0)
-            for v in i8q old; do
+            for v in i8q old br6; do
                 case $v in
                     i8q) BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
                     old) GVDB_FLAT_I8R=0 BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
+                    br6) GVDB_LIB_PATH=$PWD/grape-vector-db_amd/abl/libgvdb_pf0.so BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
                 esac
                 echo "== $v"; grep -E "B=|emit" gpurun_out/flatab_$v.log | tail -2
             done ;;
