@@ -310,6 +310,7 @@ def main():
         for r in (1000, 4000):
             run_point(f"bq R={r}", gvdb.SearchParams(rescore_count=r))
         run_point("exact flat (i8/bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1))
+        points[-1]["emit_roofline"] = flat_emit_roofline(L, ix, q, k, n_local, D)
         if planted:
             ptruth = pi.cpu().numpy()
             for r in (R, 1000):
@@ -553,16 +554,17 @@ def main():
 
 
 PMC_FILE = "profiles/r03/pmc_bench_10M.json"
+PMC_FLAT_FILE = "profiles/r03/pmc_flat_i8q_10M.json"  # scripts/gpu.sh pmc:flat:k_flat_i8q (10M x 768, B = 256)
 
 
-def pmc_traffic(kernel_prefix, n_local, D):
+def pmc_traffic(kernel_prefix, n_local, D, pmc_file=None):
     """HBM read bytes per launch of `kernel_prefix` from the committed PMC pass of
     this round (PMC_FILE: rocprofv3 --pmc FETCH_SIZE over bench.py's own command,
     x2 gfx950 streaming correction), only when collected at this workload's
     shard size."""
     if n_local != 10_000_000 or D != 768:
         return None
-    for rel in (PMC_FILE.split("/")[1:],):
+    for rel in ((pmc_file or PMC_FILE).split("/")[1:],):
         path = os.path.join(ROOT, "profiles", *rel)
         if not os.path.exists(path):
             continue
@@ -572,6 +574,36 @@ def pmc_traffic(kernel_prefix, n_local, D):
             if name.startswith(kernel_prefix) and "hbm_read_bytes_per_launch" in d:
                 return d["hbm_read_bytes_per_launch"]
     return None
+
+
+def flat_emit_roofline(L, ix, q, k, n_local, D):
+    """The exact flat search's dominant kernel, its i8 candidate pass (k_flat_i8q at
+    D = 768): HIP-event time per launch (gvdb_timing slot 7, 3 searches) against the
+    algorithmic bytes of one launch (the N x ceil(D/128)*128 B int8 mirror, read
+    once) -> HBM roofline fraction; traffic from the committed PMC pass."""
+    B = q.shape[0]
+    oi = torch.zeros((B, k), dtype=torch.int64, device=q.device)
+    osc = torch.zeros((B, k), dtype=torch.float32, device=q.device)
+    L.gvdb_timing_reset()
+    L.gvdb_timing_enable(1)
+    for _ in range(3):
+        ix.search_device(q, k, oi, osc, None, gvdb.SearchParams(mode=1))
+    torch.cuda.synchronize()
+    L.gvdb_timing_enable(0)
+    em, en = timing_slot(L, 7)
+    L.gvdb_timing_reset()
+    if en == 0:
+        return None  # the bf16 tier or the exact scan answered
+    ms = em / en
+    algo = n_local * ((D + 127) // 128) * 128
+    achieved = algo / (ms * 1e-3) / 1e9
+    return {"kernel": "k_flat_i8q (exact flat, i8 MFMA candidate pass, query fragments in VGPRs, rows DMA'd to LDS)"
+                      if D > 640 and D <= 768 else "k_flat_mx (exact flat, i8 candidate pass)",
+            "bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
+            "traffic": pmc_traffic("gvdb::k_flat_i8q<", n_local, D, PMC_FLAT_FILE), "avg_launch_ms": ms,
+            "algorithmic_bytes_per_launch": algo,
+            "source": "avg_launch_ms: HIP events around each emit launch (gvdb_timing slot 7) over 3 searches; "
+                      "traffic: rocprofv3 --pmc FETCH_SIZE x 2, " + PMC_FLAT_FILE}
 
 
 def cpu_share():

@@ -1077,6 +1077,18 @@ static gvdb_status ensure_rowsq(const gvdb_index* ix, Workspace& ws, hipStream_t
 // K4 on MFMA: certified candidate pass + exact rerank (gvdb_flat.hip).  Sets
 // *certified = false when any query's list could not be proven exact (the
 // caller then runs the exact full scan); results are then meaningless.
+// host-buffer searches: slots past a query's count read as id 0 / score 0, not
+// whatever an earlier search left in the device output buffers
+static void zero_past_counts(uint64_t* ids, float* scores, const uint32_t* n, uint64_t B, uint64_t k) {
+    for (uint64_t q = 0; q < B; ++q) {
+        const uint64_t nq = n[q] <= k ? n[q] : k;  // GVDB_N_POISONED: the whole row stays as written
+        if (n[q] != GVDB_N_POISONED && nq < k) {
+            memset(ids + q * k + nq, 0, (k - nq) * 8);
+            memset(scores + q * k + nq, 0, (k - nq) * 4);
+        }
+    }
+}
+
 static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32_t B, uint32_t dim, uint32_t k, int kind,
                            int descending, uint64_t* d_ids, float* d_scores, uint32_t* d_n, Workspace& ws,
                            hipStream_t s, bool i8, bool* certified) {
@@ -1113,7 +1125,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
     uint32_t* probes = ws.fx_probe.as<uint32_t>();
     float* pscores = (float*)(probes + kFxQ * 16);
     uint32_t* pcount = probes + kFxQ * 32;
-    HIP_TRY(ws.fx_cand.ensure((size_t)kFxQ * cc * 4), "alloc candidates");
+    HIP_TRY(ws.fx_cand.ensure((size_t)kFxQ * cc * 8), "alloc candidates");  // rows, then their approx scores
     HIP_TRY(ws.fx_scores.ensure((size_t)kFxQ * cc * 4), "alloc candidate scores");
     HIP_TRY(ws.thr.ensure(kFxQ * 4), "alloc thresholds");
     HIP_TRY(ws.zero.ensure((kFxQ + 4) * 4), "alloc counts");
@@ -1131,6 +1143,11 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
     if (timed && !ws.ev.ok) ws.ev.create();
     timed = timed && ws.ev.ok;
     HIP_TRY(hipMemsetAsync(fail, 0, 16, s), "memset fail");
+    // GVDB_FLAT_PRUNE=0: rerank every nominated candidate (A/B timing)
+    static const bool prune = [] {
+        const char* e = getenv("GVDB_FLAT_PRUNE");
+        return !(e && e[0] == '0');
+    }();
     for (uint32_t g0 = 0; g0 < B; g0 += kFxQ) {
         if (timed) HIP_TRY(hipEventRecord(ws.ev.e[0], s), "event");
         const uint32_t Bg = std::min<uint32_t>(kFxQ, B - g0);
@@ -1164,6 +1181,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         a.thr = ws.thr.as<float>();
         a.counts = counts;
         a.cand = ws.fx_cand.as<uint32_t>();
+        a.cscore = prune ? (float*)(a.cand + (size_t)kFxQ * cc) : nullptr;
         a.candcap = cc;
         a.overflow = fail;
         {
@@ -1198,6 +1216,10 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         HIP_TRY(launch_flat_mx_emit(a, s), "flat candidate pass");
         if (timed) HIP_TRY(hipEventRecord(ws.ev.e[2], s), "event");
         DBG_SYNC(s, "dbg: flat candidate pass");
+        if (prune)
+            HIP_TRY(launch_flat_prune(counts, a.cand, a.cscore, cc, Bg, k, i8 ? qa : nullptr, qd, i8 ? a.rrho : nullptr,
+                                      ix->ids, s),
+                    "flat prune");
         RerankArgs rr{};
         rr.rows = ix->rows;
         rr.clen = dim;
@@ -1362,6 +1384,7 @@ gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64
     HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
     HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download n");
     HIP_TRY(hipStreamSynchronize(s), "sync");
+    zero_past_counts(out_ids, out_scores, out_n, B, k);
     return check_poisoned(out_n, B);
 }
 
@@ -1476,6 +1499,7 @@ gvdb_status gvdb_index_search_filtered(const gvdb_index* ix, const float* querie
     HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
     HIP_TRY(hipMemcpyAsync(out_n, ws.out_n.p, B * 4, hipMemcpyDeviceToHost, s), "download n");
     HIP_TRY(hipStreamSynchronize(s), "sync");
+    zero_past_counts(out_ids, out_scores, out_n, B, k);
     return check_poisoned(out_n, B);
 }
 

@@ -266,6 +266,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
     // instead of a global atomic round trip inside the MFMA loop)
     constexpr uint32_t kCl = SAMPLE ? 1u : 2048u;
     __shared__ uint64_t cl[kCl];
+    __shared__ float cs[kCl];  // the nominations' approx scores
     __shared__ uint32_t cl_n;
     // per-slot epilogue operands, staged once: qinv, thr - (i8) qa
     __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[I8 ? kFxQ : 4];
@@ -493,13 +494,18 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
 #pragma unroll
                     for (int e = 0; e < 16; ++e) {
                         const uint32_t q = qb0 + (e & 3) + 8 * (e >> 2);
-                        if (n < N && (float)acc[i][r][e] * qs[e] >= ts[e]) {
+                        const float v = (float)acc[i][r][e] * qs[e];
+                        if (n < N && v >= ts[e]) {
                             const uint32_t li = atomicAdd(&cl_n, 1u);
                             if (li < kCl) {
                                 cl[li] = ((uint64_t)q << 32) | n;
+                                cs[li] = v;
                             } else {  // block list full: straight to the global list
                                 const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-                                if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = n;
+                                if (pos < a.candcap) {
+                                    a.cand[(uint64_t)q * a.candcap + pos] = n;
+                                    if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = v;
+                                }
                             }
                         }
                     }
@@ -599,7 +605,10 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
             const uint64_t v = cl[i];
             const uint32_t q = (uint32_t)(v >> 32);
             const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-            if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = (uint32_t)v;
+            if (pos < a.candcap) {
+                a.cand[(uint64_t)q * a.candcap + pos] = (uint32_t)v;
+                if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = cs[i];
+            }
         }
     }
     __builtin_amdgcn_s_waitcnt(0);  // drain the clamped prefetches before exit
@@ -695,6 +704,116 @@ __global__ __launch_bounds__(256) void k_flat_tau(const float* __restrict__ psco
             v[j - 1] = t;
         }
     thr[q] = (c >= mk ? v[mk - 1] : -__builtin_inff()) - qd[q];
+}
+
+// Candidate pruning between the emit pass and the exact rerank.  Each
+// nomination carries its approx score v, and the emit pass's own bound puts the
+// exact f32 cosine in [v - m, v + m], m = qa*rho_x + qd (bf16: m = qd).  With L
+// the k-th largest lower bound v - m over the live (non-orphan) candidates, k
+// live rows have exact cosine >= L, so the k-th best exact cosine is >= L, and a
+// candidate whose upper bound v + m is below L can neither be in the top k nor
+// tie its k-th score: it is dropped without a rerank, as are the orphans that
+// k_flat_final skips anyway.  Both bounds are widened by kPruneSlack against
+// the f32 roundings of v, m and the sums here.  The survivors keep the list's
+// (unordered) form; k_flat_final sorts them and its certificate (k-th exact
+// score >= tau) is unchanged.  L by a 4 x 8-bit radix select over the
+// order-mapped lower bounds; one block per query.
+constexpr float kPruneSlack = 2e-6f;
+constexpr uint32_t kPrThreads = 1024;
+constexpr uint32_t kPrPer = kFxCandCap / kPrThreads;
+__global__ __launch_bounds__(kPrThreads) void k_flat_prune(uint32_t* __restrict__ counts, uint32_t* __restrict__ cand,
+                                                          const float* __restrict__ cscore, uint32_t candcap,
+                                                          uint32_t k, const float* __restrict__ qa,
+                                                          const float* __restrict__ qd,
+                                                          const float* __restrict__ rrho,
+                                                          const uint64_t* __restrict__ ids) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sel[2];  // chosen key prefix, rank still to find below it
+    __shared__ uint32_t live_n, out_n;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t c = counts[q];
+    if (k == 0 || c <= k || c > candcap) return;  // nothing to drop / overflow (k_flat_final fails it)
+    const float qaq = qa ? qa[q] : 0.0f, qdq = qd[q];
+    uint32_t row[kPrPer], key[kPrPer];
+    float ub[kPrPer];
+    uint32_t live = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPrPer; ++j) {
+        const uint32_t i = tid + j * kPrThreads;
+        row[j] = 0;
+        key[j] = 0;  // below every live key (f32_order of a finite or infinite value is > 0)
+        ub[j] = -__builtin_inff();
+        if (i < c) {
+            const uint32_t r = cand[(uint64_t)q * candcap + i];
+            const float v = cscore[(uint64_t)q * candcap + i];
+            const float m = (rrho ? qaq * rrho[r] : 0.0f) + qdq;
+            row[j] = r;
+            if (!(ids && ids[r] == kOrphan)) {
+                ub[j] = (v + m) + kPruneSlack;
+                key[j] = f32_order((v - m) - kPruneSlack);
+                ++live;
+            }
+        }
+    }
+    if (tid == 0) {
+        live_n = 0;
+        out_n = 0;
+        sel[0] = 0;
+        sel[1] = k;
+    }
+    __syncthreads();
+    if (live) atomicAdd(&live_n, live);
+    __syncthreads();
+    float L = -__builtin_inff();  // fewer than k live rows: keep them all
+    if (live_n >= k) {
+        for (int sh = 24; sh >= 0; sh -= 8) {
+            if (tid < 256) hist[tid] = 0;
+            __syncthreads();
+            const uint32_t pre = sel[0];
+            const uint32_t hm = sh == 24 ? 0u : ~0u << (sh + 8);
+#pragma unroll
+            for (uint32_t j = 0; j < kPrPer; ++j)
+                if (key[j] && (key[j] & hm) == (pre & hm)) atomicAdd(&hist[(key[j] >> sh) & 255u], 1u);
+            __syncthreads();
+            if (tid < 64) {  // digit of the rem-th largest: lane l holds bins 4l .. 4l+3
+                const uint32_t rem = sel[1];
+                const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
+                               h3 = hist[4 * lane + 3];
+                const uint32_t t = h0 + h1 + h2 + h3;
+                uint32_t x = t;  // inclusive suffix sum over lanes >= l
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_down(x, o);
+                    if (lane + o < 64) x += y;
+                }
+                uint32_t above = x - t;  // keys in higher lanes' bins
+                const uint32_t hb[4] = {h0, h1, h2, h3};
+#pragma unroll
+                for (int b = 3; b >= 0; --b) {
+                    if (above < rem && rem <= above + hb[b]) {
+                        sel[0] = pre | ((4u * lane + (uint32_t)b) << sh);
+                        sel[1] = rem - above;
+                    }
+                    above += hb[b];
+                }
+            }
+            __syncthreads();
+        }
+        const uint32_t o = sel[0];  // f32_order of the k-th largest lower bound
+        L = __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+    }
+    // every entry is in registers: compact in place
+#pragma unroll
+    for (uint32_t j = 0; j < kPrPer; ++j) {
+        if (ub[j] >= L) {  // -inf (orphans, empty slots) never passes a finite L; -inf L keeps the live rows
+            if (!(ub[j] == -__builtin_inff())) {
+                const uint32_t pos = atomicAdd(&out_n, 1u);
+                cand[(uint64_t)q * candcap + pos] = row[j];
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) counts[q] = out_n;
 }
 
 // Per query: sort the reranked candidates (exact score, then row ascending),
@@ -816,7 +935,7 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
 constexpr int kI8qBr = I8Q_BR;
 constexpr uint32_t kI8qSub = 2;    // 32-row groups per LDS sub-tile
 constexpr uint32_t kI8qBufs = 3;   // LDS sub-tile buffers
-constexpr uint32_t kI8qCl = 1792;  // block nomination list, u32 entries (flushed at a barrier once half full)
+constexpr uint32_t kI8qCl = 1024;  // block nomination list, u32 entries + scores (flushed at a barrier once half full)
 template <int KC>
 __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     constexpr int KS = 4 * KC;                          // k-steps of 32 per row group
@@ -831,6 +950,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     __shared__ __attribute__((aligned(16))) char Bs[kI8qBufs][kBufBytes];
     // nomination (slot q, block step i, row group gi, row j) as q << 24 | i << 6 | gi << 5 | j
     __shared__ uint32_t cl[kI8qCl];
+    __shared__ float cs[kI8qCl];  // their approx scores
     __shared__ uint32_t cl_n;
     __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[kFxQ];
     __shared__ __attribute__((aligned(16))) uint32_t pf_sink[64];  // the prefetches' landing words (never read)
@@ -915,7 +1035,10 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         for (uint32_t x = tid; x < m; x += kFxThreads) {
             const uint32_t e = cl[x], q = e >> 24;
             const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-            if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = row_of(e);
+            if (pos < a.candcap) {
+                a.cand[(uint64_t)q * a.candcap + pos] = row_of(e);
+                if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = cs[x];
+            }
         }
     };
     for (uint32_t i = 0; i < ns; ++i) {
@@ -990,13 +1113,18 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const uint32_t q = qb0 + (e & 3) + 8u * (e >> 2);
-                if (n < N && (float)acc[gi][e] * qs[e] >= ts[e]) {
+                const float v = (float)acc[gi][e] * qs[e];
+                if (n < N && v >= ts[e]) {
                     const uint32_t li = atomicAdd(&cl_n, 1u);
                     if (li < kI8qCl) {
                         cl[li] = (q << 24) | (i << 6) | (gi << 5) | (lane & 31u);
+                        cs[li] = v;
                     } else {  // block list full (a burst within one sub-tile): straight to the global list
                         const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-                        if (pos < a.candcap) a.cand[(uint64_t)q * a.candcap + pos] = n;
+                        if (pos < a.candcap) {
+                            a.cand[(uint64_t)q * a.candcap + pos] = n;
+                            if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = v;
+                        }
                     }
                 }
             }
@@ -1040,6 +1168,16 @@ hipError_t launch_flat_mx_emit(const FlatMxArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((k_flat_mx<false, true>), dim3(fx_grid(tiles)), dim3(kFxThreads), 0, s, a);
     else
         hipLaunchKernelGGL((k_flat_mx<false, false>), dim3(fx_grid(tiles)), dim3(kFxThreads), 0, s, a);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_flat_prune(uint32_t* counts, uint32_t* cand, const float* cscore, uint32_t candcap, uint32_t B,
+                             uint32_t k, const float* qa, const float* qd, const float* rrho, const uint64_t* ids,
+                             hipStream_t s) {
+    if (B == 0 || k == 0 || candcap > kFxCandCap) return hipSuccess;
+    hipLaunchKernelGGL(k_flat_prune, dim3(B), dim3(kPrThreads), 0, s, counts, cand, cscore, candcap, k, qa, qd, rrho,
+                       ids);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

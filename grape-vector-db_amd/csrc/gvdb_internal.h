@@ -258,6 +258,7 @@ struct FlatMxArgs {
     const float* thr;        // emit pass: [B]
     uint32_t* counts;        // emit pass: [B] (zeroed by the caller)
     uint32_t* cand;          // emit pass: [B][candcap] candidate rows
+    float* cscore;           // emit pass: [B][candcap] their approx scores (null: not stored)
     uint32_t candcap;
     uint32_t* overflow;      // emit pass: set to 1 if a wave's LDS staging slice overflowed
     int dbg;                 // unused (kept for ABI stability of the launch struct)
@@ -275,6 +276,12 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
                                 float* qa, float* qd, hipStream_t s);
 hipError_t launch_flat_mx_sample(const FlatMxArgs& a, hipStream_t s);
 hipError_t launch_flat_mx_emit(const FlatMxArgs& a, hipStream_t s);
+// Drops the candidates that cannot reach a query's top k (upper bound below the
+// k-th largest lower bound of the live candidates) and orphaned rows; counts[q]
+// becomes the survivors.  qa / rrho null for bf16 (bound = qd).
+hipError_t launch_flat_prune(uint32_t* counts, uint32_t* cand, const float* cscore, uint32_t candcap, uint32_t B,
+                             uint32_t k, const float* qa, const float* qd, const float* rrho, const uint64_t* ids,
+                             hipStream_t s);
 // probes[q][16] = rows of the 16 largest sampled MFMA scores, pcount[q] valid
 hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, uint32_t* probes,
                               uint32_t* pcount, hipStream_t s);

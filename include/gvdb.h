@@ -175,7 +175,8 @@ gvdb_status gvdb_index_add_device(gvdb_index* index, const float* d_rows, uint64
 gvdb_status gvdb_index_build(gvdb_index* index);
 /* search (index.rs:212-231) for a batch of B queries (B x dim, host memory).
  * Per query q, up to k results: out_ids[q*k + i], out_scores[q*k + i],
- * count out_n[q].  IndexNotBuilt when the index is empty (index.rs:213). */
+ * count out_n[q]; slots i >= out_n[q] are zero-filled.  IndexNotBuilt when
+ * the index is empty (index.rs:213). */
 gvdb_status gvdb_index_search(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
                               uint64_t k, const gvdb_search_params* sp, uint64_t* out_ids,
                               float* out_scores, uint32_t* out_n);

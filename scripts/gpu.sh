@@ -65,15 +65,19 @@ for t in "${TASKS[@]}"; do
         c3prof)
             run 600 gpurun_out/c3prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10
             python3 scripts/trace_summary.py gpurun_out/prof_c3/run_kernel_trace.csv | grep gvdb | head -12 ;;
+        c3floor)  # c3 per-rank step with the default sample floor vs 131072 / 262144 sample rows (same box)
+            for f in 0 131072 262144; do
+                GVDB_SAMPLE_FLOOR=$f run 600 gpurun_out/c3floor_$f.log python3 scripts/c3_emulate.py --oracle-queries 0 --steps 20
+                echo "== floor $f"; grep '^\[c3\]' gpurun_out/c3floor_$f.log | tail -2
+            done ;;
         c3clk)
             run 600 gpurun_out/c3clk.log python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10 --p2clk
             grep '^\[c3\]' gpurun_out/c3clk.log ;;
-        flatab)  # exact flat at 10M x 768, one box: k_flat_i8q (default) | k_flat_mx (GVDB_FLAT_I8R=0)
-            for v in i8q old br6; do
+        flatab)  # exact flat at 10M x 768, one box: candidate pruning (default) | every candidate reranked
+            for v in prune noprune; do
                 case $v in
-                    i8q) BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
-                    old) GVDB_FLAT_I8R=0 BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
-                    br6) GVDB_LIB_PATH=$PWD/grape-vector-db_amd/abl/libgvdb_pf0.so BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
+                    prune) BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
+                    noprune) GVDB_FLAT_PRUNE=0 BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
                 esac
                 echo "== $v"; grep -E "B=|emit" gpurun_out/flatab_$v.log | tail -2
             done ;;

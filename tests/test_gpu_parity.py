@@ -420,6 +420,43 @@ def test_flat_mfma_after_mutations(g, oracle_mod):
         assert list(ids[b, : n[b]]) == list(live[ri]) and same_f32(sc[b, : n[b]], rs)
 
 
+@pytest.mark.parametrize("kind", ["i8", "bf16"])
+def test_flat_prune_skips_orphans_and_keeps_ties(g, oracle_mod, monkeypatch, kind):
+    """Candidate pruning (k_flat_prune) between the MFMA pass and the exact rerank:
+    the k-th largest lower bound is taken over LIVE rows only.  Each query's 40
+    nearest rows are re-added under their ids with far vectors, so the orphaned
+    old rows still top the MFMA pass, and the live neighbours come in groups of 4
+    exact duplicates (ties at the k-th score).  Certified on the MFMA tier (no
+    fallback), ids and scores equal the oracle over the live rows."""
+    monkeypatch.setenv("GVDB_FLAT", kind)
+    N, D, B, k = 70_000, 64, 6, 10
+    x = rng_rows(91, N, D)
+    r = np.random.default_rng(92)
+    centers = r.choice(N, B, replace=False)
+    Q = x[centers] + np.float32(0.3) * rng_rows(93, B, D)
+    xn = x / np.linalg.norm(x, axis=1, keepdims=True)
+    order = np.argsort(-(xn @ (Q / np.linalg.norm(Q, axis=1, keepdims=True)).T), axis=0, kind="stable")
+    near = np.unique(order[:40].ravel())             # to be orphaned
+    nxt = [c for c in order[40:48].T.ravel() if c not in set(near)]
+    for j, c in enumerate(nxt[: len(nxt) // 4 * 4]):  # live neighbours in groups of 4 equal rows
+        x[c] = x[nxt[j // 4 * 4]]
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    fresh = -x[near]  # cosine -c: far from every query
+    ix.add_batch(near.astype(np.uint64), fresh)
+    keep = np.setdiff1d(np.arange(N), near)
+    live_x = np.concatenate([x[keep], fresh])
+    live_id = np.concatenate([keep, near])
+    before, before_i8 = g.lib().gvdb_flat_fallback_count(), g.lib().gvdb_flat_i8_fallback_count()
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=0))
+    assert g.lib().gvdb_flat_fallback_count() == before, "MFMA candidate pass was not certified"
+    assert g.lib().gvdb_flat_i8_fallback_count() == before_i8, "i8 candidate pass was not certified"
+    for b in range(B):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], live_x, k)
+        assert list(ids[b, : n[b]]) == list(live_id[ri]), b
+        assert same_f32(sc[b, : n[b]], rs)
+
+
 @pytest.mark.parametrize("N,k", [(4000, 1), (4000, 10), (4000, 1000), (4000, 1024), (4000, 1500), (4000, 5000),
                                  (40000, 10), (40000, 1024)])
 def test_flat_small_n_topk_matches_oracle_and_sort_path(g, oracle_mod, monkeypatch, N, k):
