@@ -927,10 +927,20 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
 // (U = approx + qa*rho_x + qd >= tau) and the block nomination list are
 // k_flat_mx's; all vector-memory ops of the loop are inline asm with counted vmcnt.
 #ifndef I8Q_PF
-#define I8Q_PF 2  // sub-tiles between a line's L2 prefetch and its DMA (A/B knob)
+#define I8Q_PF 0  // > 0: waves 2..7 prefetch sub-tile i + I8Q_PF into L2 (A/B knob; the extra line
+                  // requests slowed the DMA stream itself: 1.30 -> 2.02 ms memory-only at 10M x 768)
 #endif
 #ifndef I8Q_BR
 #define I8Q_BR 4  // B-fragment ring depth in k-steps (A/B knob)
+#endif
+#ifndef I8Q_PFW
+#define I8Q_PFW 0  // 1: a wave's prefetch op is waited for one step later than its stage (A/B knob)
+#endif
+#ifndef I8Q_ROWPOL
+#define I8Q_ROWPOL ""  // cache-policy suffix of the row DMAs (A/B knob: " nt")
+#endif
+#ifndef I8Q_ABL
+#define I8Q_ABL 0  // timing ablation builds only (results invalid): 1 no epilogue, 2 no MFMA, 4 no row DMA, 8 no step barrier
 #endif
 constexpr int kI8qBr = I8Q_BR;
 constexpr uint32_t kI8qSub = 2;    // 32-row groups per LDS sub-tile
@@ -980,7 +990,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         for (uint32_t k = 0; k < kPerWave; ++k) {
             const uint32_t p = wv * kPerWave + k, s4 = p & 3u, c = (p >> 2) % KC, gi = (p >> 2) / KC;
             const char* ga = rowsx + ((((uint64_t)t * KC + c) * 8u + kI8qSub * u + gi) * 4u + s4) * 1024u + lane * 16u;
-            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(ga), "s"(l0 + p * 1024u)
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" I8Q_ROWPOL ::"v"(ga), "s"(l0 + p * 1024u)
                          : "memory");
         }
         if (wv < 2) {
@@ -989,7 +999,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src),
                          "s"(l0 + kSubBytes + wv * kRows * 4u)
                          : "memory");
-        } else {
+        } else if constexpr (I8Q_PF > 0) {
             uint32_t tp, up;
             sub_of(i + I8Q_PF, tp, up);
             const uint32_t L = (wv - 2u) * 64u + lane, p = L >> 3, s4 = p & 3u, c = (p >> 2) % KC,
@@ -1043,15 +1053,20 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     };
     for (uint32_t i = 0; i < ns; ++i) {
         // stage i landed (stage i+1's kOps ops are the younger ones), then every wave's part
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps) : "memory");
-        __syncthreads();
+        if (wv < 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps) : "memory");
+        else if constexpr (I8Q_PF == 0)  // no prefetch op in this wave's stages
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps - 1) : "memory");
+        else  // stage i's prefetch (issued after its row DMAs) may stay in flight one more step
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps + I8Q_PFW) : "memory");
+        if constexpr (!(I8Q_ABL & 8)) __syncthreads();
         if (cl_n >= kI8qCl / 2) {  // (block-uniform) rare: empty the list before it can overflow
             flush(min(cl_n, kI8qCl));
             __syncthreads();
             if (tid == 0) cl_n = 0;
             __syncthreads();
         }
-        stage(i + 2);  // into the buffer read in step i-1
+        if constexpr (!(I8Q_ABL & 4)) stage(i + 2);  // into the buffer read in step i-1
         uint32_t t, u;
         sub_of(i, t, u);
         const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
@@ -1078,9 +1093,17 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             }
             __builtin_amdgcn_sched_barrier(0);  // the reads stay BR - 1 k-steps ahead (no sinking)
 #pragma unroll
-            for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-                acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
+            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
+                if constexpr (I8Q_ABL & 2)
+                    acc[gi][s & 15] ^= A[s][0] ^ bf[s % BR][gi][0] ^ bf[s % BR][gi][3];
+                else
+                    acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (I8Q_ABL & 1) {
+            if (acc[0][0] == 0x7fffffff && acc[1][5] == 0x7fffffff) cl_n = 0;  // keeps the MFMAs live
+            continue;
         }
 #pragma unroll
         for (uint32_t gi = 0; gi < kI8qSub; ++gi) {

@@ -81,6 +81,19 @@ for t in "${TASKS[@]}"; do
                 esac
                 echo "== $v"; grep -E "B=|emit" gpurun_out/flatab_$v.log | tail -2
             done ;;
+        flatabl)  # k_flat_i8q ablations (abl/libgvdb_ablN.so, -DI8Q_ABL=N: 1 no epilogue, 2 no MFMA, 4 no row DMA; results invalid)
+            for v in 0 1 3 5; do
+                lib=""; [ $v != 0 ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_abl$v.so
+                GVDB_FLAT=i8 GVDB_LIB_PATH=$lib BS=256 FLAT_REPS=5 run 600 gpurun_out/flatabl_$v.log python3 scripts/flat_timing.py
+                echo "== abl $v"; grep -E "emit" gpurun_out/flatabl_$v.log | tail -1
+            done ;;
+        flatvar:*)  # k_flat_i8q build variants A/B: flatvar:a,b,... runs abl/libgvdb_<a>.so ... ("base" = libgvdb.so)
+            IFS=',' read -ra VARS <<< "${t#flatvar:}"
+            for v in "${VARS[@]}"; do
+                lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_FLAT=i8 GVDB_LIB_PATH=$lib BS=256 FLAT_REPS=10 run 600 gpurun_out/flatvar_$v.log python3 scripts/flat_timing.py
+                echo "== $v"; grep -E "B=|emit" gpurun_out/flatvar_$v.log | tail -2
+            done ;;
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
             BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
             grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;
