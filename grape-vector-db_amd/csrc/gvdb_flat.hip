@@ -933,6 +933,9 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
 #ifndef I8Q_BR
 #define I8Q_BR 4  // B-fragment ring depth in k-steps (A/B knob)
 #endif
+#ifndef I8Q_SKEW
+#define I8Q_SKEW 1  // waves 4..7 test step i-1 after step i's barrier (A/B knob)
+#endif
 #ifndef I8Q_PFW
 #define I8Q_PFW 0  // 1: a wave's prefetch op is waited for one step later than its stage (A/B knob)
 #endif
@@ -1051,65 +1054,14 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             }
         }
     };
-    for (uint32_t i = 0; i < ns; ++i) {
-        // stage i landed (stage i+1's kOps ops are the younger ones), then every wave's part
-        if (wv < 2)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps) : "memory");
-        else if constexpr (I8Q_PF == 0)  // no prefetch op in this wave's stages
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps - 1) : "memory");
-        else  // stage i's prefetch (issued after its row DMAs) may stay in flight one more step
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps + I8Q_PFW) : "memory");
-        if constexpr (!(I8Q_ABL & 8)) __syncthreads();
-        if (cl_n >= kI8qCl / 2) {  // (block-uniform) rare: empty the list before it can overflow
-            flush(min(cl_n, kI8qCl));
-            __syncthreads();
-            if (tid == 0) cl_n = 0;
-            __syncthreads();
-        }
-        if constexpr (!(I8Q_ABL & 4)) stage(i + 2);  // into the buffer read in step i-1
-        uint32_t t, u;
-        sub_of(i, t, u);
-        const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
-        const float* ops = (const float*)(Bs[i % kI8qBufs] + kSubBytes);
-#pragma unroll
-        for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[gi][e] = 0;
-        // B fragments from LDS, kI8qBr k-steps ahead of their MFMAs (LDS latency > the
-        // ~64 cycles of one k-step's two MFMAs)
-        constexpr int BR = kI8qBr;
-        fx_v4i bf[BR][kI8qSub];
-#pragma unroll
-        for (int s = 0; s < BR - 1; ++s)
-#pragma unroll
-            for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-                bf[s][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)s) * 1024u);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            if (s + BR - 1 < KS) {
-#pragma unroll
-                for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-                    bf[(s + BR - 1) % BR][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)(s + BR - 1)) * 1024u);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // the reads stay BR - 1 k-steps ahead (no sinking)
-#pragma unroll
-            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
-                if constexpr (I8Q_ABL & 2)
-                    acc[gi][s & 15] ^= A[s][0] ^ bf[s % BR][gi][0] ^ bf[s % BR][gi][3];
-                else
-                    acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (I8Q_ABL & 1) {
-            if (acc[0][0] == 0x7fffffff && acc[1][5] == 0x7fffffff) cl_n = 0;  // keeps the MFMAs live
-            continue;
-        }
+    // The candidate test of step i's accumulators.  Per pair the exact f32 cosine is at most
+    // U = approx + qa*rho_x + qd; a row is nominated iff U >= tau (thr = tau - qd).
+    auto epilogue = [&](uint32_t i, uint32_t t, uint32_t u, const float* rv, const float* rh)
+                        __attribute__((always_inline)) {
 #pragma unroll
         for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
             const uint32_t n = t * kFxRows + (kI8qSub * u + gi) * 32u + (lane & 31u);
-            const uint32_t rl = gi * 32u + (lane & 31u);
-            const float rinv = n < N ? ops[rl] : 0.0f, rho = n < N ? ops[kRows + rl] : 0.0f;
+            const float rinv = n < N ? rv[gi] : 0.0f, rho = n < N ? rh[gi] : 0.0f;
             // this lane's 16 slots: qb0 + (e & 3) + 8 (e >> 2)
             uint32_t qb0 = wv * 32u + 4u * (lane >> 5);
             asm volatile("" : "+v"(qb0));  // keep the per-slot addresses out of the loop
@@ -1152,6 +1104,95 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
                 }
             }
         }
+    };
+    // Waves 4..7 (the second wave of each SIMD) run step i-1's epilogue right after the
+    // barrier of step i, before step i's MFMAs: on every SIMD one wave's candidate test
+    // overlaps the other wave's MFMAs instead of both testing while the matrix core idles.
+    const bool late = I8Q_SKEW && wv >= 4;
+    float lrv[kI8qSub] = {0.0f, 0.0f}, lrh[kI8qSub] = {0.0f, 0.0f};  // step i-1's row operands (late waves)
+    for (uint32_t i = 0; i < ns; ++i) {
+        // stage i landed (stage i+1's kOps ops are the younger ones), then every wave's part
+        if (wv < 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps) : "memory");
+        else if constexpr (I8Q_PF == 0)  // no prefetch op in this wave's stages
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps - 1) : "memory");
+        else  // stage i's prefetch (issued after its row DMAs) may stay in flight one more step
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps + I8Q_PFW) : "memory");
+        if constexpr (!(I8Q_ABL & 8)) __syncthreads();
+        // every wave reads the list count before any wave adds to it again (the late waves'
+        // epilogue follows right after this), so the flush decision is block-uniform
+        const bool full = cl_n >= kI8qCl / 2;
+        __syncthreads();
+        if (full) {  // rare: empty the list before it can overflow
+            flush(min(cl_n, kI8qCl));
+            __syncthreads();
+            if (tid == 0) cl_n = 0;
+            __syncthreads();
+        }
+        if constexpr (!(I8Q_ABL & 4)) stage(i + 2);  // into the buffer read in step i-1
+        uint32_t t, u;
+        sub_of(i, t, u);
+        const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
+        const float* ops = (const float*)(Bs[i % kI8qBufs] + kSubBytes);
+        if (late && i > 0 && !(I8Q_ABL & 1)) {
+            uint32_t tp, up;
+            sub_of(i - 1, tp, up);
+            epilogue(i - 1, tp, up, lrv, lrh);
+        }
+#pragma unroll
+        for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[gi][e] = 0;
+        // B fragments from LDS, kI8qBr k-steps ahead of their MFMAs (LDS latency > the
+        // ~64 cycles of one k-step's two MFMAs)
+        constexpr int BR = kI8qBr;
+        fx_v4i bf[BR][kI8qSub];
+#pragma unroll
+        for (int s = 0; s < BR - 1; ++s)
+#pragma unroll
+            for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+                bf[s][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)s) * 1024u);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            if (s + BR - 1 < KS) {
+#pragma unroll
+                for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+                    bf[(s + BR - 1) % BR][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)(s + BR - 1)) * 1024u);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // the reads stay BR - 1 k-steps ahead (no sinking)
+#pragma unroll
+            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
+                if constexpr (I8Q_ABL & 2)
+                    acc[gi][s & 15] ^= A[s][0] ^ bf[s % BR][gi][0] ^ bf[s % BR][gi][3];
+                else
+                    acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (I8Q_ABL & 1) {
+            if (acc[0][0] == 0x7fffffff && acc[1][5] == 0x7fffffff) cl_n = 0;  // keeps the MFMAs live
+            continue;
+        }
+        if (!late) {
+            float rv[kI8qSub], rh[kI8qSub];
+#pragma unroll
+            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
+                rv[gi] = ops[gi * 32u + (lane & 31u)];
+                rh[gi] = ops[kRows + gi * 32u + (lane & 31u)];
+            }
+            epilogue(i, t, u, rv, rh);
+        } else {  // this step's operands to registers: buffer i % 3 is refilled after the next barrier
+#pragma unroll
+            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
+                lrv[gi] = ops[gi * 32u + (lane & 31u)];
+                lrh[gi] = ops[kRows + gi * 32u + (lane & 31u)];
+            }
+        }
+    }
+    if (late && ns && !(I8Q_ABL & 1)) {
+        uint32_t t, u;
+        sub_of(ns - 1, t, u);
+        epilogue(ns - 1, t, u, lrv, lrh);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped prefetches land before exit
     __syncthreads();
