@@ -1099,7 +1099,12 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
     if (i8 ? ix->rows_nonfinite : ix->rows_have_nan) return GVDB_OK;
     const uint32_t N = (uint32_t)ix->n, KC = i8 ? fx_kc_i8(dim) : fx_kc(dim);
     const uint32_t ntiles = (N + kFxRows - 1) / kFxRows;
-    const uint32_t sampled = (ntiles + kFxSampleEvery - 1) / kFxSampleEvery;
+    static const uint32_t every = [] {  // GVDB_FLAT_EVERY: sample-pass tile stride (A/B timing)
+        const char* e = getenv("GVDB_FLAT_EVERY");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? (uint32_t)v : kFxSampleEvery;
+    }();
+    const uint32_t sampled = (ntiles + every - 1) / every;
     const uint32_t S = sampled * kFxRows;
 
     // mk: the sample rank whose score (minus eps) bounds the threshold.  The
@@ -1175,7 +1180,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         a.qa = qa;
         a.qd = qd;
         a.B = Bg;
-        a.every = kFxSampleEvery;
+        a.every = every;
         a.smp = ws.fx_smp.as<float>();
         a.S = S;
         a.thr = ws.thr.as<float>();
@@ -1191,7 +1196,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         HIP_TRY(launch_flat_mx_sample(a, s), "flat sample pass");
         DBG_SYNC(s, "dbg: flat sample pass");
         // tau from exactly re-scored probes (the 16 best sampled rows per query)
-        HIP_TRY(launch_flat_probes(a.smp, Bg, S, kFxSampleEvery, N, probes, pcount, s), "flat probes");
+        HIP_TRY(launch_flat_probes(a.smp, Bg, S, every, N, probes, pcount, s), "flat probes");
         {
             RerankArgs pr{};
             pr.rows = ix->rows;

@@ -87,6 +87,11 @@ for t in "${TASKS[@]}"; do
                 GVDB_FLAT=i8 GVDB_LIB_PATH=$lib BS=256 FLAT_REPS=5 run 600 gpurun_out/flatabl_$v.log python3 scripts/flat_timing.py
                 echo "== abl $v"; grep -E "emit" gpurun_out/flatabl_$v.log | tail -1
             done ;;
+        flatevery)  # exact flat sample-pass stride A/B (GVDB_FLAT_EVERY; default 64 tiles)
+            for v in 64 128; do
+                GVDB_FLAT_EVERY=$v BS=256 FLAT_REPS=10 run 600 gpurun_out/flatevery_$v.log python3 scripts/flat_timing.py
+                echo "== every $v"; grep -E "B=|emit" gpurun_out/flatevery_$v.log | tail -2
+            done ;;
         flatvar:*)  # k_flat_i8q build variants A/B: flatvar:a,b,... runs abl/libgvdb_<a>.so ... ("base" = libgvdb.so)
             IFS=',' read -ra VARS <<< "${t#flatvar:}"
             for v in "${VARS[@]}"; do
