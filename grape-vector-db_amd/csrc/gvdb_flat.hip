@@ -632,7 +632,10 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
     const float* src = smp + (uint64_t)q * S;
     // 8 values per lane per batch, the next batch loaded while this one is
     // merged (the scan is latency-bound otherwise: one block per query)
-    constexpr int kU = 8;
+#ifndef FX_PROBE_U
+#define FX_PROBE_U 8
+#endif
+    constexpr int kU = FX_PROBE_U;
     auto load = [&](uint32_t i0, float (&v)[kU]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {

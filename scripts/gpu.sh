@@ -92,6 +92,13 @@ for t in "${TASKS[@]}"; do
                 GVDB_FLAT_EVERY=$v BS=256 FLAT_REPS=10 run 600 gpurun_out/flatevery_$v.log python3 scripts/flat_timing.py
                 echo "== every $v"; grep -E "B=|emit" gpurun_out/flatevery_$v.log | tail -2
             done ;;
+        probeprof:*)  # k_flat_probes (and every flat kernel) per build variant: kernel stats of flat_timing
+            IFS=',' read -ra VARS <<< "${t#probeprof:}"
+            for v in "${VARS[@]}"; do
+                lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib BS=256 FLAT_REPS=5 run 600 gpurun_out/probeprof_$v.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_probe_$v -o run -- python3 scripts/flat_timing.py
+                echo "== $v"; grep -E "k_flat_probes|k_flat_i8q|k_rerank2" gpurun_out/prof_probe_$v/run_kernel_stats.csv | cut -d, -f1-4
+            done ;;
         flatvar:*)  # k_flat_i8q build variants A/B: flatvar:a,b,... runs abl/libgvdb_<a>.so ... ("base" = libgvdb.so)
             IFS=',' read -ra VARS <<< "${t#flatvar:}"
             for v in "${VARS[@]}"; do
