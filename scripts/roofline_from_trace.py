@@ -7,6 +7,7 @@ bench.py times with HIP events --
   (the search loop is the first user of the scan; warmup steps come first);
 * batch 1: the first `b1` k_b1_scan launches (the pass whose HIP events give
   batch1.roofline.avg_launch_ms);
+* exact flat: every k_flat_i8q launch (operating_points[].emit_roofline);
 
 and the fractions from the same algorithmic work bench.py uses.  Usage:
 roofline_from_trace.py TRACE.csv BENCH.json [--warmup 3 --steps 20 --b1 200]"""
@@ -49,6 +50,15 @@ def main():
                          "avg_launch_ms_hip_events": roof["avg_launch_ms"], "achieved_rocprof_GBs": ach,
                          "frac_rocprof": ach / roof["peak"], "frac_hip_events": roof["frac"],
                          "agreement": avg / roof["avg_launch_ms"]}
+    fl = durs("void gvdb::k_flat_i8q<")  # every exact-flat emit launch does the same work
+    fr = next((p.get("emit_roofline") for p in bench.get("operating_points") or [] if p.get("emit_roofline")), None)
+    if fl and fr:
+        avg = sum(fl) / len(fl)
+        ach = fr["algorithmic_bytes_per_launch"] / (avg * 1e-3) / 1e9
+        out["flat_emit"] = {"kernel": "k_flat_i8q", "launches": len(fl), "avg_launch_ms_rocprof": avg,
+                            "avg_launch_ms_hip_events": fr["avg_launch_ms"], "achieved_rocprof_GBs": ach,
+                            "frac_rocprof": ach / fr["peak"], "frac_hip_events": fr["frac"],
+                            "agreement": avg / fr["avg_launch_ms"]}
     print(json.dumps(out, indent=1))
 
 
