@@ -282,15 +282,11 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t sample_div, uint32_t& chunks
 gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D, uint32_t R, uint32_t N,
                            hipStream_t s, bool fast) {
     // GVDB_SCAN=valu forces the popcount scan for every batch size; default:
-    // FP4 MFMA for large batches.  The A/B variants (=i8, =fp4u, =fp4lds)
-    // exist only in a `make VARIANTS=1` build.
+    // FP4 MFMA for large batches.  (The round-1/2 A/B scans -- i8 MFMA, uniform
+    // FP4 waves, LDS-shared tiles, mx3 -- were removed from the tree after
+    // commit 8c12da2; DESIGN.md §4 keeps their measurements.)
     const char* scan = getenv("GVDB_SCAN");
     s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0 : 1;
-#ifdef GVDB_SCAN_VARIANTS
-    if (scan && strcmp(scan, "i8") == 0) s1.use_mfma = 2;
-    if (scan && strcmp(scan, "fp4u") == 0) s1.use_mfma = 3;
-    if (scan && strcmp(scan, "fp4lds") == 0) s1.use_mfma = 4;
-#endif
     const char* dbg = getenv("GVDB_SCAN_DBG");  // ablation timing only (results invalid when set)
     s1.dbg = dbg ? atoi(dbg) : 0;
     s1.force_rescan = getenv_flag("GVDB_FORCE_RESCAN") ? 1 : 0;  // tests of the device-side fallback
@@ -427,8 +423,21 @@ uint32_t& debug_thr_cap() {
     static uint32_t n = 0;
     return n;
 }
-static hipError_t debug_keep_thr(const uint32_t* thr, uint32_t B, hipStream_t s) {
+// ... and whether any query of that batch took the device-side all-rows rescan
+uint32_t*& debug_fail() {
+    static uint32_t* p = nullptr;
+    return p;
+}
+static hipError_t debug_keep_thr(const uint32_t* thr, uint32_t B, hipStream_t s, const uint32_t* any_fail = nullptr) {
     if (!getenv_flag("GVDB_DEBUG_THR")) return hipSuccess;
+    if (any_fail) {
+        if (!debug_fail()) {
+            hipError_t e = hipMalloc((void**)&debug_fail(), 4);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipMemcpyAsync(debug_fail(), any_fail, 4, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+    }
     uint32_t*& dt = debug_thr();
     if (debug_thr_cap() < B) {
         if (dt) (void)hipFree(dt);
@@ -620,7 +629,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             s1.R = R;
             s1.ev = ev ? ev->e : nullptr;
             HIP_TRY(launch_stage1_fast(s1, s), "stage1");
-            HIP_TRY(debug_keep_thr(s1.thr, B, s), "copy thresholds");
+            HIP_TRY(debug_keep_thr(s1.thr, B, s, s1.any_fail), "copy thresholds");
         } else if (big) {
             // R beyond the LDS select (the reference's default ratio 0.1): the
             // batched stage 1 with k_select_big (exact top-R membership)
@@ -634,6 +643,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
             s1.R = R;
             s1.ev = ev ? ev->e : nullptr;
             HIP_TRY(launch_stage1_fast(s1, s), "stage1 (large R)");
+            HIP_TRY(debug_keep_thr(s1.thr, B, s, s1.any_fail), "copy thresholds");
         } else {
             // R beyond the LDS select: every query on the exact all-rows path
             HIP_TRY(ws.slow.ensure(stage1_slow_bytes(v.N)), "alloc slow path");
@@ -1554,7 +1564,7 @@ gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queri
         s1.B = (uint32_t)B;
         s1.R = RR;
         HIP_TRY(launch_stage1_fast(s1, s), "stage1");
-        HIP_TRY(debug_keep_thr(s1.thr, (uint32_t)B, s), "copy thresholds");
+        HIP_TRY(debug_keep_thr(s1.thr, (uint32_t)B, s, s1.any_fail), "copy thresholds");
     } else {
         HIP_TRY(ws.slow.ensure(stage1_slow_bytes((uint32_t)ix->n)), "alloc slow");
         for (uint64_t q = 0; q < B; ++q)
@@ -2057,6 +2067,12 @@ extern "C" int gvdb_debug_stage1_thresholds(uint32_t* out, uint32_t B) {
     if (!debug_thr() || B > debug_thr_cap()) return -1;
     if (hipDeviceSynchronize() != hipSuccess) return -2;
     return (int)hipMemcpy(out, debug_thr(), (size_t)B * 4, hipMemcpyDeviceToHost);
+}
+// tests only: 1 if a query of the last GVDB_DEBUG_THR=1 batch took the all-rows rescan
+extern "C" int gvdb_debug_stage1_rescanned(uint32_t* out) {
+    if (!debug_fail()) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    return (int)hipMemcpy(out, debug_fail(), 4, hipMemcpyDeviceToHost);
 }
 extern "C" int gvdb_debug_b1_clock(unsigned long long* out) {
     if (!debug_b1_clk()) return -1;

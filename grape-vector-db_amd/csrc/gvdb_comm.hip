@@ -124,9 +124,10 @@ gvdb_status gvdb_comm_create(const uint8_t id[GVDB_COMM_ID_BYTES], int32_t world
 void gvdb_comm_destroy(gvdb_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipDeviceSynchronize();
+    // only this communicator's last call has to finish (not every stream of the device)
+    if (c->pending) (void)hipEventSynchronize(c->done);
     if (c->comm) (void)rccl().comm_destroy(c->comm);
-    if (c->buf) (void)hipFree(c->buf);
+    if (c->buf) (void)hipFreeAsync(c->buf, nullptr);
     if (c->done) (void)hipEventDestroy(c->done);
     delete c;
 }
@@ -169,13 +170,13 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
     const size_t need = flat ? wf * 4 * (G + 1) : ((w1 + w2) * (G + 1)) * 4 + scratch;
     if (c->pending && c->last != s) (void)hipStreamWaitEvent(s, c->done, 0);
     if (need > c->buf_bytes) {
-        if (c->buf) {
-            (void)hipDeviceSynchronize();  // every earlier call's use of the old buffer
-            (void)hipFree(c->buf);
-        }
+        // stream-ordered: s already waits for the previous call (same stream, or
+        // the event above), so the old blocks are released after their last use
+        // without a device-wide synchronisation (co-tenant streams keep running)
+        if (c->buf) (void)hipFreeAsync(c->buf, s);
         c->buf = nullptr;
         c->buf_bytes = 0;
-        he = hipMalloc(&c->buf, need);
+        he = hipMallocAsync(&c->buf, need, s);
         if (he != hipSuccess)
             return report_status(he == hipErrorOutOfMemory ? GVDB_ERR_OUT_OF_MEMORY : GVDB_ERR_DEVICE,
                                  std::string("sharded search buffers: ") + hipGetErrorString(he));
@@ -199,10 +200,9 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
         const bool ok = local == GVDB_OK && gvdb_index_len(shard) > 0;
         if (!ok) (void)hipMemsetD32Async(send + 3 * BK, 0, B, s);
         (void)hipMemsetD32Async(send + 3 * BK + B, local == GVDB_OK ? 0 : 1, 1, s);
-        if ((st = all_gather(send, recv, wf)) != GVDB_OK) return st;
-        if ((st = gvdb_shard_flat_final_device(recv, G, B, k, sp->metric, d_out_ids, d_out_scores, d_out_n, stream)) !=
-            GVDB_OK)
-            return st;
+        st = all_gather(send, recv, wf);
+        if (st == GVDB_OK)
+            st = gvdb_shard_flat_final_device(recv, G, B, k, sp->metric, d_out_ids, d_out_scores, d_out_n, stream);
     } else {
         uint32_t* send1 = base;
         uint32_t* recv1 = G > 1 ? send1 + w1 : send1;
@@ -211,22 +211,32 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
         void* scr = base + (w1 + w2) * (G + 1);
         // 1. local stage 1 (an empty or failing shard still joins with no entries)
         local = gvdb_shard_stage1_device(shard, d_q, B, dim, R, send1, stream);
-        const std::string local_err = local != GVDB_OK ? std::string(gvdb_last_error()) : std::string();
+        std::string local_err = local != GVDB_OK ? std::string(gvdb_last_error()) : std::string();
         if ((st = all_gather(send1, recv1, w1)) != GVDB_OK) return st;
-        // 2. global top-R, rerank of the owned rows, local top-k
-        st = gvdb_shard_rerank_device(shard, d_q, B, dim, R, k, recv1, G, (uint64_t)c->rank, scr, send2, stream);
-        if (st != GVDB_OK) return st;
+        // 2. global top-R, rerank of the owned rows, local top-k.  A rank whose
+        // phase 2 fails still joins exchange 2 (no entries, the merge poisoned),
+        // so its peers are never left waiting in the collective
+        const gvdb_status rr =
+            gvdb_shard_rerank_device(shard, d_q, B, dim, R, k, recv1, G, (uint64_t)c->rank, scr, send2, stream);
+        if (rr != GVDB_OK) {
+            if (local == GVDB_OK) {
+                local = rr;
+                local_err = gvdb_last_error();
+            }
+            (void)hipMemsetD32Async(send2 + 4 * B * k, 0, 2 * B, s);  // meta: no entries
+        }
         if (local != GVDB_OK) (void)hipMemsetD32Async(send2 + 4 * B * k + 2 * B, 1, 1, s);  // poison the merge
-        if ((st = all_gather(send2, recv2, w2)) != GVDB_OK) return st;
+        st = all_gather(send2, recv2, w2);
         // 3. the merged top-k on every rank
-        if ((st = gvdb_shard_final_device(recv2, G, B, k, d_out_ids, d_out_scores, d_out_n, stream)) != GVDB_OK)
-            return st;
-        if (local != GVDB_OK) report_status(local, local_err);
+        if (st == GVDB_OK) st = gvdb_shard_final_device(recv2, G, B, k, d_out_ids, d_out_scores, d_out_n, stream);
+        if (st == GVDB_OK && local != GVDB_OK) report_status(local, local_err);
     }
+    // the next call (possibly on another stream) waits for everything enqueued here,
+    // error paths included
     if (!c->done) (void)hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
     c->pending = c->done && hipEventRecord(c->done, s) == hipSuccess;
     c->last = s;
-    return local;
+    return st != GVDB_OK ? st : local;
 }
 
 }  // extern "C"

@@ -904,7 +904,7 @@ __device__ __forceinline__ void flush_stage_block(const uint64_t (*st_key)[kStag
     }
 }
 
-// geometry shared by k_scan_mx3 (VARIANTS build) and k_scan_mx4
+// geometry of k_scan_mx4
 #ifndef MX3_PF
 #define MX3_PF 4
 #endif
@@ -1950,20 +1950,10 @@ static void launch_hist_t(const Stage1Args& a, hipStream_t s) {
                        a.cap, a.N, a.D, a.sample_stride, a.qcodes, a.B, QT, a.hist);
 }
 
-#ifdef GVDB_SCAN_VARIANTS  // the A/B stage-1 scans (make VARIANTS=1), kept out of the product source
-#include "gvdb_scan_variants.inc"
-#endif
-
 static bool getenv_flag_eq(const char* name, const char* v) {  // read per launch (tests switch it)
     const char* e = getenv(name);
     return e && strcmp(e, v) == 0;
 }
-#ifdef GVDB_SCAN_VARIANTS
-static bool scan_selected(const char* v) {  // read per launch: tests switch it between calls
-    const char* e = getenv("GVDB_SCAN");
-    return e && strcmp(e, v) == 0;
-}
-#endif
 
 size_t stage1_plan(Stage1Args& a) {
     const uint32_t W4 = code_w4(a.D);
@@ -1977,9 +1967,15 @@ size_t stage1_plan(Stage1Args& a) {
     // FP4 histogram only when the dense block would exceed 1 GiB.
     if (big && !getenv_flag_eq("GVDB_SAMPLE", "valu")) {
         const bool sampled = a.target < S / 2u && a.N > S;
+        // the dense sample keeps one minimum per 16 rows: S/16 values, so it can
+        // only reach a target well below that (at R/N above ~1/64 -- the
+        // reference's default ratio 0.1 -- it would leave thr = D and every row
+        // would be emitted); such depths take the FP4 histogram / VALU form
+        const bool dense_fits = (uint64_t)a.B * (S / 16u) * 2u <= (1ull << 30);
+        const bool dense_reach = (uint64_t)a.target * 4u <= S / 16u;
         if (getenv_flag_eq("GVDB_SAMPLE", "mx")) {
             if (sampled) a.sample_mode = kSampleMxHist;
-        } else if ((uint64_t)a.B * (S / 16u) * 2u <= (1ull << 30)) {
+        } else if (dense_fits && (dense_reach || getenv_flag_eq("GVDB_SAMPLE", "dense"))) {
             a.sample_mode = kSampleDense;
         } else if (sampled) {
             a.sample_mode = kSampleMxHist;
@@ -2056,36 +2052,6 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 24: launch_scan_mx4_t<24, 6, 2>(a, s); break;
             default: launch_scan_mx4_t<32, 8, 1>(a, s); break;
         }
-#ifdef GVDB_SCAN_VARIANTS
-    } else if (mfma && a.use_mfma == 2) {  // i8 MFMA variant (A/B comparison)
-        switch (W4) {
-            case 2: launch_scan_mfma_t<2>(a, s); break;
-            case 3: launch_scan_mfma_t<3>(a, s); break;
-            case 4: launch_scan_mfma_t<4>(a, s); break;
-            default: launch_scan_mfma_t<6>(a, s); break;
-        }
-    } else if (mfma && a.use_mfma == 3) {  // FP4, uniform waves (A/B comparison)
-        switch (W4) {
-            case 2: launch_scan_mx_t<2>(a, s); break;
-            case 3: launch_scan_mx_t<3>(a, s); break;
-            case 4: launch_scan_mx_t<4>(a, s); break;
-            default: launch_scan_mx_t<6>(a, s); break;
-        }
-    } else if (mfma && a.use_mfma == 4) {  // FP4, LDS-shared candidate tiles (the previous default; A/B)
-        switch (W4) {
-            case 2: launch_scan_mx2_t<2>(a, s); break;
-            case 3: launch_scan_mx2_t<3>(a, s); break;
-            case 4: launch_scan_mx2_t<4>(a, s); break;
-            default: launch_scan_mx2_t<6>(a, s); break;
-        }
-    } else if (mfma && scan_selected("mx3")) {  // the previous default, +-1 operands (A/B)
-        switch (W4) {
-            case 2: launch_scan_mx3_t<2>(a, s); break;
-            case 3: launch_scan_mx3_t<3>(a, s); break;
-            case 4: launch_scan_mx3_t<4>(a, s); break;
-            default: launch_scan_mx3_t<6>(a, s); break;
-        }
-#endif  // GVDB_SCAN_VARIANTS
     } else if (mfma) {  // FP4 block-scaled MFMA, {0,1} x {+-1} operands (default for large batches)
         switch (W4) {
             case 2: launch_scan_mx5_t<2>(a, s); break;
@@ -3788,11 +3754,3 @@ hipError_t launch_b1_search(const B1Args& b, hipStream_t s) {
 
 }  // namespace gvdb
 
-extern "C" int gvdb_debug_stamps(unsigned long long* out) {
-#ifdef GVDB_SCAN_VARIANTS
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(gvdb::g_stamps), sizeof(gvdb::g_stamps));
-#else
-    (void)out;
-    return -1;  // k_scan_mx2's stamps exist only in a VARIANTS=1 build
-#endif
-}

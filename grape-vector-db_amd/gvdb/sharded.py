@@ -1,29 +1,31 @@
 """Exact sharded search over torch.distributed.
 
+Replaces ``ShardManager::search_vectors`` (src/distributed/shard.rs:760-786:
+scatter to shards, concat, sort, truncate) inside one node.  Each rank owns a
+contiguous row range whose ids are global row numbers (ranks in corpus order).
+
 :class:`TwoExchangeSearch` is the production protocol (the same one
 ``gvdb_index_search_sharded_device`` runs with RCCL inside libgvdb, see
 ``csrc/gvdb_shard.hip``) driven over ANY torch.distributed transport:
-local stage-1 keys -> all-gather -> global top-R + rerank of the rows this rank
-owns + local top-k -> all-gather -> merged top-k.  On a GPU it calls the
-device phases; on a CPU transport (gloo) it takes the local stage 1 and the
-cosines from callables and runs the merges' host forms.
 
-:class:`ShardedBQSearch` below is the earlier one-exchange variant (every rank
-reranks its whole local top-R and ships (id, Hamming, cosine) triplets).
+1. every rank: its exact local stage-1 top-R as (Hamming << 32 | row) keys;
+2. all-gather of those blocks (B*R*8 bytes per rank);
+3. every rank: the global top-R by (Hamming, corpus row), the exact cosine of
+   the rows IT owns among them (~R/G per query), its local top-k;
+4. all-gather of the local top-k (B*k*16 bytes per rank);
+5. every rank: the merged top-k = the first k of the stable cosine sort of the
+   global top-R, bit-identical to one multi_stage_search over the corpus.
 
-Replaces ``ShardManager::search_vectors`` (src/distributed/shard.rs:760-786:
-scatter to shards, concat, sort, truncate) inside one node.  Each rank owns a
-contiguous row range whose ids are global row numbers.  Per batch:
+A rank whose phase fails still joins both all-gathers (no entries, an error
+word that poisons every query of the merge) and raises only afterwards, so no
+peer is left waiting in a collective.  On a GPU the phases are the device
+forms; on a CPU transport (gloo) the local stage 1 and the cosines come from
+callables and the merges run as host forms.
 
-1. the rank computes its LOCAL stage-1 top-R (Hamming asc, row asc) and the
-   exact cosine of each candidate (``gvdb_index_bq_candidates_device``);
-2. ONE all-gather moves the (id, Hamming, cosine) triplets — B*R*16 bytes per
-   rank — over RCCL/xGMI (gloo on CPU in the tests);
-3. every rank merges: union sorted by (Hamming, id) -> first R -> stable sort by
-   cosine desc -> first k (``gvdb_bq_shard_merge[_device]``).
-
-The union of local top-R lists contains the global top-R, so the result is
-bit-identical to one multi_stage_search over the concatenated corpus.
+:class:`ShardedBQSearch` is the earlier ONE-exchange variant (every rank
+reranks its whole local top-R and ships (id, Hamming, cosine) triplets, B*R*16
+bytes per rank), kept as a lower-level form; :class:`RcclShardedSearch` wraps
+the in-library RCCL composition.
 """
 from __future__ import annotations
 
@@ -38,6 +40,14 @@ from ._ffi import lib
 
 # candidates_fn(queries, R_local) -> (gids int64 [B,R_local], dist int32 [B,R_local], cos f32 [B,R_local])
 CandidatesFn = Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]
+
+
+def _status_error(rc: int) -> Exception:
+    try:
+        check(rc)
+    except Exception as e:  # noqa: BLE001 -- the mapped VectorDbError
+        return e
+    return RuntimeError(f"gvdb status {rc}")
 
 
 def shard_bounds(n: int, world: int) -> List[int]:
@@ -86,48 +96,81 @@ class TwoExchangeSearch:
             parts = list(recv.unbind(0))
             dist.all_gather(parts, send, group=self.group)
 
+    # exchange-2 block: [B*k entries of 4 words | meta: count[B] | reff[B] | err]
+    def _meta2(self):
+        return 4 * self.B * self.k
+
     def search(self, q: torch.Tensor):
+        """Both all-gathers run on every rank whatever happens locally; a local
+        failure poisons the merge (every query GVDB_N_POISONED on every rank)
+        and is raised on the failing rank after the second exchange."""
         B, R, k = self.B, self.R, self.k
         L = lib()
+        err = None  # the first local failure (raised after both exchanges)
+        m2 = self._meta2()
         if self.index is not None:
             st = torch.cuda.current_stream(q.device).cuda_stream or None
             D = q.shape[1]
-            check(L.gvdb_shard_stage1_device(self.index._h, q.data_ptr(), B, D, R, self.send1.data_ptr(), st))
+            # a failing stage 1 writes zero counts + its err word itself (the C ABI contract)
+            rc = L.gvdb_shard_stage1_device(self.index._h, q.data_ptr(), B, D, R, self.send1.data_ptr(), st)
+            if rc != 0:
+                err = _status_error(rc)
             self._gather(self.send1, self.recv1)
-            check(L.gvdb_shard_rerank_device(self.index._h, q.data_ptr(), B, D, R, k, self.recv1.data_ptr(), self.world,
-                                             self.rank, self.scratch.data_ptr(), self.send2.data_ptr(), st))
+            rc = L.gvdb_shard_rerank_device(self.index._h, q.data_ptr(), B, D, R, k, self.recv1.data_ptr(), self.world,
+                                            self.rank, self.scratch.data_ptr(), self.send2.data_ptr(), st)
+            if rc != 0:
+                err = err or _status_error(rc)
+                self.send2[m2:m2 + 2 * B].zero_()  # no entries from this rank
+            if err is not None:
+                self.send2[m2 + 2 * B] = 1  # poison the merge
             self._gather(self.send2, self.recv2)
             check(L.gvdb_shard_final_device(self.recv2.data_ptr(), self.world, B, k, self.out_ids.data_ptr(),
                                             self.out_scores.data_ptr(), self.out_n.data_ptr(), st))
+            if err is not None:
+                raise err
             return self.out_ids, self.out_scores, self.out_n
         # host transport: the same blocks, host merges
-        rows, dd = self.stage1_fn(q, R)
-        rows, dd = np.asarray(rows, np.uint64), np.asarray(dd, np.uint64)
         s1 = self.send1.numpy().view(np.uint32)
         s1[:] = 0
-        keys = s1[:2 * B * R].view(np.uint64).reshape(B, R)
-        rl = rows.shape[1]
-        keys[:, :rl] = (dd << np.uint64(32)) | rows
-        s1[2 * B * R:2 * B * R + B] = rl
+        try:
+            rows, dd = self.stage1_fn(q, R)
+            rows, dd = np.asarray(rows, np.uint64), np.asarray(dd, np.uint64)
+            keys = s1[:2 * B * R].view(np.uint64).reshape(B, R)
+            rl = rows.shape[1]
+            keys[:, :rl] = (dd << np.uint64(32)) | rows
+            s1[2 * B * R:2 * B * R + B] = rl
+        except Exception as e:  # noqa: BLE001 -- re-raised after the exchanges
+            err = e
+            s1[:] = 0
+            s1[2 * B * R + B] = 1
         self._gather(self.send1, self.recv1)
         g1 = np.ascontiguousarray(self.recv1.numpy().view(np.uint32))
         own_rows = np.zeros((B, R), np.uint32)
         own_pos = np.zeros((B, R), np.uint32)
         own_cnt = np.zeros(B, np.uint32)
         reff = np.zeros(B, np.uint32)
-        check(L.gvdb_shard_merge_host(g1.ctypes.data, self.world, self.rank, B, R, own_rows.ctypes.data,
-                                      own_pos.ctypes.data, own_cnt.ctypes.data, reff.ctypes.data))
         scores = np.zeros((B, R), np.float32)
         ids = np.zeros((B, R), np.uint64)
-        for i in range(B):
-            c = int(own_cnt[i])
-            if c:
-                scores[i, :c] = self.cosine_fn(i, own_rows[i, :c])
-                ids[i, :c] = own_rows[i, :c].astype(np.uint64) + np.uint64(self.id_offset)
         s2 = self.send2.numpy().view(np.uint32)
         s2[:] = 0
-        check(L.gvdb_shard_local_topk_host(scores.ctypes.data, own_pos.ctypes.data, ids.ctypes.data,
-                                           own_cnt.ctypes.data, reff.ctypes.data, B, R, k, 0, s2.ctypes.data))
+        try:
+            check(L.gvdb_shard_merge_host(g1.ctypes.data, self.world, self.rank, B, R, own_rows.ctypes.data,
+                                          own_pos.ctypes.data, own_cnt.ctypes.data, reff.ctypes.data))
+            if err is None:
+                for i in range(B):
+                    c = int(own_cnt[i])
+                    if c:
+                        scores[i, :c] = self.cosine_fn(i, own_rows[i, :c])
+                        ids[i, :c] = own_rows[i, :c].astype(np.uint64) + np.uint64(self.id_offset)
+            else:
+                own_cnt[:] = 0
+            check(L.gvdb_shard_local_topk_host(scores.ctypes.data, own_pos.ctypes.data, ids.ctypes.data,
+                                               own_cnt.ctypes.data, reff.ctypes.data, B, R, k, int(err is not None),
+                                               s2.ctypes.data))
+        except Exception as e:  # noqa: BLE001
+            err = err or e
+            s2[:] = 0
+            s2[m2 + 2 * B] = 1
         self._gather(self.send2, self.recv2)
         g2 = np.ascontiguousarray(self.recv2.numpy().view(np.uint32))
         oi = np.zeros((B, k), np.uint64)
@@ -135,6 +178,8 @@ class TwoExchangeSearch:
         on = np.zeros(B, np.uint32)
         check(L.gvdb_shard_final_host(g2.ctypes.data, self.world, B, k, oi.ctypes.data, osc.ctypes.data,
                                       on.ctypes.data))
+        if err is not None:
+            raise err
         return torch.from_numpy(oi.view(np.int64)), torch.from_numpy(osc), torch.from_numpy(on.view(np.int32))
 
 

@@ -38,6 +38,7 @@ _SIG = {
     "orc_storage_vector_search": (None, [P, u64, P, u64, u64, u64, C.c_int, f32, P, P, P]),
     "orc_flat_cosine_distance_search": (None, [P, u64, P, u64, u64, u64, P, P, P]),
     "orc_exact_topk_cosine_batch": (None, [P, P, u64, u64, u64, u64, P, P, C.c_int]),
+    "orc_flat_cosine_distance_batch": (None, [P, P, u64, u64, u64, u64, P, P, P, C.c_int]),
     "orc_shard_merge": (None, [P, P, P, u64, u64, u64, P, P, P]),
     "orc_row_norms": (None, [P, u64, u64, P]),
     "orc_bq_shard_merge": (None, [P, P, P, P, u64, u64, u64, u64, u64, P, P, P]),
@@ -215,6 +216,18 @@ def exact_topk_cosine_batch(q, rows, k, threads=0):
     os_ = np.zeros((B, k), np.float32)
     lib().orc_exact_topk_cosine_batch(_p(q), _p(rows), N, D, B, k, _p(oi), _p(os_), threads)
     return oi, os_
+
+
+def flat_cosine_distance_batch(q, rows, k, threads=0):
+    """B independent flat_cosine_distance_search calls (one query per thread)."""
+    q, rows = _f32(q), _f32(rows)
+    B, D = q.shape
+    N = rows.shape[0]
+    oi = np.zeros((B, max(k, 1)), np.uint64)
+    os_ = np.zeros((B, max(k, 1)), np.float32)
+    on = np.zeros(B, np.uint64)
+    lib().orc_flat_cosine_distance_batch(_p(q), _p(rows), N, D, B, k, _p(oi), _p(os_), _p(on), threads)
+    return oi[:, :k], os_[:, :k], on
 
 
 def shard_merge(ids, scores, counts, limit):

@@ -388,6 +388,18 @@ void orc_exact_topk_cosine_batch(const float* q, const float* rows, uint64_t N, 
     }
 }
 
+// B independent FaissVectorIndex::search calls (index.rs:620-640), one query
+// per thread: the checker for batched GPU flat searches with metric 2.
+void orc_flat_cosine_distance_batch(const float* q, const float* rows, uint64_t N, uint64_t D, uint64_t B,
+                                    uint64_t k, uint64_t* out_idx, float* out_score, uint64_t* out_n, int threads) {
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int64_t b = 0; b < (int64_t)B; ++b)
+        orc_flat_cosine_distance_search(q + b * D, D, rows, N, D, k, out_idx + b * k, out_score + b * k, out_n + b);
+}
+
 // ShardManager::search_vectors merge (distributed/shard.rs:776-784): concat
 // the per-shard lists in shard order, stable sort by score DESCENDING
 // (NaN == Equal), truncate(limit).

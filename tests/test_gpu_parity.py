@@ -139,8 +139,7 @@ def test_stage1_mfma_batches_match_oracle(g, oracle_mod, N, D, B, R):
     """Large batches (B >= 96) take the FP4-MFMA scan: k_scan_mx5 for W4 in
     {2,3,4,6} (padded dims included: D = 200, 330, 700), k_scan_mx4 (query tiles per launch bounded by LDS, partial
     last launch) for W4 in {8,12,16,24,32}; distances must equal the popcount
-    path (GVDB_SCAN=valu) and the oracle bit for bit.  (The A/B variants
-    i8 / fp4u / fp4lds are compiled only by `make VARIANTS=1`.)"""
+    path (GVDB_SCAN=valu) and the oracle bit for bit."""
     import os
 
     x = rng_rows(N + 3 * D, N, D, dup=200)
@@ -230,6 +229,32 @@ def test_default_rescore_ratio_large_r_matches_oracle(g, oracle_mod, monkeypatch
     assert same_f32(sc, rs[:, :k])
 
 
+def test_default_ratio_sampled_mfma_takes_no_rescan(g, oracle_mod, monkeypatch):
+    """R/N = 0.1 on a SAMPLED shard (400K rows > the 262144-row exact window)
+    with an FP4-MFMA batch (B = 128): the dense FP4 sample keeps one minimum
+    per 16 rows and cannot reach a target of ~R*S/N, so stage1_plan must pick
+    the FP4 histogram instead.  Results equal the oracle and no
+    query took k_select_big's all-rows rescan."""
+    import ctypes as C
+
+    N, D, B, ratio, k = 400_000, 256, 128, 0.1, 10
+    x = rng_rows(N + 5, N, D, dup=100)
+    Q = rng_rows(D + 29, B, D)
+    Q[1] = x[77]
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    monkeypatch.setenv("GVDB_DEBUG_THR", "1")
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=ratio))
+    L = g.lib()
+    L.gvdb_debug_stage1_rescanned.argtypes = [C.POINTER(C.c_uint32)]
+    flag = C.c_uint32(7)
+    assert L.gvdb_debug_stage1_rescanned(C.byref(flag)) == 0
+    assert flag.value == 0, "a query fell back to the all-rows rescan"
+    R = int(np.float32(N) * np.float32(ratio))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (n == k).all() and (ids == ri[:, :k]).all() and same_f32(sc, rs[:, :k])
+
+
 def test_index_semantics(g):
     ix = g.GpuVectorIndex()
     with pytest.raises(g.IndexNotBuilt):  # index.rs:213
@@ -275,7 +300,8 @@ def test_index_flat_mode_matches_oracle(g, oracle_mod):
 
 
 @pytest.mark.parametrize("kind", ["i8", "bf16"])
-@pytest.mark.parametrize("N,D,B,k,metric", [(200_000, 768, 48, 10, 0), (150_000, 100, 300, 25, 0),
+@pytest.mark.parametrize("N,D,B,k,metric", [(200_000, 768, 48, 10, 0), (200_000, 768, 256, 10, 0),
+                                             (160_000, 704, 256, 10, 2), (150_000, 100, 300, 25, 0),
                                              (100_000, 200, 17, 100, 2), (70_000, 64, 1, 1, 0),
                                              (66_000, 1100, 9, 10, 0)])
 def test_flat_mfma_certified_matches_oracle(g, oracle_mod, monkeypatch, kind, N, D, B, k, metric):
@@ -283,14 +309,26 @@ def test_flat_mfma_certified_matches_oracle(g, oracle_mod, monkeypatch, kind, N,
     exact rerank, certificate.  Ids equal and scores bit-identical to the
     oracle's storage.rs / index.rs flat search, with NO fallback taken (i8:
     neither the bf16 retry nor the exact rescan).  D=1100 covers the i8
-    quantiser's second 1024-element pass and a ragged last chunk."""
+    quantiser's second 1024-element pass and a ragged last chunk.  B = 256 at
+    D in (640, 768] is the bench's exact-flat shape on k_flat_i8q: every one of
+    its 8 query tiles holds real queries (waves 4-7 run the skewed epilogue),
+    with planted and i.i.d. queries in every tile, duplicated rows (score ties)
+    and duplicated queries."""
     monkeypatch.setenv("GVDB_FLAT", kind)
     x = rng_rows(N + D, N, D, dup=40)
     x[5] = 0.0  # zero-norm row scores 0 (cosine) / +inf (distance)
     Q = rng_rows(D + 11, B, D)
     r = np.random.default_rng(B)
     planted = r.integers(0, N, size=B)
-    Q[: B // 2] = x[planted[: B // 2]] + 0.05 * Q[: B // 2]  # true near neighbours for half the batch
+    if B >= 128:  # planted and iid queries interleaved: every 32-query tile holds both
+        sel = np.arange(B) % 2 == 0
+        Q[sel] = x[planted[sel]] + 0.05 * Q[sel]
+        for j in range(0, B, 37):  # a planted row duplicated 3x: a tie at the top of the list
+            x[(planted[j] + 1) % N] = x[planted[j]]
+            x[(planted[j] + 2) % N] = x[planted[j]]
+        Q[B - 1] = Q[B - 2]  # duplicated queries in the last tile
+    else:
+        Q[: B // 2] = x[planted[: B // 2]] + 0.05 * Q[: B // 2]  # true near neighbours for half the batch
     ix = g.GpuVectorIndex(dimension=D)
     ix.add_batch(np.arange(N, dtype=np.uint64), x)
     before = g.lib().gvdb_flat_fallback_count()
@@ -298,6 +336,15 @@ def test_flat_mfma_certified_matches_oracle(g, oracle_mod, monkeypatch, kind, N,
     ids, sc, n = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=metric))
     assert g.lib().gvdb_flat_fallback_count() == before, "MFMA candidate pass was not certified"
     assert g.lib().gvdb_flat_i8_fallback_count() == before_i8, "i8 candidate pass was not certified"
+    if B >= 128:  # the oracle's storage.rs / index.rs searches, one query per thread
+        if metric == 0:
+            ri_all, rs_all = oracle_mod.exact_topk_cosine_batch(Q, x, k, threads=16)
+        else:
+            ri_all, rs_all, _ = oracle_mod.flat_cosine_distance_batch(Q, x, k, threads=16)
+        assert (n == k).all()
+        assert (ids == ri_all).all()
+        assert same_f32(sc, rs_all)
+        return
     for b in range(B):
         if metric == 0:
             ri, rs = oracle_mod.storage_vector_search(Q[b], x, k)
@@ -421,21 +468,26 @@ def test_flat_mfma_after_mutations(g, oracle_mod):
 
 
 @pytest.mark.parametrize("kind", ["i8", "bf16"])
-def test_flat_prune_skips_orphans_and_keeps_ties(g, oracle_mod, monkeypatch, kind):
+@pytest.mark.parametrize("N,D,B", [(70_000, 64, 6), (200_000, 768, 256)])
+def test_flat_prune_skips_orphans_and_keeps_ties(g, oracle_mod, monkeypatch, kind, N, D, B):
     """Candidate pruning (k_flat_prune) between the MFMA pass and the exact rerank:
     the k-th largest lower bound is taken over LIVE rows only.  Each query's 40
     nearest rows are re-added under their ids with far vectors, so the orphaned
     old rows still top the MFMA pass, and the live neighbours come in groups of 4
     exact duplicates (ties at the k-th score).  Certified on the MFMA tier (no
-    fallback), ids and scores equal the oracle over the live rows."""
+    fallback), ids and scores equal the oracle over the live rows.  The
+    200K x 768 x 256 case is the bench's shape on k_flat_i8q (all 8 query
+    tiles live, the late waves' skewed epilogue included)."""
     monkeypatch.setenv("GVDB_FLAT", kind)
-    N, D, B, k = 70_000, 64, 6, 10
+    k = 10
     x = rng_rows(91, N, D)
     r = np.random.default_rng(92)
     centers = r.choice(N, B, replace=False)
     Q = x[centers] + np.float32(0.3) * rng_rows(93, B, D)
     xn = x / np.linalg.norm(x, axis=1, keepdims=True)
-    order = np.argsort(-(xn @ (Q / np.linalg.norm(Q, axis=1, keepdims=True)).T), axis=0, kind="stable")
+    sim = xn @ (Q / np.linalg.norm(Q, axis=1, keepdims=True)).T
+    top = np.argpartition(-sim, 48, axis=0)[:48]  # the 48 nearest rows of each query (unordered)
+    order = np.take_along_axis(top, np.argsort(-np.take_along_axis(sim, top, axis=0), axis=0, kind="stable"), axis=0)
     near = np.unique(order[:40].ravel())             # to be orphaned
     nxt = [c for c in order[40:48].T.ravel() if c not in set(near)]
     for j, c in enumerate(nxt[: len(nxt) // 4 * 4]):  # live neighbours in groups of 4 equal rows
@@ -451,10 +503,11 @@ def test_flat_prune_skips_orphans_and_keeps_ties(g, oracle_mod, monkeypatch, kin
     ids, sc, n = ix.search_batch(Q, k, g.SearchParams(mode=1, metric=0))
     assert g.lib().gvdb_flat_fallback_count() == before, "MFMA candidate pass was not certified"
     assert g.lib().gvdb_flat_i8_fallback_count() == before_i8, "i8 candidate pass was not certified"
+    ri_all, rs_all = oracle_mod.exact_topk_cosine_batch(Q, live_x, k, threads=16)
     for b in range(B):
-        ri, rs = oracle_mod.storage_vector_search(Q[b], live_x, k)
-        assert list(ids[b, : n[b]]) == list(live_id[ri]), b
-        assert same_f32(sc[b, : n[b]], rs)
+        assert n[b] == k
+        assert list(ids[b, : n[b]]) == list(live_id[ri_all[b]]), b
+        assert same_f32(sc[b, : n[b]], rs_all[b])
 
 
 @pytest.mark.parametrize("N,k", [(4000, 1), (4000, 10), (4000, 1000), (4000, 1024), (4000, 1500), (4000, 5000),

@@ -176,3 +176,21 @@ def test_bq_topr_equals_stable_stage1(oracle_mod):
     for b in range(4):
         _, _, s1i, _ = oracle_mod.multi_stage_search(qb[b], 64, cb, 64, Q[b], X, 0.1, want_stage1=True)
         assert list(ti[b]) == [int(i) for i in s1i[:50]]
+
+
+def test_batched_flat_searches_equal_single(oracle_mod):
+    """The threaded batch forms (the B >= 128 GPU flat checkers) are the
+    per-query storage.rs / index.rs searches, bit for bit."""
+    rng = np.random.default_rng(6)
+    X = rng.standard_normal((700, 48)).astype(np.float32)
+    X[10:20] = X[3]  # ties
+    X[5] = 0.0
+    Q = rng.standard_normal((9, 48)).astype(np.float32)
+    Q[2] = X[3]
+    ci, cs = oracle_mod.exact_topk_cosine_batch(Q, X, 15, threads=4)
+    di, ds, dn = oracle_mod.flat_cosine_distance_batch(Q, X, 15, threads=4)
+    for b in range(9):
+        ri, rs = oracle_mod.storage_vector_search(Q[b], X, 15)
+        assert list(ci[b]) == list(ri) and cs[b].tobytes() == rs.tobytes()
+        ri, rs = oracle_mod.flat_cosine_distance_search(Q[b], X, 15)
+        assert dn[b] == len(ri) and list(di[b]) == list(ri) and ds[b].tobytes() == rs.tobytes()

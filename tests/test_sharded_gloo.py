@@ -109,6 +109,111 @@ def _worker2(rank, world, port, ret, bounds, R):
     dist.destroy_process_group()
 
 
+def _worker_fail(rank, world, port, ret, bad_rank, phase):
+    """One rank's stage 1 (phase 1) or cosine callable (phase 2) raises: every
+    rank still completes both all-gathers (no hang), every query of the merge
+    is poisoned on every rank, and only the failing rank raises."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "grape-vector-db_amd")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import oracle
+    from gvdb.sharded import TwoExchangeSearch, shard_bounds
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, q = _data()
+    bnd = shard_bounds(N, world)
+    lo, hi = bnd[rank], bnd[rank + 1]
+    xs = x[lo:hi]
+
+    def stage1(qt, r):
+        if rank == bad_rank and phase == 1:
+            raise ValueError("dimension mismatch on this shard")
+        return oracle.bq_topr_batch(oracle.quantize(qt.numpy()), oracle.quantize(xs), D, min(r, hi - lo))
+
+    def cosine(i, local_rows):
+        if rank == bad_rank and phase == 2:
+            raise ValueError("rerank failed on this shard")
+        return np.array([oracle.cosine_manual(q[i], xs[int(j)]) for j in local_rows], np.float32)
+
+    s = TwoExchangeSearch(B, R, K, torch.device("cpu"), stage1_fn=stage1, cosine_fn=cosine, id_offset=lo)
+    raised = False
+    try:
+        s.search(torch.from_numpy(q))
+    except ValueError:
+        raised = True
+    # the merge ran on every rank: its outputs are the poisoned counts
+    poisoned = bool((s.send2.numpy().view(np.uint32)[4 * B * K + 2 * B] == 1) == (rank == bad_rank))
+    # a second search on the same ranks still works (nobody is stuck in a collective)
+    s2 = TwoExchangeSearch(B, R, K, torch.device("cpu"), stage1_fn=lambda qt, r: oracle.bq_topr_batch(
+        oracle.quantize(qt.numpy()), oracle.quantize(xs), D, min(r, hi - lo)), cosine_fn=lambda i, rows: np.array(
+        [oracle.cosine_manual(q[i], xs[int(j)]) for j in rows], np.float32), id_offset=lo)
+    ids, sc, n = s2.search(torch.from_numpy(q))
+    ok_after = bool((n.numpy() == K).all())
+    ret[rank] = (raised == (rank == bad_rank), poisoned, ok_after)
+    dist.destroy_process_group()
+
+
+def _worker_fail_outputs(rank, world, port, ret):
+    """The poisoned merge's outputs on a healthy rank: every out_n is POISONED."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "grape-vector-db_amd")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import oracle
+    from gvdb._ffi import GVDB_N_POISONED
+    from gvdb.sharded import TwoExchangeSearch, shard_bounds
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, q = _data()
+    bnd = shard_bounds(N, world)
+    lo, hi = bnd[rank], bnd[rank + 1]
+    xs = x[lo:hi]
+
+    def stage1(qt, r):
+        if rank == 1:
+            raise ValueError("bad shard")
+        return oracle.bq_topr_batch(oracle.quantize(qt.numpy()), oracle.quantize(xs), D, min(r, hi - lo))
+
+    s = TwoExchangeSearch(B, R, K, torch.device("cpu"), stage1_fn=stage1,
+                          cosine_fn=lambda i, rows: np.array([oracle.cosine_manual(q[i], xs[int(j)]) for j in rows],
+                                                             np.float32), id_offset=lo)
+    try:
+        _, _, n = s.search(torch.from_numpy(q))
+        ret[rank] = bool((n.numpy().view(np.uint32) == GVDB_N_POISONED).all())
+    except ValueError:
+        ret[rank] = rank == 1
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("phase", [1, 2])
+def test_two_exchange_failing_rank_joins_both_exchanges(phase, oracle_mod, gvdb_lib_path):
+    world = 3
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_fail, args=(world, _free_port(), ret, 1, phase), nprocs=world, join=True)
+    assert dict(ret) == {r: (True, True, True) for r in range(world)}
+
+
+def test_two_exchange_failing_rank_poisons_every_query(oracle_mod, gvdb_lib_path):
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_fail_outputs, args=(2, _free_port(), ret), nprocs=2, join=True)
+    assert dict(ret) == {0: True, 1: True}
+
+
 @pytest.mark.parametrize("world,bounds,R", [(2, (0, 1500, N), 40), (3, (0, 900, 900, N), 40),
                                             (3, (0, 1000, 2000, N), 300)])
 def test_two_exchange_equals_single_corpus(world, bounds, R, oracle_mod, gvdb_lib_path):
