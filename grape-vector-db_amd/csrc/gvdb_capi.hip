@@ -1206,7 +1206,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         HIP_TRY(launch_flat_mx_sample(a, s), "flat sample pass");
         DBG_SYNC(s, "dbg: flat sample pass");
         // tau from exactly re-scored probes (the 16 best sampled rows per query)
-        HIP_TRY(launch_flat_probes(a.smp, Bg, S, every, N, probes, pcount, s), "flat probes");
+        HIP_TRY(launch_flat_probes(a.smp, Bg, S, every, N, ix->ids, probes, pcount, s), "flat probes");
         {
             RerankArgs pr{};
             pr.rows = ix->rows;

@@ -620,9 +620,12 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
 // largest exact probe score: mk rows then have exact score >= tau_q, so the
 // k-th best score is >= tau_q unless the sample holds mk of the top k-1 rows
 // (mk is sized for that to be a 1e-6 event, host side).
+// Orphan rows (an id re-added elsewhere, ids[row] == kOrphan) are never probes:
+// tau must be reached by mk LIVE rows, or the certificate would fail whenever
+// a shadowed row of a query's own neighbourhood falls into the sample.
 __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ smp, uint32_t S, uint32_t every,
-                                                      uint32_t N, uint32_t* __restrict__ probes,
-                                                      uint32_t* __restrict__ pcount) {
+                                                      uint32_t N, const uint64_t* __restrict__ ids,
+                                                      uint32_t* __restrict__ probes, uint32_t* __restrict__ pcount) {
     __shared__ uint64_t keys[256];
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     // wave-cooperative top-16: lanes 0..15 hold the wave's best keys, descending
@@ -659,6 +662,11 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
                 m &= m - 1;
                 const uint64_t kk = __shfl(key, l);
                 if (kk <= t16) continue;
+                if (ids) {  // wave-uniform: one load per insertion (rare after the first batches)
+                    const uint32_t sp = (uint32_t)kk;
+                    const uint32_t row = ((sp >> 8) * every << 8) | (sp & 255u);
+                    if (row < N && ids[row] == kOrphan) continue;
+                }
                 // insert into lanes 0..15: lanes holding a smaller key shift down
                 const uint64_t up = __shfl_up(mine, 1);
                 const bool below = lane < 16 && kk > mine;
@@ -1249,10 +1257,10 @@ hipError_t launch_flat_prune(uint32_t* counts, uint32_t* cand, const float* csco
     return hipSuccess;
 }
 
-hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, uint32_t* probes,
-                              uint32_t* pcount, hipStream_t s) {
+hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, const uint64_t* ids,
+                              uint32_t* probes, uint32_t* pcount, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_flat_probes, dim3(B), dim3(1024), 0, s, smp, S, every, N, probes, pcount);
+    hipLaunchKernelGGL(k_flat_probes, dim3(B), dim3(1024), 0, s, smp, S, every, N, ids, probes, pcount);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -283,8 +283,8 @@ hipError_t launch_flat_prune(uint32_t* counts, uint32_t* cand, const float* csco
                              uint32_t k, const float* qa, const float* qd, const float* rrho, const uint64_t* ids,
                              hipStream_t s);
 // probes[q][16] = rows of the 16 largest sampled MFMA scores, pcount[q] valid
-hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, uint32_t* probes,
-                              uint32_t* pcount, hipStream_t s);
+hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, const uint64_t* ids,
+                              uint32_t* probes, uint32_t* pcount, hipStream_t s);
 // thr[q] = (mk-th largest exact probe score) - qd[q] (mk <= 16); +inf for q >= B.
 // distance: pscores hold 1 - cos (the index metric's rerank output).
 hipError_t launch_flat_tau(const float* pscores, const uint32_t* pcount, uint32_t B, uint32_t mk, int distance,

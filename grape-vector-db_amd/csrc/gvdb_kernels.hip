@@ -1224,6 +1224,305 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
                                       buf, bufcap);
 }
 
+// ---------------------------------------------------------------------------
+// k_scan_mx6: k_scan_mx5 with the sub-tile boundary software-pipelined.
+// mx5 drains every accumulator after a sub-tile's last k-step, then runs the
+// threshold epilogue of all 8 query tiles, re-seeds them and restarts the
+// A-fragment ring: a boundary with the matrix pipe idle (ablations: epilogue
+// 15 %, seeds 7 % of the scan).  Here each wave's sub-tiles form ONE MFMA
+// stream: in k-step 0 of sub-tile i+1, tile qt of sub-tile i is tested and
+// re-seeded right before its first MFMA of sub-tile i+1, i.e. between the
+// MFMAs of the other tiles (its last MFMA of sub-tile i is 7 MFMAs old
+// there), and the A-fragment ring runs on across sub-tiles (its sequence is
+// periodic in the sub-tile).
+// One wave per SIMD (4 per CU): the 128 accumulator registers live in AGPRs
+// (the MFMAs take them as "+a"), which leaves the architectural VGPRs to the
+// code ring, the A ring and the tests -- mx5's 2 waves per SIMD had 256
+// registers each and no room to keep the A ring live through the tests.
+// Tail: the full rounds give every wave the same number of sub-tiles; the
+// last partial round (nsub mod waves sub-tiles) is split into (sub-tile,
+// query tile) units of KS MFMAs spread over all waves.
+// Same emit contract as mx5: (d << 32 | row) for every row with d <= thr[q].
+#ifndef MX6_WAVES
+#define MX6_WAVES 8  // waves per CU: 8 = 2 per SIMD, accumulators in VGPRs; 4 = 1 per SIMD, in AGPRs
+#endif
+constexpr int kMx6Threads = MX6_WAVES * 64;
+#if MX6_WAVES == 4
+#define MX6_ACC "a"
+#else
+#define MX6_ACC "v"
+#endif
+__device__ __forceinline__ void mfma_fp4_agpr(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "+" MX6_ACC(d)
+                 : "v"(a), "v"(b), "v"(scale));
+}
+// after a VALU / LDS write of an operand (B fragment just expanded, accumulator
+// just seeded): 4 wait states inside the string
+__device__ __forceinline__ void mfma_fp4_agpr_nop(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
+    asm volatile("s_nop 3\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
+                 : "+" MX6_ACC(d)
+                 : "v"(a), "v"(b), "v"(scale));
+}
+template <int W4>
+__global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                           const v4i_t* __restrict__ qfrag_g,
+                                                           const uint32_t* __restrict__ qpc,
+                                                           const uint32_t* __restrict__ thr, uint32_t B,
+                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
+                                                           uint32_t bufcap) {
+    constexpr int KW = 4 * W4;  // 32-bit code words per row
+    constexpr int KS = KW / 2;  // k-steps of 64 bits
+    constexpr int QT = 8;       // query tiles of 32
+    constexpr int NM = KS * QT;  // MFMAs per sub-tile
+    constexpr uint32_t kWaveStage = 256;  // ~90 emits per wave at 10M x 768 x 256 (overflow: global atomics)
+    constexpr int NW = kMx6Threads / 64;
+    constexpr int PF = MX6_WAVES == 4 ? 8 : 4;  // A-fragment ring depth (in MFMAs)
+    static_assert(NM % PF == 0, "the A ring's slot of MFMA m must not depend on the sub-tile");
+    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
+    __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
+    __shared__ float thrc_lds[QT * 32];
+    __shared__ uint64_t st_key[NW][kWaveStage];
+    __shared__ uint8_t st_q[NW][kWaveStage];
+    __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
+    __shared__ float tscr[NW][16 * 64];  // a hit tile's 16 values per lane ([r][lane]: conflict-free)
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t h = lane >> 5;
+    const uint32_t nsub = (N + 31u) / 32u;
+    const uint32_t W = gridDim.x * NW;        // waves in the grid
+    const uint32_t nround = nsub / W;         // full rounds (every wave the same count)
+    const uint32_t gw = blockIdx.x * NW + wv;
+    uint2 ring[2][W4];
+    auto load = [&](uint32_t sb, uint2 (&c)[W4]) __attribute__((always_inline)) {
+        const uint32_t n = min(sb * 32u + (lane & 31u), N - 1u);  // clamped: branch-free ring
+        const uint32_t voff = n * 16u + h * 8u;
+#pragma unroll
+        for (int p = 0; p < W4; ++p) {
+            const uint4* base = codes + (uint64_t)p * cap;
+            asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(c[p]) : "v"(voff), "s"(base));
+        }
+    };
+    // the first two sub-tiles' codes are in flight during the prologue
+    if (nround > 0) {
+        load(gw, ring[0]);
+        load(gw + W, ring[1]);
+    }
+#pragma unroll 4
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx6Threads) qfrag[i] = qfrag_g[i];
+    constexpr uint32_t kPadBits = 32u * KW;
+    if (tid < QT * 32) {
+        const uint32_t q = tid;
+        const uint32_t pc = qpc[q];
+        const float tc = q < B ? (float)min(thr[q], kPadBits) : 0.0f;
+        thrc_lds[q] = tc;
+        const uint32_t qt = q >> 5, j = q & 31u, hh = (j >> 2) & 1u, r = (j & 3u) + 4u * (j >> 3);
+        seed_lds[(qt * 2 + hh) * 16 + r] = q < B ? tc - (float)pc : -1.0e9f;
+        qcnt[q] = 0u;
+    }
+    __syncthreads();
+    const uint32_t nqt = (B + 31u) / 32u;
+    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
+    v16f_t acc[QT];
+    const int scale1 = 0x7f7f7f7f;
+    auto seed_into = [&](v16f_t& A, uint32_t qt) __attribute__((always_inline)) {
+        const float4* sp = (const float4*)(seed_lds + (qt * 2 + h) * 16);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 v = sp[g];
+            A[4 * g + 0] = v.x;
+            A[4 * g + 1] = v.y;
+            A[4 * g + 2] = v.z;
+            A[4 * g + 3] = v.w;
+        }
+    };
+    // threshold test of one query tile (acc = thr - Hamming; a hit is acc >= 0),
+    // emits staged in LDS (overflow straight to the query's buffer)
+    // threshold test of one query tile (acc = thr - Hamming; a hit is acc >= 0).
+    // Common path: the AND of the 16 accumulators (sign bit clear <=> some
+    // value >= 0) and one ballot.  Rare hit path, kept compact (a fully
+    // unrolled per-value path in every inlined copy stops the k-loop unroll):
+    // the tile's values go to the wave's LDS scratch, then a runtime loop over
+    // the groups of 4 values that hold a hit emits them.
+    auto test = [&](const v16f_t& A, uint32_t qt, uint32_t n) __attribute__((always_inline)) {
+        int pa[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            pa[g] = __float_as_int(A[4 * g]) & __float_as_int(A[4 * g + 1]) & __float_as_int(A[4 * g + 2]) &
+                    __float_as_int(A[4 * g + 3]);
+        const int aand = (pa[0] & pa[1]) & (pa[2] & pa[3]);
+        const bool ok = qt < nqt && n < N;  // padded query tile / row past the end: no emits
+        if (__ballot(ok && aand >= 0)) {
+            float* sc = tscr[wv];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[r * 64 + lane] = A[r];
+            uint32_t gm = 0;  // groups of 4 with a hit (wave-uniform)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) gm |= __ballot(ok && pa[g] >= 0) ? (1u << g) : 0u;
+            // global (address space 1) pointers: a flat atomic / store here would count in
+            // lgkmcnt too and make every later LDS wait of the stream a full lgkmcnt(0)
+            typedef __attribute__((address_space(1))) uint32_t g_u32;
+            typedef __attribute__((address_space(1))) uint64_t g_u64;
+            g_u32* cnt = (g_u32*)counts;
+            g_u64* bf = (g_u64*)buf;
+            uint32_t bcap = bufcap;
+            asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
+            const uint32_t rb = qt * 32u + 4u * h;
+#pragma unroll 1
+            while (gm) {
+                const uint32_t g = __builtin_ctz(gm);
+                gm &= gm - 1u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t r = 4u * g + (uint32_t)j;
+                    const float v = sc[r * 64u + lane];
+                    const bool hit = ok && v >= 0.0f;
+                    const uint64_t m = __ballot(hit);
+                    if (hit) {
+                        const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
+                                                       (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        const uint32_t qi = rb + (uint32_t)j + 8u * g;
+                        const uint32_t d = (uint32_t)(int)(thrc_lds[qi] - v);
+                        const uint64_t key = ((uint64_t)d << 32) | n;
+                        if (sp < kWaveStage) {
+                            st_key[wv][sp] = key;
+                            st_q[wv][sp] = (uint8_t)qi;
+                        } else {
+                            const uint32_t pos = __hip_atomic_fetch_add(cnt + qi, 1u, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT);
+                            if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = key;
+                        }
+                    }
+                    wcnt += (uint32_t)__popcll(m);
+                }
+            }
+        }
+    };
+    const v4i_t* qf = qfrag + lane;
+    // A fragment mm of the sub-tile: two base registers, one per 64 KiB of
+    // fragments (a ds_read offset is 16 bits; without the split hipcc keeps one
+    // address VGPR per fragment past 64 KiB)
+    typedef __attribute__((address_space(3))) const v4i_t lds_v4i_t;
+    const uint32_t qf_lo = (uint32_t)(uintptr_t)qf;  // LDS byte address
+    uint32_t qf_hi = qf_lo + 64u * 64u * 16u;
+    asm volatile("" : "+v"(qf_hi));  // opaque: hipcc folds it back into qf_lo otherwise
+    auto afrag = [&](int mm) __attribute__((always_inline)) -> v4i_t {
+        const uint32_t ad = mm < 64 ? qf_lo + (uint32_t)mm * 1024u : qf_hi + (uint32_t)(mm - 64) * 1024u;
+        return *(lds_v4i_t*)ad;
+    };
+    if (nround > 0) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) seed_into(acc[qt], qt);
+        v4i_t ar[PF];
+#pragma unroll
+        for (int m = 0; m < PF; ++m) ar[m] = afrag(m);
+        // one sub-tile of the stream: slot c holds its codes; tile qt of the
+        // previous sub-tile (rows of sub-tile sbp) is tested just before its
+        // first MFMA here; the slot is refilled with sub-tile sb + 2W after its
+        // last expansion
+        auto step = [&](uint2 (&c)[W4], uint32_t sb, bool prev, uint32_t sbp) __attribute__((always_inline)) {
+            const uint32_t np = sbp * 32u + (lane & 31u);
+#pragma unroll
+            for (int p = 0; p < W4; ++p)  // this slot's loads are the older of the two in flight
+                asm volatile("s_waitcnt vmcnt(%1)" : "+v"(c[p]) : "n"(W4));
+            v4i_t bcur = fp4_row01(c[0].x);
+            v4i_t bnext;
+            // k-step 0, peeled (its control flow would stop the k-loop unroll):
+            // position qt tests tile qt of the previous sub-tile (its last MFMA is
+            // 7 MFMAs old; the pad + the asm naming acc[qt] keep every read below
+            // it), re-seeds it, then issues its first MFMA of this sub-tile
+#define GVDB_MX6_POS0(qt)                                                      \
+            {                                                                  \
+                __builtin_amdgcn_sched_barrier(0);                             \
+                if (prev) {                                                    \
+                    asm volatile("s_nop 4" : "+" MX6_ACC(acc[qt]));                   \
+                    test(acc[qt], (uint32_t)(qt), np);                         \
+                    seed_into(acc[qt], (uint32_t)(qt));                        \
+                }                                                              \
+                const v4i_t a = ar[(qt) % PF];                                 \
+                ar[(qt) % PF] = afrag(((qt) + PF) % NM);                        \
+                mfma_fp4_agpr_nop(acc[qt], a, bcur, scale1);                   \
+                if ((qt) == 1) {                                               \
+                    const uint2 v = c[0];                                      \
+                    bnext = fp4_row01(v.y);                                    \
+                }                                                              \
+            }
+            GVDB_MX6_POS0(0)
+            GVDB_MX6_POS0(1)
+            GVDB_MX6_POS0(2)
+            GVDB_MX6_POS0(3)
+            GVDB_MX6_POS0(4)
+            GVDB_MX6_POS0(5)
+            GVDB_MX6_POS0(6)
+            GVDB_MX6_POS0(7)
+#undef GVDB_MX6_POS0
+            bcur = bnext;
+#pragma unroll
+            for (int s = 1; s < KS; ++s) {
+                __builtin_amdgcn_sched_barrier(0);
+                bnext = bcur;
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    const int m = s * QT + qt;
+                    const v4i_t a = ar[m % PF];
+                    ar[m % PF] = afrag((m + PF) % NM);  // the ring runs on into the next sub-tile
+                    mfma_fp4_agpr(acc[qt], a, bcur, scale1);
+                    if (qt == 1 && s + 1 < KS) {  // next k-step's row fragment under this one's MFMAs
+                        const uint2 v = c[(s + 1) >> 1];
+                        bnext = fp4_row01(((s + 1) & 1) ? v.y : v.x);
+                    }
+                }
+                bcur = bnext;
+            }
+            load(sb + 2u * W, c);  // every expansion of this slot is done
+        };
+        // two inlined copies of step() (one per ring slot); the first sub-tile
+        // has no predecessor to test, an odd count ends after slot 0
+        for (uint32_t i = 0; i < nround; i += 2) {
+            const uint32_t sb = gw + i * W;
+            step(ring[0], sb, i > 0, sb - W);
+            if (i + 1 < nround) step(ring[1], sb + W, true, sb);
+        }
+        asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+        const uint32_t nl = (gw + (nround - 1u) * W) * 32u + (lane & 31u);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            asm volatile("" : "+" MX6_ACC(acc[qt]));
+            test(acc[qt], (uint32_t)qt, nl);
+        }
+        // the refills past the end (clamped rows) must land before the registers are reused
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int p = 0; p < W4; ++p) asm volatile("s_waitcnt vmcnt(0)" : "+v"(ring[k][p]));
+    }
+    // the partial last round: (sub-tile, query tile) units of KS MFMAs over all waves
+    const uint32_t sb0 = nround * W;
+    const uint32_t nunits = (nsub - sb0) * nqt;
+    for (uint32_t u = gw; u < nunits; u += W) {
+        const uint32_t sb = sb0 + u / nqt, qt = u % nqt;
+        const uint32_t n = sb * 32u + (lane & 31u);
+        const uint32_t voff = min(n, N - 1u) * 16u + h * 8u;
+        uint2 c[W4];
+#pragma unroll
+        for (int p = 0; p < W4; ++p) c[p] = *(const uint2*)((const char*)(codes + (uint64_t)p * cap) + voff);
+        v16f_t& A = acc[0];
+        seed_into(A, qt);
+        const v4i_t* qa = qf + qt * 64u;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const uint2 v = c[s >> 1];
+            const v4i_t b = fp4_row01((s & 1) ? v.y : v.x);
+            const v4i_t a = qa[s * QT * 64];
+            mfma_fp4_agpr_nop(A, a, b, scale1);
+        }
+        asm volatile("s_nop 15\n\ts_nop 15" : "+" MX6_ACC(A));
+        test(A, qt, n);
+    }
+    flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase, counts,
+                                      buf, bufcap);
+}
+
 // CUs of the current device (cached per device: read on every launch)
 static uint32_t cu_count() {
     static int cached[64] = {0};
@@ -1295,17 +1594,29 @@ static void launch_qfrag_t(const Stage1Args& a, hipStream_t s) {
                        (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero);
 }
 
+// GVDB_SCAN=mx5: the previous (non-pipelined) scan, for same-box A/B timing
+static bool scan_mx5_selected() {
+    const char* e = getenv("GVDB_SCAN");
+    return e && strcmp(e, "mx5") == 0;
+}
+
 template <int W4>
 static void launch_scan_mx5_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t nsub = (a.N + 31u) / 32u;
     const uint32_t wpb = kMx5Threads / 64;
     const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(cu_count(), (nsub + wpb - 1) / wpb));
     constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
+    const bool mx5 = scan_mx5_selected();
     for (uint32_t g = 0; g < a.B; g += 256) {
         const uint32_t bg = min(256u, a.B - g);
-        hipLaunchKernelGGL((k_scan_mx5<W4>), dim3(grid), dim3(kMx5Threads), 0, s, a.codes, a.cap, a.N,
-                           (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+        if (mx5)
+            hipLaunchKernelGGL((k_scan_mx5<W4>), dim3(grid), dim3(kMx5Threads), 0, s, a.codes, a.cap, a.N,
+                               (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
+                               a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+        else
+            hipLaunchKernelGGL((k_scan_mx6<W4>), dim3(cu_count()), dim3(kMx6Threads), 0, s, a.codes, a.cap, a.N,
+                               (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
+                               a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
 }
 

@@ -8,6 +8,7 @@
 #   bench        python bench.py (the driver's default command)         -> gpurun_out/bench.json / .log
 #   benchprof    the same command under rocprofv3 --kernel-trace --stats -> gpurun_out/prof_bench/
 #   b256         scripts/b256_timing.py at 10M (SHARD_N / RCCL env pass through)
+#   scanab       scripts/scan_ab.py: k_scan_mx5 vs the default scan, 10M and 1.25M rows -> gpurun_out/scanab.log
 #   c3           scripts/c3_emulate.py (config 3, 8 shards on one GPU)  -> gpurun_out/c3.json / .log
 #   c3prof       c3_emulate (no single index, no oracle) under rocprofv3 -> gpurun_out/prof_c3/
 #   c4           scripts/c4_emulate.py (config 4, 8 shards of 1.25M x 3072)
@@ -56,6 +57,9 @@ for t in "${TASKS[@]}"; do
         benchprof)
             run 900 gpurun_out/benchprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py
             grep '^{' gpurun_out/benchprof.log > gpurun_out/benchprof.json || true ;;
+        scanab)  # same-box A/B: k_scan_mx5 vs the default scan at 10M and the 1.25M shard
+            SHARD_N=10000000,1250000 SCANS=mx5, REPS=3 run 900 gpurun_out/scanab.log python3 -u scripts/scan_ab.py
+            grep '^\[scan_ab\]' gpurun_out/scanab.log ;;
         b256)
             run 600 gpurun_out/b256.log python3 -u scripts/b256_timing.py
             grep -v amdgpu.ids gpurun_out/b256.log | tail -4 ;;
