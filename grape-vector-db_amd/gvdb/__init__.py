@@ -558,6 +558,51 @@ class GpuVectorIndex:
 
 
 @dataclass
+class RequestCoalescer:
+    """Concurrent batch-1 searches over one index (gvdb_coalescer_*): callers on
+    any number of threads each ask for ONE query's top-k, as the reference's
+    concurrent readers of Arc<RwLock<dyn VectorIndex>> do (src/lib.rs:238,
+    index.rs:212-231); queries that arrive while a batch runs are searched
+    together in the next one, and every caller gets exactly its own
+    gvdb_index_search result.  ctypes releases the GIL around the call, so
+    Python threads really wait in parallel."""
+
+    def __init__(self, index: "GpuVectorIndex", dim: int, k: int, params: Optional[SearchParams] = None,
+                 max_batch: int = 256, max_inflight: int = 1):
+        self._lib = lib()
+        self.index, self.dim, self.k = index, dim, k
+        self._sp = (params or index.params).to_c()
+        h = C.c_void_p()
+        check(self._lib.gvdb_coalescer_create(index._h, dim, k, C.byref(self._sp), max_batch, max_inflight,
+                                              C.byref(h)))
+        self._h = h
+
+    def search(self, query) -> Tuple[np.ndarray, np.ndarray, int]:
+        q = _f32(query).reshape(-1)
+        if q.size != self.dim:
+            raise DimensionMismatch(f"query has {q.size} dims, coalescer {self.dim}", self.dim, q.size)
+        ids = np.zeros(self.k, np.uint64)
+        sc = np.zeros(self.k, np.float32)
+        n = C.c_uint32(0)
+        check(self._lib.gvdb_coalescer_search(self._h, ptr(q), ptr(ids), ptr(sc), C.byref(n)))
+        return ids, sc, int(n.value)
+
+    def stats(self) -> Tuple[int, int, int]:
+        """(batches run, queries served, largest batch)."""
+        b, q, m = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(self._lib.gvdb_coalescer_stats(self._h, C.byref(b), C.byref(q), C.byref(m)))
+        return b.value, q.value, m.value
+
+    def close(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.gvdb_coalescer_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
 class HnswConfig:
     """config.rs:196-209 (defaults config.rs:413-422)."""
     m: int = 16

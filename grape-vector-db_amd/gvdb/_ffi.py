@@ -117,6 +117,10 @@ SIGNATURES = {
     "gvdb_index_bq_topr_device": (C.c_int, [P, P, u64, u32, u64, P, P, P]),
     "gvdb_index_bq_candidates_device": (C.c_int, [P, P, u64, u32, u64, P, P, P, P]),
     "gvdb_index_search_filtered": (C.c_int, [P, P, u64, u32, u64, C.POINTER(gvdb_search_params), P, u64, P, P, P]),
+    "gvdb_coalescer_create": (C.c_int, [P, u32, u64, C.POINTER(gvdb_search_params), u32, u32, C.POINTER(P)]),
+    "gvdb_coalescer_search": (C.c_int, [P, P, P, P, P]),
+    "gvdb_coalescer_stats": (C.c_int, [P, PU64, PU64, PU64]),
+    "gvdb_coalescer_destroy": (None, [P]),
     "gvdb_index_remove": (C.c_int, [P, u64, C.POINTER(i32)]),
     "gvdb_index_len": (u64, [P]),
     "gvdb_index_is_empty": (i32, [P]),

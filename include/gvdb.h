@@ -219,6 +219,27 @@ gvdb_status gvdb_index_bq_candidates_device(const gvdb_index* index, const float
 gvdb_status gvdb_index_search_filtered(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
                                        uint64_t k, const gvdb_search_params* sp, const uint64_t* allowed,
                                        uint64_t n_allowed, uint64_t* out_ids, float* out_scores, uint32_t* out_n);
+/* ---- batch-1 request coalescing (concurrent readers) ----------------------
+ * Replaces the reference's concurrent single-query readers of
+ * Arc<RwLock<dyn VectorIndex>> (src/lib.rs:238), each running
+ * HnswVectorIndex::search(q, k) (src/index.rs:212-231).  A coalescer holds one
+ * (index, dim, k, search params) triple; gvdb_coalescer_search is one query
+ * from any thread: concurrent callers' queries are run together as one
+ * gvdb_index_search (the first caller to find no batch executing takes up to
+ * max_batch pending queries; requests that arrive meanwhile form the next
+ * batch), so the code array is read once per batch instead of once per query.
+ * A caller's results are exactly those of its own gvdb_index_search call.
+ * max_batch 0 = 256; max_inflight 0 = 1 batch executing at a time.  The index
+ * must not be mutated while the coalescer is in use (the reader lock). */
+typedef struct gvdb_coalescer gvdb_coalescer;
+gvdb_status gvdb_coalescer_create(const gvdb_index* index, uint32_t dim, uint64_t k, const gvdb_search_params* sp,
+                                  uint32_t max_batch, uint32_t max_inflight, gvdb_coalescer** out);
+/* query: dim floats; out_ids / out_scores: k entries; out_n may be NULL (host buffers) */
+gvdb_status gvdb_coalescer_search(gvdb_coalescer* c, const float* query, uint64_t* out_ids, float* out_scores,
+                                  uint32_t* out_n);
+gvdb_status gvdb_coalescer_stats(gvdb_coalescer* c, uint64_t* batches, uint64_t* queries, uint64_t* max_batch);
+void gvdb_coalescer_destroy(gvdb_coalescer* c);
+
 gvdb_status gvdb_index_remove(gvdb_index* index, uint64_t id, int32_t* removed);
 uint64_t gvdb_index_len(const gvdb_index* index);
 int32_t gvdb_index_is_empty(const gvdb_index* index);

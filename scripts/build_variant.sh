@@ -15,7 +15,8 @@ for f in csrc/*.hip; do
     objs+=("$o")
 done
 g++ -O2 -std=c++17 -fPIC -Wall -c csrc/gvdb_persist.cpp -o "$b/gvdb_persist.o"
+g++ -O2 -std=c++17 -fPIC -Wall -c csrc/gvdb_coalesce.cpp -o "$b/gvdb_coalesce.o"
 wait
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -o "abl/libgvdb_$name.so" "${objs[@]}" "$b/gvdb_persist.o" -lz -ldl
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -o "abl/libgvdb_$name.so" "${objs[@]}" "$b/gvdb_persist.o" "$b/gvdb_coalesce.o" -lz -ldl -lpthread
 rm -rf "$b"
 echo "abl/libgvdb_$name.so"

@@ -8,10 +8,13 @@
 #   bench        python bench.py (the driver's default command)         -> gpurun_out/bench.json / .log
 #   benchprof    the same command under rocprofv3 --kernel-trace --stats -> gpurun_out/prof_bench/
 #   b256         scripts/b256_timing.py at 10M (SHARD_N / RCCL env pass through)
+#   coalesce     build/coalesce_bench: concurrent batch-1 callers, B=1 searches vs the coalescer -> gpurun_out/coalesce.json
+#   bigr         scripts/bigr_timing.py: R = 0.1 N at 1M / 10M rows -> gpurun_out/bigr.json
 #   scanab       scripts/scan_ab.py: k_scan_mx5 vs the default scan, 10M and 1.25M rows -> gpurun_out/scanab.log
 #   c3           scripts/c3_emulate.py (config 3, 8 shards on one GPU)  -> gpurun_out/c3.json / .log
 #   c3prof       c3_emulate (no single index, no oracle) under rocprofv3 -> gpurun_out/prof_c3/
-#   c4           scripts/c4_emulate.py (config 4, 8 shards of 1.25M x 3072)
+#   c4           scripts/c4_emulate.py (config 4, 8 shards of 1.25M x 3072; one-exchange merge)
+#   c4x2         scripts/c3_emulate.py --dim 3072: config 4 on the two-exchange protocol
 #   hybrid       scripts/bench_hybrid.py (config 5)                     -> gpurun_out/hybrid.json / .log
 #   hnsw10m      scripts/hnsw10m_gpu.py (GPU side of the 10M equal-recall experiment)
 #   pmc:NAME:REGEX:CMD[:FIRST]   rocprofv3 --pmc passes (one counter set per run) over python3 CMD (spaces as ','),
@@ -60,6 +63,12 @@ for t in "${TASKS[@]}"; do
         scanab)  # same-box A/B: k_scan_mx5 vs the default scan at 10M and the 1.25M shard
             SHARD_N=10000000,1250000 SCANS=mx5, REPS=3 run 900 gpurun_out/scanab.log python3 -u scripts/scan_ab.py
             grep '^\[scan_ab\]' gpurun_out/scanab.log ;;
+        coalesce)  # concurrent batch-1 callers at 10M x 768: B=1 searches vs the request coalescer
+            run 900 gpurun_out/coalesce.log grape-vector-db_amd/build/coalesce_bench 10000000 768 100 10 4 1 8 64
+            grep '^{' gpurun_out/coalesce.log > gpurun_out/coalesce.json; cat gpurun_out/coalesce.json ;;
+        bigr)  # the reference's default depth R = 0.1 N at 1M and 10M rows, batch 8 / 64 / 256
+            run 1100 gpurun_out/bigr.log python3 -u scripts/bigr_timing.py
+            grep '^{' gpurun_out/bigr.log > gpurun_out/bigr.json; cat gpurun_out/bigr.json ;;
         b256)
             run 600 gpurun_out/b256.log python3 -u scripts/b256_timing.py
             grep -v amdgpu.ids gpurun_out/b256.log | tail -4 ;;
@@ -113,6 +122,9 @@ for t in "${TASKS[@]}"; do
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
             BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
             grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;
+        c4x2)  # config 4 (10M x 3072, 8 shards) on the TWO-exchange protocol, vs one 10M x 3072 index
+            run 1100 gpurun_out/c4x2.log python -u scripts/c3_emulate.py --dim 3072 --oracle-queries 0 --steps 10
+            grep '^{' gpurun_out/c4x2.log > gpurun_out/c4x2.json; grep '^\[c3\]' gpurun_out/c4x2.log | tail -4 ;;
         c4)
             run 1100 gpurun_out/c4.log python -u scripts/c4_emulate.py
             grep '^{' gpurun_out/c4.log > gpurun_out/c4.json; tail -3 gpurun_out/c4.log ;;
