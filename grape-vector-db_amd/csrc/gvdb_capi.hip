@@ -287,8 +287,6 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     // commit 8c12da2; DESIGN.md §4 keeps their measurements.)
     const char* scan = getenv("GVDB_SCAN");
     s1.use_mfma = (scan && strcmp(scan, "valu") == 0) ? 0 : 1;
-    const char* dbg = getenv("GVDB_SCAN_DBG");  // ablation timing only (results invalid when set)
-    s1.dbg = dbg ? atoi(dbg) : 0;
     s1.force_rescan = getenv_flag("GVDB_FORCE_RESCAN") ? 1 : 0;  // tests of the device-side fallback
     // GVDB_SAMPLE_DIV: sample ~N/div rows for large batches (timing experiments; default 64)
     static const uint32_t big_div = [] {
@@ -1199,10 +1197,6 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         a.cscore = prune ? (float*)(a.cand + (size_t)kFxQ * cc) : nullptr;
         a.candcap = cc;
         a.overflow = fail;
-        {
-            const char* d = getenv("GVDB_FLAT_DBG");  // ablation timing only (results invalid when set)
-            a.dbg = d ? atoi(d) : 0;
-        }
         HIP_TRY(launch_flat_mx_sample(a, s), "flat sample pass");
         DBG_SYNC(s, "dbg: flat sample pass");
         // tau from exactly re-scored probes (the 16 best sampled rows per query)
@@ -1222,8 +1216,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
             pr.counts = pcount;
             HIP_TRY(launch_rerank(pr, s), "flat probe rerank");
         }
-        const bool dbg_noemit = getenv_flag("GVDB_FLAT_DBG_NOEMIT");  // ablation timing only (results invalid)
-        HIP_TRY(launch_flat_tau(pscores, pcount, dbg_noemit ? 0 : Bg, mk, kind == kScoreCosineDistance, qd,
+        HIP_TRY(launch_flat_tau(pscores, pcount, Bg, mk, kind == kScoreCosineDistance, qd,
                                 ws.thr.as<float>(), s),
                 "flat thresholds");
         DBG_SYNC(s, "dbg: flat thresholds");

@@ -635,10 +635,7 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
     const float* src = smp + (uint64_t)q * S;
     // 8 values per lane per batch, the next batch loaded while this one is
     // merged (the scan is latency-bound otherwise: one block per query)
-#ifndef FX_PROBE_U
-#define FX_PROBE_U 8
-#endif
-    constexpr int kU = FX_PROBE_U;
+    constexpr int kU = 8;  // 16 / 32 measured the same (round 3)
     auto load = [&](uint32_t i0, float (&v)[kU]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -937,28 +934,13 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
 // sub-tile; the mirror is read from HBM exactly once.  Epilogue, candidate rule
 // (U = approx + qa*rho_x + qd >= tau) and the block nomination list are
 // k_flat_mx's; all vector-memory ops of the loop are inline asm with counted vmcnt.
-#ifndef I8Q_PF
-#define I8Q_PF 0  // > 0: waves 2..7 prefetch sub-tile i + I8Q_PF into L2 (A/B knob; the extra line
-                  // requests slowed the DMA stream itself: 1.30 -> 2.02 ms memory-only at 10M x 768)
-#endif
-#ifndef I8Q_BR
-#define I8Q_BR 4  // B-fragment ring depth in k-steps (A/B knob)
-#endif
-#ifndef I8Q_SKEW
-#define I8Q_SKEW 1  // waves 4..7 test step i-1 after step i's barrier (A/B knob)
-#endif
-#ifndef I8Q_PFW
-#define I8Q_PFW 0  // 1: a wave's prefetch op is waited for one step later than its stage (A/B knob)
-#endif
-#ifndef I8Q_ROWPOL
-#define I8Q_ROWPOL ""  // cache-policy suffix of the row DMAs (A/B knob: " nt")
-#endif
-#ifndef I8Q_ABL
-#define I8Q_ABL 0  // timing ablation builds only (results invalid): 1 no epilogue, 2 no MFMA, 4 no row DMA, 8 no step barrier
-#endif
-constexpr int kI8qBr = I8Q_BR;
-constexpr uint32_t kI8qSub = 2;    // 32-row groups per LDS sub-tile
-constexpr uint32_t kI8qBufs = 3;   // LDS sub-tile buffers
+// Round-3/4 A/B results behind these constants: an L2 line
+// prefetch of later sub-tiles slowed the row DMA stream itself (memory-only
+// 1.30 -> 2.02 ms); the skewed epilogue of waves 4..7 saved 4 %; 32-row
+// sub-tiles with 6 buffers (a deeper DMA pipeline) were 7 % slower.
+constexpr int kI8qBr = 4;           // B-fragment ring depth in k-steps
+constexpr uint32_t kI8qSub = 2;     // 32-row groups per LDS sub-tile
+constexpr uint32_t kI8qBufs = 3;    // LDS sub-tile buffers (kI8qBufs - 1 sub-tiles in flight)
 constexpr uint32_t kI8qCl = 1024;  // block nomination list, u32 entries + scores (flushed at a barrier once half full)
 template <int KC>
 __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
@@ -968,16 +950,16 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     constexpr uint32_t kSubBytes = kPieces * 1024u;
     constexpr uint32_t kRows = kI8qSub * 32u;           // rows per sub-tile (one per lane)
     constexpr uint32_t kBufBytes = kSubBytes + 2u * kRows * 4u;  // + the rows' s_x/|x| and rho_x
-    constexpr uint32_t kOps = kPerWave + 1u;            // vector-memory ops per wave per stage
+    constexpr uint32_t kOps = kPerWave + 1u;            // vector-memory ops per stage of a wave with an operand DMA
+    constexpr uint32_t kOpsWaves = kRows == 64 ? 2u : 1u;  // waves that DMA the rows' s_x/|x| and rho_x
     static_assert(kPieces % 8 == 0, "pieces split evenly over the waves");
-    static_assert(kRows == 64, "one operand word per lane");
+    static_assert(kRows == 64 || kRows == 32, "one operand word per lane");
     __shared__ __attribute__((aligned(16))) char Bs[kI8qBufs][kBufBytes];
     // nomination (slot q, block step i, row group gi, row j) as q << 24 | i << 6 | gi << 5 | j
     __shared__ uint32_t cl[kI8qCl];
     __shared__ float cs[kI8qCl];  // their approx scores
     __shared__ uint32_t cl_n;
     __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[kFxQ];
-    __shared__ __attribute__((aligned(16))) uint32_t pf_sink[64];  // the prefetches' landing words (never read)
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t N = a.N, G = gridDim.x;
@@ -991,11 +973,9 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         t = v / kSubPerTile;
         u = v % kSubPerTile;
     };
-    // stage i: the block's i-th sub-tile -> buffer i % 3, as kOps vector-memory ops per
-    // wave: kPerWave 1 KiB row pieces (piece p = (gi*KC + c)*4 + s4: row group
-    // kI8qSub*u + gi of tile t), then one more op -- waves 0 / 1 DMA the 64 rows' s_x/|x|
-    // / rho_x, waves 2..7 prefetch one 128-B line each (384 lines = one whole sub-tile)
-    // of sub-tile i + I8Q_PF into L2 / MALL ahead of its DMA
+    // stage i: the block's i-th sub-tile -> buffer i % kI8qBufs, as kPerWave 1 KiB row
+    // pieces per wave (piece p = (gi*KC + c)*4 + s4: row group kI8qSub*u + gi of tile
+    // t), plus one op of the operand waves: the rows' s_x/|x| and rho_x
     auto stage = [&](uint32_t i) __attribute__((always_inline)) {
         uint32_t t, u;
         sub_of(i, t, u);
@@ -1004,26 +984,17 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         for (uint32_t k = 0; k < kPerWave; ++k) {
             const uint32_t p = wv * kPerWave + k, s4 = p & 3u, c = (p >> 2) % KC, gi = (p >> 2) / KC;
             const char* ga = rowsx + ((((uint64_t)t * KC + c) * 8u + kI8qSub * u + gi) * 4u + s4) * 1024u + lane * 16u;
-            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" I8Q_ROWPOL ::"v"(ga), "s"(l0 + p * 1024u)
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(ga), "s"(l0 + p * 1024u)
                          : "memory");
         }
-        if (wv < 2) {
-            const uint32_t n = min(t * kFxRows + u * kRows + lane, N - 1u);
-            const float* src = (wv == 0 ? a.rscale : a.rrho) + n;
+        if (wv < kOpsWaves) {
+            // 64 rows: wave 0 s_x/|x|, wave 1 rho_x; 32 rows: wave 0, lanes 0-31 / 32-63
+            const uint32_t r = kRows == 64 ? lane : (lane & 31u);
+            const uint32_t n = min(t * kFxRows + u * kRows + r, N - 1u);
+            const bool rho = kRows == 64 ? wv == 1 : lane >= 32u;
+            const float* src = (rho ? a.rrho : a.rscale) + n;
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src),
-                         "s"(l0 + kSubBytes + wv * kRows * 4u)
-                         : "memory");
-        } else if constexpr (I8Q_PF > 0) {
-            uint32_t tp, up;
-            sub_of(i + I8Q_PF, tp, up);
-            const uint32_t L = (wv - 2u) * 64u + lane, p = L >> 3, s4 = p & 3u, c = (p >> 2) % KC,
-                           gi = (p >> 2) / KC;
-            const char* ga = rowsx + ((((uint64_t)tp * KC + c) * 8u + kI8qSub * up + gi) * 4u + s4) * 1024u +
-                             (L & 7u) * 128u;
-            // into a scratch LDS word per lane (no VGPR destination: a register written
-            // when the load returns could already hold another value)
-            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(ga),
-                         "s"((uint32_t)(uintptr_t)pf_sink)
+                         "s"(l0 + kSubBytes + (kRows == 64 ? wv * kRows * 4u : 0u))
                          : "memory");
         }
     };
@@ -1046,10 +1017,9 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     }
     if (tid == 0) cl_n = 0;
     __syncthreads();  // the compiler-visible loads above are complete from here on
-    if (ns) {
-        stage(0);
-        stage(1);
-    }
+    if (ns)
+#pragma unroll
+        for (uint32_t j = 0; j + 1 < kI8qBufs; ++j) stage(j);
     fx_v16i acc[kI8qSub];
     auto row_of = [&](uint32_t e) {  // a list entry's row
         const uint32_t v = blockIdx.x + ((e >> 6) & 0x3ffffu) * G;
@@ -1119,17 +1089,15 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     // Waves 4..7 (the second wave of each SIMD) run step i-1's epilogue right after the
     // barrier of step i, before step i's MFMAs: on every SIMD one wave's candidate test
     // overlaps the other wave's MFMAs instead of both testing while the matrix core idles.
-    const bool late = I8Q_SKEW && wv >= 4;
-    float lrv[kI8qSub] = {0.0f, 0.0f}, lrh[kI8qSub] = {0.0f, 0.0f};  // step i-1's row operands (late waves)
+    const bool late = wv >= 4;
+    float lrv[kI8qSub] = {}, lrh[kI8qSub] = {};  // step i-1's row operands (late waves)
     for (uint32_t i = 0; i < ns; ++i) {
-        // stage i landed (stage i+1's kOps ops are the younger ones), then every wave's part
-        if (wv < 2)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps) : "memory");
-        else if constexpr (I8Q_PF == 0)  // no prefetch op in this wave's stages
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps - 1) : "memory");
-        else  // stage i's prefetch (issued after its row DMAs) may stay in flight one more step
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps + I8Q_PFW) : "memory");
-        if constexpr (!(I8Q_ABL & 8)) __syncthreads();
+        // stage i landed (stages i+1 .. i+kI8qBufs-2 are the younger ops), then every wave's part
+        if (wv < kOpsWaves)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kI8qBufs - 2u) * kOps) : "memory");
+        else  // no operand op in this wave's stages
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kI8qBufs - 2u) * (kOps - 1u)) : "memory");
+        __syncthreads();
         // every wave reads the list count before any wave adds to it again (the late waves'
         // epilogue follows right after this), so the flush decision is block-uniform
         const bool full = cl_n >= kI8qCl / 2;
@@ -1140,12 +1108,12 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             if (tid == 0) cl_n = 0;
             __syncthreads();
         }
-        if constexpr (!(I8Q_ABL & 4)) stage(i + 2);  // into the buffer read in step i-1
+        stage(i + kI8qBufs - 1u);  // into the buffer read in step i-1
         uint32_t t, u;
         sub_of(i, t, u);
         const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
         const float* ops = (const float*)(Bs[i % kI8qBufs] + kSubBytes);
-        if (late && i > 0 && !(I8Q_ABL & 1)) {
+        if (late && i > 0) {
             uint32_t tp, up;
             sub_of(i - 1, tp, up);
             epilogue(i - 1, tp, up, lrv, lrh);
@@ -1173,16 +1141,9 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             __builtin_amdgcn_sched_barrier(0);  // the reads stay BR - 1 k-steps ahead (no sinking)
 #pragma unroll
             for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
-                if constexpr (I8Q_ABL & 2)
-                    acc[gi][s & 15] ^= A[s][0] ^ bf[s % BR][gi][0] ^ bf[s % BR][gi][3];
-                else
-                    acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
+                acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (I8Q_ABL & 1) {
-            if (acc[0][0] == 0x7fffffff && acc[1][5] == 0x7fffffff) cl_n = 0;  // keeps the MFMAs live
-            continue;
         }
         if (!late) {
             float rv[kI8qSub], rh[kI8qSub];
@@ -1200,7 +1161,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             }
         }
     }
-    if (late && ns && !(I8Q_ABL & 1)) {
+    if (late && ns) {
         uint32_t t, u;
         sub_of(ns - 1, t, u);
         epilogue(ns - 1, t, u, lrv, lrh);

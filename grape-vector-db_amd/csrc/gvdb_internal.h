@@ -79,7 +79,6 @@ struct Stage1Args {
     uint32_t* s1_dist;       // [B][R]
     hipEvent_t* ev;          // optional [4]: before hist, before scan, after scan, after select
     int use_mfma;            // large batches: 0 popcount only, 1 FP4 MFMA scan, 2 i8 MFMA scan
-    int dbg;                 // ablation switches for timing studies (GVDB_SCAN_DBG); 0 in production
     int force_rescan;        // tests: every query takes k_select's exact all-rows rescan (GVDB_FORCE_RESCAN)
     // FP4-MFMA paths (stage1_plan): query fragments built once per batch by k_qfrag
     int sample_mode;         // kSampleValu / kSampleMxHist / kSampleDense
@@ -261,7 +260,6 @@ struct FlatMxArgs {
     float* cscore;           // emit pass: [B][candcap] their approx scores (null: not stored)
     uint32_t candcap;
     uint32_t* overflow;      // emit pass: set to 1 if a wave's LDS staging slice overflowed
-    int dbg;                 // unused (kept for ABI stability of the launch struct)
 };
 float flat_eps(uint32_t D);
 hipError_t launch_rows_to_bf16(const float* rows, uint64_t n, uint32_t D, uint16_t* rowsb, uint64_t cap,

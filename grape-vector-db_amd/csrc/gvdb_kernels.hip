@@ -904,30 +904,15 @@ __device__ __forceinline__ void flush_stage_block(const uint64_t (*st_key)[kStag
     }
 }
 
-// geometry of k_scan_mx4
-#ifndef MX3_PF
-#define MX3_PF 4
-#endif
+// geometry of k_scan_mx4: 8 waves per CU (2 per SIMD), 32-row sub-tiles
 constexpr int kMx3Rows = 32;  // candidates per wave sub-tile
-// 8 waves per CU (2 per SIMD), all eight query tiles in one pass (MX3_PASSES
-// below), a 2-deep code-plane ring.
 constexpr int kMx3Threads = 512;
-// MX3_PASSES=1 (default): all 8 query tiles' accumulators live (128 VGPRs), each
-// row fragment expanded once per k-step.  It spilled until the emit pointers were
-// made opaque (hipcc hoisted the per-(tile, row) overflow addresses); now 256
-// VGPRs, no spills, 3-4 % faster per batch than two passes (scripts/gpu_p1.sh).
-#ifndef MX3_PASSES
-#define MX3_PASSES 1
-#endif
-[[maybe_unused]] constexpr int kMx3Passes = MX3_PASSES;
-#ifndef MX3_RING
-#define MX3_RING 2
-#endif
-[[maybe_unused]] constexpr int kMx3Ring = MX3_RING;
+
 
 // ---------------------------------------------------------------------------
-// k_scan_mx5: the stage-1 FP4 scan for D <= 768 (the bench's 10M x 768, B=256).
-// Same contract as k_scan_mx3 (emit (d << 32 | row) for every row with Hamming
+// The FP4 stage-1 operands (k_scan_mx5, the round-2/3 scan, replaced by
+// k_scan_mx6 below; k_sample_dense / k_sample_mx use them too).  mx5 had the
+// same contract as k_scan_mx3 (emit (d << 32 | row) for every row with Hamming
 // d <= thr[q]), three changes measured against it:
 //  * {0,1} x {+-1} operands: a row bit b becomes e2m1 {0, v_c} and a query bit
 //    e2m1 +-1/v_c, so dot = sum over the row's set bits of (q ? +1 : -1)
@@ -946,20 +931,7 @@ constexpr int kMx3Threads = 512;
 //    vector-memory op (the rare overflow emit) only makes that wait stricter.
 // The next k-step's row fragment is expanded between the current k-step's
 // MFMAs, so a wave's own VALU runs under its MFMA pipe time.
-#ifndef MX5_ABL
-#define MX5_ABL 0  // timing ablations (results invalid): 1 no epilogue, 2 no code loads, 4 no LDS A reads, 16 no flush
-#endif
-#ifndef MX5_PRIO
-#define MX5_PRIO 0
-#endif
-#ifndef MX5_PF
-#define MX5_PF 8
-#endif
-constexpr int kMx5Threads = 512;
-#ifndef MX5_RING
-#define MX5_RING 2
-#endif
-constexpr int kMx5Ring = MX5_RING;
+constexpr int kMx5Threads = 512;  // 8 waves per CU (2 per SIMD): the FP4 stage-1 kernels
 __device__ __forceinline__ v4i_t fp4_row01(uint32_t w) {
     v4i_t r;
     r.x = (int)(w & 0x11111111u);         // 0.5
@@ -1011,219 +983,6 @@ __global__ __launch_bounds__(256) void k_qfrag(const uint32_t* __restrict__ qwor
     }
 }
 
-template <int W4>
-__global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
-                                                           const v4i_t* __restrict__ qfrag_g,
-                                                           const uint32_t* __restrict__ qpc,
-                                                           const uint32_t* __restrict__ thr, uint32_t B,
-                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
-                                                           uint32_t bufcap) {
-    constexpr int KW = 4 * W4;  // 32-bit code words per row
-    constexpr int KS = KW / 2;  // k-steps of 64 bits
-    constexpr int QT = 8;       // query tiles of 32
-    constexpr uint32_t kWaveStage = 512;
-    constexpr int NW = kMx5Threads / 64;
-    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
-    // accumulator seed per (tile, lane half, row r): thr - |q|, so acc = thr - Hamming
-    __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
-    __shared__ float thrc_lds[QT * 32];
-    __shared__ uint64_t st_key[NW][kWaveStage];
-    __shared__ uint8_t st_q[NW][kWaveStage];
-    __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t h = lane >> 5;
-#if MX5_PRIO == 1
-    // static priority for the second wave of each SIMD (waves 4-7): the pair
-    // then drifts out of phase, so one wave's epilogue runs under the other's MFMAs
-    if (wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
-#elif MX5_PRIO == 2
-    if (wv < NW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-    // query fragments (k_qfrag): k-step-major (s, qt, lane), so MFMA m = s*QT + qt
-    // reads fragment m and the A reads of the loop need one base register per
-    // 64 KiB (tile-major needed one per read above 64 KiB: ~20 VGPRs of addresses)
-#pragma unroll 4
-    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx5Threads) qfrag[i] = qfrag_g[i];
-    // thr is clamped to the padded width (every Hamming distance is <= it, so
-    // the hit set is unchanged) to keep thr - |q| exact in f32
-    constexpr uint32_t kPadBits = 32u * KW;
-    if (tid < QT * 32) {
-        const uint32_t q = tid;
-        const uint32_t pc = qpc[q];
-        const float tc = q < B ? (float)min(thr[q], kPadBits) : 0.0f;
-        thrc_lds[q] = tc;
-        // query q sits in tile q/32, lane half ((q&31)>>2)&1, row r = (q&3) + 4*((q&31)>>3)
-        const uint32_t qt = q >> 5, j = q & 31u, hh = (j >> 2) & 1u, r = (j & 3u) + 4u * (j >> 3);
-        seed_lds[(qt * 2 + hh) * 16 + r] = q < B ? tc - (float)pc : -1.0e9f;
-        qcnt[q] = 0u;
-    }
-    __syncthreads();
-    const uint32_t nqt = (B + 31u) / 32u;
-    const uint32_t nsub = (N + 31u) / 32u;
-    const uint32_t W = gridDim.x * NW;  // waves in the grid
-    // ring slot: this lane's half of the W4 planes of one 32-row sub-tile
-    uint2 ring[kMx5Ring][W4];
-    auto load = [&](uint32_t sb, uint2 (&c)[W4]) __attribute__((always_inline)) {
-        const uint32_t n = min(sb * 32u + (lane & 31u), N - 1u);  // clamped: branch-free ring
-        const uint32_t voff = n * 16u + h * 8u;
-#pragma unroll
-        for (int p = 0; p < W4; ++p) {
-            const uint4* base = codes + (uint64_t)p * cap;
-            if constexpr (MX5_ABL & 2)  // timing ablation: no code loads
-                c[p] = make_uint2(voff * 2654435761u + p, voff ^ (0x9e3779b9u * p));
-            else
-                asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(c[p]) : "v"(voff), "s"(base));
-        }
-    };
-    auto wait_slot = [&](uint2 (&c)[W4]) __attribute__((always_inline)) {
-        // the slot's W4 loads are the oldest of kMx5Ring in-flight sets
-#pragma unroll
-        for (int p = 0; p < W4; ++p)
-            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(c[p]) : "n"((kMx5Ring - 1) * W4));
-    };
-    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
-    v16f_t acc[QT];
-    const int scale1 = 0x7f7f7f7f;
-    // accumulator seeds of tile qt (LDS broadcast: all 32 lanes of a half read the same
-    // 64 B); issued right after tile qt's epilogue, so the next sub-tile's seeds are in
-    // flight during the remaining tiles' epilogues
-    auto seed = [&](int qt) __attribute__((always_inline)) {
-        if constexpr (MX5_ABL & 8) return;
-        const float4* sp = (const float4*)(seed_lds + (qt * 2 + h) * 16);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float4 v = sp[g];
-            acc[qt][4 * g + 0] = v.x;
-            acc[qt][4 * g + 1] = v.y;
-            acc[qt][4 * g + 2] = v.z;
-            acc[qt][4 * g + 3] = v.w;
-        }
-    };
-    auto process = [&](uint32_t sb, uint2 (&c)[W4], bool reload, uint32_t sb_next) __attribute__((always_inline)) {
-        const uint32_t n = sb * 32u + (lane & 31u);
-        uint32_t* cnt = counts;
-        uint64_t* bf = buf;
-        uint32_t bcap = bufcap;
-        asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
-        wait_slot(c);
-        const v4i_t* qf = qfrag + lane;
-        constexpr int PF = MX5_PF;  // A-fragment LDS ring depth (in MFMAs)
-        v4i_t ar[PF];
-#pragma unroll
-        for (int m = 0; m < PF; ++m) ar[m] = qf[m * 64];
-        v4i_t bcur = fp4_row01(c[0].x);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            __builtin_amdgcn_sched_barrier(0);
-            v4i_t bnext = bcur;
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-                const int m = s * QT + qt;
-                const v4i_t a = ar[m % PF];
-                if (!(MX5_ABL & 4) || s == 0)  // ablation 4: A fragments of k-step 0 only
-                    if (m + PF < KS * QT) ar[m % PF] = qf[(m + PF) * 64];
-                if (s == 0 && (MX5_ABL & 8))  // ablation 8: no seeds (no hits below)
-                    mfma_fp4_first_nop(acc[qt], a, bcur, scale1);
-                else if (s == 0 && qt == 0)
-                    mfma_fp4_acc_nop(acc[qt], a, bcur, scale1);
-                else
-                    mfma_fp4_acc(acc[qt], a, bcur, scale1);
-                if (qt == 1 && s + 1 < KS) {  // next k-step's row fragment under this one's MFMAs
-                    const uint2 v = c[(s + 1) >> 1];
-                    bnext = fp4_row01(((s + 1) & 1) ? v.y : v.x);
-                }
-            }
-            bcur = bnext;
-        }
-        mfma_fp4_drain_acc(acc);
-        if (reload) load(sb_next, c);  // the slot is free once the MFMAs have read it
-        // threshold epilogue: acc = thr - Hamming, a hit is acc >= 0; one max over
-        // the lane's 16 queries rejects a tile with no hit
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            if (qt < (int)nqt) do {  // (a `continue` below leaves this do-while)
-            const v16f_t& A = acc[qt];
-            if constexpr (MX5_ABL & 1) {  // ablation: results consumed, nothing emitted
-                float t = A[0];
-#pragma unroll
-                for (int r = 1; r < 16; ++r) t += A[r];
-                if (t == 12345.678f) wcnt += 1;
-                continue;
-            }
-            // any acc >= 0 <=> some sign bit clear <=> the AND of the 16 words is
-            // non-negative as an int (acc is never -0.0: the seed thr - |q| is +0 when
-            // zero and an exact zero sum of nonzero terms rounds to +0); v_and3_b32, no
-            // canonicalising max
-            // four partial ANDs (same 15 v_and as one chain): a tile with a hit
-            // then tests its 16 accumulators only in the groups of 4 that hold one
-            int pa[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                pa[g] = __float_as_int(A[4 * g]) & __float_as_int(A[4 * g + 1]) & __float_as_int(A[4 * g + 2]) &
-                        __float_as_int(A[4 * g + 3]);
-            const int aand = (pa[0] & pa[1]) & (pa[2] & pa[3]);
-            if (!__ballot(((MX5_ABL & 8) ? false : aand >= 0) && n < N)) continue;
-            uint32_t rb = qt * 32u + 4u * h;
-            asm volatile("" : "+v"(rb));  // keeps the 128 per-(tile, r) query indices from being hoisted
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                if ((r & 3) == 0 && !__ballot(pa[r >> 2] >= 0 && n < N)) {
-                    r += 3;  // no hit in this group of 4
-                    continue;
-                }
-                const bool hit = A[r] >= 0.0f && n < N;
-                const uint64_t m = __ballot(hit);
-                if (m) {
-                    if (hit) {
-                        const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
-                            (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
-                        const uint32_t d = (uint32_t)(int)(thrc_lds[qi] - A[r]);
-                        const uint64_t key = ((uint64_t)d << 32) | n;
-                        if (sp < kWaveStage) {
-                            st_key[wv][sp] = key;
-                            st_q[wv][sp] = (uint8_t)qi;
-                        } else {
-                            const uint32_t pos = atomicAdd(&cnt[qi], 1u);
-                            if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = key;
-                        }
-                    }
-                    wcnt += (uint32_t)__popcll(m);
-                }
-            }
-            } while (0);
-            seed(qt);  // the next sub-tile's seeds
-        }
-    };
-    // static ring: trip t processes slots 0,1,2 (sub-tiles sb, sb+W, sb+2W) and
-    // refills each with the sub-tile three strides ahead
-    uint32_t sb = blockIdx.x * NW + wv;
-    constexpr uint32_t RW = kMx5Ring;
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) seed(qt);  // the first sub-tile's
-    load(sb, ring[0]);
-    load(sb + W, ring[1]);
-    if constexpr (kMx5Ring == 3) load(sb + 2 * W, ring[kMx5Ring - 1]);
-    for (; sb < nsub; sb += RW * W) {  // explicit slots: the ring stays in fixed registers
-        process(sb, ring[0], true, sb + RW * W);
-        if (sb + W >= nsub) break;
-        process(sb + W, ring[1], true, sb + W + RW * W);
-        if constexpr (kMx5Ring == 3) {
-            if (sb + 2 * W >= nsub) break;
-            process(sb + 2 * W, ring[kMx5Ring - 1], true, sb + 2 * W + RW * W);
-        }
-    }
-    // drain the clamped prefetches before the LDS stage is flushed
-#pragma unroll
-    for (int k = 0; k < kMx5Ring; ++k)
-#pragma unroll
-        for (int p = 0; p < W4; ++p) asm volatile("s_waitcnt vmcnt(0)" : "+v"(ring[k][p]));
-    if constexpr (MX5_ABL & 16) return;  // timing ablation: no flush (results invalid)
-    flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase, counts,
-                                      buf, bufcap);
-}
-
 // ---------------------------------------------------------------------------
 // k_scan_mx6: k_scan_mx5 with the sub-tile boundary software-pipelined.
 // mx5 drains every accumulator after a sub-tile's last k-step, then runs the
@@ -1243,27 +1002,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_scan_mx5(const uint4* __rest
 // last partial round (nsub mod waves sub-tiles) is split into (sub-tile,
 // query tile) units of KS MFMAs spread over all waves.
 // Same emit contract as mx5: (d << 32 | row) for every row with d <= thr[q].
-#ifndef MX6_WAVES
-#define MX6_WAVES 8  // waves per CU: 8 = 2 per SIMD, accumulators in VGPRs; 4 = 1 per SIMD, in AGPRs
-#endif
-constexpr int kMx6Threads = MX6_WAVES * 64;
-#if MX6_WAVES == 4
-#define MX6_ACC "a"
-#else
-#define MX6_ACC "v"
-#endif
-__device__ __forceinline__ void mfma_fp4_agpr(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
-    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
-                 : "+" MX6_ACC(d)
-                 : "v"(a), "v"(b), "v"(scale));
-}
-// after a VALU / LDS write of an operand (B fragment just expanded, accumulator
-// just seeded): 4 wait states inside the string
-__device__ __forceinline__ void mfma_fp4_agpr_nop(v16f_t& d, const v4i_t& a, const v4i_t& b, int scale) {
-    asm volatile("s_nop 3\n\tv_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0] cbsz:4 blgp:4"
-                 : "+" MX6_ACC(d)
-                 : "v"(a), "v"(b), "v"(scale));
-}
+constexpr int kMx6Threads = 512;  // 8 waves per CU, 2 per SIMD
 template <int W4>
 __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const v4i_t* __restrict__ qfrag_g,
@@ -1277,7 +1016,7 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
     constexpr int NM = KS * QT;  // MFMAs per sub-tile
     constexpr uint32_t kWaveStage = 256;  // ~90 emits per wave at 10M x 768 x 256 (overflow: global atomics)
     constexpr int NW = kMx6Threads / 64;
-    constexpr int PF = MX6_WAVES == 4 ? 8 : 4;  // A-fragment ring depth (in MFMAs)
+    constexpr int PF = 4;  // A-fragment ring depth (in MFMAs): live through the tests, so short
     static_assert(NM % PF == 0, "the A ring's slot of MFMA m must not depend on the sub-tile");
     __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
     __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
@@ -1435,13 +1174,13 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
             {                                                                  \
                 __builtin_amdgcn_sched_barrier(0);                             \
                 if (prev) {                                                    \
-                    asm volatile("s_nop 4" : "+" MX6_ACC(acc[qt]));                   \
+                    asm volatile("s_nop 4" : "+v"(acc[qt]));                   \
                     test(acc[qt], (uint32_t)(qt), np);                         \
                     seed_into(acc[qt], (uint32_t)(qt));                        \
                 }                                                              \
                 const v4i_t a = ar[(qt) % PF];                                 \
                 ar[(qt) % PF] = afrag(((qt) + PF) % NM);                        \
-                mfma_fp4_agpr_nop(acc[qt], a, bcur, scale1);                   \
+                mfma_fp4_acc_nop(acc[qt], a, bcur, scale1);                   \
                 if ((qt) == 1) {                                               \
                     const uint2 v = c[0];                                      \
                     bnext = fp4_row01(v.y);                                    \
@@ -1466,7 +1205,7 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
                     const int m = s * QT + qt;
                     const v4i_t a = ar[m % PF];
                     ar[m % PF] = afrag((m + PF) % NM);  // the ring runs on into the next sub-tile
-                    mfma_fp4_agpr(acc[qt], a, bcur, scale1);
+                    mfma_fp4_acc(acc[qt], a, bcur, scale1);
                     if (qt == 1 && s + 1 < KS) {  // next k-step's row fragment under this one's MFMAs
                         const uint2 v = c[(s + 1) >> 1];
                         bnext = fp4_row01(((s + 1) & 1) ? v.y : v.x);
@@ -1487,7 +1226,7 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
         const uint32_t nl = (gw + (nround - 1u) * W) * 32u + (lane & 31u);
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
-            asm volatile("" : "+" MX6_ACC(acc[qt]));
+            asm volatile("" : "+v"(acc[qt]));
             test(acc[qt], (uint32_t)qt, nl);
         }
         // the refills past the end (clamped rows) must land before the registers are reused
@@ -1514,9 +1253,9 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
             const uint2 v = c[s >> 1];
             const v4i_t b = fp4_row01((s & 1) ? v.y : v.x);
             const v4i_t a = qa[s * QT * 64];
-            mfma_fp4_agpr_nop(A, a, b, scale1);
+            mfma_fp4_acc_nop(A, a, b, scale1);
         }
-        asm volatile("s_nop 15\n\ts_nop 15" : "+" MX6_ACC(A));
+        asm volatile("s_nop 15\n\ts_nop 15" : "+v"(A));
         test(A, qt, n);
     }
     flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase, counts,
@@ -1594,29 +1333,14 @@ static void launch_qfrag_t(const Stage1Args& a, hipStream_t s) {
                        (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero);
 }
 
-// GVDB_SCAN=mx5: the previous (non-pipelined) scan, for same-box A/B timing
-static bool scan_mx5_selected() {
-    const char* e = getenv("GVDB_SCAN");
-    return e && strcmp(e, "mx5") == 0;
-}
-
 template <int W4>
-static void launch_scan_mx5_t(const Stage1Args& a, hipStream_t s) {
-    const uint32_t nsub = (a.N + 31u) / 32u;
-    const uint32_t wpb = kMx5Threads / 64;
-    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(cu_count(), (nsub + wpb - 1) / wpb));
+static void launch_scan_mx6_t(const Stage1Args& a, hipStream_t s) {
     constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
-    const bool mx5 = scan_mx5_selected();
     for (uint32_t g = 0; g < a.B; g += 256) {
         const uint32_t bg = min(256u, a.B - g);
-        if (mx5)
-            hipLaunchKernelGGL((k_scan_mx5<W4>), dim3(grid), dim3(kMx5Threads), 0, s, a.codes, a.cap, a.N,
-                               (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                               a.buf + (uint64_t)g * a.bufcap, a.bufcap);
-        else
-            hipLaunchKernelGGL((k_scan_mx6<W4>), dim3(cu_count()), dim3(kMx6Threads), 0, s, a.codes, a.cap, a.N,
-                               (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                               a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+        hipLaunchKernelGGL((k_scan_mx6<W4>), dim3(cu_count()), dim3(kMx6Threads), 0, s, a.codes, a.cap, a.N,
+                           (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
+                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
 }
 
@@ -1684,7 +1408,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
     v16f_t acc[QT];
     auto chunk = [&](int c) __attribute__((always_inline)) {
         const v4i_t* qf = qfrag + lane;
-        constexpr int PF = MX3_PF;
+        constexpr int PF = 4;  // A-fragment LDS ring depth
         constexpr int M = KC * QT;  // MFMAs of this chunk: m = s*QT + qt
         v4i_t ar[PF];
         auto aidx = [&](int m) { return ((m % QT) * KS + c * KC + m / QT) * 64; };
@@ -2365,10 +2089,10 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
         }
     } else if (mfma) {  // FP4 block-scaled MFMA, {0,1} x {+-1} operands (default for large batches)
         switch (W4) {
-            case 2: launch_scan_mx5_t<2>(a, s); break;
-            case 3: launch_scan_mx5_t<3>(a, s); break;
-            case 4: launch_scan_mx5_t<4>(a, s); break;
-            default: launch_scan_mx5_t<6>(a, s); break;
+            case 2: launch_scan_mx6_t<2>(a, s); break;
+            case 3: launch_scan_mx6_t<3>(a, s); break;
+            case 4: launch_scan_mx6_t<4>(a, s); break;
+            default: launch_scan_mx6_t<6>(a, s); break;
         }
     } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \

@@ -10,7 +10,7 @@
 #   b256         scripts/b256_timing.py at 10M (SHARD_N / RCCL env pass through)
 #   coalesce     build/coalesce_bench: concurrent batch-1 callers, B=1 searches vs the coalescer -> gpurun_out/coalesce.json
 #   bigr         scripts/bigr_timing.py: R = 0.1 N at 1M / 10M rows -> gpurun_out/bigr.json
-#   scanab       scripts/scan_ab.py: k_scan_mx5 vs the default scan, 10M and 1.25M rows -> gpurun_out/scanab.log
+#   scanab       scripts/scan_ab.py: stage-1 scan timing at 10M and 1.25M rows (SCANS: GVDB_SCAN values) -> gpurun_out/scanab.log
 #   c3           scripts/c3_emulate.py (config 3, 8 shards on one GPU)  -> gpurun_out/c3.json / .log
 #   c3prof       c3_emulate (no single index, no oracle) under rocprofv3 -> gpurun_out/prof_c3/
 #   c4           scripts/c4_emulate.py (config 4, 8 shards of 1.25M x 3072; one-exchange merge)
@@ -60,8 +60,8 @@ for t in "${TASKS[@]}"; do
         benchprof)
             run 900 gpurun_out/benchprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py
             grep '^{' gpurun_out/benchprof.log > gpurun_out/benchprof.json || true ;;
-        scanab)  # same-box A/B: k_scan_mx5 vs the default scan at 10M and the 1.25M shard
-            SHARD_N=10000000,1250000 SCANS=mx5, REPS=3 run 900 gpurun_out/scanab.log python3 -u scripts/scan_ab.py
+        scanab)  # stage-1 scan timing at 10M and the 1.25M shard (same box, alternating SCANS)
+            SHARD_N=10000000,1250000 SCANS="${SCANS:-,}" REPS=3 run 900 gpurun_out/scanab.log python3 -u scripts/scan_ab.py
             grep '^\[scan_ab\]' gpurun_out/scanab.log ;;
         coalesce)  # concurrent batch-1 callers at 10M x 768: B=1 searches vs the request coalescer
             run 900 gpurun_out/coalesce.log grape-vector-db_amd/build/coalesce_bench 10000000 768 100 10 4 1 8 64
@@ -93,12 +93,6 @@ for t in "${TASKS[@]}"; do
                     noprune) GVDB_FLAT_PRUNE=0 BS=256 FLAT_REPS=10 run 600 gpurun_out/flatab_$v.log python3 scripts/flat_timing.py ;;
                 esac
                 echo "== $v"; grep -E "B=|emit" gpurun_out/flatab_$v.log | tail -2
-            done ;;
-        flatabl)  # k_flat_i8q ablations (abl/libgvdb_ablN.so, -DI8Q_ABL=N: 1 no epilogue, 2 no MFMA, 4 no row DMA; results invalid)
-            for v in 0 1 3 5; do
-                lib=""; [ $v != 0 ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_abl$v.so
-                GVDB_FLAT=i8 GVDB_LIB_PATH=$lib BS=256 FLAT_REPS=5 run 600 gpurun_out/flatabl_$v.log python3 scripts/flat_timing.py
-                echo "== abl $v"; grep -E "emit" gpurun_out/flatabl_$v.log | tail -1
             done ;;
         flatevery)  # exact flat sample-pass stride A/B (GVDB_FLAT_EVERY; default 64 tiles)
             for v in 64 128; do
