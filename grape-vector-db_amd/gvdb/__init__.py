@@ -557,7 +557,6 @@ class GpuVectorIndex:
                                HnswConfig(int(m.m), int(m.ef_construction), int(m.ef_search), int(m.max_layers)))
 
 
-@dataclass
 class RequestCoalescer:
     """Concurrent batch-1 searches over one index (gvdb_coalescer_*): callers on
     any number of threads each ask for ONE query's top-k, as the reference's
@@ -603,6 +602,7 @@ class RequestCoalescer:
         self.close()
 
 
+@dataclass
 class HnswConfig:
     """config.rs:196-209 (defaults config.rs:413-422)."""
     m: int = 16
