@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--b1-queries", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ref-faithful", dest="ref_faithful", action="store_false",
+                    help="skip the ref-faithful id-remap side number of the CPU baseline")
     ap.add_argument("--hnsw-rows", type=int, default=100_000,
                     help="corpus prefix for the CPU-HNSW leg and its matched-N GPU points (0 = skip)")
     ap.add_argument("--no-points", dest="points", action="store_false", help="skip the QPS/recall operating points")
@@ -356,15 +358,14 @@ def main():
     if mfma:
         bpad = ((B + 31) // 32) * 32
         ops = float(n_local) * bpad * words * 32 * 2  # MACs x 2: one +/-1 product per code bit
-        if variant == "i8":
-            peak, kname = PEAK_I8_TOPS, "k_scan_mfma (+/-1 i8 dot, v_mfma_i32_32x32x32_i8)"
-        elif wide:
+        if wide:
             peak, kname = PEAK_FP4_TFLOPS, (f"k_scan_mx4 (+/-1 e2m1 dot, v_mfma_scale_f32_32x32x64_f8f6f4, rows in "
                                             f"VGPRs, {32 * MX4_QT[w4]} queries per launch, {scan_launches} launches "
                                             f"per batch; achieved over the batch's launches)")
         else:
-            peak, kname = PEAK_FP4_TFLOPS, ("k_scan_mx5 ({0,1} x {+-1} e2m1 dot seeded with thr - |q|, "
-                                            "v_mfma_scale_f32_32x32x64_f8f6f4, rows in VGPRs)")
+            peak, kname = PEAK_FP4_TFLOPS, ("k_scan_mx6 ({0,1} x {+-1} e2m1 dot seeded with thr - |q|, "
+                                            "v_mfma_scale_f32_32x32x64_f8f6f4, rows in VGPRs, sub-tile "
+                                            "boundary pipelined into the next sub-tile's first k-step)")
         roof = {
             "kernel": "stage-1 BQ Hamming filter: " + kname,
             "bound": "mfma",
@@ -384,7 +385,7 @@ def main():
         }
     roof.update({
         "frac": roof["achieved"] / peak,
-        "traffic": pmc_traffic("gvdb::k_scan_mx5<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
+        "traffic": pmc_traffic("gvdb::k_scan_mx6<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
         "hbm_bytes_per_launch": n_local * w4 * 16 * scan_launches,
@@ -427,6 +428,20 @@ def main():
                       f"one query per thread",
             "single_thread_s_per_query": t_one,
         }
+        # ref-faithful side number: HnswVectorIndex::search's O(N k) id remap
+        # alone (index.rs:219-228), one query per thread -- an upper bound on the reference's
+        # own search QPS at this N, before any graph traversal
+        if args.ref_faithful:
+            t1 = time.perf_counter()
+            remap_s = oracle.ref_id_remap_seconds(N, k, threads, threads)
+            cpu["ref_faithful"] = {
+                "hnsw_search_id_remap_s_per_query": remap_s,
+                "qps_upper_bound": threads / remap_s if remap_s > 0 else None,
+                "cores": threads,
+                "sample": f"{threads} queries x {k} hits, id_to_index of {N} entries (index.rs:219-228 restated: "
+                          f"a heap-allocated format!(\"vec_{{}}\") per entry until the hit's value matches)",
+                "wall_s_incl_map_build": time.perf_counter() - t1,
+            }
         # full-scale parity on the CPU sample: GPU top-k == oracle top-k (ids + bit-exact cosine)
         gpu_sc = out_sc.cpu().numpy()
         ok_ids = bool((oi[:, :k] == found[:nq].astype(np.uint64)).all())
@@ -436,7 +451,9 @@ def main():
 
     # ---------------- CPU-HNSW leg at matched N: HnswVectorIndex's graph search
     # (instant-distance 0.6.1 restated, oracle/hnsw_oracle.cpp) on the first
-    # --hnsw-rows rows of the same corpus (a 10M-row build takes days), and the
+    # --hnsw-rows rows of the same corpus (the full 10M-row CPU build took 2.5 h on
+    # 8 threads -- profiles/r03/equal_recall_10000000x768.json -- so the in-run leg
+    # is bounded to fit the driver's time budget), and the
     # GPU on THE SAME rows: a BQ rescore sweep and the exact flat search, all
     # scored against the exact top-10 of that prefix.  gpu_vs_cpu_hnsw pairs
     # every ef_search point with the fastest GPU point of recall >= its recall - 0.02.
@@ -553,7 +570,7 @@ def main():
         dist.destroy_process_group()
 
 
-PMC_FILE = "profiles/r03/pmc_bench_10M.json"
+PMC_FILE = "profiles/r04/pmc_bench_10M.json"
 PMC_FLAT_FILE = "profiles/r03/pmc_flat_i8q_10M.json"  # scripts/gpu.sh pmc:flat:k_flat_i8q (10M x 768, B = 256)
 
 

@@ -38,6 +38,7 @@ _SIG = {
     "orc_storage_vector_search": (None, [P, u64, P, u64, u64, u64, C.c_int, f32, P, P, P]),
     "orc_flat_cosine_distance_search": (None, [P, u64, P, u64, u64, u64, P, P, P]),
     "orc_exact_topk_cosine_batch": (None, [P, P, u64, u64, u64, u64, P, P, C.c_int]),
+    "orc_ref_id_remap_seconds": (C.c_double, [u64, u64, u64, C.c_int]),
     "orc_flat_cosine_distance_batch": (None, [P, P, u64, u64, u64, u64, P, P, P, C.c_int]),
     "orc_shard_merge": (None, [P, P, P, u64, u64, u64, P, P, P]),
     "orc_row_norms": (None, [P, u64, u64, P]),
@@ -228,6 +229,13 @@ def flat_cosine_distance_batch(q, rows, k, threads=0):
     on = np.zeros(B, np.uint64)
     lib().orc_flat_cosine_distance_batch(_p(q), _p(rows), N, D, B, k, _p(oi), _p(os_), _p(on), threads)
     return oi[:, :k], os_[:, :k], on
+
+
+def ref_id_remap_seconds(N, k, nq, threads=0):
+    """Mean seconds per query of HnswVectorIndex::search's O(N k) id remap
+    (index.rs:219-228) restated with its string formatting (the ref-faithful
+    variant's extra cost)."""
+    return float(lib().orc_ref_id_remap_seconds(N, k, nq, threads))
 
 
 def shard_merge(ids, scores, counts, limit):

@@ -33,6 +33,9 @@
 #include <limits>
 #include <numeric>
 #include <vector>
+#include <unordered_map>
+#include <string>
+#include <chrono>
 
 #ifdef _OPENMP
 #include <omp.h>
@@ -398,6 +401,54 @@ void orc_flat_cosine_distance_batch(const float* q, const float* rows, uint64_t 
 #endif
     for (int64_t b = 0; b < (int64_t)B; ++b)
         orc_flat_cosine_distance_search(q + b * D, D, rows, N, D, k, out_idx + b * k, out_score + b * k, out_n + b);
+}
+
+// The "ref-faithful" cost of HnswVectorIndex::search's id remap (index.rs:219-228,
+// BASELINE.md §2): for each of the k hits, the reference walks id_to_index
+// (HashMap<String, usize>) and format!s "vec_{index}" for every entry until it
+// equals the hit's value -- O(N k) string formatting per query.  Restated with a
+// heap-allocated string per format! (a Rust String always allocates); the map holds
+// N ids "doc_{i}" -> i, hits are k rows drawn per query.  Returns the mean wall
+// seconds of the remap per query (nq queries, one per thread).
+double orc_ref_id_remap_seconds(uint64_t N, uint64_t k, uint64_t nq, int threads) {
+    std::unordered_map<std::string, uint64_t> id_to_index;
+    id_to_index.reserve(N);
+    for (uint64_t i = 0; i < N; ++i) id_to_index.emplace("doc_" + std::to_string(i), i);
+    std::vector<double> secs(nq, 0.0);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int64_t qi = 0; qi < (int64_t)nq; ++qi) {
+        uint64_t st = 0x6772617065ull + (uint64_t)qi * 0x9e3779b97f4a7c15ull;
+        std::vector<std::string> hits;
+        for (uint64_t j = 0; j < k; ++j) {
+            st = st * 6364136223846793005ull + 1442695040888963407ull;
+            hits.push_back("vec_" + std::to_string((st >> 17) % N));
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::string> found;
+        for (const std::string& value : hits) {
+            for (const auto& e : id_to_index) {
+                std::string f;
+                f.reserve(32);  // past the SSO buffer: one heap allocation, as format! makes
+                f += "vec_";
+                f += std::to_string(e.second);
+                if (f == value) {
+                    found.push_back(e.first);
+                    break;
+                }
+            }
+        }
+        secs[qi] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (found.size() != k) secs[qi] = -1.0;
+    }
+    double sum = 0.0;
+    for (double v : secs) {
+        if (v < 0) return -1.0;
+        sum += v;
+    }
+    return nq ? sum / (double)nq : 0.0;
 }
 
 // ShardManager::search_vectors merge (distributed/shard.rs:776-784): concat
