@@ -571,7 +571,7 @@ def main():
 
 
 PMC_FILE = "profiles/r04/pmc_bench_10M.json"
-PMC_FLAT_FILE = "profiles/r03/pmc_flat_i8q_10M.json"  # scripts/gpu.sh pmc:flat:k_flat_i8q (10M x 768, B = 256)
+PMC_FLAT_FILE = PMC_FILE  # the same passes cover k_flat_i8q (bench.py operating points, 10M x 768, B = 256)
 
 
 def pmc_traffic(kernel_prefix, n_local, D, pmc_file=None):
