@@ -42,23 +42,6 @@ __device__ __forceinline__ uint32_t big_dist(const uint4* __restrict__ codes, ui
     return d;
 }
 
-// Block-wide exclusive prefix of a flag in thread order; *total = block count.
-__device__ __forceinline__ uint32_t big_prefix(bool f, uint32_t* wcnt, uint32_t* total) {
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const uint64_t m = __ballot(f);
-    if (lane == 0) wcnt[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), tot = 0;
-    for (uint32_t i = 0; i < nw; ++i) {
-        const uint32_t c = wcnt[i];
-        if (i < w) pre += c;
-        tot += c;
-    }
-    __syncthreads();
-    *total = tot;
-    return pre;
-}
-
 // Wave-aggregated append of (row, d) to the query's member list.
 __device__ __forceinline__ void big_append(bool keep, uint32_t row, uint32_t d, uint32_t* s_n, uint32_t* rows,
                                            uint32_t* dist, uint32_t R) {
@@ -186,89 +169,87 @@ hipError_t launch_select_big(const Stage1Args& a, hipStream_t s) {
 constexpr uint32_t kTopkBigMax = 1024;  // k
 constexpr uint32_t kTieLds = 4096;      // tied entries sorted in LDS (more: radix select)
 
-__global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restrict__ scores,
-                                                          const uint32_t* __restrict__ s1_rows,
-                                                          const uint32_t* __restrict__ s1_dist, uint32_t R,
-                                                          uint32_t kout, int descending,
-                                                          const uint64_t* __restrict__ ids, uint64_t row_offset,
-                                                          uint64_t* __restrict__ out_ids,
-                                                          float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
-                                                          uint32_t* __restrict__ nan_flag) {
-    __shared__ uint32_t bins[256];
-    __shared__ uint64_t tk[kTieLds];          // ties: (d << 32 | row)
-    __shared__ uint32_t sel[kTopkBigMax];     // selected entry indices
-    __shared__ uint32_t srt[kTopkBigMax];     // sorted order
-    __shared__ uint32_t su[kTopkBigMax];      // selected: ukey
-    __shared__ uint64_t sdr[kTopkBigMax];     // selected: (d << 32 | row)
-    __shared__ uint32_t s_nan, s_cut, s_below, s_nsel, s_ntie;
-    __shared__ uint64_t s_tcut;
-    const uint32_t q = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-    const float* sc = scores + (uint64_t)q * R;
-    const uint32_t* rw = s1_rows + (uint64_t)q * R;
-    const uint32_t* dd = s1_dist + (uint64_t)q * R;
-    const uint32_t k = min(kout, R);
+struct TopkLds {
+    uint32_t bins[256];
+    uint64_t tk[kTieLds];       // ties: (d << 32 | row)
+    uint32_t sel[kTopkBigMax];  // selected entry indices
+    uint32_t srt[kTopkBigMax];  // sorted order
+    uint32_t su[kTopkBigMax];   // selected: ukey
+    uint64_t sdr[kTopkBigMax];  // selected: (d << 32 | row)
+    uint32_t s_nan, s_cut, s_below, s_nsel, s_ntie;
+    uint64_t s_tcut;
+};
+
+// The first k = min(kout, n) entries of the unordered list (sc, rw, dd)[0..n)
+// by (score order, Hamming, row) -- the stable score sort of the (Hamming,
+// row)-ordered stage-1 list -- as entry indices into L.srt[0..k), ascending;
+// L.s_nan = a NaN score among the n.  Whole block; returns k.
+__device__ uint32_t big_topk_order(TopkLds& L, const float* __restrict__ sc, const uint32_t* __restrict__ rw,
+                                   const uint32_t* __restrict__ dd, uint32_t n, uint32_t kout, int descending) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t k = min(kout, n);
     auto ukey = [&](uint32_t i) {
         const uint32_t o = f32_order(sc[i]);
         return descending ? ~o : o;  // ascending = better first
     };
     if (tid == 0) {
-        s_nan = 0u;
-        s_nsel = 0u;
-        s_ntie = 0u;
+        L.s_nan = 0u;
+        L.s_nsel = 0u;
+        L.s_ntie = 0u;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < R; i += nt)
-        if (sc[i] != sc[i]) s_nan = 1u;
+    for (uint32_t i = tid; i < n; i += nt)
+        if (sc[i] != sc[i]) L.s_nan = 1u;
     // U = the k-th smallest ukey: 4 radix passes of 8 bits
     uint32_t left = k, prefix = 0u, pmask = 0u;
     for (int pass = 0; pass < 4 && k > 0; ++pass) {
         const int shift = 24 - 8 * pass;
-        for (uint32_t i = tid; i < 256; i += nt) bins[i] = 0u;
+        for (uint32_t i = tid; i < 256; i += nt) L.bins[i] = 0u;
         __syncthreads();
-        for (uint32_t i = tid; i < R; i += nt) {
+        for (uint32_t i = tid; i < n; i += nt) {
             const uint32_t u = ukey(i);
-            if ((u & pmask) == prefix) atomicAdd(&bins[(u >> shift) & 255u], 1u);
+            if ((u & pmask) == prefix) atomicAdd(&L.bins[(u >> shift) & 255u], 1u);
         }
         __syncthreads();
         if (tid < 64) {
-            const uint32_t bin = wave_find_cum(bins, 256, left);
-            const uint32_t below = wave_sum_below(bins, bin);
+            const uint32_t bin = wave_find_cum(L.bins, 256, left);
+            const uint32_t below = wave_sum_below(L.bins, bin);
             if (tid == 0) {
-                s_cut = bin;
-                s_below = below;
+                L.s_cut = bin;
+                L.s_below = below;
             }
         }
         __syncthreads();
-        left -= s_below;
-        prefix |= s_cut << shift;
+        left -= L.s_below;
+        prefix |= L.s_cut << shift;
         pmask |= 255u << shift;
         __syncthreads();
     }
     const uint32_t U = prefix, need = left;  // `need` entries tied at U complete the top k
     // entries strictly better than U (fewer than k), and the ties at U
-    for (uint32_t i = tid; i < R && k > 0; i += nt) {
+    for (uint32_t i = tid; i < n && k > 0; i += nt) {
         const uint32_t u = ukey(i);
         if (u < U) {
-            sel[atomicAdd(&s_nsel, 1u)] = i;
+            L.sel[atomicAdd(&L.s_nsel, 1u)] = i;
         } else if (u == U) {
-            const uint32_t t = atomicAdd(&s_ntie, 1u);
-            if (t < kTieLds) tk[t] = ((uint64_t)dd[i] << 32) | i;  // stage-1 order (d, row) resolved below
+            const uint32_t t = atomicAdd(&L.s_ntie, 1u);
+            if (t < kTieLds) L.tk[t] = ((uint64_t)dd[i] << 32) | i;  // stage-1 order (d, row) resolved below
         }
     }
     __syncthreads();
-    const uint32_t nties = s_ntie;
+    const uint32_t nties = L.s_ntie;
     if (k > 0 && nties <= kTieLds) {
         // order the ties by (d, row): re-key with the row, sort, take `need`
         for (uint32_t t = tid; t < nties; t += nt) {
-            const uint32_t i = (uint32_t)tk[t];
-            tk[t] = ((uint64_t)dd[i] << 52) | ((uint64_t)rw[i] << 20) | i;  // d < 2^12, row < 2^32, i < 2^20
+            const uint32_t i = (uint32_t)L.tk[t];
+            L.tk[t] = ((uint64_t)dd[i] << 52) | ((uint64_t)rw[i] << 20) | i;  // d < 2^12, row < 2^32, i < 2^20
         }
         __syncthreads();
         const uint32_t P = next_pow2(max(nties, 1u));
-        for (uint32_t t = nties + tid; t < P; t += nt) tk[t] = ~0ull;
+        for (uint32_t t = nties + tid; t < P; t += nt) L.tk[t] = ~0ull;
         __syncthreads();
-        bitonic_sort_lds(tk, P);
-        for (uint32_t t = tid; t < need; t += nt) sel[s_nsel + t] = (uint32_t)tk[t] & 0xfffffu;
+        bitonic_sort_lds(L.tk, P);
+        for (uint32_t t = tid; t < need; t += nt) L.sel[L.s_nsel + t] = (uint32_t)L.tk[t] & 0xfffffu;
         __syncthreads();
     } else if (k > 0) {
         // massive tie (more than kTieLds equal scores): radix select the need-th
@@ -277,52 +258,68 @@ __global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restric
         uint32_t tl = need;
         for (int pass = 0; pass < 8; ++pass) {
             const int shift = 56 - 8 * pass;
-            for (uint32_t i = tid; i < 256; i += nt) bins[i] = 0u;
+            for (uint32_t i = tid; i < 256; i += nt) L.bins[i] = 0u;
             __syncthreads();
-            for (uint32_t i = tid; i < R; i += nt) {
+            for (uint32_t i = tid; i < n; i += nt) {
                 if (ukey(i) != U) continue;
                 const uint64_t key = ((uint64_t)dd[i] << 32) | rw[i];
-                if ((key & tmask) == tpre) atomicAdd(&bins[(uint32_t)(key >> shift) & 255u], 1u);
+                if ((key & tmask) == tpre) atomicAdd(&L.bins[(uint32_t)(key >> shift) & 255u], 1u);
             }
             __syncthreads();
             if (tid < 64) {
-                const uint32_t bin = wave_find_cum(bins, 256, tl);
-                const uint32_t below = wave_sum_below(bins, bin);
+                const uint32_t bin = wave_find_cum(L.bins, 256, tl);
+                const uint32_t below = wave_sum_below(L.bins, bin);
                 if (tid == 0) {
-                    s_cut = bin;
-                    s_below = below;
+                    L.s_cut = bin;
+                    L.s_below = below;
                 }
             }
             __syncthreads();
-            tl -= s_below;
-            tpre |= (uint64_t)s_cut << shift;
+            tl -= L.s_below;
+            tpre |= (uint64_t)L.s_cut << shift;
             tmask |= 255ull << shift;
             __syncthreads();
         }
-        if (tid == 0) s_tcut = tpre;
+        if (tid == 0) L.s_tcut = tpre;
         __syncthreads();
-        for (uint32_t i = tid; i < R; i += nt) {
+        for (uint32_t i = tid; i < n; i += nt) {
             if (ukey(i) != U) continue;
             const uint64_t key = ((uint64_t)dd[i] << 32) | rw[i];
-            if (key <= s_tcut) sel[atomicAdd(&s_nsel, 1u)] = i;  // distinct rows: exactly `need` keys
+            if (key <= L.s_tcut) L.sel[atomicAdd(&L.s_nsel, 1u)] = i;  // distinct rows: exactly `need` keys
         }
         __syncthreads();
     }
     // sort the k selected by (ukey, d, row): rank counting over LDS copies
     for (uint32_t a = tid; a < k; a += nt) {
-        const uint32_t ia = sel[a];
-        su[a] = ukey(ia);
-        sdr[a] = ((uint64_t)dd[ia] << 32) | rw[ia];
+        const uint32_t ia = L.sel[a];
+        L.su[a] = ukey(ia);
+        L.sdr[a] = ((uint64_t)dd[ia] << 32) | rw[ia];
     }
     __syncthreads();
     for (uint32_t a = tid; a < k; a += nt) {
-        const uint32_t ua = su[a];
-        const uint64_t da = sdr[a];
+        const uint32_t ua = L.su[a];
+        const uint64_t da = L.sdr[a];
         uint32_t rank = 0;
-        for (uint32_t c = 0; c < k; ++c) rank += su[c] < ua || (su[c] == ua && sdr[c] < da);
-        srt[rank] = sel[a];
+        for (uint32_t c = 0; c < k; ++c) rank += L.su[c] < ua || (L.su[c] == ua && L.sdr[c] < da);
+        L.srt[rank] = L.sel[a];
     }
     __syncthreads();
+    return k;
+}
+
+__global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restrict__ scores,
+                                                          const uint32_t* __restrict__ s1_rows,
+                                                          const uint32_t* __restrict__ s1_dist, uint32_t R,
+                                                          uint32_t kout, int descending,
+                                                          const uint64_t* __restrict__ ids, uint64_t row_offset,
+                                                          uint64_t* __restrict__ out_ids,
+                                                          float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
+                                                          uint32_t* __restrict__ nan_flag) {
+    __shared__ TopkLds L;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    const float* sc = scores + (uint64_t)q * R;
+    const uint32_t* rw = s1_rows + (uint64_t)q * R;
+    const uint32_t k = big_topk_order(L, sc, rw, s1_dist + (uint64_t)q * R, R, kout, descending);
     if (tid < 64) {  // take(k), then drop orphan rows (index.rs:217-228)
         uint32_t o = 0;
         for (uint32_t i0 = 0; i0 < k; i0 += 64) {
@@ -330,7 +327,7 @@ __global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restric
             uint64_t id = kOrphan;
             uint32_t e = 0;
             if (i < k) {
-                e = srt[i];
+                e = L.srt[i];
                 id = ids ? ids[rw[e]] : (uint64_t)rw[e] + row_offset;
             }
             const bool keep = i < k && id != kOrphan;
@@ -342,12 +339,59 @@ __global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restric
             }
             o += __popcll(m);
         }
-        const bool poisoned = s_nan && R >= 2;
+        const bool poisoned = L.s_nan && R >= 2;
         if (tid == 0) {
             if (poisoned) atomicOr(nan_flag, 1u);
             if (out_n) out_n[q] = poisoned ? GVDB_N_POISONED : o;
         }
     }
+}
+
+// Deep sharded search, step 3 (iii): this rank's local top-k of its owned
+// entries (m_cos / m_rows / m_dist [B][Rl], own_cnt[q] valid) by (cosine desc,
+// Hamming, row) -> the exchange-2 block: {cos bits, Hamming, id lo, id hi}
+// (orphans kept: the merge drops them after the global truncation), meta.
+__global__ __launch_bounds__(kBigThreads) void k_shard_deep_topk(const float* __restrict__ m_cos,
+                                                                 const uint32_t* __restrict__ m_rows,
+                                                                 const uint32_t* __restrict__ m_dist,
+                                                                 const uint32_t* __restrict__ own_cnt,
+                                                                 const uint32_t* __restrict__ reff, uint32_t B,
+                                                                 uint32_t Rl, uint32_t kout,
+                                                                 const uint64_t* __restrict__ ids, uint32_t err,
+                                                                 uint32_t* __restrict__ block2) {
+    __shared__ TopkLds L;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    const uint64_t base = (uint64_t)q * Rl;
+    const uint32_t c = Rl ? min(own_cnt[q], Rl) : 0u;
+    const uint32_t take = big_topk_order(L, m_cos + base, m_rows + base, m_dist + base, c, kout, 1);
+    uint32_t* ent = block2 + (uint64_t)q * kout * 4u;
+    for (uint32_t t = tid; t < take; t += blockDim.x) {
+        const uint32_t e = L.srt[t];
+        const uint32_t row = m_rows[base + e];
+        const uint64_t id = ids ? ids[row] : (uint64_t)row;
+        ent[4 * t + 0] = __float_as_uint(m_cos[base + e]);
+        ent[4 * t + 1] = m_dist[base + e];
+        ent[4 * t + 2] = (uint32_t)id;
+        ent[4 * t + 3] = (uint32_t)(id >> 32);
+    }
+    if (tid == 0) {
+        uint32_t* meta = block2 + 4ull * B * kout;
+        const uint32_t re = reff[q];
+        meta[q] = take | ((L.s_nan && re >= 2u) ? 0x80000000u : 0u);
+        meta[B + q] = re;
+        if (q == 0) meta[2 * B] = err;
+    }
+}
+
+hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
+                                  const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,
+                                  const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (k > kTopkBigMax || Rl > kBigRMax) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_shard_deep_topk, dim3(B), dim3(kBigThreads), 0, s, m_cos, m_rows, m_dist, own_cnt, reff, B,
+                       Rl, k, ids, err, block2);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 hipError_t launch_topk_big(const FinalArgs& a, const uint32_t* s1_dist, hipStream_t s) {

@@ -280,7 +280,7 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t sample_div, uint32_t& chunks
 // sit contiguously in ws.zero (flags[0] = any stage-1 failure, flags[1] = NaN).
 // fast: launch_stage1_fast will run (its first kernel may zero the state)
 gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D, uint32_t R, uint32_t N,
-                           hipStream_t s, bool fast) {
+                           hipStream_t s, bool fast, bool lists = true) {
     // GVDB_SCAN=valu forces the popcount scan for every batch size; default:
     // FP4 MFMA for large batches.  (The round-1/2 A/B scans -- i8 MFMA, uniform
     // FP4 waves, LDS-shared tiles, mx3 -- were removed from the tree after
@@ -327,8 +327,10 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     }
     HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
     HIP_TRY(ws.buf.ensure((size_t)B * s1.bufcap * 8), "alloc candidate buffer");
-    HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
-    HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
+    if (lists) {  // else the caller points s1_rows / s1_dist at its own buffers
+        HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
+        HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
+    }
     uint32_t* z = ws.zero.as<uint32_t>();
     if (fast && s1.mfma_scan && s1.sample_mode == kSampleDense) {  // k_qfrag, the first stage-1 kernel, zeroes them
         s1.zero = z;
@@ -342,8 +344,8 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     s1.hist = z + 4 + 2 * (size_t)B;
     s1.thr = ws.thr.as<uint32_t>();
     s1.buf = ws.buf.as<uint64_t>();
-    s1.s1_rows = ws.s1_rows.as<uint32_t>();
-    s1.s1_dist = ws.s1_dist.as<uint32_t>();
+    s1.s1_rows = lists ? ws.s1_rows.as<uint32_t>() : nullptr;
+    s1.s1_dist = lists ? ws.s1_dist.as<uint32_t>() : nullptr;
     return GVDB_OK;
 }
 
@@ -2138,5 +2140,46 @@ gvdb_status gvdb::shard_stage1_keys(const gvdb_index* ix, const float* d_q, uint
         timing().free_sets.push_back(ev);
     }
     if (e != hipSuccess) return dev_fail(e, "sharded stage 1");
+    return GVDB_OK;
+}
+
+// Deep sharded search (R > kSelectLdsCap): this shard's exact stage-1
+// top-min(R, rows) MEMBERSHIP (rows + Hamming, unordered: k_select_big; a
+// shard of at most kSelectLdsCap rows: k_select's sorted list) into
+// m_rows / m_dist [B][Rl], then its per-query Hamming histogram and count into
+// the deep exchange-1 block (gvdb_shard.hip).  Nothing for an empty shard.
+gvdb_status gvdb::shard_stage1_members(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
+                                       uint32_t* m_rows, uint32_t* m_dist, uint32_t* block1, hipStream_t s) {
+    if (!ix) return fail(GVDB_ERR_INVALID_ARGUMENT, "null index");
+    if (ix->n == 0 || B == 0 || R == 0) return GVDB_OK;
+    if (dim != ix->dim) return dim_mismatch(ix->dim, dim);
+    if (ix->n > 0xFFFFFFFFull) return fail(GVDB_ERR_INDEX, "shard exceeds 2^32 rows");
+    if (dim >= 4096 || R > kBigRMax) return fail(GVDB_ERR_INVALID_ARGUMENT, "deep sharded search: dim < 4096, R <= 2^20");
+    const uint32_t Rl = (uint32_t)std::min<uint64_t>(R, ix->n);
+    gvdb_status st = set_device(ix->device);
+    if (st != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    g.begin(s);
+    UseGuard ug{ix, s};
+    const uint32_t W4 = code_w4(dim);
+    HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc qcodes");
+    Stage1Args s1{};
+    st = prepare_stage1(ws, s1, (uint32_t)B, dim, Rl, (uint32_t)ix->n, s, true, false);
+    if (st != GVDB_OK) return st;
+    if (s1.mfma_scan) {
+        s1.qf32 = d_q;  // packed by k_qprep
+        s1.qthr = ix->thr;
+    } else {
+        HIP_TRY(launch_pack(d_q, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
+    }
+    s1.codes = ix->codes;
+    s1.cap = ix->cap;
+    s1.qcodes = ws.qcodes.as<uint4>();
+    s1.s1_rows = m_rows;
+    s1.s1_dist = m_dist;
+    HIP_TRY(launch_stage1_fast(s1, s), "deep sharded stage 1");
+    HIP_TRY(launch_shard_member_hist(m_dist, (uint32_t)B, Rl, dim + 1u, block1, s), "deep sharded stage 1 histogram");
     return GVDB_OK;
 }

@@ -157,14 +157,18 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "shard and communicator on different devices");
     const uint64_t G = (uint64_t)c->world;
     const uint64_t R = flat ? k : std::max<uint64_t>(sp->rescore_count, k);
-    if (R > kSelectLdsCap || G * k > kSelectLdsCap || B > 0xFFFFFFFFull || dim > 8192)
-        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: R <= 8192, world * k <= 8192, dim <= 8192");
+    if (G * k > kSelectLdsCap || B > 0xFFFFFFFFull || dim > 8192)
+        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: world * k <= 8192, dim <= 8192");
+    // R > 8192 (the reference's default ratio at scale): the deep protocol
+    // (histogram exchange, gvdb_shard.hip) -- R <= 2^20, dim < 4096, k <= 1024
+    if (!flat && shard_deep(R) && (R > kBigRMax || dim == 0 || dim >= 4096 || k > 1024))
+        return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search, R > 8192: R <= 2^20, 0 < dim < 4096, k <= 1024");
     std::lock_guard<std::mutex> g(c->mu);
     hipError_t he = hipSetDevice(c->device);
     if (he != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(he));
     hipStream_t s = (hipStream_t)stream;
     uint64_t w1 = 0, w2 = 0, scratch = 0;
-    gvdb_shard_sizes(B, R, k, &w1, &w2, &scratch);
+    gvdb_shard_sizes(B, R, k, dim, &w1, &w2, &scratch);
     const uint64_t wf = shard_words_flat(B, k);
     // layout: send1 | recv1 [G] | send2 | recv2 [G] | scratch   (FLAT: sendF | recvF [G])
     const size_t need = flat ? wf * 4 * (G + 1) : ((w1 + w2) * (G + 1)) * 4 + scratch;
@@ -210,7 +214,7 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
         uint32_t* recv2 = G > 1 ? send2 + w2 : send2;
         void* scr = base + (w1 + w2) * (G + 1);
         // 1. local stage 1 (an empty or failing shard still joins with no entries)
-        local = gvdb_shard_stage1_device(shard, d_q, B, dim, R, send1, stream);
+        local = gvdb_shard_stage1_device(shard, d_q, B, dim, R, send1, scr, stream);
         std::string local_err = local != GVDB_OK ? std::string(gvdb_last_error()) : std::string();
         if ((st = all_gather(send1, recv1, w1)) != GVDB_OK) return st;
         // 2. global top-R, rerank of the owned rows, local top-k.  A rank whose

@@ -87,4 +87,21 @@ __device__ inline uint32_t wave_sum_below(const uint32_t* h, uint32_t t) {
     return s;
 }
 
+// Block-wide exclusive prefix of a flag in thread order; *total = block count.
+__device__ __forceinline__ uint32_t big_prefix(bool f, uint32_t* wcnt, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wcnt[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), tot = 0;
+    for (uint32_t i = 0; i < nw; ++i) {
+        const uint32_t c = wcnt[i];
+        if (i < w) pre += c;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre;
+}
+
 }  // namespace gvdb

@@ -356,6 +356,24 @@ hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint3
                                uint32_t R, uint32_t D, const float* rows, const float* norms, const uint64_t* ids,
                                const float* queries, uint32_t k, uint32_t err, uint32_t* block2, uint32_t* opos,
                                uint32_t* orow, float* ocos, hipStream_t s);
+// Deep two-exchange (R > kSelectLdsCap; gvdb_shard.hip):
+//   block 1 deep: hist u32 [B][dim+1] (Hamming histogram of the local top-min(R, n)
+//                 membership) | counts u32 [B] | err u32 | pad
+//   scratch deep: member rows u32 [B][R] | member dist u32 [B][R] | cosines f32 [B][R]
+//                 | own count u32 [B] | reff u32 [B]   (lists dense with stride Rl = min(R, n))
+inline bool shard_deep(uint64_t R) { return R > kSelectLdsCap; }
+inline uint64_t shard_words1_deep(uint64_t B, uint32_t dim) { return (B * (dim + 1ull) + B + 1 + 1) & ~1ull; }
+gvdb_status shard_stage1_members(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
+                                 uint32_t* m_rows, uint32_t* m_dist, uint32_t* block1, hipStream_t s);
+hipError_t launch_shard_member_hist(const uint32_t* m_dist, uint32_t B, uint32_t Rl, uint32_t H, uint32_t* block1,
+                                    hipStream_t s);
+hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
+                                 uint32_t R, uint32_t Rl, uint32_t H, uint32_t* m_rows, uint32_t* m_dist,
+                                 uint32_t* own_cnt, uint32_t* reff, hipStream_t s);
+// gvdb_bigr.hip: the owned entries' local top-k (k <= 1024) -> the exchange-2 block
+hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
+                                  const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,
+                                  const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s);
 // sharded FLAT: gathered blocks of the ranks' exact top-k -> merged top-k
 //   block F (sharded FLAT): ids u64 [B][k] | scores f32 [B][k] | counts [B] | err | pad
 inline uint64_t shard_words_flat(uint64_t B, uint64_t k) { return (3 * B * k + B + 1 + 1) & ~1ull; }

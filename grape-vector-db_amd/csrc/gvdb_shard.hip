@@ -516,6 +516,161 @@ hipError_t launch_shard_flat_final(const uint32_t* gathered, uint64_t words, uin
     return hipSuccess;
 }
 
+// ---- deep two-exchange (R > kSelectLdsCap: the reference's default ratio) -------
+// Exchange 1 carries, per query, the Hamming histogram of the rank's local
+// top-min(R, n_g) membership instead of its keys (B*(dim+1)*4 bytes per rank,
+// independent of R).  Every rank then knows the global top-R by (d, rank, row)
+// exactly: its threshold T = the smallest t with sum_g #{list g: d <= t} >= Re,
+// the ties at T taken in rank order (ranks before this one first), and within
+// this rank the first `quota` tied rows by row.  Its owned entries are its own
+// members below T plus those tied rows.  The local top-k then orders by
+// (cosine desc, Hamming, row) and exchange 2 carries the Hamming distance in
+// the entry's order-key word: the merge's (cosine, Hamming, rank, list index)
+// order is the global stable order (cosine, d, rank, row).
+
+// block 1 (deep): per query the histogram of the member distances, counts = Rl
+__global__ __launch_bounds__(256) void k_shard_member_hist(const uint32_t* __restrict__ m_dist, uint32_t B,
+                                                           uint32_t Rl, uint32_t H, uint32_t* __restrict__ block1) {
+    extern __shared__ uint32_t h[];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    for (uint32_t t = tid; t < H; t += 256) h[t] = 0u;
+    __syncthreads();
+    const uint32_t* d = m_dist + (uint64_t)q * Rl;
+    for (uint32_t i = tid; i < Rl; i += 256) atomicAdd(&h[min(d[i], H - 1u)], 1u);
+    __syncthreads();
+    uint32_t* out = block1 + (uint64_t)q * H;
+    for (uint32_t t = tid; t < H; t += 256) out[t] = h[t];
+    if (tid == 0) block1[(uint64_t)B * H + q] = Rl;
+}
+
+hipError_t launch_shard_member_hist(const uint32_t* m_dist, uint32_t B, uint32_t Rl, uint32_t H, uint32_t* block1,
+                                    hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_shard_member_hist, dim3(B), dim3(256), (size_t)H * 4u, s, m_dist, B, Rl, H, block1);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// step 3 (i) deep: this rank's owned entries of the global top-R, compacted in
+// place (order kept) at the front of its member lists; own_cnt / reff [B].
+constexpr uint32_t kDeepThreads = 1024;
+__global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t* __restrict__ gathered,
+                                                                 uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
+                                                                 uint32_t R, uint32_t Rl, uint32_t H,
+                                                                 uint32_t* __restrict__ m_rows,
+                                                                 uint32_t* __restrict__ m_dist,
+                                                                 uint32_t* __restrict__ own_cnt,
+                                                                 uint32_t* __restrict__ reff) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tot[];  // [H] global histogram, then bins [2048]
+    uint32_t* bins = tot + ((H + 3u) & ~3u);
+    __shared__ uint32_t s_S, s_T, s_lt, s_tb, s_cut, s_below, wcnt[kDeepThreads / 64];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    auto hist = [&](uint32_t g) { return gathered + (uint64_t)g * words1 + (uint64_t)q * H; };
+    auto count = [&](uint32_t g) { return min(gathered[(uint64_t)g * words1 + (uint64_t)B * H + q], R); };
+    if (tid == 0) s_S = 0u;
+    __syncthreads();
+    for (uint32_t t = tid; t < H; t += nt) {
+        uint32_t s = 0;
+        for (uint32_t g = 0; g < G; ++g) s += hist(g)[t];
+        tot[t] = s;
+    }
+    for (uint32_t g = tid; g < G; g += nt) atomicAdd(&s_S, count(g));
+    __syncthreads();
+    const uint32_t Re = min(R, s_S);
+    const uint32_t n = Rl ? min(count(me), Rl) : 0u;  // this rank's members
+    if (Re == 0 || n == 0) {
+        if (tid == 0) {
+            own_cnt[q] = 0u;
+            reff[q] = Re;
+        }
+        return;
+    }
+    if (tid < 64) {
+        const uint32_t t = wave_find_cum(tot, H, Re);
+        const uint32_t lt = wave_sum_below(tot, t);
+        if (tid == 0) {
+            s_T = t;
+            s_lt = lt;
+            uint32_t tb = 0;
+            for (uint32_t g = 0; g < me; ++g) tb += hist(g)[t];  // ties at T of the ranks before this one
+            s_tb = tb;
+        }
+    }
+    __syncthreads();
+    const uint32_t T = s_T, need = Re - s_lt, tb = s_tb, mine = hist(me)[T];
+    const uint32_t quota = need > tb ? min(need - tb, mine) : 0u;  // this rank's tied rows in the top-R
+    // the quota-th smallest row among this rank's members at d == T: 11 + 11 + 10 bits
+    uint32_t cut = 0u;
+    const bool all_ties = quota == mine, no_ties = quota == 0u;
+    if (!all_ties && !no_ties) {
+        uint32_t left = quota, prefix = 0u, pmask = 0u;
+        const uint32_t* rw = m_rows + (uint64_t)q * Rl;
+        const uint32_t* dd = m_dist + (uint64_t)q * Rl;
+        for (int pass = 0; pass < 3; ++pass) {
+            const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+            const uint32_t nb = pass == 2 ? 1024u : 2048u, dm = nb - 1u;
+            for (uint32_t i = tid; i < nb; i += nt) bins[i] = 0u;
+            __syncthreads();
+            for (uint32_t i = tid; i < n; i += nt) {
+                const uint32_t row = rw[i];
+                if (dd[i] == T && (row & pmask) == prefix) atomicAdd(&bins[(row >> shift) & dm], 1u);
+            }
+            __syncthreads();
+            if (tid < 64) {
+                const uint32_t bin = wave_find_cum(bins, nb, left);
+                const uint32_t below = wave_sum_below(bins, bin);
+                if (tid == 0) {
+                    s_cut = bin;
+                    s_below = below;
+                }
+            }
+            __syncthreads();
+            left -= s_below;
+            prefix |= s_cut << shift;
+            pmask |= dm << shift;
+            __syncthreads();
+        }
+        cut = prefix;
+    }
+    // order-preserving in-place compaction: a chunk's entries are read before the
+    // block prefix (its barriers), and written at or before their own slots
+    uint32_t* rw = m_rows + (uint64_t)q * Rl;
+    uint32_t* dd = m_dist + (uint64_t)q * Rl;
+    uint32_t o = 0;
+    for (uint32_t base = 0; base < n; base += nt) {
+        const uint32_t i = base + tid;
+        uint32_t row = 0u, d = ~0u;
+        if (i < n) {
+            row = rw[i];
+            d = dd[i];
+        }
+        const bool keep = i < n && (d < T || (d == T && (all_ties || (!no_ties && row <= cut))));
+        uint32_t total;
+        const uint32_t pos = o + big_prefix(keep, wcnt, &total);
+        if (keep) {
+            rw[pos] = row;
+            dd[pos] = d;
+        }
+        o += total;
+    }
+    if (tid == 0) {
+        own_cnt[q] = o;
+        reff[q] = Re;
+    }
+}
+
+hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
+                                 uint32_t R, uint32_t Rl, uint32_t H, uint32_t* m_rows, uint32_t* m_dist,
+                                 uint32_t* own_cnt, uint32_t* reff, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    const size_t lds = (size_t)((H + 3u) & ~3u) * 4u + 2048u * 4u;
+    if (lds > 160u * 1024u) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_shard_deep_own, dim3(B), dim3(kDeepThreads), lds, s, gathered1, words1, G, me, B, R, Rl, H,
+                       m_rows, m_dist, own_cnt, reff);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 // ---- host forms of the merges (same block layouts; CPU transports and tests) -----
 namespace {
 inline uint32_t f32_order_h(float f) {
@@ -532,31 +687,48 @@ using namespace gvdb;
 
 extern "C" {
 
-void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint64_t* words1, uint64_t* words2,
+void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint32_t dim, uint64_t* words1, uint64_t* words2,
                       uint64_t* scratch_bytes) {
-    if (words1) *words1 = shard_words1(B, R);
+    if (words1) *words1 = shard_deep(R) ? shard_words1_deep(B, dim) : shard_words1(B, R);
     if (words2) *words2 = shard_words2(B, k);
-    // the owned positions, rows and cosines [B][R] of phase 2 (used when R > 2048)
-    if (scratch_bytes) *scratch_bytes = 12 * B * R + 256;
+    // key form: the owned positions, rows and cosines [B][R] of phase 2 (used when R > 2048);
+    // deep form: the member rows, distances and cosines [B][R], own counts and reff [B]
+    if (scratch_bytes) *scratch_bytes = 12 * B * R + 8 * B + 256;
 }
 
 uint64_t gvdb_shard_flat_words(uint64_t B, uint64_t k) { return shard_words_flat(B, k); }
 
 gvdb_status gvdb_shard_stage1_device(const gvdb_index* shard, const float* d_queries, uint64_t B, uint32_t dim,
-                                     uint64_t R, uint32_t* d_block1, void* stream) {
+                                     uint64_t R, uint32_t* d_block1, void* d_scratch, void* stream) {
     if (!shard || !d_block1 || (B && !d_queries)) return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (B == 0) return GVDB_OK;
-    if (R == 0 || R > kSelectLdsCap) return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: 1 <= R <= 8192");
+    const bool deep = shard_deep(R);
+    if (R == 0 || R > kBigRMax) return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: 1 <= R <= 2^20");
+    if (deep && (!d_scratch || dim == 0 || dim >= 4096))
+        return report_status(GVDB_ERR_INVALID_ARGUMENT, "deep sharded search (R > 8192): scratch, 0 < dim < 4096");
     hipStream_t s = (hipStream_t)stream;
     const ShardInfo si = index_shard_info(shard);
     if (hipSetDevice(si.device) != hipSuccess) return report_status(GVDB_ERR_DEVICE, "hipSetDevice");
     const uint64_t BR = B * R;
-    uint32_t* counts = d_block1 + 2 * BR;
     gvdb_status st = GVDB_OK;
-    if (si.n > 0 && dim > kShardMaxD) st = report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: dim > 8192");
-    if (st == GVDB_OK) st = shard_stage1_keys(shard, d_queries, B, dim, R, reinterpret_cast<uint64_t*>(d_block1), s);
     // every rank joins the exchange: a failed or empty shard contributes no
     // entries (and a failure flag that poisons every query of the merge)
+    if (deep) {
+        uint32_t* m_rows = (uint32_t*)d_scratch;
+        const uint64_t hw = B * (dim + 1ull);  // histogram words before the counts
+        st = shard_stage1_members(shard, d_queries, B, dim, R, m_rows, m_rows + BR, d_block1, s);
+        if (st != GVDB_OK || si.n == 0) {
+            if (hipMemsetD32Async(d_block1, 0, hw + B, s) != hipSuccess ||
+                hipMemsetD32Async(d_block1 + hw + B, st == GVDB_OK ? 0 : 1, 1, s) != hipSuccess)
+                return report_status(GVDB_ERR_DEVICE, "sharded stage 1: counts");
+        } else if (hipMemsetD32Async(d_block1 + hw + B, 0, 1, s) != hipSuccess) {
+            return report_status(GVDB_ERR_DEVICE, "sharded stage 1: err word");
+        }
+        return st;
+    }
+    uint32_t* counts = d_block1 + 2 * BR;
+    if (si.n > 0 && dim > kShardMaxD) st = report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: dim > 8192");
+    if (st == GVDB_OK) st = shard_stage1_keys(shard, d_queries, B, dim, R, reinterpret_cast<uint64_t*>(d_block1), s);
     // (k_select writes the counts of a searched shard; err is informational: a
     // failure is propagated through the exchange-2 block)
     if (st != GVDB_OK || si.n == 0) {
@@ -573,18 +745,52 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
     if (!shard || !d_gathered1 || !d_scratch || !d_block2 || (B && !d_queries))
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
     if (B == 0) return GVDB_OK;
-    if (R == 0 || R > kSelectLdsCap || k == 0 || G == 0 || G > kShardMaxG || rank >= G || G * k > kSelectLdsCap ||
-        B > 0xFFFFFFFFull || dim == 0 || dim > kShardMaxD)
+    const bool deep = shard_deep(R);
+    if (R == 0 || R > kBigRMax || k == 0 || G == 0 || G > kShardMaxG || rank >= G || G * k > kSelectLdsCap ||
+        B > 0xFFFFFFFFull || dim == 0 || dim > kShardMaxD || (deep && (dim >= 4096 || k > 1024)))
         return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: bad R / k / G / rank / dim");
     hipStream_t s = (hipStream_t)stream;
     const ShardInfo si = index_shard_info(shard);
     if (hipSetDevice(si.device) != hipSuccess) return report_status(GVDB_ERR_DEVICE, "hipSetDevice");
     const uint64_t BR = B * R;
-    uint32_t* opos = (uint32_t*)d_scratch;
-    uint32_t* orow = opos + BR;
     // a shard that cannot rerank (empty, or a dimension mismatch already reported by
     // phase 1) sent no entries, so it owns none: its rows are never read
     const bool usable = si.n > 0 && si.dim == dim;
+    if (deep) {
+        uint32_t* m_rows = (uint32_t*)d_scratch;
+        uint32_t* m_dist = m_rows + BR;
+        float* m_cos = (float*)(m_dist + BR);
+        uint32_t* own_cnt = (uint32_t*)(m_cos + BR);
+        uint32_t* reff = own_cnt + B;
+        const uint32_t Rl = usable ? (uint32_t)std::min<uint64_t>(R, si.n) : 0u;
+        hipError_t e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
+                                             (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, own_cnt, reff, s);
+        if (e == hipSuccess && Rl > 0) {
+            RerankArgs rr{};
+            rr.rows = si.rows;
+            rr.clen = dim;
+            rr.norms = si.norms;
+            rr.q = d_queries;
+            rr.qlen = dim;
+            rr.s1_rows = m_rows;
+            rr.B = (uint32_t)B;
+            rr.R = Rl;
+            rr.kind = kScoreCosine;
+            rr.scores = m_cos;
+            rr.counts = own_cnt;
+            e = launch_rerank(rr, s);
+        }
+        if (e == hipSuccess)
+            e = launch_shard_deep_topk(m_cos, m_rows, m_dist, own_cnt, reff, (uint32_t)B, Rl, (uint32_t)k,
+                                       usable ? si.ids : nullptr, 0u, d_block2, s);
+        if (e != hipSuccess)
+            return report_status(GVDB_ERR_DEVICE, std::string("deep shard phase 2: ") + hipGetErrorString(e));
+        if (usable) index_track_use(shard, s);
+        return GVDB_OK;
+    }
+    if (R > kSelectLdsCap) return report_status(GVDB_ERR_INVALID_ARGUMENT, "sharded search: R");
+    uint32_t* opos = (uint32_t*)d_scratch;
+    uint32_t* orow = opos + BR;
     const hipError_t e = launch_shard_phase2(d_gathered1, shard_words1(B, R), (uint32_t)G, (uint32_t)rank, (uint32_t)B,
                                              (uint32_t)R, dim, usable ? si.rows : nullptr,
                                              usable ? si.norms : nullptr, usable ? si.ids : nullptr, d_queries,
@@ -662,6 +868,56 @@ gvdb_status gvdb_shard_merge_host(const uint32_t* gathered1, uint64_t G, uint64_
         }
         own_cnt[q] = c;
         reff[q] = (uint32_t)re;
+    }
+    return GVDB_OK;
+}
+
+// Host form of the deep step 3 (i) (k_shard_deep_own): from the gathered deep
+// exchange-1 blocks and this rank's members (m_rows / m_dist [B][R], the
+// first min(count, R) valid, any order), its owned entries sorted by
+// (Hamming, row) -> own_rows / own_dist [B][R], own_cnt, reff.  Their
+// Hamming distances are the order keys gvdb_shard_local_topk_host takes as
+// own_pos (a list sorted by (d, row) breaks (cosine, d) ties by row).
+gvdb_status gvdb_shard_deep_own_host(const uint32_t* gathered1, uint64_t G, uint64_t rank, uint64_t B, uint64_t R,
+                                     uint32_t dim, const uint32_t* m_rows, const uint32_t* m_dist,
+                                     uint32_t* own_rows, uint32_t* own_dist, uint32_t* own_cnt, uint32_t* reff) {
+    if (!gathered1 || !m_rows || !m_dist || !own_rows || !own_dist || !own_cnt || !reff)
+        return report_status(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    if (rank >= G || dim == 0) return report_status(GVDB_ERR_INVALID_ARGUMENT, "bad rank / dim");
+    const uint64_t H = dim + 1ull, w1 = shard_words1_deep(B, dim);
+    std::vector<uint64_t> tot(H), mine;
+    for (uint64_t q = 0; q < B; ++q) {
+        std::fill(tot.begin(), tot.end(), 0ull);
+        uint64_t S = 0;
+        for (uint64_t g = 0; g < G; ++g) {
+            const uint32_t* blk = gathered1 + g * w1;
+            for (uint64_t t = 0; t < H; ++t) tot[t] += blk[q * H + t];
+            S += std::min<uint64_t>(blk[B * H + q], R);
+        }
+        const uint64_t re = std::min<uint64_t>(R, S);
+        reff[q] = (uint32_t)re;
+        own_cnt[q] = 0;
+        const uint64_t n = std::min<uint64_t>(gathered1[rank * w1 + B * H + q], R);
+        if (re == 0 || n == 0) continue;
+        uint64_t T = 0, cum = 0;
+        while (T < H && cum + tot[T] < re) cum += tot[T++];  // cum = entries below T
+        if (T == H) T = H - 1;
+        uint64_t tb = 0;
+        for (uint64_t g = 0; g < rank; ++g) tb += gathered1[g * w1 + q * H + T];
+        const uint64_t need = re - cum, tied = gathered1[rank * w1 + q * H + T];
+        const uint64_t quota = need > tb ? std::min(need - tb, tied) : 0;
+        mine.clear();
+        for (uint64_t i = 0; i < n; ++i) mine.push_back(((uint64_t)m_dist[q * R + i] << 32) | m_rows[q * R + i]);
+        std::sort(mine.begin(), mine.end());
+        uint32_t c = 0, ties = 0;
+        for (const uint64_t key : mine) {
+            const uint64_t d = key >> 32;
+            if (d > T || (d == T && ties++ >= quota)) break;
+            own_rows[q * R + c] = (uint32_t)key;
+            own_dist[q * R + c] = (uint32_t)d;
+            ++c;
+        }
+        own_cnt[q] = c;
     }
     return GVDB_OK;
 }

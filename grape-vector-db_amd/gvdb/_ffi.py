@@ -151,13 +151,14 @@ SIGNATURES = {
     "gvdb_comm_info": (C.c_int, [P, C.POINTER(i32), C.POINTER(i32)]),
     "gvdb_index_search_sharded_device": (C.c_int, [P, P, P, u64, u32, u64, C.POINTER(gvdb_search_params), P, P, P,
                                                    P]),
-    "gvdb_shard_sizes": (None, [u64, u64, u64, PU64, PU64, PU64]),
+    "gvdb_shard_sizes": (None, [u64, u64, u64, u32, PU64, PU64, PU64]),
     "gvdb_shard_flat_words": (u64, [u64, u64]),
-    "gvdb_shard_stage1_device": (C.c_int, [P, P, u64, u32, u64, P, P]),
+    "gvdb_shard_stage1_device": (C.c_int, [P, P, u64, u32, u64, P, P, P]),
     "gvdb_shard_rerank_device": (C.c_int, [P, P, u64, u32, u64, u64, P, u64, u64, P, P, P]),
     "gvdb_shard_final_device": (C.c_int, [P, u64, u64, u64, P, P, P, P]),
     "gvdb_shard_flat_final_device": (C.c_int, [P, u64, u64, u64, u32, P, P, P, P]),
     "gvdb_shard_merge_host": (C.c_int, [P, u64, u64, u64, u64, P, P, P, P]),
+    "gvdb_shard_deep_own_host": (C.c_int, [P, u64, u64, u64, u64, u32, P, P, P, P, P, P]),
     "gvdb_shard_local_topk_host": (C.c_int, [P, P, P, P, P, u64, u64, u64, u32, P]),
     "gvdb_shard_final_host": (C.c_int, [P, u64, u64, u64, P, P, P]),
     "gvdb_sparse_create": (C.c_int, [C.POINTER(gvdb_bm25_params), C.POINTER(P)]),

@@ -9,7 +9,9 @@ contiguous row range whose ids are global row numbers (ranks in corpus order).
 ``csrc/gvdb_shard.hip``) driven over ANY torch.distributed transport:
 
 1. every rank: its exact local stage-1 top-R as (Hamming << 32 | row) keys;
-2. all-gather of those blocks (B*R*8 bytes per rank);
+   for R > 8192 (the reference's default ratio at scale, the "deep" form) the
+   per-query Hamming histogram of that local top-R instead;
+2. all-gather of those blocks (B*R*8 bytes per rank; deep: B*(dim+1)*4);
 3. every rank: the global top-R by (Hamming, corpus row), the exact cosine of
    the rows IT owns among them (~R/G per query), its local top-k;
 4. all-gather of the local top-k (B*k*16 bytes per rank);
@@ -64,19 +66,26 @@ class TwoExchangeSearch:
     -> (local rows int [B, Rl], Hamming int [B, Rl]) sorted by (d, row) with
     Rl = min(R, shard rows); cosine_fn(q_index, local_rows) -> f32 cosines;
     ``id_offset`` turns local rows into the ids reported (global row numbers).
+    ``dim`` (the vectors' dimension) sizes the deep form's histograms and is
+    required when R > 8192.
     """
 
+    DEEP_R = 8192  # R above this: the deep form (histogram exchange)
+
     def __init__(self, B: int, R: int, k: int, device: torch.device, group=None, index=None, stage1_fn=None,
-                 cosine_fn=None, id_offset: int = 0):
+                 cosine_fn=None, id_offset: int = 0, dim: int = 0):
         import ctypes as C
 
-        self.B, self.R, self.k = B, R, k
+        self.B, self.R, self.k, self.dim = B, R, k, dim
+        self.deep = R > self.DEEP_R
+        if self.deep and dim <= 0:
+            raise ValueError("TwoExchangeSearch: R > 8192 (deep form) needs dim")
         self.dev, self.group = device, group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.index, self.stage1_fn, self.cosine_fn, self.id_offset = index, stage1_fn, cosine_fn, id_offset
         w1, w2, scr = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        lib().gvdb_shard_sizes(B, R, k, C.byref(w1), C.byref(w2), C.byref(scr))
+        lib().gvdb_shard_sizes(B, R, k, dim, C.byref(w1), C.byref(w2), C.byref(scr))
         self.w1, self.w2 = w1.value, w2.value
         self.send1 = torch.zeros(self.w1, dtype=torch.int32, device=device)
         self.recv1 = torch.zeros((self.world, self.w1), dtype=torch.int32, device=device)
@@ -112,7 +121,8 @@ class TwoExchangeSearch:
             st = torch.cuda.current_stream(q.device).cuda_stream or None
             D = q.shape[1]
             # a failing stage 1 writes zero counts + its err word itself (the C ABI contract)
-            rc = L.gvdb_shard_stage1_device(self.index._h, q.data_ptr(), B, D, R, self.send1.data_ptr(), st)
+            rc = L.gvdb_shard_stage1_device(self.index._h, q.data_ptr(), B, D, R, self.send1.data_ptr(),
+                                            self.scratch.data_ptr(), st)
             if rc != 0:
                 err = _status_error(rc)
             self._gather(self.send1, self.recv1)
@@ -132,21 +142,32 @@ class TwoExchangeSearch:
         # host transport: the same blocks, host merges
         s1 = self.send1.numpy().view(np.uint32)
         s1[:] = 0
+        H = self.dim + 1
+        cnt_at = B * H if self.deep else 2 * B * R  # word of counts[0]
+        m_rows = np.zeros((B, R), np.uint32)
+        m_dist = np.zeros((B, R), np.uint32)
         try:
             rows, dd = self.stage1_fn(q, R)
             rows, dd = np.asarray(rows, np.uint64), np.asarray(dd, np.uint64)
-            keys = s1[:2 * B * R].view(np.uint64).reshape(B, R)
             rl = rows.shape[1]
-            keys[:, :rl] = (dd << np.uint64(32)) | rows
-            s1[2 * B * R:2 * B * R + B] = rl
+            if self.deep:  # this rank's top-R membership stays local; its histogram goes out
+                m_rows[:, :rl] = rows
+                m_dist[:, :rl] = dd
+                hist = s1[:B * H].reshape(B, H)
+                for i in range(B):
+                    hist[i] = np.bincount(dd[i].astype(np.int64), minlength=H)[:H]
+            else:
+                keys = s1[:2 * B * R].view(np.uint64).reshape(B, R)
+                keys[:, :rl] = (dd << np.uint64(32)) | rows
+            s1[cnt_at:cnt_at + B] = rl
         except Exception as e:  # noqa: BLE001 -- re-raised after the exchanges
             err = e
             s1[:] = 0
-            s1[2 * B * R + B] = 1
+            s1[cnt_at + B] = 1
         self._gather(self.send1, self.recv1)
         g1 = np.ascontiguousarray(self.recv1.numpy().view(np.uint32))
         own_rows = np.zeros((B, R), np.uint32)
-        own_pos = np.zeros((B, R), np.uint32)
+        own_pos = np.zeros((B, R), np.uint32)  # deep: the Hamming distances (the merge's order key)
         own_cnt = np.zeros(B, np.uint32)
         reff = np.zeros(B, np.uint32)
         scores = np.zeros((B, R), np.float32)
@@ -154,8 +175,13 @@ class TwoExchangeSearch:
         s2 = self.send2.numpy().view(np.uint32)
         s2[:] = 0
         try:
-            check(L.gvdb_shard_merge_host(g1.ctypes.data, self.world, self.rank, B, R, own_rows.ctypes.data,
-                                          own_pos.ctypes.data, own_cnt.ctypes.data, reff.ctypes.data))
+            if self.deep:
+                check(L.gvdb_shard_deep_own_host(g1.ctypes.data, self.world, self.rank, B, R, self.dim,
+                                                 m_rows.ctypes.data, m_dist.ctypes.data, own_rows.ctypes.data,
+                                                 own_pos.ctypes.data, own_cnt.ctypes.data, reff.ctypes.data))
+            else:
+                check(L.gvdb_shard_merge_host(g1.ctypes.data, self.world, self.rank, B, R, own_rows.ctypes.data,
+                                              own_pos.ctypes.data, own_cnt.ctypes.data, reff.ctypes.data))
             if err is None:
                 for i in range(B):
                     c = int(own_cnt[i])

@@ -339,7 +339,9 @@ gvdb_status gvdb_comm_info(const gvdb_comm* comm, int32_t* world, int32_t* rank)
  * -> ncclAllGather -> merge by (score, corpus row).  Bit-identical to one
  * search over the concatenated shards.  R = max(sp->rescore_count, k) (> 0;
  * the global rescore_ratio form needs the global row count: pass the count),
- * R <= 8192, world * k <= 8192, dim <= 8192.  Results land on every rank, on
+ * world * k <= 8192, dim <= 8192; R > 8192 (the reference's default ratio at
+ * scale) runs the deep form of the protocol (exchange 1 = Hamming histograms,
+ * below) with R <= 2^20, dim < 4096, k <= 1024.  Results land on every rank, on
  * `stream`; no host sync in BQ mode.  An empty shard contributes nothing; a
  * rank whose local part fails still joins both collectives (no deadlock),
  * returns its error, and poisons every query of the merge (out_n =
@@ -353,18 +355,26 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
 
 /* ---- the two-exchange protocol as phases (for hosts with their own transport:
  * MPI, torch.distributed, a CPU fabric).  Block layouts in u32 words:
- *   exchange 1 (per rank, words1): keys u64 [B][R] (Hamming << 32 | local row,
- *     sorted) | counts u32 [B] | err u32 | pad;
- *   exchange 2 (per rank, words2): [B][k] x {cosine bits, global stage-1
- *     position, id lo, id hi} | meta u32 [B] (count | NaN << 31) | reff [B] |
- *     err | pad.
+ *   exchange 1 (per rank, words1), R <= 8192: keys u64 [B][R] (Hamming << 32 |
+ *     local row, sorted) | counts u32 [B] | err u32 | pad;
+ *   exchange 1, deep form (R > 8192): hist u32 [B][dim+1] (Hamming histogram
+ *     of the rank's local top-min(R, rows)) | counts u32 [B] | err u32 | pad
+ *     -- B*(dim+1)*4 bytes per rank whatever R is;
+ *   exchange 2 (per rank, words2): [B][k] x {cosine bits, order key, id lo,
+ *     id hi} | meta u32 [B] (count | NaN << 31) | reff [B] | err | pad; the
+ *     order key is the entry's global stage-1 position (key form) or its
+ *     Hamming distance (deep form): the merge orders by (cosine desc, order
+ *     key, rank, list index), in both forms the stable order of the global
+ *     top-R.
  * Gathered buffers hold rank g's block at word g * words. ------------------- */
-void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint64_t* words1, uint64_t* words2,
+void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint32_t dim, uint64_t* words1, uint64_t* words2,
                       uint64_t* scratch_bytes);
 uint64_t gvdb_shard_flat_words(uint64_t B, uint64_t k);
-/* Phase 1: this rank's exchange-1 block (an empty shard: count 0). */
+/* Phase 1: this rank's exchange-1 block (an empty shard: count 0).  d_scratch
+ * (scratch_bytes of device memory, NULL allowed when R <= 8192) keeps the deep
+ * form's local membership for phase 2: pass the same scratch to both. */
 gvdb_status gvdb_shard_stage1_device(const gvdb_index* shard, const float* d_queries, uint64_t B, uint32_t dim,
-                                     uint64_t R, uint32_t* d_block1, void* stream);
+                                     uint64_t R, uint32_t* d_block1, void* d_scratch, void* stream);
 /* Phase 2: from the gathered exchange-1 blocks, this rank's exchange-2 block
  * (global top-R, exact cosine of the owned rows, local top-k).  d_scratch:
  * scratch_bytes of device memory. */
@@ -388,6 +398,13 @@ gvdb_status gvdb_shard_flat_final_device(const uint32_t* d_gathered, uint64_t G,
  * entries' cosines and ids (in own_pos order); final = phase 3. */
 gvdb_status gvdb_shard_merge_host(const uint32_t* gathered1, uint64_t G, uint64_t rank, uint64_t B, uint64_t R,
                                   uint32_t* own_rows, uint32_t* own_pos, uint32_t* own_cnt, uint32_t* reff);
+/* Deep form of phase 2's merge: this rank's members (m_rows / m_dist [B][R],
+ * the first min(its count, R) valid, any order) -> its owned entries sorted by
+ * (Hamming, row) in own_rows / own_dist [B][R]; pass own_dist as local_topk's
+ * own_pos. */
+gvdb_status gvdb_shard_deep_own_host(const uint32_t* gathered1, uint64_t G, uint64_t rank, uint64_t B, uint64_t R,
+                                     uint32_t dim, const uint32_t* m_rows, const uint32_t* m_dist,
+                                     uint32_t* own_rows, uint32_t* own_dist, uint32_t* own_cnt, uint32_t* reff);
 gvdb_status gvdb_shard_local_topk_host(const float* scores, const uint32_t* own_pos, const uint64_t* own_ids,
                                        const uint32_t* own_cnt, const uint32_t* reff, uint64_t B, uint64_t R,
                                        uint64_t k, uint32_t err, uint32_t* block2);

@@ -87,7 +87,7 @@ def main():
     log(f"[c3] corpus + {G} shards{' + single index' if single is not None else ''}: {time.time() - t0:.0f}s")
 
     w1, w2, scr = C.c_uint64(), C.c_uint64(), C.c_uint64()
-    L.gvdb_shard_sizes(B, R, k, C.byref(w1), C.byref(w2), C.byref(scr))
+    L.gvdb_shard_sizes(B, R, k, D, C.byref(w1), C.byref(w2), C.byref(scr))
     g1 = torch.zeros((G, w1.value), dtype=torch.int32, device=dev)
     g2 = torch.zeros((G, w2.value), dtype=torch.int32, device=dev)
     scratch = torch.zeros(scr.value, dtype=torch.uint8, device=dev)
@@ -96,7 +96,7 @@ def main():
     on = torch.zeros(B, dtype=torch.int32, device=dev)
 
     def p1(r):
-        gvdb.check(L.gvdb_shard_stage1_device(shards[r]._h, q.data_ptr(), B, D, R, g1[r].data_ptr(), None))
+        gvdb.check(L.gvdb_shard_stage1_device(shards[r]._h, q.data_ptr(), B, D, R, g1[r].data_ptr(), None, None))
 
     def p2(r):
         gvdb.check(L.gvdb_shard_rerank_device(shards[r]._h, q.data_ptr(), B, D, R, k, g1.data_ptr(), G, r,

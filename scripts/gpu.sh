@@ -60,6 +60,12 @@ for t in "${TASKS[@]}"; do
         benchprof)
             run 900 gpurun_out/benchprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python3 bench.py
             grep '^{' gpurun_out/benchprof.log > gpurun_out/benchprof.json || true ;;
+        warm)  # bench.py's scan time vs its warmup count (clock ramp?), then scan_ab, one box
+            run 600 gpurun_out/warm_w3.log python3 -u bench.py --no-cpu-baseline --no-points --b1-queries 0
+            run 600 gpurun_out/warm_w200.log python3 -u bench.py --no-cpu-baseline --no-points --b1-queries 0 --warmup 200
+            SHARD_N=10000000 SCANS="," REPS=1 run 600 gpurun_out/warm_scanab.log python3 -u scripts/scan_ab.py
+            for f in warm_w3 warm_w200; do grep -o '"ms_per_step": [0-9.]*\|"scan": [0-9.]*' gpurun_out/$f.log | tr '\n' ' '; echo; done
+            grep '^\[scan_ab\]' gpurun_out/warm_scanab.log ;;
         scanab)  # stage-1 scan timing at 10M and the 1.25M shard (same box, alternating SCANS)
             SHARD_N=10000000,1250000 SCANS="${SCANS:-,}" REPS=3 run 900 gpurun_out/scanab.log python3 -u scripts/scan_ab.py
             grep '^\[scan_ab\]' gpurun_out/scanab.log ;;

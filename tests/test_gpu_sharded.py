@@ -109,14 +109,15 @@ def emulate_two_exchange(g, shards, q, D, R, k):
     L = g.lib()
     G, B = len(shards), q.shape[0]
     w1, w2, scr = C.c_uint64(), C.c_uint64(), C.c_uint64()
-    L.gvdb_shard_sizes(B, R, k, C.byref(w1), C.byref(w2), C.byref(scr))
+    L.gvdb_shard_sizes(B, R, k, D, C.byref(w1), C.byref(w2), C.byref(scr))
     g1 = torch.zeros((G, w1.value), dtype=torch.int32, device="cuda")
     g2 = torch.zeros((G, w2.value), dtype=torch.int32, device="cuda")
-    scratch = torch.zeros(scr.value, dtype=torch.uint8, device="cuda")
+    scratch = torch.zeros((G, scr.value), dtype=torch.uint8, device="cuda")  # per rank (deep: members kept)
     for r, ix in enumerate(shards):
-        g.check(L.gvdb_shard_stage1_device(ix._h, q.data_ptr(), B, D, R, g1[r].data_ptr(), None))
+        g.check(L.gvdb_shard_stage1_device(ix._h, q.data_ptr(), B, D, R, g1[r].data_ptr(), scratch[r].data_ptr(),
+                                           None))
     for r, ix in enumerate(shards):
-        g.check(L.gvdb_shard_rerank_device(ix._h, q.data_ptr(), B, D, R, k, g1.data_ptr(), G, r, scratch.data_ptr(),
+        g.check(L.gvdb_shard_rerank_device(ix._h, q.data_ptr(), B, D, R, k, g1.data_ptr(), G, r, scratch[r].data_ptr(),
                                            g2[r].data_ptr(), None))
     outs = []
     for _ in range(2):  # every rank runs the same final merge
@@ -168,6 +169,48 @@ def test_two_exchange_g8_equals_single_index_and_oracle(g, oracle_mod, sizes, D,
     assert (got_n == sn).all() and (got_i == si).all() and same_f32(got_s, ss)
     ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R, kind=0)
     assert (got_i == ri[:, :k]).all() and same_f32(got_s, rs[:, :k])
+
+
+@pytest.mark.parametrize("sizes,D,B,R", [
+    # the reference's default depth at shard scale (R > 8192: the deep form,
+    # histogram exchange): uneven shards, an empty one, a shard smaller than the
+    # LDS select (k_select's sorted list), one of 15000 rows < R (every row a
+    # member through k_select_big), batch 128 (FP4-MFMA stage 1)
+    ((60000, 5000, 0, 15000, 80000, 40000, 60000, 60000), 768, 128, 20000),
+    ((9000, 11000, 0, 10000, 12500, 7000, 10000, 10500), 130, 8, 12000),
+])
+def test_deep_two_exchange_g8_equals_single_index_and_oracle(g, oracle_mod, sizes, D, B, R):
+    """The deep two-exchange protocol (R > 8192) with G = 8 ranks emulated on
+    one GPU: bit-identical to one index over the concatenated corpus (the
+    single-device large-R path) and to the oracle's multi_stage_search."""
+    import torch
+
+    k = 10
+    N = sum(sizes)
+    x = rows(700 + D, N, D, dup=120)
+    bounds = np.cumsum((0,) + sizes)
+    for j in range(1, 8):  # equal rows across shard boundaries: cosine ties broken by corpus row
+        if sizes[j] and bounds[j] > 0:
+            x[bounds[j]] = x[3]
+    Q = rows(701 + D, B, D)
+    Q[0] = x[3]
+    Q[1] = x[N - 1]
+    Q[2] = x[bounds[4] + 7]
+    q = torch.from_numpy(Q).cuda()
+    shards = []
+    for r in range(8):
+        ix = g.GpuVectorIndex(dimension=D)
+        if sizes[r]:
+            ix.add_batch(np.arange(bounds[r], bounds[r + 1], dtype=np.uint64), x[bounds[r]:bounds[r + 1]])
+        shards.append(ix)
+    got_i, got_s, got_n = emulate_two_exchange(g, shards, q, D, R, k)
+    si, ss, sn = single_device(g, x, Q, R, k)
+    assert (got_n == sn).all() and (got_i == si).all() and same_f32(got_s, ss)
+    assert got_i[0, 0] == 3 and got_i[1, 0] == N - 1
+    nq = min(B, 12)  # the oracle's stage 1 sorts the whole corpus per query
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q[:nq]), oracle_mod.quantize(x), Q[:nq], x, R,
+                                                   kind=0)
+    assert (got_i[:nq] == ri[:, :k]).all() and same_f32(got_s[:nq], rs[:, :k])
 
 
 def test_sharded_flat_g8_d3072_equals_single_index_and_oracle(g, oracle_mod):
@@ -295,7 +338,7 @@ def test_rccl_sharded_argument_checks(g):
     oi = torch.zeros((2, 10), dtype=torch.int64, device="cuda")
     osc = torch.zeros((2, 10), dtype=torch.float32, device="cuda")
     L = g.lib()
-    for sp in (g.SearchParams(rescore_count=0), g.SearchParams(rescore_count=9000),
+    for sp in (g.SearchParams(rescore_count=0), g.SearchParams(rescore_count=(1 << 20) + 1),
                g.SearchParams(rescore_count=100, metric=1)):
         c = sp.to_c()
         st = L.gvdb_index_search_sharded_device(ix._h, sh._h, q.data_ptr(), 2, D, 10, C.byref(c), oi.data_ptr(),

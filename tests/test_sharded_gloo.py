@@ -231,3 +231,61 @@ def test_sharded_equals_single_corpus(world, oracle_mod, gvdb_lib_path):
     ret = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), ret), nprocs=world, join=True)
     assert dict(ret) == {r: 1 for r in range(world)}
+
+
+N3, D3, B3 = 26000, 64, 4
+
+
+def _worker_deep(rank, world, port, ret, bounds, R):
+    """The deep form (R > 8192): exchange 1 carries the Hamming histograms of
+    the ranks' local top-R; the owned entries and the merge come from the host
+    forms (gvdb_shard_deep_own_host / _local_topk_host / _final_host)."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "grape-vector-db_amd")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import oracle
+    from gvdb.sharded import TwoExchangeSearch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(321)
+    x = rng.standard_normal((N3, D3)).astype(np.float32)
+    x[bounds[1]:bounds[1] + 30] = x[4]  # equal rows across a shard boundary
+    x[7000:7030] = x[4]
+    q = rng.standard_normal((B3, D3)).astype(np.float32)
+    q[0] = x[4]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    xs = x[lo:hi]
+
+    def stage1(qt, r):
+        if hi == lo:
+            return np.zeros((B3, 0), np.uint64), np.zeros((B3, 0), np.uint64)
+        idx, dd = oracle.bq_topr_batch(oracle.quantize(qt.numpy()), oracle.quantize(xs), D3, min(r, hi - lo))
+        perm = np.random.default_rng(rank).permutation(idx.shape[1])  # membership, any order
+        return idx[:, perm], dd[:, perm]
+
+    def cosine(i, local_rows):
+        return np.array([oracle.cosine_manual(q[i], xs[int(j)]) for j in local_rows], np.float32)
+
+    s = TwoExchangeSearch(B3, R, K, torch.device("cpu"), stage1_fn=stage1, cosine_fn=cosine, id_offset=lo, dim=D3)
+    ids, sc, n = s.search(torch.from_numpy(q))
+    ri, rs = oracle.multi_stage_search_batch_r(oracle.quantize(q), oracle.quantize(x), q, x, R)
+    ok = bool((n.numpy() == K).all() and (ids.numpy().astype(np.uint64) == ri[:, :K]).all()
+              and sc.numpy().tobytes() == rs[:, :K].tobytes())
+    ret[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bounds,R", [(2, (0, 13000, N3), 9000), (3, (0, 9000, 9000, N3), 12000),
+                                            (3, (0, 2000, 20000, N3), 20000)])
+def test_deep_two_exchange_equals_single_corpus(world, bounds, R, oracle_mod, gvdb_lib_path):
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_deep, args=(world, _free_port(), ret, bounds, R), nprocs=world, join=True)
+    assert dict(ret) == {r: 1 for r in range(world)}
