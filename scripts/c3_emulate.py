@@ -90,17 +90,19 @@ def main():
     L.gvdb_shard_sizes(B, R, k, D, C.byref(w1), C.byref(w2), C.byref(scr))
     g1 = torch.zeros((G, w1.value), dtype=torch.int32, device=dev)
     g2 = torch.zeros((G, w2.value), dtype=torch.int32, device=dev)
-    scratch = torch.zeros(scr.value, dtype=torch.uint8, device=dev)
+    deep = R > 8192  # the deep form keeps each rank's stage-1 membership in its scratch until phase 2
+    scratch = torch.zeros((G if deep else 1, scr.value), dtype=torch.uint8, device=dev)
     oi = torch.zeros((B, k), dtype=torch.int64, device=dev)
     osc = torch.zeros((B, k), dtype=torch.float32, device=dev)
     on = torch.zeros(B, dtype=torch.int32, device=dev)
 
     def p1(r):
-        gvdb.check(L.gvdb_shard_stage1_device(shards[r]._h, q.data_ptr(), B, D, R, g1[r].data_ptr(), None, None))
+        gvdb.check(L.gvdb_shard_stage1_device(shards[r]._h, q.data_ptr(), B, D, R, g1[r].data_ptr(),
+                                              scratch[r if deep else 0].data_ptr(), None))
 
     def p2(r):
         gvdb.check(L.gvdb_shard_rerank_device(shards[r]._h, q.data_ptr(), B, D, R, k, g1.data_ptr(), G, r,
-                                              scratch.data_ptr(), g2[r].data_ptr(), None))
+                                              scratch[r if deep else 0].data_ptr(), g2[r].data_ptr(), None))
 
     def p3():
         gvdb.check(L.gvdb_shard_final_device(g2.data_ptr(), G, B, k, oi.data_ptr(), osc.data_ptr(), on.data_ptr(),
@@ -161,7 +163,8 @@ def main():
         f"mean {np.mean([p['step_ms'] for p in per_rank]):.4f} ms; final merge {1e3 * t3:.4f} ms")
     cfg = "configs[3]" if D == 3072 else "configs[2]"
     line = {"workload": f"BASELINE {cfg} corpus ({N / 1e6:g}M x {D}) in {G} contiguous shards on one GPU, "
-                        f"two-exchange BQ top-{R} + exact cosine rerank, k={k}, batch {B}",
+                        f"two-exchange{' (deep form)' if deep else ''} BQ top-{R} + exact cosine rerank, k={k}, "
+                        f"batch {B}",
             "per_rank": per_rank, "final_merge_ms": 1e3 * t3, "per_rank_step_max_ms": worst,
             "emulated_qps": B / (worst * 1e-3),
             "emulated_qps_with_surrogates": B / ((worst + 1e3 * (ag1 + ag2)) * 1e-3),

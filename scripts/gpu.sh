@@ -84,6 +84,11 @@ for t in "${TASKS[@]}"; do
         c3prof)
             run 600 gpurun_out/c3prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10
             python3 scripts/trace_summary.py gpurun_out/prof_c3/run_kernel_trace.csv | grep gvdb | head -12 ;;
+        deepprof)  # kernel trace of the deep form (1M, R = 100K, batch 256; 10M, R = 1M, batch 64)
+            run 600 gpurun_out/deepprof_1M.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_deep1M -o run -- python3 scripts/c3_emulate.py --n 1000000 --R 100000 --no-single --oracle-queries 0 --steps 2
+            python3 scripts/trace_summary.py gpurun_out/prof_deep1M/run_kernel_trace.csv > gpurun_out/deep1M_kernels.txt
+            run 900 gpurun_out/deepprof_10M.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_deep10M -o run -- python3 scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --no-single --oracle-queries 0 --steps 2
+            python3 scripts/trace_summary.py gpurun_out/prof_deep10M/run_kernel_trace.csv > gpurun_out/deep10M_kernels.txt ;;
         c3floor)  # c3 per-rank step with the default sample floor vs 131072 / 262144 sample rows (same box)
             for f in 0 131072 262144; do
                 GVDB_SAMPLE_FLOOR=$f run 600 gpurun_out/c3floor_$f.log python3 scripts/c3_emulate.py --oracle-queries 0 --steps 20
@@ -122,6 +127,12 @@ for t in "${TASKS[@]}"; do
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
             BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
             grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;
+        deep)  # the deep two-exchange form at the reference's default ratio: 8 shards of 1M (R = 100K) and 10M (R = 1M)
+            run 900 gpurun_out/deep_1M.log python3 -u scripts/c3_emulate.py --n 1000000 --R 100000 --batch 256 --steps 3 --oracle-queries 8
+            grep '^{' gpurun_out/deep_1M.log > gpurun_out/deep_1M.json
+            run 1100 gpurun_out/deep_10M.log python3 -u scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --steps 2 --oracle-queries 2
+            grep '^{' gpurun_out/deep_10M.log > gpurun_out/deep_10M.json
+            grep '\[c3\]' gpurun_out/deep_1M.log gpurun_out/deep_10M.log ;;
         c4x2)  # config 4 (10M x 3072, 8 shards) on the TWO-exchange protocol, vs one 10M x 3072 index
             run 1100 gpurun_out/c4x2.log python -u scripts/c3_emulate.py --dim 3072 --oracle-queries 0 --steps 10
             grep '^{' gpurun_out/c4x2.log > gpurun_out/c4x2.json; grep '^\[c3\]' gpurun_out/c4x2.log | tail -4 ;;
