@@ -363,9 +363,10 @@ def main():
                                             f"VGPRs, {32 * MX4_QT[w4]} queries per launch, {scan_launches} launches "
                                             f"per batch; achieved over the batch's launches)")
         else:
-            peak, kname = PEAK_FP4_TFLOPS, ("k_scan_mx6 ({0,1} x {+-1} e2m1 dot seeded with thr - |q|, "
-                                            "v_mfma_scale_f32_32x32x64_f8f6f4, rows in VGPRs, sub-tile "
-                                            "boundary pipelined into the next sub-tile's first k-step)")
+            peak, kname = PEAK_FP4_TFLOPS, ("k_scan_mx7 ({0,1} x {+-1} e2m1 dot, rows as the A operand so a "
+                                            "lane's 16 dots share one threshold, v_mfma_scale_f32_32x32x64_f8f6f4, "
+                                            "rows in VGPRs, sub-tile boundary pipelined into the next sub-tile's "
+                                            "first k-step)")
         roof = {
             "kernel": "stage-1 BQ Hamming filter: " + kname,
             "bound": "mfma",
@@ -385,7 +386,7 @@ def main():
         }
     roof.update({
         "frac": roof["achieved"] / peak,
-        "traffic": pmc_traffic("gvdb::k_scan_mx6<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
+        "traffic": pmc_traffic("gvdb::k_scan_mx7<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
         "hbm_bytes_per_launch": n_local * w4 * 16 * scan_launches,

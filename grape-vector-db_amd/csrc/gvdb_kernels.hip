@@ -911,7 +911,7 @@ constexpr int kMx3Threads = 512;
 
 // ---------------------------------------------------------------------------
 // The FP4 stage-1 operands (k_scan_mx5, the round-2/3 scan, replaced by
-// k_scan_mx6 below; k_sample_dense / k_sample_mx use them too).  mx5 had the
+// k_scan_mx7 below; k_sample_dense / k_sample_mx use them too).  mx5 had the
 // same contract as k_scan_mx3 (emit (d << 32 | row) for every row with Hamming
 // d <= thr[q]), three changes measured against it:
 //  * {0,1} x {+-1} operands: a row bit b becomes e2m1 {0, v_c} and a query bit
@@ -984,7 +984,16 @@ __global__ __launch_bounds__(256) void k_qfrag(const uint32_t* __restrict__ qwor
 }
 
 // ---------------------------------------------------------------------------
-// k_scan_mx6: k_scan_mx5 with the sub-tile boundary software-pipelined.
+// k_scan_mx7: k_scan_mx6 with the MFMA operands swapped (A = the rows' FP4
+// fragment, B = the queries'), so D is transposed: lane l holds query
+// 32 qt + (l & 31) and 16 corpus rows.  A lane's 16 accumulators then share
+// ONE threshold, so the sub-tile's first MFMA of a tile takes C = 0 (no seed
+// tile read from LDS right before it, no seed registers) and the test compares
+// the max of the 16 dots with the lane's cq = |q| - thr: d = |q| - dot <= thr
+// <=> dot >= cq.  Same speed as mx6 (0.645 vs 0.649 ms at 10M x 768 x 256,
+// same box), less code; mx6 / mx5 history in DESIGN.md §4.
+//
+// From k_scan_mx6: k_scan_mx5 with the sub-tile boundary software-pipelined.
 // mx5 drains every accumulator after a sub-tile's last k-step, then runs the
 // threshold epilogue of all 8 query tiles, re-seeds them and restarts the
 // A-fragment ring: a boundary with the matrix pipe idle (ablations: epilogue
@@ -1002,9 +1011,9 @@ __global__ __launch_bounds__(256) void k_qfrag(const uint32_t* __restrict__ qwor
 // last partial round (nsub mod waves sub-tiles) is split into (sub-tile,
 // query tile) units of KS MFMAs spread over all waves.
 // Same emit contract as mx5: (d << 32 | row) for every row with d <= thr[q].
-constexpr int kMx6Threads = 512;  // 8 waves per CU, 2 per SIMD
+constexpr int kMx7Threads = 512;  // 8 waves per CU, 2 per SIMD
 template <int W4>
-__global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+__global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const v4i_t* __restrict__ qfrag_g,
                                                            const uint32_t* __restrict__ qpc,
                                                            const uint32_t* __restrict__ thr, uint32_t B,
@@ -1015,12 +1024,12 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
     constexpr int QT = 8;       // query tiles of 32
     constexpr int NM = KS * QT;  // MFMAs per sub-tile
     constexpr uint32_t kWaveStage = 256;  // ~90 emits per wave at 10M x 768 x 256 (overflow: global atomics)
-    constexpr int NW = kMx6Threads / 64;
-    constexpr int PF = 4;  // A-fragment ring depth (in MFMAs): live through the tests, so short
+    constexpr int NW = kMx7Threads / 64;
+    constexpr int PF = 4;  // A-fragment ring depth (in MFMAs; 8: same time)
     static_assert(NM % PF == 0, "the A ring's slot of MFMA m must not depend on the sub-tile");
     __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
-    __shared__ __attribute__((aligned(16))) float seed_lds[QT * 2 * 16];
-    __shared__ float thrc_lds[QT * 32];
+    __shared__ float cq_lds[QT * 32];  // |q| - thr (a query past B: never reached)
+    __shared__ float pc_lds[QT * 32];  // |q|
     __shared__ uint64_t st_key[NW][kWaveStage];
     __shared__ uint8_t st_q[NW][kWaveStage];
     __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
@@ -1048,56 +1057,45 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
         load(gw + W, ring[1]);
     }
 #pragma unroll 4
-    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx6Threads) qfrag[i] = qfrag_g[i];
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx7Threads) qfrag[i] = qfrag_g[i];
     constexpr uint32_t kPadBits = 32u * KW;
     if (tid < QT * 32) {
         const uint32_t q = tid;
         const uint32_t pc = qpc[q];
-        const float tc = q < B ? (float)min(thr[q], kPadBits) : 0.0f;
-        thrc_lds[q] = tc;
-        const uint32_t qt = q >> 5, j = q & 31u, hh = (j >> 2) & 1u, r = (j & 3u) + 4u * (j >> 3);
-        seed_lds[(qt * 2 + hh) * 16 + r] = q < B ? tc - (float)pc : -1.0e9f;
+        cq_lds[q] = q < B ? (float)pc - (float)min(thr[q], kPadBits) : 1.0e9f;
+        pc_lds[q] = (float)pc;
         qcnt[q] = 0u;
     }
     __syncthreads();
+    float cq[QT];  // this lane's query of each tile
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) cq[qt] = cq_lds[qt * 32 + (lane & 31u)];
     const uint32_t nqt = (B + 31u) / 32u;
     uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
     v16f_t acc[QT];
     const int scale1 = 0x7f7f7f7f;
-    auto seed_into = [&](v16f_t& A, uint32_t qt) __attribute__((always_inline)) {
-        const float4* sp = (const float4*)(seed_lds + (qt * 2 + h) * 16);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float4 v = sp[g];
-            A[4 * g + 0] = v.x;
-            A[4 * g + 1] = v.y;
-            A[4 * g + 2] = v.z;
-            A[4 * g + 3] = v.w;
-        }
-    };
-    // threshold test of one query tile (acc = thr - Hamming; a hit is acc >= 0),
-    // emits staged in LDS (overflow straight to the query's buffer)
-    // threshold test of one query tile (acc = thr - Hamming; a hit is acc >= 0).
-    // Common path: the AND of the 16 accumulators (sign bit clear <=> some
-    // value >= 0) and one ballot.  Rare hit path, kept compact (a fully
-    // unrolled per-value path in every inlined copy stops the k-loop unroll):
-    // the tile's values go to the wave's LDS scratch, then a runtime loop over
-    // the groups of 4 values that hold a hit emits them.
-    auto test = [&](const v16f_t& A, uint32_t qt, uint32_t n) __attribute__((always_inline)) {
-        int pa[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-            pa[g] = __float_as_int(A[4 * g]) & __float_as_int(A[4 * g + 1]) & __float_as_int(A[4 * g + 2]) &
-                    __float_as_int(A[4 * g + 3]);
-        const int aand = (pa[0] & pa[1]) & (pa[2] & pa[3]);
-        const bool ok = qt < nqt && n < N;  // padded query tile / row past the end: no emits
-        if (__ballot(ok && aand >= 0)) {
+    // threshold test of one query tile (a hit: dot >= cq).  Common path: the max
+    // of the lane's 16 dots against its cq and one ballot.  Rare hit path, kept
+    // compact: the tile's values go to the wave's LDS scratch, then a runtime
+    // loop over the groups of 4 registers (4 consecutive rows) that hold a hit.
+    // Register r holds row 8 (r / 4) + 4 h + (r % 4) of the sub-tile at n0.
+    auto test = [&](const v16f_t& A, uint32_t qt, uint32_t n0) __attribute__((always_inline)) {
+        // (v_max3_f32 through asm: the dots are finite, no canonicalisation needed)
+        const float m0 = max3f(A[0], A[1], A[2]), m1 = max3f(A[3], A[4], A[5]), m2 = max3f(A[6], A[7], A[8]);
+        const float m3 = max3f(A[9], A[10], A[11]), m4 = max3f(A[12], A[13], A[14]);
+        const float mx = max3f(max3f(m0, m1, m2), m3, max3f(m4, A[15], A[15]));
+        const float c = cq[qt];
+        const bool ok = qt < nqt;  // padded query tile: no emits (a query past B has cq = 1e9)
+        if (__ballot(ok && mx >= c)) {
             float* sc = tscr[wv];
 #pragma unroll
             for (int r = 0; r < 16; ++r) sc[r * 64 + lane] = A[r];
             uint32_t gm = 0;  // groups of 4 with a hit (wave-uniform)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) gm |= __ballot(ok && pa[g] >= 0) ? (1u << g) : 0u;
+            for (int g = 0; g < 4; ++g) {
+                const float gx = max3f(A[4 * g], A[4 * g + 1], max3f(A[4 * g + 2], A[4 * g + 3], A[4 * g + 3]));
+                gm |= __ballot(ok && gx >= c) ? (1u << g) : 0u;
+            }
             // global (address space 1) pointers: a flat atomic / store here would count in
             // lgkmcnt too and make every later LDS wait of the stream a full lgkmcnt(0)
             typedef __attribute__((address_space(1))) uint32_t g_u32;
@@ -1106,7 +1104,8 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
             g_u64* bf = (g_u64*)buf;
             uint32_t bcap = bufcap;
             asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
-            const uint32_t rb = qt * 32u + 4u * h;
+            const uint32_t qi = qt * 32u + (lane & 31u);
+            const float pcl = pc_lds[qi];
 #pragma unroll 1
             while (gm) {
                 const uint32_t g = __builtin_ctz(gm);
@@ -1115,13 +1114,13 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t r = 4u * g + (uint32_t)j;
                     const float v = sc[r * 64u + lane];
-                    const bool hit = ok && v >= 0.0f;
+                    const uint32_t n = n0 + 8u * g + 4u * h + (uint32_t)j;
+                    const bool hit = ok && v >= c && n < N;
                     const uint64_t m = __ballot(hit);
                     if (hit) {
                         const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
                                                        (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        const uint32_t qi = rb + (uint32_t)j + 8u * g;
-                        const uint32_t d = (uint32_t)(int)(thrc_lds[qi] - v);
+                        const uint32_t d = (uint32_t)(int)(pcl - v);
                         const uint64_t key = ((uint64_t)d << 32) | n;
                         if (sp < kWaveStage) {
                             st_key[wv][sp] = key;
@@ -1150,8 +1149,6 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
         return *(lds_v4i_t*)ad;
     };
     if (nround > 0) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) seed_into(acc[qt], qt);
         v4i_t ar[PF];
 #pragma unroll
         for (int m = 0; m < PF; ++m) ar[m] = afrag(m);
@@ -1160,7 +1157,7 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
         // first MFMA here; the slot is refilled with sub-tile sb + 2W after its
         // last expansion
         auto step = [&](uint2 (&c)[W4], uint32_t sb, bool prev, uint32_t sbp) __attribute__((always_inline)) {
-            const uint32_t np = sbp * 32u + (lane & 31u);
+            const uint32_t np = sbp * 32u;  // the previous sub-tile's first row
 #pragma unroll
             for (int p = 0; p < W4; ++p)  // this slot's loads are the older of the two in flight
                 asm volatile("s_waitcnt vmcnt(%1)" : "+v"(c[p]) : "n"(W4));
@@ -1170,31 +1167,30 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
             // position qt tests tile qt of the previous sub-tile (its last MFMA is
             // 7 MFMAs old; the pad + the asm naming acc[qt] keep every read below
             // it), re-seeds it, then issues its first MFMA of this sub-tile
-#define GVDB_MX6_POS0(qt)                                                      \
+#define GVDB_MX7_POS0(qt)                                                      \
             {                                                                  \
                 __builtin_amdgcn_sched_barrier(0);                             \
                 if (prev) {                                                    \
                     asm volatile("s_nop 4" : "+v"(acc[qt]));                   \
                     test(acc[qt], (uint32_t)(qt), np);                         \
-                    seed_into(acc[qt], (uint32_t)(qt));                        \
                 }                                                              \
                 const v4i_t a = ar[(qt) % PF];                                 \
                 ar[(qt) % PF] = afrag(((qt) + PF) % NM);                        \
-                mfma_fp4_acc_nop(acc[qt], a, bcur, scale1);                   \
+                mfma_fp4_first_nop(acc[qt], bcur, a, scale1);                 \
                 if ((qt) == 1) {                                               \
                     const uint2 v = c[0];                                      \
                     bnext = fp4_row01(v.y);                                    \
                 }                                                              \
             }
-            GVDB_MX6_POS0(0)
-            GVDB_MX6_POS0(1)
-            GVDB_MX6_POS0(2)
-            GVDB_MX6_POS0(3)
-            GVDB_MX6_POS0(4)
-            GVDB_MX6_POS0(5)
-            GVDB_MX6_POS0(6)
-            GVDB_MX6_POS0(7)
-#undef GVDB_MX6_POS0
+            GVDB_MX7_POS0(0)
+            GVDB_MX7_POS0(1)
+            GVDB_MX7_POS0(2)
+            GVDB_MX7_POS0(3)
+            GVDB_MX7_POS0(4)
+            GVDB_MX7_POS0(5)
+            GVDB_MX7_POS0(6)
+            GVDB_MX7_POS0(7)
+#undef GVDB_MX7_POS0
             bcur = bnext;
 #pragma unroll
             for (int s = 1; s < KS; ++s) {
@@ -1205,7 +1201,7 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
                     const int m = s * QT + qt;
                     const v4i_t a = ar[m % PF];
                     ar[m % PF] = afrag((m + PF) % NM);  // the ring runs on into the next sub-tile
-                    mfma_fp4_acc(acc[qt], a, bcur, scale1);
+                    mfma_fp4_acc(acc[qt], bcur, a, scale1);
                     if (qt == 1 && s + 1 < KS) {  // next k-step's row fragment under this one's MFMAs
                         const uint2 v = c[(s + 1) >> 1];
                         bnext = fp4_row01(((s + 1) & 1) ? v.y : v.x);
@@ -1223,7 +1219,7 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
             if (i + 1 < nround) step(ring[1], sb + W, true, sb);
         }
         asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
-        const uint32_t nl = (gw + (nround - 1u) * W) * 32u + (lane & 31u);
+        const uint32_t nl = (gw + (nround - 1u) * W) * 32u;
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             asm volatile("" : "+v"(acc[qt]));
@@ -1246,17 +1242,19 @@ __global__ __launch_bounds__(kMx6Threads, 1) void k_scan_mx6(const uint4* __rest
 #pragma unroll
         for (int p = 0; p < W4; ++p) c[p] = *(const uint2*)((const char*)(codes + (uint64_t)p * cap) + voff);
         v16f_t& A = acc[0];
-        seed_into(A, qt);
         const v4i_t* qa = qf + qt * 64u;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const uint2 v = c[s >> 1];
             const v4i_t b = fp4_row01((s & 1) ? v.y : v.x);
             const v4i_t a = qa[s * QT * 64];
-            mfma_fp4_acc_nop(A, a, b, scale1);
+            if (s == 0)
+                mfma_fp4_first_nop(A, b, a, scale1);
+            else
+                mfma_fp4_acc_nop(A, b, a, scale1);
         }
         asm volatile("s_nop 15\n\ts_nop 15" : "+v"(A));
-        test(A, qt, n);
+        test(A, qt, sb * 32u);
     }
     flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase, counts,
                                       buf, bufcap);
@@ -1334,15 +1332,16 @@ static void launch_qfrag_t(const Stage1Args& a, hipStream_t s) {
 }
 
 template <int W4>
-static void launch_scan_mx6_t(const Stage1Args& a, hipStream_t s) {
+static void launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
     constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
     for (uint32_t g = 0; g < a.B; g += 256) {
         const uint32_t bg = min(256u, a.B - g);
-        hipLaunchKernelGGL((k_scan_mx6<W4>), dim3(cu_count()), dim3(kMx6Threads), 0, s, a.codes, a.cap, a.N,
+        hipLaunchKernelGGL((k_scan_mx7<W4>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap, a.N,
                            (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
                            a.buf + (uint64_t)g * a.bufcap, a.bufcap);
     }
 }
+
 
 // k_scan_mx4: k_scan_mx3 for WIDE codes (D > 768, e.g. 3072 bits = 24 planes,
 // SURVEY config 4).  The whole batch's expanded query fragments no longer fit
@@ -2089,10 +2088,10 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
         }
     } else if (mfma) {  // FP4 block-scaled MFMA, {0,1} x {+-1} operands (default for large batches)
         switch (W4) {
-            case 2: launch_scan_mx6_t<2>(a, s); break;
-            case 3: launch_scan_mx6_t<3>(a, s); break;
-            case 4: launch_scan_mx6_t<4>(a, s); break;
-            default: launch_scan_mx6_t<6>(a, s); break;
+            case 2: launch_scan_mx7_t<2>(a, s); break;
+            case 3: launch_scan_mx7_t<3>(a, s); break;
+            case 4: launch_scan_mx7_t<4>(a, s); break;
+            default: launch_scan_mx7_t<6>(a, s); break;
         }
     } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \

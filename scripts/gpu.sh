@@ -66,6 +66,13 @@ for t in "${TASKS[@]}"; do
             SHARD_N=10000000 SCANS="," REPS=1 run 600 gpurun_out/warm_scanab.log python3 -u scripts/scan_ab.py
             for f in warm_w3 warm_w200; do grep -o '"ms_per_step": [0-9.]*\|"scan": [0-9.]*' gpurun_out/$f.log | tr '\n' ' '; echo; done
             grep '^\[scan_ab\]' gpurun_out/warm_scanab.log ;;
+        ablscan)  # k_scan timing variants (abl/libgvdb_NAME.so, scripts/build_variant.sh) against the product
+                  # build, one box; VARIANTS: space-separated names ("base" = the product build)
+            for v in ${VARIANTS:-base}; do
+                lib=""; [ "$v" != base ] && lib=grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib SHARD_N=10000000 SCANS="" REPS=2 run 300 gpurun_out/ablscan_$v.log python3 -u scripts/scan_ab.py
+                echo "$v $(grep '^\[scan_ab\]' gpurun_out/ablscan_$v.log | tail -1)"
+            done ;;
         scanab)  # stage-1 scan timing at 10M and the 1.25M shard (same box, alternating SCANS)
             SHARD_N=10000000,1250000 SCANS="${SCANS:-,}" REPS=3 run 900 gpurun_out/scanab.log python3 -u scripts/scan_ab.py
             grep '^\[scan_ab\]' gpurun_out/scanab.log ;;

@@ -3,7 +3,7 @@
 same command (profiles/rNN/): the average duration of exactly the launches
 bench.py times with HIP events --
 
-* batch 256: k_scan_mx6 launches (warmup + 1) .. (warmup + steps) in order
+* batch 256: k_scan_mx7 launches (warmup + 1) .. (warmup + steps) in order
   (the search loop is the first user of the scan; warmup steps come first);
 * batch 1: the first `b1` k_b1_scan launches (the pass whose HIP events give
   batch1.roofline.avg_launch_ms);
@@ -33,12 +33,12 @@ def main():
                 if r["Kernel_Name"].startswith(prefix)]
 
     out = {}
-    scan = durs("void gvdb::k_scan_mx6<")[a.warmup:a.warmup + a.steps]
+    scan = durs("void gvdb::k_scan_mx7<")[a.warmup:a.warmup + a.steps]
     if scan:
         roof = bench["roofline"]
         avg = sum(scan) / len(scan)
         ach = roof["algorithmic_ops_per_launch"] / (avg * 1e-3) / 1e12
-        out["batch256"] = {"kernel": "k_scan_mx6", "launches": len(scan), "avg_launch_ms_rocprof": avg,
+        out["batch256"] = {"kernel": "k_scan_mx7", "launches": len(scan), "avg_launch_ms_rocprof": avg,
                            "avg_launch_ms_hip_events": roof["avg_launch_ms"], "achieved_rocprof": ach,
                            "frac_rocprof": ach / roof["peak"], "frac_hip_events": roof["frac"],
                            "agreement": avg / roof["avg_launch_ms"]}
