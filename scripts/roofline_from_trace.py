@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("bench")
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--b1", type=int, default=200)
     a = ap.parse_args()
