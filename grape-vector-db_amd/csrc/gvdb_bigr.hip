@@ -165,6 +165,110 @@ hipError_t launch_select_big(const Stage1Args& a, hipStream_t s) {
     return hipSuccess;
 }
 
+// ---- dense select (Stage1Args::dense_sel): one block per query over its row of
+// f16 dots (k_scan_mx7<DENSE>): the Hamming distance of row n is |q| - dot; the
+// members are every row with d < T plus the first R - count(< T) rows tied at
+// T in row order -- k_select_big's rule, with every distance known (no
+// candidate buffer, nothing to certify).
+__device__ __forceinline__ uint32_t dense_d(uint32_t h16, float pc) {
+    return (uint32_t)(int)(pc - (float)__builtin_bit_cast(_Float16, (uint16_t)h16));
+}
+
+__global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __restrict__ dense, uint32_t np,
+                                                              uint32_t N, uint32_t D, uint32_t R,
+                                                              const uint32_t* __restrict__ qpc,
+                                                              uint32_t* __restrict__ s1_rows,
+                                                              uint32_t* __restrict__ s1_dist) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+    uint32_t* bins = hist + ((D + 4u) & ~3u);
+    __shared__ uint32_t s_T, s_lt, s_n, s_cut, s_below;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const uint16_t* dq = dense + (uint64_t)q * np;
+    const float pc = (float)qpc[q];
+    uint32_t* orow = s1_rows + (uint64_t)q * R;
+    uint32_t* odist = s1_dist + (uint64_t)q * R;
+    const uint32_t nv = (N + 7u) / 8u;  // 8 rows per 16-B load (the row stride is a multiple of 32)
+    // visit(fn): fn(row, d) for every row, 16-B coalesced loads
+    auto visit = [&](auto fn) __attribute__((always_inline)) {
+        for (uint32_t v = tid; v < nv; v += nt) {
+            const uint4 w = ((const uint4*)dq)[v];
+            const uint32_t n0 = 8u * v;
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (n0 + 2u * j < N) fn(n0 + 2u * j, dense_d(ws[j] & 0xffffu, pc));
+                if (n0 + 2u * j + 1u < N) fn(n0 + 2u * j + 1u, dense_d(ws[j] >> 16, pc));
+            }
+        }
+    };
+    for (uint32_t i = tid; i <= D; i += nt) hist[i] = 0u;
+    if (tid == 0) s_n = 0u;
+    __syncthreads();
+    visit([&](uint32_t, uint32_t d) { atomicAdd(&hist[min(d, D)], 1u); });
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t t = wave_find_cum(hist, D + 1u, R);
+        const uint32_t lt = wave_sum_below(hist, t);
+        if (tid == 0) {
+            s_T = t;
+            s_lt = lt;
+        }
+    }
+    __syncthreads();
+    const uint32_t T = s_T, need = R - s_lt;
+    uint32_t cut = ~0u;  // tied rows with row <= cut are members
+    if (hist[T] > need) {
+        uint32_t left = need, prefix = 0u, pmask = 0u;
+        for (int pass = 0; pass < 3; ++pass) {
+            const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+            const uint32_t nb = pass == 2 ? 1024u : 2048u, dm = nb - 1u;
+            for (uint32_t i = tid; i < nb; i += nt) bins[i] = 0u;
+            __syncthreads();
+            visit([&](uint32_t n, uint32_t d) {
+                if (d == T && (n & pmask) == prefix) atomicAdd(&bins[(n >> shift) & dm], 1u);
+            });
+            __syncthreads();
+            if (tid < 64) {
+                const uint32_t bin = wave_find_cum(bins, nb, left);
+                const uint32_t below = wave_sum_below(bins, bin);
+                if (tid == 0) {
+                    s_cut = bin;
+                    s_below = below;
+                }
+            }
+            __syncthreads();
+            left -= s_below;
+            prefix |= s_cut << shift;
+            pmask |= dm << shift;
+            __syncthreads();
+        }
+        cut = prefix;
+    }
+    // members (wave-aggregated appends: the list is unordered, as k_select_big's)
+    for (uint32_t v0 = 0; v0 < nv; v0 += nt) {
+        const uint32_t v = v0 + tid;
+        uint4 w = make_uint4(0u, 0u, 0u, 0u);
+        if (v < nv) w = ((const uint4*)dq)[v];
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t n = 8u * v + (uint32_t)j;
+            const uint32_t d = dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc);
+            const bool keep = v < nv && n < N && (d < T || (d == T && n <= cut));
+            big_append(keep, n, d, &s_n, orow, odist, R);
+        }
+    }
+}
+
+hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hipStream_t s) {
+    if (bg == 0) return hipSuccess;
+    const size_t lds = (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
+    hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
+                       a.qpc + g0, a.s1_rows + (uint64_t)g0 * a.R, a.s1_dist + (uint64_t)g0 * a.R);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 // ---- final: the first k of the stable cosine sort of an unordered stage-1 list
 constexpr uint32_t kTopkBigMax = 1024;  // k
 constexpr uint32_t kTieLds = 4096;      // tied entries sorted in LDS (more: radix select)
@@ -327,7 +431,7 @@ __global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restric
             uint64_t id = kOrphan;
             uint32_t e = 0;
             if (i < k) {
-                e = L.srt[i];
+                e = min(L.srt[i], R - 1u);  // (an index past the list would need duplicate rows in it)
                 id = ids ? ids[rw[e]] : (uint64_t)rw[e] + row_offset;
             }
             const bool keep = i < k && id != kOrphan;
@@ -366,7 +470,7 @@ __global__ __launch_bounds__(kBigThreads) void k_shard_deep_topk(const float* __
     const uint32_t take = big_topk_order(L, m_cos + base, m_rows + base, m_dist + base, c, kout, 1);
     uint32_t* ent = block2 + (uint64_t)q * kout * 4u;
     for (uint32_t t = tid; t < take; t += blockDim.x) {
-        const uint32_t e = L.srt[t];
+        const uint32_t e = min(L.srt[t], c - 1u);  // (an index past the list would need duplicate rows in it)
         const uint32_t row = m_rows[base + e];
         const uint64_t id = ids ? ids[row] : (uint64_t)row;
         ent[4 * t + 0] = __float_as_uint(m_cos[base + e]);

@@ -324,8 +324,10 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
             p += ng * 256u * 4u;
         }
         if (s1.sample_mode == kSampleDense) s1.smp = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+        if (s1.dense_sel) s1.dense = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
     }
     HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
+    if (s1.dense_sel) s1.bufcap = 1;  // no candidate buffer: every distance goes to the dense block
     HIP_TRY(ws.buf.ensure((size_t)B * s1.bufcap * 8), "alloc candidate buffer");
     if (lists) {  // else the caller points s1_rows / s1_dist at its own buffers
         HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");

@@ -92,12 +92,18 @@ struct Stage1Args {
     uint32_t* zero;          // mfma_scan: words k_qfrag zeroes before stage 1 (else the caller memsets)
     uint32_t nzero;
     int big_select;          // R > kSelectLdsCap: k_select_big (unordered exact top-R membership)
+    int dense_sel;           // big_select at density R/N >= 1/64 with an FP4 scan width: every distance is
+                             // written (k_scan_mx7<DENSE>, f16 dots) and k_select_dense picks the members
+    uint16_t* dense;         // dense_sel: [min(B, 256)][dense_np] f16 dots of one 256-query group
+    uint32_t dense_np;       //   row stride (N rounded up to 32)
     const float* qf32;       // mfma_scan: the f32 queries [B][D] -- k_qprep packs qcodes itself
     float qthr;              //   (packing threshold)
 };
 // ---- large rescore depth (gvdb_bigr.hip): R up to 2^20, D < 4096, k <= 1024 --------
 constexpr uint32_t kBigRMax = 1u << 20;
 hipError_t launch_select_big(const Stage1Args& a, hipStream_t s);
+// dense_sel: the members of queries [g0, g0 + bg) from their dense f16 dots (gvdb_bigr.hip)
+hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hipStream_t s);
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
@@ -359,8 +365,9 @@ hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint3
 // Deep two-exchange (R > kSelectLdsCap; gvdb_shard.hip):
 //   block 1 deep: hist u32 [B][dim+1] (Hamming histogram of the local top-min(R, n)
 //                 membership) | counts u32 [B] | err u32 | pad
-//   scratch deep: member rows u32 [B][R] | member dist u32 [B][R] | cosines f32 [B][R]
-//                 | own count u32 [B] | reff u32 [B]   (lists dense with stride Rl = min(R, n))
+//   scratch deep: member rows u32 [B][R] | member dist u32 [B][R] | owned rows u32 [B][R] |
+//                 owned dist u32 [B][R] | cosines f32 [B][R] | own count u32 [B] | reff u32 [B]
+//                 (lists dense with stride Rl = min(R, n); phase 2 reads the members only)
 inline bool shard_deep(uint64_t R) { return R > kSelectLdsCap; }
 inline uint64_t shard_words1_deep(uint64_t B, uint32_t dim) { return (B * (dim + 1ull) + B + 1 + 1) & ~1ull; }
 gvdb_status shard_stage1_members(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t R,
@@ -368,8 +375,9 @@ gvdb_status shard_stage1_members(const gvdb_index* ix, const float* d_q, uint64_
 hipError_t launch_shard_member_hist(const uint32_t* m_dist, uint32_t B, uint32_t Rl, uint32_t H, uint32_t* block1,
                                     hipStream_t s);
 hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
-                                 uint32_t R, uint32_t Rl, uint32_t H, uint32_t* m_rows, uint32_t* m_dist,
-                                 uint32_t* own_cnt, uint32_t* reff, hipStream_t s);
+                                 uint32_t R, uint32_t Rl, uint32_t H, const uint32_t* m_rows, const uint32_t* m_dist,
+                                 uint32_t* o_rows, uint32_t* o_dist, uint32_t* own_cnt, uint32_t* reff,
+                                 hipStream_t s);
 // gvdb_bigr.hip: the owned entries' local top-k (k <= 1024) -> the exchange-2 block
 hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,

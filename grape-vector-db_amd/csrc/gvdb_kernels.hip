@@ -1012,13 +1012,17 @@ __global__ __launch_bounds__(256) void k_qfrag(const uint32_t* __restrict__ qwor
 // query tile) units of KS MFMAs spread over all waves.
 // Same emit contract as mx5: (d << 32 | row) for every row with d <= thr[q].
 constexpr int kMx7Threads = 512;  // 8 waves per CU, 2 per SIMD
-template <int W4>
+// DENSE (the reference's default depth, R/N >= 1/64): no threshold test; every
+// tile's 16 dots per lane go to dense[q][row] as f16 (exact: |dot| <= 768),
+// four consecutive rows per 8-byte store; the select reads d = |q| - dot.
+template <int W4, bool DENSE>
 __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const v4i_t* __restrict__ qfrag_g,
                                                            const uint32_t* __restrict__ qpc,
                                                            const uint32_t* __restrict__ thr, uint32_t B,
                                                            uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
-                                                           uint32_t bufcap) {
+                                                           uint32_t bufcap, uint16_t* __restrict__ dense,
+                                                           uint32_t dense_np) {
     constexpr int KW = 4 * W4;  // 32-bit code words per row
     constexpr int KS = KW / 2;  // k-steps of 64 bits
     constexpr int QT = 8;       // query tiles of 32
@@ -1062,7 +1066,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     if (tid < QT * 32) {
         const uint32_t q = tid;
         const uint32_t pc = qpc[q];
-        cq_lds[q] = q < B ? (float)pc - (float)min(thr[q], kPadBits) : 1.0e9f;
+        cq_lds[q] = DENSE ? 0.0f : q < B ? (float)pc - (float)min(thr[q], kPadBits) : 1.0e9f;
         pc_lds[q] = (float)pc;
         qcnt[q] = 0u;
     }
@@ -1080,6 +1084,30 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     // loop over the groups of 4 registers (4 consecutive rows) that hold a hit.
     // Register r holds row 8 (r / 4) + 4 h + (r % 4) of the sub-tile at n0.
     auto test = [&](const v16f_t& A, uint32_t qt, uint32_t n0) __attribute__((always_inline)) {
+        if constexpr (DENSE) {
+            const uint32_t qi = qt * 32u + (lane & 31u);
+            if (qt < nqt && qi < B) {
+                typedef __attribute__((address_space(1))) uint64_t g_u64;
+                typedef __attribute__((address_space(1))) uint16_t g_u16;
+                const uint64_t base = (uint64_t)qi * dense_np;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const uint32_t row = n0 + 8u * (uint32_t)g + 4u * h;  // rows row .. row + 3
+                    const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[4 * g], A[4 * g + 1]));
+                    const uint32_t hi =
+                        __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[4 * g + 2], A[4 * g + 3]));
+                    if (row + 3u < N) {
+                        *(g_u64*)(dense + base + row) = ((uint64_t)hi << 32) | lo;
+                    } else {
+                        const uint32_t v4[4] = {lo & 0xffffu, lo >> 16, hi & 0xffffu, hi >> 16};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (row + (uint32_t)j < N) *(g_u16*)(dense + base + row + j) = (uint16_t)v4[j];
+                    }
+                }
+            }
+            return;
+        }
         // (v_max3_f32 through asm: the dots are finite, no canonicalisation needed)
         const float m0 = max3f(A[0], A[1], A[2]), m1 = max3f(A[3], A[4], A[5]), m2 = max3f(A[6], A[7], A[8]);
         const float m3 = max3f(A[9], A[10], A[11]), m4 = max3f(A[12], A[13], A[14]);
@@ -1256,8 +1284,9 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         asm volatile("s_nop 15\n\ts_nop 15" : "+v"(A));
         test(A, qt, sb * 32u);
     }
-    flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase, counts,
-                                      buf, bufcap);
+    if constexpr (!DENSE)
+        flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase,
+                                          counts, buf, bufcap);
 }
 
 // CUs of the current device (cached per device: read on every launch)
@@ -1332,14 +1361,25 @@ static void launch_qfrag_t(const Stage1Args& a, hipStream_t s) {
 }
 
 template <int W4>
-static void launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
+static hipError_t launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
     constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
     for (uint32_t g = 0; g < a.B; g += 256) {
         const uint32_t bg = min(256u, a.B - g);
-        hipLaunchKernelGGL((k_scan_mx7<W4>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap, a.N,
-                           (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
+        if (a.dense_sel) {  // every distance of the group, then its members (the dense block is reused per group)
+            hipLaunchKernelGGL((k_scan_mx7<W4, true>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap, a.N,
+                               (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
+                               a.buf, a.bufcap, a.dense, a.dense_np);
+            GVDB_LAUNCH_CHECK();
+            const hipError_t e = launch_select_dense(a, g, bg, s);
+            if (e != hipSuccess) return e;
+        } else {
+            hipLaunchKernelGGL((k_scan_mx7<W4, false>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap,
+                               a.N, (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
+                               a.buf + (uint64_t)g * a.bufcap, a.bufcap, nullptr, 0u);
+            GVDB_LAUNCH_CHECK();
+        }
     }
+    return hipSuccess;
 }
 
 
@@ -2015,12 +2055,23 @@ size_t stage1_plan(Stage1Args& a) {
             a.sample_mode = kSampleMxHist;
         }
     }
+    // the reference's default depth (R = 0.1 N): at R/N >= 1/64 the threshold scan would emit
+    // a large share of all (row, query) pairs through its hit path; write every distance
+    // instead (one f16 per pair, 256 queries at a time) and select from the dense block
+    a.dense_sel = a.big_select && a.use_mfma == 1 && mfma_scan_supported(W4) && (uint64_t)a.R * 64u >= a.N &&
+                  !getenv_flag_eq("GVDB_DENSE_SEL", "0");
+    if (a.dense_sel) {
+        a.mfma_scan = true;  // the FP4 scan at any batch size (padded query slots)
+        a.sample_mode = kSampleValu;
+        a.dense_np = (a.N + 31u) & ~31u;
+    }
     size_t bytes = 0;
-    if (big) {
+    if (a.mfma_scan) {
         const uint64_t ng = (a.B + 255u) / 256u;
         bytes += ng * (8u * 2u * W4 * 64u * 16u + 256u * 4u);
     }
     if (a.sample_mode == kSampleDense) bytes += (size_t)a.B * (S / 16u) * 2u + 256u;
+    if (a.dense_sel) bytes += (size_t)std::min<uint32_t>(a.B, 256u) * a.dense_np * 2u + 256u;
     return bytes;
 }
 
@@ -2035,6 +2086,23 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             default: launch_qfrag_t<6>(a, s); break;
         }
         GVDB_LAUNCH_CHECK();
+    }
+    if (a.dense_sel) {
+        // no threshold: every distance is written and selected exactly (the scan below)
+        if (a.ev) (void)hipEventRecord(a.ev[1], s);
+        hipError_t e = hipSuccess;
+        switch (W4) {
+            case 2: e = launch_scan_mx7_t<2>(a, s); break;
+            case 3: e = launch_scan_mx7_t<3>(a, s); break;
+            case 4: e = launch_scan_mx7_t<4>(a, s); break;
+            default: e = launch_scan_mx7_t<6>(a, s); break;
+        }
+        if (e != hipSuccess) return e;
+        if (a.ev) {
+            (void)hipEventRecord(a.ev[2], s);
+            (void)hipEventRecord(a.ev[3], s);
+        }
+        return hipSuccess;
     }
     if (a.sample_mode == kSampleDense) {
         switch (W4) {
@@ -2087,12 +2155,14 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             default: launch_scan_mx4_t<32, 8, 1>(a, s); break;
         }
     } else if (mfma) {  // FP4 block-scaled MFMA, {0,1} x {+-1} operands (default for large batches)
+        hipError_t e = hipSuccess;
         switch (W4) {
-            case 2: launch_scan_mx7_t<2>(a, s); break;
-            case 3: launch_scan_mx7_t<3>(a, s); break;
-            case 4: launch_scan_mx7_t<4>(a, s); break;
-            default: launch_scan_mx7_t<6>(a, s); break;
+            case 2: e = launch_scan_mx7_t<2>(a, s); break;
+            case 3: e = launch_scan_mx7_t<3>(a, s); break;
+            case 4: e = launch_scan_mx7_t<4>(a, s); break;
+            default: e = launch_scan_mx7_t<6>(a, s); break;
         }
+        if (e != hipSuccess) return e;
     } else switch (W4) {
 #define GVDB_CASE(w, cpl)             \
     case w:                           \

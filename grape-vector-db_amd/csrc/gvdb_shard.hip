@@ -551,14 +551,17 @@ hipError_t launch_shard_member_hist(const uint32_t* m_dist, uint32_t B, uint32_t
     return hipSuccess;
 }
 
-// step 3 (i) deep: this rank's owned entries of the global top-R, compacted in
-// place (order kept) at the front of its member lists; own_cnt / reff [B].
+// step 3 (i) deep: this rank's owned entries of the global top-R, compacted
+// (order kept) into o_rows / o_dist; own_cnt / reff [B].  The member lists are
+// only read: phase 2 can run again on the same phase-1 scratch.
 constexpr uint32_t kDeepThreads = 1024;
 __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t* __restrict__ gathered,
                                                                  uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
                                                                  uint32_t R, uint32_t Rl, uint32_t H,
-                                                                 uint32_t* __restrict__ m_rows,
-                                                                 uint32_t* __restrict__ m_dist,
+                                                                 const uint32_t* __restrict__ m_rows,
+                                                                 const uint32_t* __restrict__ m_dist,
+                                                                 uint32_t* __restrict__ o_rows,
+                                                                 uint32_t* __restrict__ o_dist,
                                                                  uint32_t* __restrict__ own_cnt,
                                                                  uint32_t* __restrict__ reff) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tot[];  // [H] global histogram, then bins [2048]
@@ -632,10 +635,11 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
         }
         cut = prefix;
     }
-    // order-preserving in-place compaction: a chunk's entries are read before the
-    // block prefix (its barriers), and written at or before their own slots
-    uint32_t* rw = m_rows + (uint64_t)q * Rl;
-    uint32_t* dd = m_dist + (uint64_t)q * Rl;
+    // order-preserving compaction into the owned lists
+    const uint32_t* rw = m_rows + (uint64_t)q * Rl;
+    const uint32_t* dd = m_dist + (uint64_t)q * Rl;
+    uint32_t* orw = o_rows + (uint64_t)q * Rl;
+    uint32_t* odd = o_dist + (uint64_t)q * Rl;
     uint32_t o = 0;
     for (uint32_t base = 0; base < n; base += nt) {
         const uint32_t i = base + tid;
@@ -648,8 +652,8 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
         uint32_t total;
         const uint32_t pos = o + big_prefix(keep, wcnt, &total);
         if (keep) {
-            rw[pos] = row;
-            dd[pos] = d;
+            orw[pos] = row;
+            odd[pos] = d;
         }
         o += total;
     }
@@ -660,13 +664,14 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
 }
 
 hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
-                                 uint32_t R, uint32_t Rl, uint32_t H, uint32_t* m_rows, uint32_t* m_dist,
-                                 uint32_t* own_cnt, uint32_t* reff, hipStream_t s) {
+                                 uint32_t R, uint32_t Rl, uint32_t H, const uint32_t* m_rows, const uint32_t* m_dist,
+                                 uint32_t* o_rows, uint32_t* o_dist, uint32_t* own_cnt, uint32_t* reff,
+                                 hipStream_t s) {
     if (B == 0) return hipSuccess;
     const size_t lds = (size_t)((H + 3u) & ~3u) * 4u + 2048u * 4u;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_shard_deep_own, dim3(B), dim3(kDeepThreads), lds, s, gathered1, words1, G, me, B, R, Rl, H,
-                       m_rows, m_dist, own_cnt, reff);
+                       m_rows, m_dist, o_rows, o_dist, own_cnt, reff);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -692,8 +697,9 @@ void gvdb_shard_sizes(uint64_t B, uint64_t R, uint64_t k, uint32_t dim, uint64_t
     if (words1) *words1 = shard_deep(R) ? shard_words1_deep(B, dim) : shard_words1(B, R);
     if (words2) *words2 = shard_words2(B, k);
     // key form: the owned positions, rows and cosines [B][R] of phase 2 (used when R > 2048);
-    // deep form: the member rows, distances and cosines [B][R], own counts and reff [B]
-    if (scratch_bytes) *scratch_bytes = 12 * B * R + 8 * B + 256;
+    // deep form: the member rows and distances, the owned rows and distances, their
+    // cosines [B][R], own counts and reff [B]
+    if (scratch_bytes) *scratch_bytes = (shard_deep(R) ? 20 : 12) * B * R + 8 * B + 256;
 }
 
 uint64_t gvdb_shard_flat_words(uint64_t B, uint64_t k) { return shard_words_flat(B, k); }
@@ -757,14 +763,17 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
     // phase 1) sent no entries, so it owns none: its rows are never read
     const bool usable = si.n > 0 && si.dim == dim;
     if (deep) {
-        uint32_t* m_rows = (uint32_t*)d_scratch;
+        uint32_t* m_rows = (uint32_t*)d_scratch;  // phase 1's members (read only here)
         uint32_t* m_dist = m_rows + BR;
-        float* m_cos = (float*)(m_dist + BR);
+        uint32_t* o_rows = m_dist + BR;            // the owned members
+        uint32_t* o_dist = o_rows + BR;
+        float* m_cos = (float*)(o_dist + BR);
         uint32_t* own_cnt = (uint32_t*)(m_cos + BR);
         uint32_t* reff = own_cnt + B;
         const uint32_t Rl = usable ? (uint32_t)std::min<uint64_t>(R, si.n) : 0u;
         hipError_t e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
-                                             (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, own_cnt, reff, s);
+                                             (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist,
+                                             own_cnt, reff, s);
         if (e == hipSuccess && Rl > 0) {
             RerankArgs rr{};
             rr.rows = si.rows;
@@ -772,7 +781,7 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
             rr.norms = si.norms;
             rr.q = d_queries;
             rr.qlen = dim;
-            rr.s1_rows = m_rows;
+            rr.s1_rows = o_rows;
             rr.B = (uint32_t)B;
             rr.R = Rl;
             rr.kind = kScoreCosine;
@@ -781,7 +790,7 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
             e = launch_rerank(rr, s);
         }
         if (e == hipSuccess)
-            e = launch_shard_deep_topk(m_cos, m_rows, m_dist, own_cnt, reff, (uint32_t)B, Rl, (uint32_t)k,
+            e = launch_shard_deep_topk(m_cos, o_rows, o_dist, own_cnt, reff, (uint32_t)B, Rl, (uint32_t)k,
                                        usable ? si.ids : nullptr, 0u, d_block2, s);
         if (e != hipSuccess)
             return report_status(GVDB_ERR_DEVICE, std::string("deep shard phase 2: ") + hipGetErrorString(e));

@@ -66,6 +66,12 @@ for t in "${TASKS[@]}"; do
             SHARD_N=10000000 SCANS="," REPS=1 run 600 gpurun_out/warm_scanab.log python3 -u scripts/scan_ab.py
             for f in warm_w3 warm_w200; do grep -o '"ms_per_step": [0-9.]*\|"scan": [0-9.]*' gpurun_out/$f.log | tr '\n' ' '; echo; done
             grep '^\[scan_ab\]' gpurun_out/warm_scanab.log ;;
+        c2)  # BASELINE configs[1]: 1M x 768, batch 256, bench.py's own pipeline at N = 1M
+            run 900 gpurun_out/c2.log python3 -u bench.py --n 1000000
+            grep '^{' gpurun_out/c2.log > gpurun_out/c2.json; tail -c 300 gpurun_out/c2.json; echo ;;
+        c1)  # BASELINE configs[0]: MockEmbeddingProvider 10k x 128
+            run 600 gpurun_out/c1.log python3 -u scripts/config1_mock.py
+            grep '^{' gpurun_out/c1.log > gpurun_out/c1.json; tail -c 300 gpurun_out/c1.json; echo ;;
         ablscan)  # k_scan timing variants (abl/libgvdb_NAME.so, scripts/build_variant.sh) against the product
                   # build, one box; VARIANTS: space-separated names ("base" = the product build)
             for v in ${VARIANTS:-base}; do

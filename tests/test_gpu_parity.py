@@ -229,6 +229,31 @@ def test_default_rescore_ratio_large_r_matches_oracle(g, oracle_mod, monkeypatch
     assert same_f32(sc, rs[:, :k])
 
 
+@pytest.mark.parametrize("dense", ["0", "1"])
+def test_large_r_emit_and_dense_selects_match_oracle(g, oracle_mod, monkeypatch, dense):
+    """Both large-R stage-1 forms at the reference's default ratio on one corpus:
+    GVDB_DENSE_SEL=0 keeps the threshold scan + candidate buffer + k_select_big;
+    the default at R/N >= 1/64 writes every distance (k_scan_mx7<DENSE>, f16 dots)
+    and k_select_dense picks the members.  Duplicate rows make ties at the
+    threshold; a row count that is not a multiple of 8 or 32 leaves a ragged last row block (100001 rows)."""
+    if dense == "0":
+        monkeypatch.setenv("GVDB_DENSE_SEL", "0")
+    N, D, B, k = 100_001, 768, 20, 10
+    x = rng_rows(N + 3, N, D, dup=300)
+    Q = rng_rows(D + 41, B, D)
+    Q[0] = x[N - 1]
+    Q[1] = x[5]
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=0.1))
+    R = int(np.float32(N) * np.float32(0.1))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (n == k).all()
+    assert (ids == ri[:, :k]).all()
+    assert same_f32(sc, rs[:, :k])
+    assert ids[0, 0] == N - 1
+
+
 def test_default_ratio_sampled_mfma_takes_no_rescan(g, oracle_mod, monkeypatch):
     """R/N = 0.1 on a SAMPLED shard (400K rows > the 262144-row exact window)
     with an FP4-MFMA batch (B = 128): the dense FP4 sample keeps one minimum

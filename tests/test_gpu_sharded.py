@@ -99,9 +99,10 @@ def test_g8_packed_merge_d3072_equals_single_index_and_oracle(g, oracle_mod):
     assert got_i[3, 0] == 12_345 and got_i[9, 0] == N - 1
 
 
-def emulate_two_exchange(g, shards, q, D, R, k):
+def emulate_two_exchange(g, shards, q, D, R, k, rerank_twice=False):
     """Run the three phases for every rank on one GPU; returns the merged
-    results of every rank (they must all agree)."""
+    results of every rank (they must all agree).  rerank_twice: phase 2 runs
+    twice on the same phase-1 scratch (it must only read it)."""
     import ctypes as C
 
     import torch
@@ -116,9 +117,10 @@ def emulate_two_exchange(g, shards, q, D, R, k):
     for r, ix in enumerate(shards):
         g.check(L.gvdb_shard_stage1_device(ix._h, q.data_ptr(), B, D, R, g1[r].data_ptr(), scratch[r].data_ptr(),
                                            None))
-    for r, ix in enumerate(shards):
-        g.check(L.gvdb_shard_rerank_device(ix._h, q.data_ptr(), B, D, R, k, g1.data_ptr(), G, r, scratch[r].data_ptr(),
-                                           g2[r].data_ptr(), None))
+    for _ in range(2 if rerank_twice else 1):
+        for r, ix in enumerate(shards):
+            g.check(L.gvdb_shard_rerank_device(ix._h, q.data_ptr(), B, D, R, k, g1.data_ptr(), G, r,
+                                               scratch[r].data_ptr(), g2[r].data_ptr(), None))
     outs = []
     for _ in range(2):  # every rank runs the same final merge
         oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
@@ -203,7 +205,7 @@ def test_deep_two_exchange_g8_equals_single_index_and_oracle(g, oracle_mod, size
         if sizes[r]:
             ix.add_batch(np.arange(bounds[r], bounds[r + 1], dtype=np.uint64), x[bounds[r]:bounds[r + 1]])
         shards.append(ix)
-    got_i, got_s, got_n = emulate_two_exchange(g, shards, q, D, R, k)
+    got_i, got_s, got_n = emulate_two_exchange(g, shards, q, D, R, k, rerank_twice=True)
     si, ss, sn = single_device(g, x, Q, R, k)
     assert (got_n == sn).all() and (got_i == si).all() and same_f32(got_s, ss)
     assert got_i[0, 0] == 3 and got_i[1, 0] == N - 1
