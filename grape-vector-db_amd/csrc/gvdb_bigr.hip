@@ -262,6 +262,7 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
 
 hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hipStream_t s) {
     if (bg == 0) return hipSuccess;
+    if (a.R > a.N || !a.dense) return hipErrorInvalidValue;  // every list slot must be filled
     const size_t lds = (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
     hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
                        a.qpc + g0, a.s1_rows + (uint64_t)g0 * a.R, a.s1_dist + (uint64_t)g0 * a.R);
