@@ -109,7 +109,7 @@ def _worker2(rank, world, port, ret, bounds, R):
     dist.destroy_process_group()
 
 
-def _worker_fail(rank, world, port, ret, bad_rank, phase):
+def _worker_fail(rank, world, port, ret, bad_rank, phase, R=R):
     """One rank's stage 1 (phase 1) or cosine callable (phase 2) raises: every
     rank still completes both all-gathers (no hang), every query of the merge
     is poisoned on every rank, and only the failing rank raises."""
@@ -141,7 +141,7 @@ def _worker_fail(rank, world, port, ret, bad_rank, phase):
             raise ValueError("rerank failed on this shard")
         return np.array([oracle.cosine_manual(q[i], xs[int(j)]) for j in local_rows], np.float32)
 
-    s = TwoExchangeSearch(B, R, K, torch.device("cpu"), stage1_fn=stage1, cosine_fn=cosine, id_offset=lo)
+    s = TwoExchangeSearch(B, R, K, torch.device("cpu"), stage1_fn=stage1, cosine_fn=cosine, id_offset=lo, dim=D)
     raised = False
     try:
         s.search(torch.from_numpy(q))
@@ -152,7 +152,7 @@ def _worker_fail(rank, world, port, ret, bad_rank, phase):
     # a second search on the same ranks still works (nobody is stuck in a collective)
     s2 = TwoExchangeSearch(B, R, K, torch.device("cpu"), stage1_fn=lambda qt, r: oracle.bq_topr_batch(
         oracle.quantize(qt.numpy()), oracle.quantize(xs), D, min(r, hi - lo)), cosine_fn=lambda i, rows: np.array(
-        [oracle.cosine_manual(q[i], xs[int(j)]) for j in rows], np.float32), id_offset=lo)
+        [oracle.cosine_manual(q[i], xs[int(j)]) for j in rows], np.float32), id_offset=lo, dim=D)
     ids, sc, n = s2.search(torch.from_numpy(q))
     ok_after = bool((n.numpy() == K).all())
     ret[rank] = (raised == (rank == bad_rank), poisoned, ok_after)
@@ -196,13 +196,14 @@ def _worker_fail_outputs(rank, world, port, ret):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("phase", [1, 2])
-def test_two_exchange_failing_rank_joins_both_exchanges(phase, oracle_mod, gvdb_lib_path):
+@pytest.mark.parametrize("phase,r", [(1, R), (2, R), (1, 9000), (2, 9000)])
+def test_two_exchange_failing_rank_joins_both_exchanges(phase, r, oracle_mod, gvdb_lib_path):
+    """Key form (R = 40) and deep form (R = 9000 > 8192: histogram exchange)."""
     world = 3
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     ret = mgr.dict()
-    mp.spawn(_worker_fail, args=(world, _free_port(), ret, 1, phase), nprocs=world, join=True)
+    mp.spawn(_worker_fail, args=(world, _free_port(), ret, 1, phase, r), nprocs=world, join=True)
     assert dict(ret) == {r: (True, True, True) for r in range(world)}
 
 
