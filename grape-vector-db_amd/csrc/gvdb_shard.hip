@@ -256,7 +256,9 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
             const uint32_t j0 = ch * kP2Ch, m = min(kP2Ch, D - j0);
             if (tid < nr || fold_q) {
                 const float* tr = fold_q ? qv + j0 : tile + tid * kP2Ld;
-                const float* qc = qv + j0;
+                // the query through the scalar cache (block-uniform address: s_load), not
+                // LDS: half the LDS reads of the fold and no LDS latency on its operand
+                const float* qc = queries + (uint64_t)q * D + j0;
                 float a2 = fold_q ? qq : acc;
                 uint32_t j = 0;
                 if (vec) {

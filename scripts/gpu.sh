@@ -72,6 +72,12 @@ for t in "${TASKS[@]}"; do
         c1)  # BASELINE configs[0]: MockEmbeddingProvider 10k x 128
             run 600 gpurun_out/c1.log python3 -u scripts/config1_mock.py
             grep '^{' gpurun_out/c1.log > gpurun_out/c1.json; tail -c 300 gpurun_out/c1.json; echo ;;
+        c3ab)  # config-3 emulation A/B: VARIANTS (abl/libgvdb_NAME.so, "base" = product) alternating, one box
+            for v in ${VARIANTS:-base}; do
+                lib=""; [ "$v" != base ] && lib=grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib run 300 gpurun_out/c3ab_$v.log python3 -u scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 20
+                echo "$v $(grep 'per-rank step' gpurun_out/c3ab_$v.log) p2 $(grep -o '"merge_rerank_topk_ms": [0-9.]*' gpurun_out/c3ab_$v.log | head -8 | awk '{s+=$2} END {print s/NR}')"
+            done ;;
         ablscan)  # k_scan timing variants (abl/libgvdb_NAME.so, scripts/build_variant.sh) against the product
                   # build, one box; VARIANTS: space-separated names ("base" = the product build)
             for v in ${VARIANTS:-base}; do
