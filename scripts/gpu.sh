@@ -78,6 +78,13 @@ for t in "${TASKS[@]}"; do
                 GVDB_LIB_PATH=$lib run 300 gpurun_out/c3ab_$v.log python3 -u scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 20
                 echo "$v $(grep 'per-rank step' gpurun_out/c3ab_$v.log) p2 $(grep -o '"merge_rerank_topk_ms": [0-9.]*' gpurun_out/c3ab_$v.log | head -8 | awk '{s+=$2} END {print s/NR}')"
             done ;;
+        envab)  # bench.py's batch-256 step under env variants (ENVS: ';'-separated "NAME=V,NAME=V" sets, "-" = none), one box
+            IFS=';' read -ra SETS <<< "${ENVS:--}"
+            for e in "${SETS[@]}" "${SETS[@]}"; do
+                envs=(); [ "$e" != "-" ] && IFS=',' read -ra envs <<< "$e"
+                env "${envs[@]}" timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-points --b1-queries 0 > gpurun_out/envab.log 2>&1 || { tail -20 gpurun_out/envab.log; exit 1; }
+                echo "[$e] $(grep -o '"ms_per_step": [0-9.]*\|"stage_ms_per_step": {[^}]*}' gpurun_out/envab.log | tr '\n' ' ')"
+            done ;;
         ablscan)  # k_scan timing variants (abl/libgvdb_NAME.so, scripts/build_variant.sh) against the product
                   # build, one box; VARIANTS: space-separated names ("base" = the product build)
             for v in ${VARIANTS:-base}; do
