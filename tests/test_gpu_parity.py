@@ -254,6 +254,26 @@ def test_large_r_emit_and_dense_selects_match_oracle(g, oracle_mod, monkeypatch,
     assert ids[0, 0] == N - 1
 
 
+def test_dense_select_query_groups_match_oracle(g, oracle_mod):
+    """Dense large-R stage 1 over more than one 256-query group (B = 300: the
+    dense block is reused by the second group of 44 queries), D = 256."""
+    N, D, B, ratio, k = 60_000, 256, 300, 0.2, 10
+    x = rng_rows(N + 9, N, D, dup=150)
+    Q = rng_rows(D + 53, B, D)
+    Q[0] = x[17]
+    Q[299] = x[N - 2]
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=ratio))
+    R = int(np.float32(N) * np.float32(ratio))
+    assert R > 8192
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (n == k).all()
+    assert (ids == ri[:, :k]).all()
+    assert same_f32(sc, rs[:, :k])
+    assert ids[299, 0] == N - 2
+
+
 def test_default_ratio_sampled_mfma_takes_no_rescan(g, oracle_mod, monkeypatch):
     """R/N = 0.1 on a SAMPLED shard (400K rows > the 262144-row exact window)
     with an FP4-MFMA batch (B = 128): the dense FP4 sample keeps one minimum
@@ -713,6 +733,7 @@ def test_search_filtered_matches_oracle_on_subset(g, oracle_mod, metric):
     (3_000, 48, 5, 0.3, 0, 1),           # R from the subset (M as f32 * 0.1) as usize, L2
     (700_000, 768, 2, 0.6, 100, 0),      # sampled threshold over the 420K-row subset
     (400_000, 768, 128, 0.8, 100, 2),    # the FP4-MFMA scan over the subset, 1 - cosine
+    (200_000, 256, 20, 0.5, 0, 0),       # default ratio over the ~100K-row subset: R ~ 10K, dense stage 1
 ])
 def test_search_filtered_bq_matches_multi_stage_on_subset(g, oracle_mod, N, D, B, keep, R, metric):
     """BQ mode + filter = multi_stage_search (quantization.rs:151-193) over the

@@ -305,6 +305,36 @@ def test_rccl_world1_equals_single_device(g, N, B):
     shf.close()
 
 
+def test_rccl_world1_deep_form_equals_single_device(g):
+    """gvdb_index_search_sharded_device at R = 20000 > 8192 (the deep form:
+    histogram exchange) over a 1-rank communicator: equal to the single-device
+    large-R search."""
+    import torch
+
+    from gvdb.sharded import RcclShardedSearch
+
+    N, D, B, R, k = 150_000, 768, 40, 20_000, 10
+    x = rows(407, N, D, dup=40)
+    Q = rows(408, B, D)
+    Q[2] = x[N // 3]
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    sh = RcclShardedSearch(ix, R, k)
+    q = torch.from_numpy(Q).cuda()
+    oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+    osc = torch.zeros((B, k), dtype=torch.float32, device="cuda")
+    on = torch.zeros(B, dtype=torch.int32, device="cuda")
+    sh.search_into(q, oi, osc, on)
+    sh.search_into(q, oi, osc, on)  # the communicator's buffers reused
+    torch.cuda.synchronize()
+    si, ss, sn = single_device(g, x, Q, R, k)
+    assert (oi.cpu().numpy().view(np.uint64) == si).all()
+    assert same_f32(osc.cpu().numpy(), ss)
+    assert (on.cpu().numpy() == sn).all()
+    assert si[2, 0] == N // 3
+    sh.close()
+
+
 def test_rccl_world1_empty_shard_joins_and_returns_nothing(g):
     """An empty shard still runs the protocol (no early return that would
     leave other ranks in the collective): every query gets 0 results."""
