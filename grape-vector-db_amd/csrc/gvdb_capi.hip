@@ -753,7 +753,9 @@ struct gvdb_index {
     // its stream after its last read of this index; a mutation waits for those
     // events only (not for the whole device)
     mutable std::mutex use_mu;
-    mutable std::vector<hipEvent_t> inflight, ev_free;
+    // per stream that searched this index: an event re-recorded at each search's end
+    // (stream order: the latest record covers the earlier ones on that stream)
+    mutable std::vector<std::pair<hipStream_t, hipEvent_t>> use_ev;
 
     uint32_t w4() const { return code_w4(dim); }
     size_t device_bytes() const {
@@ -793,41 +795,44 @@ gvdb_status quiesce(const gvdb_index* ix) {
     if (st != GVDB_OK) return st;
     std::lock_guard<std::mutex> g(ix->use_mu);
     hipError_t e = hipSuccess;
-    for (hipEvent_t ev : ix->inflight) {
-        const hipError_t e2 = hipEventSynchronize(ev);
+    for (auto& p : ix->use_ev) {
+        const hipError_t e2 = hipEventSynchronize(p.second);
         if (e == hipSuccess) e = e2;
-        ix->ev_free.push_back(ev);
     }
-    ix->inflight.clear();
     if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
     if (e != hipSuccess) return dev_fail(e, "drain in-flight searches");
     return GVDB_OK;
 }
 
-// Record the end of this call's reads of ix on stream s (see quiesce).
+// Record the end of this call's reads of ix on stream s (see quiesce): one
+// event per stream, re-recorded -- O(1) per search (the earlier form queried
+// every in-flight search's event on each call, ~10 us of host time per call
+// once a few dozen searches were queued).
 void track_use(const gvdb_index* ix, hipStream_t s) {
     std::lock_guard<std::mutex> g(ix->use_mu);
-    // recycle the events of searches that have finished
-    size_t w = 0;
-    for (size_t i = 0; i < ix->inflight.size(); ++i) {
-        if (hipEventQuery(ix->inflight[i]) == hipSuccess)
-            ix->ev_free.push_back(ix->inflight[i]);
-        else
-            ix->inflight[w++] = ix->inflight[i];
-    }
-    ix->inflight.resize(w);
+    for (auto& p : ix->use_ev)
+        if (p.first == s) {
+            if (hipEventRecord(p.second, s) != hipSuccess) (void)hipStreamSynchronize(s);
+            return;
+        }
+    if (ix->use_ev.size() >= 16)  // many streams: take over the entry of one whose last search finished
+        for (auto& p : ix->use_ev)
+            if (hipEventQuery(p.second) == hipSuccess) {
+                p.first = s;
+                if (hipEventRecord(p.second, s) != hipSuccess) (void)hipStreamSynchronize(s);
+                return;
+            }
     hipEvent_t ev = nullptr;
-    if (!ix->ev_free.empty()) {
-        ev = ix->ev_free.back();
-        ix->ev_free.pop_back();
-    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
         (void)hipStreamSynchronize(s);  // no event: make this call synchronous instead
         return;
     }
-    if (hipEventRecord(ev, s) == hipSuccess)
-        ix->inflight.push_back(ev);
-    else
-        ix->ev_free.push_back(ev);
+    if (hipEventRecord(ev, s) == hipSuccess) {
+        ix->use_ev.push_back({s, ev});
+    } else {
+        (void)hipEventDestroy(ev);
+        (void)hipStreamSynchronize(s);
+    }
 }
 struct UseGuard {  // records the use when the entry point returns (any path)
     const gvdb_index* ix;
@@ -989,7 +994,7 @@ gvdb_status gvdb_index_create(const gvdb_params* params, gvdb_index** out) {
 void gvdb_index_destroy(gvdb_index* ix) {
     if (!ix) return;
     (void)quiesce(ix);
-    for (hipEvent_t ev : ix->ev_free) (void)hipEventDestroy(ev);
+    for (auto& p : ix->use_ev) (void)hipEventDestroy(p.second);
     ix->free_all();
     (void)hipStreamDestroy(ix->stream);
     delete ix;

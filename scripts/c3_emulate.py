@@ -142,6 +142,16 @@ def main():
         per_rank.append({"rank": r, "rows": bounds[r + 1] - bounds[r], "step_ms": 1e3 * step,
                          "stage1_ms": 1e3 * t1, "merge_rerank_topk_ms": 1e3 * t2})
     t3 = timed(p3, a.steps)
+    # host enqueue cost per phase call (no sync inside the loop; the GPU queue absorbs it)
+    host_us = {}
+    for nm, fn in (("stage1", lambda: p1(0)), ("rerank", lambda: p2(0)), ("final", p3)):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            fn()
+        host_us[nm] = 1e6 * (time.perf_counter() - t) / a.steps
+        torch.cuda.synchronize()
+    log(f"[c3] host enqueue per call (us): {host_us}")
     if a.p2clk:  # phase clocks of one rank's phase 2 (GVDB_P2_CLK timing study)
         os.environ["GVDB_P2_CLK"] = "1"
         p2(0)
@@ -173,6 +183,7 @@ def main():
                                        "what": f"one device copy of the G x block bytes a rank receives "
                                                f"({4 * G * w1.value} + {4 * G * w2.value} B)"},
             "per_rank_step_plus_surrogates_ms": worst + 1e3 * (ag1 + ag2),
+            "host_enqueue_us_per_call": host_us,
             "note": "per-rank step = stage 1 + merge/rerank/top-k + final merge of one rank, back to back on the "
                     "GPU (host launch overhead included); the 8-GPU step adds the two ncclAllGather calls"}
     if single is not None:

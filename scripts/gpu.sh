@@ -76,7 +76,7 @@ for t in "${TASKS[@]}"; do
             for v in ${VARIANTS:-base}; do
                 lib=""; [ "$v" != base ] && lib=grape-vector-db_amd/abl/libgvdb_$v.so
                 GVDB_LIB_PATH=$lib run 300 gpurun_out/c3ab_$v.log python3 -u scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 20
-                echo "$v $(grep 'per-rank step' gpurun_out/c3ab_$v.log) p2 $(grep -o '"merge_rerank_topk_ms": [0-9.]*' gpurun_out/c3ab_$v.log | head -8 | awk '{s+=$2} END {print s/NR}')"
+                echo "$v $(grep 'per-rank step' gpurun_out/c3ab_$v.log) p2 $(grep -o '"merge_rerank_topk_ms": [0-9.]*' gpurun_out/c3ab_$v.log | head -8 | awk '{s+=$2} END {print s/NR}') $(grep -o '"host_enqueue_us_per_call": {[^}]*}' gpurun_out/c3ab_$v.log || true)"
             done ;;
         envab)  # bench.py's batch-256 step under env variants (ENVS: ';'-separated "NAME=V,NAME=V" sets, "-" = none), one box
             IFS=';' read -ra SETS <<< "${ENVS:--}"
