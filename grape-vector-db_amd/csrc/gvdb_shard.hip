@@ -51,12 +51,15 @@ constexpr uint32_t kShardMaxD = 8192;   // distance histogram of the merge in LD
 // exactly their ranks in the global top-R.  (ii) Exact cosine of the owned
 // rows, kP2Rows at a time: the rows of the first group are loaded
 // speculatively (the first kP2Rows own-list entries) while (i) runs, through
-// LDS in chunks of kP2Ch dimensions; lane r < kP2Rows of wave 0 folds row r in
-// the reference's order (acc = acc + q_j * x_j from -0.0), wave 1's lane 0
-// folds q_j * q_j.  (iii) The owned entries ranked by (cosine desc, position)
+// LDS in chunks of kP2Ch dimensions, multiplied by the query as they are
+// staged (every product q_j * x_j rounded once, by all threads); lane r <
+// kP2Rows of wave 0 then folds row r's products in the reference's order
+// (acc = acc + p_j from -0.0: the same sums as acc + q_j * x_j without
+// contraction), wave 1's lane 0 folds the staged q_j * q_j.  The serial
+// chains carry one add and a quarter of a ds_read_b128 per dimension.  (iii) The owned entries ranked by (cosine desc, position)
 // (rank counting; a bitonic sort beyond kP2RankMax) -> the first k go to the
 // exchange-2 block.
-// LDS (dynamic): qv [D] | cg [G] | dist [G*R] when G*R <= kP2DistLds |
+// LDS (dynamic): qv [D] | qsq [D] | cg [G] | dist [G*R] when G*R <= kP2DistLds |
 // own pos / row / cos [R] when R <= kP2OwnLds (else the global scratch) | tile.
 constexpr uint32_t kP2Threads = 256;
 constexpr uint32_t kP2Rows = 24;    // rows re-scored together (one lane each)
@@ -115,7 +118,8 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
     constexpr bool dstaged = DSTAGED;
     constexpr bool own_lds = OWN_LDS;
     float* qv = (float*)lds;                                   // [D]
-    uint32_t* cg = lds + ((D + 3u) & ~3u);                     // [G]
+    float* qsq = qv + ((D + 3u) & ~3u);                        // [D]: q_j * q_j
+    uint32_t* cg = lds + 2u * ((D + 3u) & ~3u);                // [G]
     uint32_t* dist = cg + ((G + 3u) & ~3u);                    // [G*R] (dstaged)
     uint32_t* own = dist + (dstaged ? ((G * R + 3u) & ~3u) : 0u);
     float* tile = (float*)(own + (own_lds ? ((3u * R + 3u) & ~3u) : 0u));  // [kP2Rows][kP2Ld]
@@ -161,7 +165,11 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
             if (g != me) dist[x] = (uint32_t)(glist(g)[i] >> 32);
         }
     const float* qg = queries + (uint64_t)q * D;
-    for (uint32_t j = tid; j < D; j += kP2Threads) qv[j] = qg[j];
+    for (uint32_t j = tid; j < D; j += kP2Threads) {
+        const float v = qg[j];
+        qv[j] = v;
+        qsq[j] = v * v;
+    }
     __syncthreads();
     mark(0);
     const uint32_t cnt_me = cg[me];
@@ -247,32 +255,41 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
         const float nb = r0 == 0 ? nb0 : tid < nr ? norms[orow[r0 + tid]] : 0.0f;
         for (uint32_t ch = 0; ch < nch; ++ch) {
 #pragma unroll
-            for (uint32_t e = 0; e < kP2F4; ++e) {
-                const uint32_t L = tid + e * kP2Threads;
-                *(float4*)(tile + (L / (kP2Ch / 4)) * kP2Ld + 4u * (L % (kP2Ch / 4))) = xr[e];
+            for (uint32_t e = 0; e < kP2F4; ++e) {  // staged as the products q_j * x_j
+                const uint32_t L = tid + e * kP2Threads, c4 = 4u * (L % (kP2Ch / 4)), j = ch * kP2Ch + c4;
+                float4 v = xr[e];
+                if (j + 3u < D) {
+                    const float4 w = *(const float4*)(qv + j);
+                    v.x = w.x * v.x;
+                    v.y = w.y * v.y;
+                    v.z = w.z * v.z;
+                    v.w = w.w * v.w;
+                } else {  // the row's last dimensions (D % 4 != 0); past D unused by the fold
+                    v.x = j < D ? qv[j] * v.x : 0.0f;
+                    v.y = j + 1u < D ? qv[j + 1u] * v.y : 0.0f;
+                    v.z = j + 2u < D ? qv[j + 2u] * v.z : 0.0f;
+                    v.w = 0.0f;
+                }
+                *(float4*)(tile + (L / (kP2Ch / 4)) * kP2Ld + c4) = v;
             }
             __syncthreads();
             if (ch + 1 < nch) load(r0, nr, ch + 1);  // next chunk in flight during the folds
             const uint32_t j0 = ch * kP2Ch, m = min(kP2Ch, D - j0);
             if (tid < nr || fold_q) {
-                const float* tr = fold_q ? qv + j0 : tile + tid * kP2Ld;
-                // the query through the scalar cache (block-uniform address: s_load), not
-                // LDS: half the LDS reads of the fold and no LDS latency on its operand
-                const float* qc = queries + (uint64_t)q * D + j0;
+                const float* tr = fold_q ? qsq + j0 : tile + tid * kP2Ld;  // products
                 float a2 = fold_q ? qq : acc;
                 uint32_t j = 0;
                 if (vec) {
 #pragma unroll 8
                     for (; j + 4 <= m; j += 4) {
-                        const float4 x4 = *(const float4*)(tr + j);
-                        const float4 w4 = *(const float4*)(qc + j);
-                        a2 = a2 + w4.x * x4.x;
-                        a2 = a2 + w4.y * x4.y;
-                        a2 = a2 + w4.z * x4.z;
-                        a2 = a2 + w4.w * x4.w;
+                        const float4 p4 = *(const float4*)(tr + j);
+                        a2 = a2 + p4.x;
+                        a2 = a2 + p4.y;
+                        a2 = a2 + p4.z;
+                        a2 = a2 + p4.w;
                     }
                 }
-                for (; j < m; ++j) a2 = a2 + qc[j] * tr[j];
+                for (; j < m; ++j) a2 = a2 + tr[j];
                 if (fold_q) qq = a2; else acc = a2;
             }
             if (fold_q && ch + 1 == nch) s_qq = qq;
@@ -330,7 +347,7 @@ size_t shard_phase2_lds(uint32_t G, uint32_t R, uint32_t D) {
     const size_t own = R <= kP2OwnLds ? (size_t)((3u * R + 3u) & ~3u) * 4u : 0u;
     const size_t tile = std::max<size_t>((size_t)kP2Rows * kP2Ld * 4u,
                                          R > kP2RankMax ? (size_t)next_pow2(R) * 8u : 0u);
-    return (size_t)((D + 3u) & ~3u) * 4u + (size_t)((G + 3u) & ~3u) * 4u + dist + own + tile;
+    return (size_t)((D + 3u) & ~3u) * 8u + (size_t)((G + 3u) & ~3u) * 4u + dist + own + tile;
 }
 
 struct ShardClk {
