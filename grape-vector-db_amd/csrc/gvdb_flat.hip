@@ -937,8 +937,12 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
 // Round-3/4 A/B results behind these constants: an L2 line
 // prefetch of later sub-tiles slowed the row DMA stream itself (memory-only
 // 1.30 -> 2.02 ms); the skewed epilogue of waves 4..7 saved 4 %; 32-row
-// sub-tiles with 6 buffers (a deeper DMA pipeline) were 7 % slower.
+// sub-tiles with 6 buffers (a deeper DMA pipeline) were 7 % slower; issuing a
+// wave's 6 row pieces of sub-tile i+2 one per 2 k-steps of step i's MFMAs
+// instead of all after the barrier saved 7 % (every 1, 2, 3 or 4 k-steps, at
+// any offset: the same within noise).
 constexpr int kI8qBr = 4;           // B-fragment ring depth in k-steps
+constexpr int kI8qSpread = 2;       // a row piece of the sub-tile two ahead every kI8qSpread k-steps
 constexpr uint32_t kI8qSub = 2;     // 32-row groups per LDS sub-tile
 constexpr uint32_t kI8qBufs = 3;    // LDS sub-tile buffers (kI8qBufs - 1 sub-tiles in flight)
 constexpr uint32_t kI8qCl = 1024;  // block nomination list, u32 entries + scores (flushed at a barrier once half full)
@@ -952,6 +956,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     constexpr uint32_t kBufBytes = kSubBytes + 2u * kRows * 4u;  // + the rows' s_x/|x| and rho_x
     constexpr uint32_t kOps = kPerWave + 1u;            // vector-memory ops per stage of a wave with an operand DMA
     constexpr uint32_t kOpsWaves = kRows == 64 ? 2u : 1u;  // waves that DMA the rows' s_x/|x| and rho_x
+    static_assert((kPerWave - 1u) * kI8qSpread < (uint32_t)KS, "every row piece issued within its step");
     static_assert(kPieces % 8 == 0, "pieces split evenly over the waves");
     static_assert(kRows == 64 || kRows == 32, "one operand word per lane");
     __shared__ __attribute__((aligned(16))) char Bs[kI8qBufs][kBufBytes];
@@ -976,17 +981,19 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     // stage i: the block's i-th sub-tile -> buffer i % kI8qBufs, as kPerWave 1 KiB row
     // pieces per wave (piece p = (gi*KC + c)*4 + s4: row group kI8qSub*u + gi of tile
     // t), plus one op of the operand waves: the rows' s_x/|x| and rho_x
-    auto stage = [&](uint32_t i) __attribute__((always_inline)) {
+    auto piece = [&](uint32_t i, uint32_t k) __attribute__((always_inline)) {
         uint32_t t, u;
         sub_of(i, t, u);
         const uint32_t l0 = (uint32_t)(uintptr_t)Bs[i % kI8qBufs];
-#pragma unroll
-        for (uint32_t k = 0; k < kPerWave; ++k) {
-            const uint32_t p = wv * kPerWave + k, s4 = p & 3u, c = (p >> 2) % KC, gi = (p >> 2) / KC;
-            const char* ga = rowsx + ((((uint64_t)t * KC + c) * 8u + kI8qSub * u + gi) * 4u + s4) * 1024u + lane * 16u;
-            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(ga), "s"(l0 + p * 1024u)
-                         : "memory");
-        }
+        const uint32_t p = wv * kPerWave + k, s4 = p & 3u, c = (p >> 2) % KC, gi = (p >> 2) / KC;
+        const char* ga = rowsx + ((((uint64_t)t * KC + c) * 8u + kI8qSub * u + gi) * 4u + s4) * 1024u + lane * 16u;
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(ga), "s"(l0 + p * 1024u)
+                     : "memory");
+    };
+    auto stage_ops = [&](uint32_t i) __attribute__((always_inline)) {
+        uint32_t t, u;
+        sub_of(i, t, u);
+        const uint32_t l0 = (uint32_t)(uintptr_t)Bs[i % kI8qBufs];
         if (wv < kOpsWaves) {
             // 64 rows: wave 0 s_x/|x|, wave 1 rho_x; 32 rows: wave 0, lanes 0-31 / 32-63
             const uint32_t r = kRows == 64 ? lane : (lane & 31u);
@@ -997,6 +1004,11 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
                          "s"(l0 + kSubBytes + (kRows == 64 ? wv * kRows * 4u : 0u))
                          : "memory");
         }
+    };
+    auto stage = [&](uint32_t i) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t k = 0; k < kPerWave; ++k) piece(i, k);
+        stage_ops(i);
     };
     // this wave's query fragments (A) and per-slot epilogue operands
     fx_v4i A[KS];
@@ -1108,7 +1120,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             if (tid == 0) cl_n = 0;
             __syncthreads();
         }
-        stage(i + kI8qBufs - 1u);  // into the buffer read in step i-1
+        stage_ops(i + kI8qBufs - 1u);  // into the buffer read in step i-1 (its row pieces: below)
         uint32_t t, u;
         sub_of(i, t, u);
         const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
@@ -1139,6 +1151,12 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
                     bf[(s + BR - 1) % BR][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)(s + BR - 1)) * 1024u);
             }
             __builtin_amdgcn_sched_barrier(0);  // the reads stay BR - 1 k-steps ahead (no sinking)
+            // the row pieces of sub-tile i + kI8qBufs - 1 spread over the MFMAs rather than
+            // issued together after the barrier (the DMA issue of all waves at once left the
+            // matrix cores idle: emit 2.26 -> 2.09 ms, profiles/r04/flat_spread/); all of them
+            // within this step, which the vmcnt count at the next barrier assumes
+            if (s % kI8qSpread == 0 && (uint32_t)(s / kI8qSpread) < kPerWave)
+                piece(i + kI8qBufs - 1u, (uint32_t)(s / kI8qSpread));
 #pragma unroll
             for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
                 acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
