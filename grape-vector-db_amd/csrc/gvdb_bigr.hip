@@ -169,7 +169,9 @@ hipError_t launch_select_big(const Stage1Args& a, hipStream_t s) {
 // f16 dots (k_scan_mx7<DENSE>): the Hamming distance of row n is |q| - dot; the
 // members are every row with d < T plus the first R - count(< T) rows tied at
 // T in row order -- k_select_big's rule, with every distance known (no
-// candidate buffer, nothing to certify).
+// candidate buffer, nothing to certify).  With `tcut` set the block writes only
+// the membership rule itself, (T, cut) -- row n is a member iff d_n < T or
+// (d_n == T and n <= cut) -- for the certified search below, and no list.
 __device__ __forceinline__ uint32_t dense_d(uint32_t h16, float pc) {
     return (uint32_t)(int)(pc - (float)__builtin_bit_cast(_Float16, (uint16_t)h16));
 }
@@ -178,7 +180,8 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
                                                               uint32_t N, uint32_t D, uint32_t R,
                                                               const uint32_t* __restrict__ qpc,
                                                               uint32_t* __restrict__ s1_rows,
-                                                              uint32_t* __restrict__ s1_dist) {
+                                                              uint32_t* __restrict__ s1_dist,
+                                                              uint32_t* __restrict__ tcut) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint32_t* bins = hist + ((D + 4u) & ~3u);
     __shared__ uint32_t s_T, s_lt, s_n, s_cut, s_below;
@@ -244,6 +247,13 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
         }
         cut = prefix;
     }
+    if (tcut) {
+        if (tid == 0) {
+            tcut[2u * q] = T;
+            tcut[2u * q + 1u] = cut;
+        }
+        return;
+    }
     // members (wave-aggregated appends: the list is unordered, as k_select_big's)
     for (uint32_t v0 = 0; v0 < nv; v0 += nt) {
         const uint32_t v = v0 + tid;
@@ -265,7 +275,74 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
     if (a.R > a.N || !a.dense) return hipErrorInvalidValue;  // every list slot must be filled
     const size_t lds = (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
     hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
-                       a.qpc + g0, a.s1_rows + (uint64_t)g0 * a.R, a.s1_dist + (uint64_t)g0 * a.R);
+                       a.qpc + g0, a.tcut ? nullptr : a.s1_rows + (uint64_t)g0 * a.R,
+                       a.tcut ? nullptr : a.s1_dist + (uint64_t)g0 * a.R, a.tcut ? a.tcut + 2ull * g0 : nullptr);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ---- certified default depth: multi_stage_search at R = 0.1 N without the
+// rerank of R rows per query.  The exact cosine top-K2 list of the WHOLE shard
+// (the flat path: i8 / bf16 candidates, exact rerank in the reference's fold,
+// certified; entries in (cos desc, row) order) holds every row whose cosine
+// exceeds its last entry's.  The stage-1 members among it (the rule (T, cut) of
+// k_select_dense, Hamming recomputed from the codes), ordered by (cos desc,
+// Hamming, row) -- the reference's stable cosine sort of its Hamming-ordered
+// candidates (quantization.rs:165-190) -- are the query's result whenever the
+// min(k, R)-th of them scores STRICTLY above the list's last entry: every
+// member scoring that high is then in the list, ties included.  Otherwise the
+// query fails and the caller reranks the batch the regular way.  One wave per
+// query, one lane per list entry (K2 <= 64).
+__global__ __launch_bounds__(64) void k_deep_certify(const uint64_t* __restrict__ frow, const float* __restrict__ fsc,
+                                                     const uint32_t* __restrict__ fn, uint32_t K2,
+                                                     const uint32_t* __restrict__ tcut, const uint4* __restrict__ codes,
+                                                     uint64_t cap, uint32_t W4, const uint4* __restrict__ qcodes,
+                                                     uint32_t k, uint32_t R, const uint64_t* __restrict__ ids,
+                                                     uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
+                                                     uint32_t* __restrict__ out_n, uint32_t* __restrict__ fail) {
+    const uint32_t q = blockIdx.x, lane = threadIdx.x;
+    const uint32_t n = min(fn[q], K2);
+    const uint32_t T = tcut[2u * q], cut = tcut[2u * q + 1u];
+    bool mem = false;
+    uint32_t row = 0u, d = 0u, o = ~0u;  // o: ascending = cosine descending
+    if (lane < n) {
+        row = (uint32_t)frow[(uint64_t)q * K2 + lane];
+        const float sc = fsc[(uint64_t)q * K2 + lane];
+        d = big_dist(codes, cap, W4, qcodes + (uint64_t)q * W4, row);
+        mem = d < T || (d == T && row <= cut);
+        o = ~f32_order(sc);
+    }
+    uint32_t rank = 0u;  // among the members by (cos desc, Hamming, row)
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t oj = __shfl(o, j), dj = __shfl(d, j), rj = __shfl(row, j);
+        const bool mj = __shfl((int)mem, j) != 0;
+        if (mj && (oj < o || (oj == o && (dj < d || (dj == d && rj < row))))) ++rank;
+    }
+    const uint32_t m = (uint32_t)__popcll(__ballot(mem));
+    const uint32_t kk = min(k, R);
+    const uint32_t o_last = __shfl(o, n > 0u ? n - 1u : 0u);
+    const uint64_t at_k = __ballot(mem && kk > 0u && rank == kk - 1u);
+    const uint32_t o_k = __shfl(o, at_k ? (uint32_t)__builtin_ctzll(at_k) : 0u);
+    const bool ok = kk == 0u || (n == K2 && m >= kk && o_k < o_last);
+    if (!ok) {
+        if (lane == 0) atomicOr(fail, 1u);
+        return;
+    }
+    if (mem && rank < kk) {
+        out_ids[(uint64_t)q * k + rank] = ids ? ids[row] : (uint64_t)row;
+        out_scores[(uint64_t)q * k + rank] = fsc[(uint64_t)q * K2 + lane];
+    }
+    if (lane == 0 && out_n) out_n[q] = kk;
+}
+
+hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uint32_t* fn, uint32_t K2,
+                               const uint32_t* tcut, const uint4* codes, uint64_t cap, uint32_t W4,
+                               const uint4* qcodes, uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids,
+                               uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (K2 == 0 || K2 > 64u) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(64), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4, qcodes, k, R,
+                       ids, out_ids, out_scores, out_n, fail);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -147,7 +147,8 @@ struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
     DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
-        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids, flt_codes, s1_mx;
+        rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids, flt_codes, s1_mx,
+        deep;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     // Searches return without a host sync: the workspace goes back to the pool
@@ -165,7 +166,7 @@ struct Workspace {
         if (done) (void)hipEventDestroy(done);
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
                         &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
-                        &fx_scores, &flt_rows, &flt_ids, &flt_codes, &s1_mx, &b1})
+                        &fx_scores, &flt_rows, &flt_ids, &flt_codes, &s1_mx, &deep, &b1})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1108,7 +1109,7 @@ static void zero_past_counts(uint64_t* ids, float* scores, const uint32_t* n, ui
 
 static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32_t B, uint32_t dim, uint32_t k, int kind,
                            int descending, uint64_t* d_ids, float* d_scores, uint32_t* d_n, Workspace& ws,
-                           hipStream_t s, bool i8, bool* certified) {
+                           hipStream_t s, bool i8, bool* certified, bool rows_out = false) {
     *certified = false;
     gvdb_status st = i8 ? ensure_rowsq(ix, ws, s) : ensure_rowsb(ix, ws, s);
     if (st != GVDB_OK) return st;
@@ -1251,7 +1252,8 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         rr.counts = counts;
         HIP_TRY(launch_rerank(rr, s), "flat rerank");
         DBG_SYNC(s, "dbg: flat rerank");
-        HIP_TRY(launch_flat_final(counts, a.cand, cc, rr.scores, ws.thr.as<float>(), qd, Bg, k, descending, ix->ids,
+        HIP_TRY(launch_flat_final(counts, a.cand, cc, rr.scores, ws.thr.as<float>(), qd, Bg, k, descending,
+                                  rows_out ? nullptr : ix->ids,
                                   d_ids + (size_t)g0 * k, d_scores + (size_t)g0 * k, d_n ? d_n + g0 : nullptr, fail, s),
                 "flat final");
         DBG_SYNC(s, "dbg: flat final");
@@ -1272,6 +1274,75 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
     HIP_TRY(hipMemcpyAsync(ws.h_flags, fail, 4, hipMemcpyDeviceToHost, s), "fail flag");
     HIP_TRY(hipStreamSynchronize(s), "sync");
     *certified = ws.h_flags[0] == 0;
+    return GVDB_OK;
+}
+
+// Certified search at the reference's DEFAULT rescore depth (R = 0.1 N,
+// quantization.rs:27,178) without the rerank of B x R rows (3 KiB each: 256 ms
+// per batch-256 step at 10M rows): the exact cosine top-kDeepK2 of the whole
+// shard (flat_mx_search, rows instead of ids) is filtered by the stage-1
+// membership rule -- the dense FP4 scan and k_select_dense's (T, cut), no member
+// lists -- and k_deep_certify keeps the first min(k, R) members in the
+// reference's (cosine desc, Hamming, row) order when the list certifies them
+// (gvdb_bigr.hip).  Any query it cannot certify (members below the list's last
+// score, a flat tier that cannot certify, non-finite rows) sends the whole batch
+// to bq_search; *done tells the caller which.  Shards with orphan rows (the
+// reference truncates before dropping them) and metrics other than cosine take
+// bq_search directly.  Synchronises the host, as GVDB_SEARCH_FLAT does.
+static std::atomic<uint64_t>& deep_cert_count(int which) {  // [0] certified batches, [1] batches sent to bq_search
+    static std::atomic<uint64_t> c[2];
+    return c[which & 1];
+}
+
+static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint32_t B, uint32_t dim, uint32_t k,
+                                    uint32_t R, int kind, uint64_t* d_ids, float* d_scores, uint32_t* d_n,
+                                    Workspace& ws, hipStream_t s, bool* done) {
+    *done = false;
+    const uint32_t N = (uint32_t)ix->n, W4 = code_w4(dim);
+    const char* env = getenv("GVDB_DEEP_CERT");
+    if ((env && env[0] == '0') || kind != kScoreCosine || k == 0 || k > 32 || B == 0 || N < kFxMinN ||
+        R <= kSelectLdsCap || R > N || R > kBigRMax || dim == 0 || dim >= 4096 || !mfma_scan_supported(W4) ||
+        (uint64_t)R * 64u < N || ix->n != ix->id_row.size())
+        return GVDB_OK;
+    Stage1Args s1{};
+    gvdb_status pst = prepare_stage1(ws, s1, B, dim, R, N, s, true, false);
+    if (pst != GVDB_OK) return pst;
+    if (!s1.dense_sel || !s1.mfma_scan) return GVDB_OK;
+    const uint32_t K2 = kDeepK2;
+    HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
+    HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 12 + 16), "alloc certified-depth lists");
+    char* p = ws.deep.as<char>();
+    uint64_t* frow = (uint64_t*)p;
+    float* fsc = (float*)(p + (size_t)B * K2 * 8);
+    uint32_t* tcut = (uint32_t*)(p + (size_t)B * K2 * 12);
+    uint32_t* fn = tcut + 2ull * B;
+    uint32_t* dfail = fn + B;
+    s1.qf32 = d_q;  // k_qprep packs the query codes (the certify pass reads them)
+    s1.qthr = ix->thr;
+    s1.codes = ix->codes;
+    s1.cap = ix->cap;
+    s1.qcodes = ws.qcodes.as<uint4>();
+    s1.ev = nullptr;
+    s1.tcut = tcut;
+    HIP_TRY(launch_stage1_fast(s1, s), "certified depth: stage 1");
+    bool cert = false;
+    gvdb_status st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, ws, s, true, &cert, true);
+    if (st != GVDB_OK) return st;
+    if (!cert) {
+        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, ws, s, false, &cert, true);
+        if (st != GVDB_OK) return st;
+    }
+    if (cert) {
+        HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
+        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), B, k, R,
+                                    ix->ids, d_ids, d_scores, d_n, dfail, s),
+                "certified depth: certify");
+        HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        cert = ws.h_flags[0] == 0;
+    }
+    deep_cert_count(cert ? 0 : 1).fetch_add(1);
+    *done = cert;
     return GVDB_OK;
 }
 
@@ -1346,6 +1417,13 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
         HIP_TRY(hipStreamSynchronize(s), "sync");
         return GVDB_OK;
     }
+    const uint32_t R = effective_R(ix, &sp, k);
+    if (sp.mode == GVDB_SEARCH_BQ_RERANK) {  // the reference's default depth: certified, no B x R rerank
+        bool done = false;
+        gvdb_status st = deep_cert_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, R, kind, d_ids, d_scores, d_n, ws, s,
+                                          &done);
+        if (st != GVDB_OK || done) return st;
+    }
     BqSearchArgs a{};
     a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, (uint32_t)ix->n, dim, ix->ids, 0};
     a.d_q = d_q;
@@ -1353,7 +1431,7 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
     a.B = (uint32_t)B;
     a.thr = ix->thr;
     a.dims_match = true;
-    a.R = effective_R(ix, &sp, k);
+    a.R = R;
     a.kout = (uint32_t)k;
     a.kind = kind;
     a.descending = descending;
@@ -2071,6 +2149,13 @@ extern "C" int gvdb_debug_stage1_thresholds(uint32_t* out, uint32_t B) {
     return (int)hipMemcpy(out, debug_thr(), (size_t)B * 4, hipMemcpyDeviceToHost);
 }
 // tests only: 1 if a query of the last GVDB_DEBUG_THR=1 batch took the all-rows rescan
+extern "C" int gvdb_debug_deep_cert(uint64_t* out) {  // [0] certified batches, [1] sent to the rerank path
+    if (!out) return 1;
+    out[0] = deep_cert_count(0).load();
+    out[1] = deep_cert_count(1).load();
+    return 0;
+}
+
 extern "C" int gvdb_debug_stage1_rescanned(uint32_t* out) {
     if (!debug_fail()) return -1;
     if (hipDeviceSynchronize() != hipSuccess) return -2;

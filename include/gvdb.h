@@ -183,7 +183,11 @@ gvdb_status gvdb_index_search(const gvdb_index* index, const float* queries, uin
 /* Same with queries and outputs in HBM.  out_n may be NULL.  The work is
  * enqueued on `stream`: results are ready once the caller synchronises that
  * stream (BQ mode returns without any host sync; FLAT mode synchronises
- * internally because its tier decision reads a device flag).  A query whose
+ * internally because its tier decision reads a device flag, and so does BQ mode
+ * at the reference's default depth -- R > 8192 with R >= N / 64, cosine, k <= 32,
+ * N >= 65536, no orphan rows -- which answers from a certified exact cosine
+ * top-64 list filtered by the stage-1 membership rule instead of reranking
+ * B x R rows, the regular rerank whenever the list cannot certify).  A query whose
  * top-R holds a NaN score (the reference's partial_cmp().unwrap() sort would
  * panic) is reported ONLY through out_n[q] = GVDB_N_POISONED: callers that need
  * the reference's failure must pass out_n (with out_n == NULL such a query's

@@ -2,8 +2,10 @@
 """The reference's DEFAULT rescore depth at scale (src/quantization.rs:27,178:
 R = (N as f32 * 0.1) as usize): batched BQ search with rescore_ratio 0.1 on
 the bench corpus at N = 1M (R = 100K) and 10M (R = 1M), batch 8 / 64 / 256,
-k = 10, through gvdb_index_search_device (gvdb_bigr.hip: exact top-R stage 1,
-rerank of all R rows, k_topk_big).  With --check the first queries of the
+k = 10, through gvdb_index_search_device: by default the certified search
+(exact cosine top-64 of the shard filtered by the stage-1 membership rule;
+"certified" counts the batches it answered), with GVDB_DEEP_CERT=0 the exact
+top-R stage 1, rerank of all R rows and k_topk_big (gvdb_bigr.hip).  With --check the first queries of the
 1M run are compared with the oracle's multi_stage_search (ids + cosine bits).
 Prints one JSON line per point."""
 import argparse
@@ -20,6 +22,16 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 import gvdb  # noqa: E402
+
+
+def deep_counts():
+    import ctypes as C
+
+    L = gvdb.lib()
+    L.gvdb_debug_deep_cert.argtypes = [C.POINTER(C.c_uint64)]
+    out = (C.c_uint64 * 2)()
+    L.gvdb_debug_deep_cert(out)
+    return int(out[0]), int(out[1])
 
 
 def main():
@@ -50,6 +62,7 @@ def main():
             on = torch.zeros(B, dtype=torch.int32, device=dev)
             ix.search_device(q, k, oi, osc, on, sp)
             torch.cuda.synchronize()
+            c0 = deep_counts()
             ts = []
             for _ in range(a.steps):
                 t = time.perf_counter()
@@ -59,6 +72,8 @@ def main():
             ms = 1e3 * float(np.median(ts))
             line = {"rows": n, "dim": D, "R": R, "batch": B, "k": k, "ms_per_batch": ms, "qps": B / ms * 1e3,
                     "rerank_bytes_per_batch": B * R * (4 * D + 12), "all_k": bool((on.cpu() == k).all())}
+            c1 = deep_counts()
+            line["certified_batches"], line["rerank_batches"] = c1[0] - c0[0], c1[1] - c0[1]
             if host is not None and B == 8:
                 import oracle  # checker only
 

@@ -245,13 +245,81 @@ def test_large_r_emit_and_dense_selects_match_oracle(g, oracle_mod, monkeypatch,
     Q[1] = x[5]
     ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
     ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    c0 = deep_cert_counts(g)
     ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=0.1))
+    c1 = deep_cert_counts(g)
     R = int(np.float32(N) * np.float32(0.1))
     ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
     assert (n == k).all()
     assert (ids == ri[:, :k]).all()
     assert same_f32(sc, rs[:, :k])
     assert ids[0, 0] == N - 1
+    # the dense form answers through the certified default-depth search (no B x R rerank)
+    assert c1[0] - c0[0] == (1 if dense == "1" else 0) and c1[1] == c0[1]
+
+
+def deep_cert_counts(g):
+    """(certified batches, batches sent to the B x R rerank) of the certified
+    default-depth search (gvdb_capi.hip: deep_cert_search)."""
+    import ctypes as C
+
+    L = g.lib()
+    L.gvdb_debug_deep_cert.argtypes = [C.POINTER(C.c_uint64)]
+    out = (C.c_uint64 * 2)()
+    assert L.gvdb_debug_deep_cert(out) == 0
+    return int(out[0]), int(out[1])
+
+
+def test_default_depth_certified_over_query_groups(g, oracle_mod):
+    """The certified default-depth search over more than one 256-query group
+    (B = 300: stage 1, the flat list and the certify pass all run per group or
+    over the whole batch), D = 256, duplicate rows (cosine AND Hamming ties)."""
+    N, D, B, ratio, k = 70_003, 256, 300, 0.2, 10
+    x = rng_rows(N + 13, N, D, dup=150)
+    Q = rng_rows(D + 59, B, D)
+    Q[0] = x[19]
+    Q[299] = x[N - 1]
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    c0 = deep_cert_counts(g)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=ratio))
+    c1 = deep_cert_counts(g)
+    R = int(np.float32(N) * np.float32(ratio))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (n == k).all() and (ids == ri[:, :k]).all() and same_f32(sc, rs[:, :k])
+    assert ids[299, 0] == N - 1
+    assert (c1[0] - c0[0], c1[1] - c0[1]) == (1, 0)
+
+
+def test_default_depth_certificate_falls_back_to_rerank(g, oracle_mod):
+    """Rows whose cosine with a query is high (~0.84) but whose Hamming distance
+    is beyond the query's top 10 % (400 of 768 signs flipped on the query's
+    smallest components): 70 of them fill the exact cosine top-64, so fewer than
+    k members remain in the list and the certificate must fail.  The batch then
+    takes the B x R rerank, and the results still equal the oracle's."""
+    N, D, B, k = 100_000, 768, 6, 10
+    r = np.random.default_rng(91)
+    x = rng_rows(N + 21, N, D)
+    Q = rng_rows(D + 23, B, D)
+    for qi in range(2):
+        q = Q[qi]
+        base = q.copy()
+        small = np.argsort(np.abs(q))[:400]
+        base[small] = -q[small]
+        for j in range(70):
+            x[5000 * qi + 11 * j] = base + 0.01 * r.standard_normal(D).astype(np.float32)
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    c0 = deep_cert_counts(g)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=0.1))
+    c1 = deep_cert_counts(g)
+    R = int(np.float32(N) * np.float32(0.1))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (n == k).all() and (ids == ri[:, :k]).all() and same_f32(sc, rs[:, :k])
+    assert (c1[0] - c0[0], c1[1] - c0[1]) == (0, 1)
+    # the planted rows are not members: the answer holds none of them
+    planted = {5000 * qi + 11 * j for qi in range(2) for j in range(70)}
+    assert not planted & set(ids[:2].ravel().tolist())
 
 
 def test_dense_select_query_groups_match_oracle(g, oracle_mod):
@@ -289,6 +357,7 @@ def test_default_ratio_sampled_mfma_takes_no_rescan(g, oracle_mod, monkeypatch):
     ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
     ix.add_batch(np.arange(N, dtype=np.uint64), x)
     monkeypatch.setenv("GVDB_DEBUG_THR", "1")
+    monkeypatch.setenv("GVDB_DEEP_CERT", "0")  # the B x R rerank path, whose stage 1 this test inspects
     ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=ratio))
     L = g.lib()
     L.gvdb_debug_stage1_rescanned.argtypes = [C.POINTER(C.c_uint32)]
