@@ -170,8 +170,11 @@ hipError_t launch_select_big(const Stage1Args& a, hipStream_t s) {
 // members are every row with d < T plus the first R - count(< T) rows tied at
 // T in row order -- k_select_big's rule, with every distance known (no
 // candidate buffer, nothing to certify).  With `tcut` set the block writes only
-// the membership rule itself, (T, cut) -- row n is a member iff d_n < T or
-// (d_n == T and n <= cut) -- for the certified search below, and no list.
+// the membership rule itself, tcut[q] = (T, cut, need, lazy) -- row n is a member
+// iff d_n < T or (d_n == T and n <= cut) -- for the certified search below, and
+// no list; with `lazy` it stops after the histogram (lazy = 1 when the tie cut is
+// needed at all: the certify pass counts the ties below the few rows it asks
+// about instead of three radix passes over every row).
 __device__ __forceinline__ uint32_t dense_d(uint32_t h16, float pc) {
     return (uint32_t)(int)(pc - (float)__builtin_bit_cast(_Float16, (uint16_t)h16));
 }
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
                                                               const uint32_t* __restrict__ qpc,
                                                               uint32_t* __restrict__ s1_rows,
                                                               uint32_t* __restrict__ s1_dist,
-                                                              uint32_t* __restrict__ tcut) {
+                                                              uint32_t* __restrict__ tcut, int lazy) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint32_t* bins = hist + ((D + 4u) & ~3u);
     __shared__ uint32_t s_T, s_lt, s_n, s_cut, s_below;
@@ -219,6 +222,16 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
     }
     __syncthreads();
     const uint32_t T = s_T, need = R - s_lt;
+    if (tcut && lazy) {
+        if (tid == 0) {
+            const bool cut_needed = hist[T] > need;
+            tcut[4u * q] = T;
+            tcut[4u * q + 1u] = ~0u;
+            tcut[4u * q + 2u] = need;
+            tcut[4u * q + 3u] = cut_needed ? 1u : 0u;
+        }
+        return;
+    }
     uint32_t cut = ~0u;  // tied rows with row <= cut are members
     if (hist[T] > need) {
         uint32_t left = need, prefix = 0u, pmask = 0u;
@@ -249,8 +262,10 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
     }
     if (tcut) {
         if (tid == 0) {
-            tcut[2u * q] = T;
-            tcut[2u * q + 1u] = cut;
+            tcut[4u * q] = T;
+            tcut[4u * q + 1u] = cut;
+            tcut[4u * q + 2u] = need;
+            tcut[4u * q + 3u] = 0u;
         }
         return;
     }
@@ -276,7 +291,8 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
     const size_t lds = (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
     hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
                        a.qpc + g0, a.tcut ? nullptr : a.s1_rows + (uint64_t)g0 * a.R,
-                       a.tcut ? nullptr : a.s1_dist + (uint64_t)g0 * a.R, a.tcut ? a.tcut + 2ull * g0 : nullptr);
+                       a.tcut ? nullptr : a.s1_dist + (uint64_t)g0 * a.R, a.tcut ? a.tcut + 4ull * g0 : nullptr,
+                       a.tcut_lazy);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -285,32 +301,84 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
 // rerank of R rows per query.  The exact cosine top-K2 list of the WHOLE shard
 // (the flat path: i8 / bf16 candidates, exact rerank in the reference's fold,
 // certified; entries in (cos desc, row) order) holds every row whose cosine
-// exceeds its last entry's.  The stage-1 members among it (the rule (T, cut) of
-// k_select_dense, Hamming recomputed from the codes), ordered by (cos desc,
+// exceeds its last entry's.  The stage-1 members among it (k_select_dense's
+// rule (T, cut), Hamming recomputed from the codes), ordered by (cos desc,
 // Hamming, row) -- the reference's stable cosine sort of its Hamming-ordered
 // candidates (quantization.rs:165-190) -- are the query's result whenever the
 // min(k, R)-th of them scores STRICTLY above the list's last entry: every
 // member scoring that high is then in the list, ties included.  Otherwise the
-// query fails and the caller reranks the batch the regular way.  One wave per
-// query, one lane per list entry (K2 <= 64).
-__global__ __launch_bounds__(64) void k_deep_certify(const uint64_t* __restrict__ frow, const float* __restrict__ fsc,
-                                                     const uint32_t* __restrict__ fn, uint32_t K2,
-                                                     const uint32_t* __restrict__ tcut, const uint4* __restrict__ codes,
-                                                     uint64_t cap, uint32_t W4, const uint4* __restrict__ qcodes,
-                                                     uint32_t k, uint32_t R, const uint64_t* __restrict__ ids,
-                                                     uint64_t* __restrict__ out_ids, float* __restrict__ out_scores,
-                                                     uint32_t* __restrict__ out_n, uint32_t* __restrict__ fail) {
-    const uint32_t q = blockIdx.x, lane = threadIdx.x;
+// query fails and the caller reranks the batch the regular way.  A lazy rule
+// (cut not computed) resolves a listed row tied at T by counting the rows tied
+// at T below it in the query's dense f16 block (member iff fewer than `need`):
+// one pass over at most the query's block, only for queries with such a row.
+// One block per query; wave 0 holds the list, one lane per entry (K2 <= 64).
+constexpr uint32_t kCertThreads = 1024;
+constexpr uint32_t kCertU = 8;  // 16-B loads in flight per thread (the count pass is latency-bound otherwise)
+__global__ __launch_bounds__(kCertThreads) void k_deep_certify(
+    const uint64_t* __restrict__ frow, const float* __restrict__ fsc, const uint32_t* __restrict__ fn, uint32_t K2,
+    const uint32_t* __restrict__ tcut, const uint4* __restrict__ codes, uint64_t cap, uint32_t W4,
+    const uint4* __restrict__ qcodes, const uint16_t* __restrict__ dense, uint32_t np,
+    const uint32_t* __restrict__ qpc, uint32_t k, uint32_t R, const uint64_t* __restrict__ ids,
+    uint64_t* __restrict__ out_ids, float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
+    uint32_t* __restrict__ fail) {
+    __shared__ uint32_t s_trow[64], s_cnt[64];
+    __shared__ uint32_t s_nt;
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
     const uint32_t n = min(fn[q], K2);
-    const uint32_t T = tcut[2u * q], cut = tcut[2u * q + 1u];
-    bool mem = false;
+    const uint32_t T = tcut[4u * q], cut = tcut[4u * q + 1u], need = tcut[4u * q + 2u];
+    const bool lazy = tcut[4u * q + 3u] != 0u && dense;
+    bool mem = false, tied = false;
     uint32_t row = 0u, d = 0u, o = ~0u;  // o: ascending = cosine descending
-    if (lane < n) {
-        row = (uint32_t)frow[(uint64_t)q * K2 + lane];
-        const float sc = fsc[(uint64_t)q * K2 + lane];
-        d = big_dist(codes, cap, W4, qcodes + (uint64_t)q * W4, row);
-        mem = d < T || (d == T && row <= cut);
-        o = ~f32_order(sc);
+    if (tid < 64u) {
+        if (lane < n) {
+            row = (uint32_t)frow[(uint64_t)q * K2 + lane];
+            const float sc = fsc[(uint64_t)q * K2 + lane];
+            d = big_dist(codes, cap, W4, qcodes + (uint64_t)q * W4, row);
+            tied = d == T;
+            mem = d < T || (tied && !lazy && row <= cut);
+            o = ~f32_order(sc);
+        }
+        const uint64_t tm = __ballot(tied && lazy);
+        if (tied && lazy) {
+            const uint32_t i = (uint32_t)__popcll(tm & ((1ull << lane) - 1ull));
+            s_trow[i] = row;
+            s_cnt[i] = 0u;
+        }
+        if (lane == 0) s_nt = (uint32_t)__popcll(tm);
+    }
+    __syncthreads();
+    const uint32_t nt = s_nt;
+    if (nt) {  // block-uniform: count the rows tied at T below each listed tied row
+        uint32_t maxr = 0u;
+        for (uint32_t i = 0; i < nt; ++i) maxr = max(maxr, s_trow[i]);
+        const float pc = (float)qpc[q];
+        const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);
+        for (uint32_t v0 = 0; 8u * v0 < maxr; v0 += kCertThreads * kCertU) {
+            uint4 w[kCertU];
+#pragma unroll
+            for (uint32_t u = 0; u < kCertU; ++u) {
+                const uint32_t v = v0 + u * kCertThreads + tid;
+                w[u] = 8u * v < maxr ? dq[v] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kCertU; ++u) {
+                const uint32_t v = v0 + u * kCertThreads + tid;
+                const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t r = 8u * v + (uint32_t)j;
+                    if (r < maxr && dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) == T)
+                        for (uint32_t i = 0; i < nt; ++i)
+                            if (r < s_trow[i]) atomicAdd(&s_cnt[i], 1u);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid >= 64u) return;
+    if (nt) {
+        const uint64_t tm = __ballot(tied && lazy);
+        if (tied && lazy) mem = s_cnt[(uint32_t)__popcll(tm & ((1ull << lane) - 1ull))] < need;
     }
     uint32_t rank = 0u;  // among the members by (cos desc, Hamming, row)
     for (uint32_t j = 0; j < n; ++j) {
@@ -337,12 +405,13 @@ __global__ __launch_bounds__(64) void k_deep_certify(const uint64_t* __restrict_
 
 hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uint32_t* fn, uint32_t K2,
                                const uint32_t* tcut, const uint4* codes, uint64_t cap, uint32_t W4,
-                               const uint4* qcodes, uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids,
-                               uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s) {
+                               const uint4* qcodes, const uint16_t* dense, uint32_t np, const uint32_t* qpc,
+                               uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
+                               float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s) {
     if (B == 0) return hipSuccess;
     if (K2 == 0 || K2 > 64u) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(64), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4, qcodes, k, R,
-                       ids, out_ids, out_scores, out_n, fail);
+    hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(kCertThreads), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4,
+                       qcodes, dense, np, qpc, k, R, ids, out_ids, out_scores, out_n, fail);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -1310,12 +1310,12 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     if (!s1.dense_sel || !s1.mfma_scan) return GVDB_OK;
     const uint32_t K2 = kDeepK2;
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
-    HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 12 + 16), "alloc certified-depth lists");
+    HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 20 + 16), "alloc certified-depth lists");
     char* p = ws.deep.as<char>();
     uint64_t* frow = (uint64_t*)p;
     float* fsc = (float*)(p + (size_t)B * K2 * 8);
     uint32_t* tcut = (uint32_t*)(p + (size_t)B * K2 * 12);
-    uint32_t* fn = tcut + 2ull * B;
+    uint32_t* fn = tcut + 4ull * B;
     uint32_t* dfail = fn + B;
     s1.qf32 = d_q;  // k_qprep packs the query codes (the certify pass reads them)
     s1.qthr = ix->thr;
@@ -1324,6 +1324,8 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     s1.qcodes = ws.qcodes.as<uint4>();
     s1.ev = nullptr;
     s1.tcut = tcut;
+    // one 256-query group: its dense block outlives stage 1, so the tie cut is resolved lazily (certify pass)
+    s1.tcut_lazy = B <= 256u ? 1 : 0;
     HIP_TRY(launch_stage1_fast(s1, s), "certified depth: stage 1");
     bool cert = false;
     gvdb_status st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, ws, s, true, &cert, true);
@@ -1334,8 +1336,9 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     }
     if (cert) {
         HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
-        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), B, k, R,
-                                    ix->ids, d_ids, d_scores, d_n, dfail, s),
+        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(),
+                                    s1.tcut_lazy ? s1.dense : nullptr, s1.dense_np, s1.qpc, B, k, R, ix->ids, d_ids,
+                                    d_scores, d_n, dfail, s),
                 "certified depth: certify");
         HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
         HIP_TRY(hipStreamSynchronize(s), "sync");

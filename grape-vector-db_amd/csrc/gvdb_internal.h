@@ -98,7 +98,9 @@ struct Stage1Args {
     uint32_t dense_np;       //   row stride (N rounded up to 32)
     const float* qf32;       // mfma_scan: the f32 queries [B][D] -- k_qprep packs qcodes itself
     float qthr;              //   (packing threshold)
-    uint32_t* tcut;          // optional, dense_sel: [B][2] the membership rule (T, cut) instead of the lists
+    uint32_t* tcut;          // optional, dense_sel: [B][4] the membership rule (T, cut, need, lazy) instead of
+                             // the lists
+    int tcut_lazy;           //   skip the tie-cut passes (the dense block stays valid for k_deep_certify)
 };
 // ---- large rescore depth (gvdb_bigr.hip): R up to 2^20, D < 4096, k <= 1024 --------
 constexpr uint32_t kBigRMax = 1u << 20;
@@ -109,10 +111,12 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
 // list (rows + scores, (cos desc, row) order, fn[q] entries) under the membership rule tcut; fail[0] |= 1
 // for a query the list cannot certify
 constexpr uint32_t kDeepK2 = 64;  // exact cosine list length (one lane per entry)
+// (dense / np / qpc: the stage-1 dense block of the batch, for a lazy rule; nullptr = every rule resolved)
 hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uint32_t* fn, uint32_t K2,
                                const uint32_t* tcut, const uint4* codes, uint64_t cap, uint32_t W4,
-                               const uint4* qcodes, uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids,
-                               uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s);
+                               const uint4* qcodes, const uint16_t* dense, uint32_t np, const uint32_t* qpc,
+                               uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
+                               float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s);
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
