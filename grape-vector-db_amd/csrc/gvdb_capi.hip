@@ -1308,7 +1308,9 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     gvdb_status pst = prepare_stage1(ws, s1, B, dim, R, N, s, true, false);
     if (pst != GVDB_OK) return pst;
     if (!s1.dense_sel || !s1.mfma_scan) return GVDB_OK;
-    const uint32_t K2 = kDeepK2;
+    // list length: 32 entries certify k <= 16 on all but adversarial data at half the exact
+    // rerank of 64 (the i8 pass nominates by the K2-th score)
+    const uint32_t K2 = k <= 16u ? 32u : kDeepK2;
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
     HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 20 + 16), "alloc certified-depth lists");
     char* p = ws.deep.as<char>();

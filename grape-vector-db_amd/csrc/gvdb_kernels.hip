@@ -1085,26 +1085,37 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     // Register r holds row 8 (r / 4) + 4 h + (r % 4) of the sub-tile at n0.
     auto test = [&](const v16f_t& A, uint32_t qt, uint32_t n0) __attribute__((always_inline)) {
         if constexpr (DENSE) {
-            const uint32_t qi = qt * 32u + (lane & 31u);
-            if (qt < nqt && qi < B) {
-                typedef __attribute__((address_space(1))) uint64_t g_u64;
-                typedef __attribute__((address_space(1))) uint16_t g_u16;
-                const uint64_t base = (uint64_t)qi * dense_np;
+            // the tile's 32 x 32 f16 dots go through the wave's LDS scratch ([query][row
+            // pair], padded rows) so that lane L stores rows 16 (L & 1) .. +15 of query
+            // L / 2 as 32 contiguous bytes: 64-B segments per query instead of 8-B pieces
+            // (rows past N land in the block's padding: its row stride is N rounded up to 32)
+            if (qt < nqt) {
+                constexpr uint32_t kLd = 18;  // u32 per query row of the scratch (16 + 2 pad)
+                uint32_t* tw = (uint32_t*)tscr[wv];
+                const uint32_t j = lane & 31u;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const uint32_t row = n0 + 8u * (uint32_t)g + 4u * h;  // rows row .. row + 3
-                    const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[4 * g], A[4 * g + 1]));
-                    const uint32_t hi =
+                    const uint32_t p = 4u * (uint32_t)g + 2u * h;  // row pair of rows 8g + 4h, 8g + 4h + 1
+                    tw[j * kLd + p] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[4 * g], A[4 * g + 1]));
+                    tw[j * kLd + p + 1u] =
                         __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[4 * g + 2], A[4 * g + 3]));
-                    if (row + 3u < N) {
-                        *(g_u64*)(dense + base + row) = ((uint64_t)hi << 32) | lo;
-                    } else {
-                        const uint32_t v4[4] = {lo & 0xffffu, lo >> 16, hi & 0xffffu, hi >> 16};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (row + (uint32_t)j < N) *(g_u16*)(dense + base + row + j) = (uint16_t)v4[j];
-                    }
                 }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const uint32_t qo = lane >> 1, half = lane & 1u;
+                const uint32_t* src = tw + qo * kLd + 8u * half;
+                typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+                const u4v_t v0 = {src[0], src[1], src[2], src[3]};
+                const u4v_t v1 = {src[4], src[5], src[6], src[7]};
+                const uint32_t qi = qt * 32u + qo;
+                if (qi < B) {
+                    typedef __attribute__((address_space(1))) u4v_t g_u4;
+                    g_u4* dst = (g_u4*)(dense + (uint64_t)qi * dense_np + n0 + 16u * half);
+                    dst[0] = v0;
+                    dst[1] = v1;
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
             return;
         }
