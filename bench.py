@@ -311,6 +311,12 @@ def main():
                        "steps": args.steps})
         for r in (1000, 4000):
             run_point(f"bq R={r}", gvdb.SearchParams(rescore_count=r))
+        # the reference's DEFAULT depth, R = (N as f32 * 0.1) as usize (quantization.rs:27,178), answered by
+        # the certified search (exact cosine top-32 filtered by the stage-1 membership rule)
+        c0 = deep_cert_counts(L)
+        run_point("bq R=0.1 N (reference default rescore_ratio, certified)", gvdb.SearchParams(rescore_ratio=0.1))
+        c1 = deep_cert_counts(L)
+        points[-1]["certified_batches"], points[-1]["rerank_batches"] = c1[0] - c0[0], c1[1] - c0[1]
         run_point("exact flat (i8/bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1))
         points[-1]["emit_roofline"] = flat_emit_roofline(L, ix, q, k, n_local, D)
         if planted:
@@ -592,6 +598,16 @@ def pmc_traffic(kernel_prefix, n_local, D, pmc_file=None):
             if name.startswith(kernel_prefix) and "hbm_read_bytes_per_launch" in d:
                 return d["hbm_read_bytes_per_launch"]
     return None
+
+
+def deep_cert_counts(L):
+    """(certified, reranked) batch counters of the certified default-depth search."""
+    import ctypes
+
+    L.gvdb_debug_deep_cert.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    out = (ctypes.c_uint64 * 2)()
+    L.gvdb_debug_deep_cert(out)
+    return int(out[0]), int(out[1])
 
 
 def flat_emit_roofline(L, ix, q, k, n_local, D):
