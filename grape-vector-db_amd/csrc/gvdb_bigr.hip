@@ -320,13 +320,15 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     const uint4* __restrict__ qcodes, const uint16_t* __restrict__ dense, uint32_t np,
     const uint32_t* __restrict__ qpc, uint32_t k, uint32_t R, const uint64_t* __restrict__ ids,
     uint64_t* __restrict__ out_ids, float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
-    uint32_t* __restrict__ fail) {
+    uint32_t* __restrict__ fail, const uint32_t* __restrict__ kcnt, uint32_t* __restrict__ block2,
+    const uint32_t* __restrict__ reff) {
     __shared__ uint32_t s_trow[64], s_cnt[64];
     __shared__ uint32_t s_nt;
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
     const uint32_t n = min(fn[q], K2);
     const uint32_t T = tcut[4u * q], cut = tcut[4u * q + 1u], need = tcut[4u * q + 2u];
-    const bool lazy = tcut[4u * q + 3u] != 0u && dense;
+    const uint32_t mode = tcut[4u * q + 3u];  // 0: cut, 1: lazy (count in the dense block), 2: no tied member
+    const bool lazy = mode == 1u && dense;
     bool mem = false, tied = false;
     uint32_t row = 0u, d = 0u, o = ~0u;  // o: ascending = cosine descending
     if (tid < 64u) {
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
             const float sc = fsc[(uint64_t)q * K2 + lane];
             d = big_dist(codes, cap, W4, qcodes + (uint64_t)q * W4, row);
             tied = d == T;
-            mem = d < T || (tied && !lazy && row <= cut);
+            mem = d < T || (tied && mode == 0u && row <= cut);
             o = ~f32_order(sc);
         }
         const uint64_t tm = __ballot(tied && lazy);
@@ -387,13 +389,31 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
         if (mj && (oj < o || (oj == o && (dj < d || (dj == d && rj < row))))) ++rank;
     }
     const uint32_t m = (uint32_t)__popcll(__ballot(mem));
-    const uint32_t kk = min(k, R);
+    const uint32_t kk = min(k, kcnt ? kcnt[q] : R);
     const uint32_t o_last = __shfl(o, n > 0u ? n - 1u : 0u);
     const uint64_t at_k = __ballot(mem && kk > 0u && rank == kk - 1u);
     const uint32_t o_k = __shfl(o, at_k ? (uint32_t)__builtin_ctzll(at_k) : 0u);
     const bool ok = kk == 0u || (n == K2 && m >= kk && o_k < o_last);
     if (!ok) {
         if (lane == 0) atomicOr(fail, 1u);
+        return;
+    }
+    if (block2) {  // the deep sharded exchange-2 entry: {cos bits, Hamming, id lo, id hi}, then meta
+        if (mem && rank < kk) {
+            const uint64_t id = ids ? ids[row] : (uint64_t)row;
+            uint32_t* ent = block2 + ((uint64_t)q * k + rank) * 4u;
+            ent[0] = __float_as_uint(fsc[(uint64_t)q * K2 + lane]);
+            ent[1] = d;
+            ent[2] = (uint32_t)id;
+            ent[3] = (uint32_t)(id >> 32);
+        }
+        if (lane == 0) {
+            const uint32_t Bt = gridDim.x;
+            uint32_t* meta = block2 + 4ull * Bt * k;
+            meta[q] = kk;
+            meta[Bt + q] = reff[q];
+            if (q == 0) meta[2 * Bt] = 0u;
+        }
         return;
     }
     if (mem && rank < kk) {
@@ -407,11 +427,12 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                const uint32_t* tcut, const uint4* codes, uint64_t cap, uint32_t W4,
                                const uint4* qcodes, const uint16_t* dense, uint32_t np, const uint32_t* qpc,
                                uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
-                               float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s) {
+                               float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
+                               const uint32_t* kcnt, uint32_t* block2, const uint32_t* reff) {
     if (B == 0) return hipSuccess;
-    if (K2 == 0 || K2 > 64u) return hipErrorInvalidValue;
+    if (K2 == 0 || K2 > 64u || (block2 && !reff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(kCertThreads), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4,
-                       qcodes, dense, np, qpc, k, R, ids, out_ids, out_scores, out_n, fail);
+                       qcodes, dense, np, qpc, k, R, ids, out_ids, out_scores, out_n, fail, kcnt, block2, reff);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -2280,3 +2280,55 @@ gvdb_status gvdb::shard_stage1_members(const gvdb_index* ix, const float* d_q, u
     HIP_TRY(launch_shard_member_hist(m_dist, (uint32_t)B, Rl, dim + 1u, block1, s), "deep sharded stage 1 histogram");
     return GVDB_OK;
 }
+
+// The certified deep phase 2 (gvdb_shard.hip, R > 8192): this rank's exact cosine
+// top-K2 over its shard (flat_mx_search, rows), filtered by the rule of its owned
+// rows that k_shard_deep_own wrote (tcut), gives its local top-min(k, own) entries
+// whenever the list certifies them (k_deep_certify) -- instead of reranking
+// ~R / G owned rows per query.  Shards with orphan rows, k > 32 or fewer than
+// kFxMinN rows, and batches the list cannot certify, leave *done = false.
+gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
+                                         const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
+                                         uint32_t* block2, hipStream_t s, bool* done) {
+    *done = false;
+    const char* env = getenv("GVDB_DEEP_CERT");
+    if ((env && env[0] == '0') || !ix || k == 0 || k > 32 || B == 0 || B > 0xFFFFFFFFull || ix->n < kFxMinN ||
+        ix->n > 0xFFFFFFFFull || ix->n != ix->id_row.size() || dim != ix->dim || dim == 0)
+        return GVDB_OK;
+    gvdb_status st = set_device(ix->device);
+    if (st != GVDB_OK) return st;
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    g.begin(s);
+    UseGuard ug{ix, s};
+    const uint32_t W4 = code_w4(dim), K2 = k <= 16 ? 32u : kDeepK2;
+    HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc qcodes");
+    HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 4 + 16), "alloc certified lists");
+    char* p = ws.deep.as<char>();
+    uint64_t* frow = (uint64_t*)p;
+    float* fsc = (float*)(p + (size_t)B * K2 * 8);
+    uint32_t* fn = (uint32_t*)(p + (size_t)B * K2 * 12);
+    uint32_t* dfail = fn + B;
+    HIP_TRY(launch_pack(d_q, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
+    bool cert = false;
+    st = flat_mx_search(ix, d_q, (uint32_t)B, dim, K2, kScoreCosine, 1, frow, fsc, fn, ws, s, true, &cert, true);
+    if (st != GVDB_OK) return st;
+    if (!cert) {
+        st = flat_mx_search(ix, d_q, (uint32_t)B, dim, K2, kScoreCosine, 1, frow, fsc, fn, ws, s, false, &cert, true);
+        if (st != GVDB_OK) return st;
+    }
+    if (cert) {
+        HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
+        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), nullptr, 0,
+                                    nullptr, (uint32_t)B, (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s,
+                                    own_cnt, block2, reff),
+                "certified deep phase 2");
+        HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        cert = ws.h_flags[0] == 0;
+    }
+    deep_cert_count(cert ? 0 : 1).fetch_add(1);
+    *done = cert;
+    return GVDB_OK;
+}

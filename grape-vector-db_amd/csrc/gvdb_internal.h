@@ -112,11 +112,15 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
 // for a query the list cannot certify
 constexpr uint32_t kDeepK2 = 64;  // exact cosine list length (one lane per entry)
 // (dense / np / qpc: the stage-1 dense block of the batch, for a lazy rule; nullptr = every rule resolved)
+// (kcnt: per-query member counts instead of R; block2 / reff: write the exchange-2 block of the deep sharded
+// form -- {cos bits, Hamming, id lo, id hi} [B][k] + meta -- instead of out_ids / out_scores / out_n)
 hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uint32_t* fn, uint32_t K2,
                                const uint32_t* tcut, const uint4* codes, uint64_t cap, uint32_t W4,
                                const uint4* qcodes, const uint16_t* dense, uint32_t np, const uint32_t* qpc,
                                uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
-                               float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s);
+                               float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
+                               const uint32_t* kcnt = nullptr, uint32_t* block2 = nullptr,
+                               const uint32_t* reff = nullptr);
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
@@ -390,7 +394,13 @@ hipError_t launch_shard_member_hist(const uint32_t* m_dist, uint32_t B, uint32_t
 hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
                                  uint32_t R, uint32_t Rl, uint32_t H, const uint32_t* m_rows, const uint32_t* m_dist,
                                  uint32_t* o_rows, uint32_t* o_dist, uint32_t* own_cnt, uint32_t* reff,
-                                 hipStream_t s);
+                                 hipStream_t s, uint32_t* tcut = nullptr);
+// the certified deep phase 2 (gvdb_capi.hip): this rank's local top-k of its owned rows (rule tcut [B][4],
+// counts own_cnt) from its exact cosine top-K2 list, into the exchange-2 block; *done = false: the caller
+// reranks the owned lists instead (nothing written that it relies on)
+gvdb_status shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
+                                   const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
+                                   uint32_t* block2, hipStream_t s, bool* done);
 // gvdb_bigr.hip: the owned entries' local top-k (k <= 1024) -> the exchange-2 block
 hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,

@@ -582,7 +582,8 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
                                                                  uint32_t* __restrict__ o_rows,
                                                                  uint32_t* __restrict__ o_dist,
                                                                  uint32_t* __restrict__ own_cnt,
-                                                                 uint32_t* __restrict__ reff) {
+                                                                 uint32_t* __restrict__ reff,
+                                                                 uint32_t* __restrict__ tcut) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tot[];  // [H] global histogram, then bins [2048]
     uint32_t* bins = tot + ((H + 3u) & ~3u);
     __shared__ uint32_t s_S, s_T, s_lt, s_tb, s_cut, s_below, wcnt[kDeepThreads / 64];
@@ -624,7 +625,9 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
     // the quota-th smallest row among this rank's members at d == T: 11 + 11 + 10 bits
     uint32_t cut = 0u;
     const bool all_ties = quota == mine, no_ties = quota == 0u;
-    if (!all_ties && !no_ties) {
+    // tcut (the certified phase 2): the rule for ANY row of the shard, so the cut is the
+    // quota-th tied row even when every listed tie is owned (the list may stop inside T)
+    if ((!all_ties || tcut) && !no_ties) {
         uint32_t left = quota, prefix = 0u, pmask = 0u;
         const uint32_t* rw = m_rows + (uint64_t)q * Rl;
         const uint32_t* dd = m_dist + (uint64_t)q * Rl;
@@ -653,6 +656,12 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
             __syncthreads();
         }
         cut = prefix;
+    }
+    if (tcut && tid == 0) {  // member iff d < T, or d == T and row <= cut (mode 2: no tied row)
+        tcut[4u * q] = T;
+        tcut[4u * q + 1u] = cut;
+        tcut[4u * q + 2u] = 0u;
+        tcut[4u * q + 3u] = no_ties ? 2u : 0u;
     }
     // order-preserving compaction into the owned lists
     const uint32_t* rw = m_rows + (uint64_t)q * Rl;
@@ -685,12 +694,12 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
 hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
                                  uint32_t R, uint32_t Rl, uint32_t H, const uint32_t* m_rows, const uint32_t* m_dist,
                                  uint32_t* o_rows, uint32_t* o_dist, uint32_t* own_cnt, uint32_t* reff,
-                                 hipStream_t s) {
+                                 hipStream_t s, uint32_t* tcut) {
     if (B == 0) return hipSuccess;
     const size_t lds = (size_t)((H + 3u) & ~3u) * 4u + 2048u * 4u;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_shard_deep_own, dim3(B), dim3(kDeepThreads), lds, s, gathered1, words1, G, me, B, R, Rl, H,
-                       m_rows, m_dist, o_rows, o_dist, own_cnt, reff);
+                       m_rows, m_dist, o_rows, o_dist, own_cnt, reff, tcut);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -789,10 +798,23 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
         float* m_cos = (float*)(o_dist + BR);
         uint32_t* own_cnt = (uint32_t*)(m_cos + BR);
         uint32_t* reff = own_cnt + B;
+        uint32_t* tcut = (uint32_t*)m_cos;  // the certified form's rule [B][4] (the cosines are not written then)
         const uint32_t Rl = usable ? (uint32_t)std::min<uint64_t>(R, si.n) : 0u;
+        const bool try_cert = usable && Rl > 0 && B * 4 <= BR;
         hipError_t e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
                                              (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist,
-                                             own_cnt, reff, s);
+                                             own_cnt, reff, s, try_cert ? tcut : nullptr);
+        if (e == hipSuccess && try_cert) {
+            // the certified form: the rank's exact cosine top-32 / 64 filtered by its owned-row rule
+            bool done = false;
+            const gvdb_status st = shard_certified_phase2(shard, d_queries, B, dim, k, tcut, own_cnt, reff, d_block2,
+                                                          s, &done);
+            if (st != GVDB_OK) return st;
+            if (done) {
+                index_track_use(shard, s);
+                return GVDB_OK;
+            }
+        }
         if (e == hipSuccess && Rl > 0) {
             RerankArgs rr{};
             rr.rows = si.rows;

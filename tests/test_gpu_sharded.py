@@ -215,6 +215,63 @@ def test_deep_two_exchange_g8_equals_single_index_and_oracle(g, oracle_mod, size
     assert (got_i[:nq] == ri[:, :k]).all() and same_f32(got_s[:nq], rs[:, :k])
 
 
+def deep_cert_counts(g):
+    import ctypes as C
+
+    L = g.lib()
+    L.gvdb_debug_deep_cert.argtypes = [C.POINTER(C.c_uint64)]
+    out = (C.c_uint64 * 2)()
+    assert L.gvdb_debug_deep_cert(out) == 0
+    return int(out[0]), int(out[1])
+
+
+@pytest.mark.parametrize("plant", [False, True])
+def test_deep_certified_phase2_equals_single_index_and_oracle(g, oracle_mod, plant):
+    """The certified deep phase 2 (shards of >= 65536 rows, k <= 32): each rank's
+    local top-k comes from its exact cosine top-32 filtered by the owned-row rule
+    k_shard_deep_own writes, not from reranking its ~R / G owned rows.  Equal rows
+    across the shard boundary make cross-shard cosine ties.  plant: 70 rows of
+    cosine ~0.85 but Hamming 400 (> T) in shard 1 for query 0 fill that rank's list,
+    so rank 1 cannot certify and reranks its owned rows while rank 0 certifies;
+    the merged results are the same either way."""
+    import torch
+
+    sizes, D, B, R, k = (70_000, 90_000), 768, 48, 16_000, 10
+    N = sum(sizes)
+    x = rows(733, N, D, dup=100)
+    x[sizes[0]] = x[5]
+    x[sizes[0] + 9] = x[N - 3]
+    Q = rows(734, B, D)
+    Q[1] = x[5]
+    Q[2] = x[N - 3]
+    if plant:
+        r = np.random.default_rng(92)
+        base = Q[0].copy()
+        small = np.argsort(np.abs(Q[0]))[:400]
+        base[small] = -Q[0][small]
+        for j in range(70):
+            x[sizes[0] + 100 + 13 * j] = base + 0.01 * r.standard_normal(D).astype(np.float32)
+    q = torch.from_numpy(Q).cuda()
+    bounds = np.cumsum((0,) + sizes)
+    shards = []
+    for j in range(2):
+        ix = g.GpuVectorIndex(dimension=D)
+        ix.add_batch(np.arange(bounds[j], bounds[j + 1], dtype=np.uint64), x[bounds[j]:bounds[j + 1]])
+        shards.append(ix)
+    c0 = deep_cert_counts(g)
+    got_i, got_s, got_n = emulate_two_exchange(g, shards, q, D, R, k, rerank_twice=True)
+    c1 = deep_cert_counts(g)
+    # phase 2 ran twice per rank: (certified, reranked) batches
+    assert (c1[0] - c0[0], c1[1] - c0[1]) == ((2, 2) if plant else (4, 0))
+    si, ss, sn = single_device(g, x, Q, R, k)
+    assert (got_n == sn).all() and (got_i == si).all() and same_f32(got_s, ss)
+    assert got_i[1, 0] in (5, sizes[0]) and got_i[2, 0] in (N - 3, sizes[0] + 9)
+    nq = 8
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q[:nq]), oracle_mod.quantize(x), Q[:nq], x, R,
+                                                   kind=0)
+    assert (got_i[:nq] == ri[:, :k]).all() and same_f32(got_s[:nq], rs[:, :k])
+
+
 def test_sharded_flat_g8_d3072_equals_single_index_and_oracle(g, oracle_mod):
     """Sharded FLAT (the recall-1.0 mode) at the config-4 width: 8 shards of
     9K rows (> the 65536-row MFMA floor on no shard: exact scans) and 2 shards
