@@ -382,7 +382,11 @@ gvdb_status gvdb_shard_stage1_device(const gvdb_index* shard, const float* d_que
 /* Phase 2: from the gathered exchange-1 blocks, this rank's exchange-2 block
  * (global top-R, exact cosine of the owned rows, local top-k).  d_scratch:
  * scratch_bytes of device memory (deep form: the scratch phase 1 filled; phase
- * 2 only reads its member lists, so it may run again on them). */
+ * 2 only reads its member lists, so it may run again on them).  Deep form on a
+ * shard of >= 65536 rows without orphan rows, k <= 32: the rank's local top-k
+ * comes from its certified exact cosine top-32 / 64 filtered by its owned-row
+ * rule (no rerank of the ~R / G owned rows); this synchronises the host, and
+ * falls back to the rerank when the list cannot certify. */
 gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_queries, uint64_t B, uint32_t dim,
                                      uint64_t R, uint64_t k, const uint32_t* d_gathered1, uint64_t G, uint64_t rank,
                                      void* d_scratch, uint32_t* d_block2, void* stream);
