@@ -321,14 +321,16 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     const uint32_t* __restrict__ qpc, uint32_t k, uint32_t R, const uint64_t* __restrict__ ids,
     uint64_t* __restrict__ out_ids, float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
     uint32_t* __restrict__ fail, const uint32_t* __restrict__ kcnt, uint32_t* __restrict__ block2,
-    const uint32_t* __restrict__ reff) {
+    const uint32_t* __restrict__ reff, const uint32_t* __restrict__ m_rows, const uint32_t* __restrict__ m_dist,
+    uint32_t mlen) {
     __shared__ uint32_t s_trow[64], s_cnt[64];
     __shared__ uint32_t s_nt;
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
     const uint32_t n = min(fn[q], K2);
     const uint32_t T = tcut[4u * q], cut = tcut[4u * q + 1u], need = tcut[4u * q + 2u];
-    const uint32_t mode = tcut[4u * q + 3u];  // 0: cut, 1: lazy (count in the dense block), 2: no tied member
-    const bool lazy = mode == 1u && dense;
+    // 0: cut, 1: lazy, counted in the dense block, 2: no tied member, 3: lazy, counted in the member list
+    const uint32_t mode = tcut[4u * q + 3u];
+    const bool lazy = (mode == 1u && dense) || (mode == 3u && m_rows);
     bool mem = false, tied = false;
     uint32_t row = 0u, d = 0u, o = ~0u;  // o: ascending = cosine descending
     if (tid < 64u) {
@@ -350,7 +352,26 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     }
     __syncthreads();
     const uint32_t nt = s_nt;
-    if (nt) {  // block-uniform: count the rows tied at T below each listed tied row
+    if (nt && mode == 3u) {  // block-uniform: the member list's rows tied at T below each listed tied row
+        const uint32_t* mr = m_rows + (uint64_t)q * mlen;
+        const uint32_t* md = m_dist + (uint64_t)q * mlen;
+        for (uint32_t i0 = 0; i0 < mlen; i0 += kCertThreads * kCertU) {
+            uint32_t dv[kCertU];
+#pragma unroll
+            for (uint32_t u = 0; u < kCertU; ++u) {
+                const uint32_t i = i0 + u * kCertThreads + tid;
+                dv[u] = i < mlen ? md[i] : ~0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kCertU; ++u) {
+                if (dv[u] != T) continue;
+                const uint32_t r = mr[i0 + u * kCertThreads + tid];
+                for (uint32_t i = 0; i < nt; ++i)
+                    if (r < s_trow[i]) atomicAdd(&s_cnt[i], 1u);
+            }
+        }
+        __syncthreads();
+    } else if (nt) {  // block-uniform: count the rows tied at T below each listed tied row
         uint32_t maxr = 0u;
         for (uint32_t i = 0; i < nt; ++i) maxr = max(maxr, s_trow[i]);
         const float pc = (float)qpc[q];
@@ -428,11 +449,13 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                const uint4* qcodes, const uint16_t* dense, uint32_t np, const uint32_t* qpc,
                                uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
                                float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
-                               const uint32_t* kcnt, uint32_t* block2, const uint32_t* reff) {
+                               const uint32_t* kcnt, uint32_t* block2, const uint32_t* reff,
+                               const uint32_t* m_rows, const uint32_t* m_dist, uint32_t mlen) {
     if (B == 0) return hipSuccess;
     if (K2 == 0 || K2 > 64u || (block2 && !reff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(kCertThreads), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4,
-                       qcodes, dense, np, qpc, k, R, ids, out_ids, out_scores, out_n, fail, kcnt, block2, reff);
+                       qcodes, dense, np, qpc, k, R, ids, out_ids, out_scores, out_n, fail, kcnt, block2, reff, m_rows,
+                       m_dist, mlen);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -2287,14 +2287,18 @@ gvdb_status gvdb::shard_stage1_members(const gvdb_index* ix, const float* d_q, u
 // whenever the list certifies them (k_deep_certify) -- instead of reranking
 // ~R / G owned rows per query.  Shards with orphan rows, k > 32 or fewer than
 // kFxMinN rows, and batches the list cannot certify, leave *done = false.
+bool gvdb::shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t k) {
+    const char* env = getenv("GVDB_DEEP_CERT");
+    return !(env && env[0] == '0') && ix && k >= 1 && k <= 32 && ix->n >= kFxMinN && ix->n <= 0xFFFFFFFFull &&
+           ix->n == ix->id_row.size() && dim == ix->dim && dim > 0;
+}
+
 gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                          const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
+                                         const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl,
                                          uint32_t* block2, hipStream_t s, bool* done) {
     *done = false;
-    const char* env = getenv("GVDB_DEEP_CERT");
-    if ((env && env[0] == '0') || !ix || k == 0 || k > 32 || B == 0 || B > 0xFFFFFFFFull || ix->n < kFxMinN ||
-        ix->n > 0xFFFFFFFFull || ix->n != ix->id_row.size() || dim != ix->dim || dim == 0)
-        return GVDB_OK;
+    if (!shard_certified_eligible(ix, dim, k) || B == 0 || B > 0xFFFFFFFFull) return GVDB_OK;
     gvdb_status st = set_device(ix->device);
     if (st != GVDB_OK) return st;
     WsGuard g(ix->device);
@@ -2322,7 +2326,7 @@ gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q,
         HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
         HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), nullptr, 0,
                                     nullptr, (uint32_t)B, (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s,
-                                    own_cnt, block2, reff),
+                                    own_cnt, block2, reff, m_rows, m_dist, Rl),
                 "certified deep phase 2");
         HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
         HIP_TRY(hipStreamSynchronize(s), "sync");

@@ -120,7 +120,8 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
                                float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
                                const uint32_t* kcnt = nullptr, uint32_t* block2 = nullptr,
-                               const uint32_t* reff = nullptr);
+                               const uint32_t* reff = nullptr, const uint32_t* m_rows = nullptr,
+                               const uint32_t* m_dist = nullptr, uint32_t mlen = 0);
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
@@ -398,9 +399,11 @@ hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uin
 // the certified deep phase 2 (gvdb_capi.hip): this rank's local top-k of its owned rows (rule tcut [B][4],
 // counts own_cnt) from its exact cosine top-K2 list, into the exchange-2 block; *done = false: the caller
 // reranks the owned lists instead (nothing written that it relies on)
+bool shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t k);
 gvdb_status shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                    const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
-                                   uint32_t* block2, hipStream_t s, bool* done);
+                                   const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl, uint32_t* block2,
+                                   hipStream_t s, bool* done);
 // gvdb_bigr.hip: the owned entries' local top-k (k <= 1024) -> the exchange-2 block
 hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,

@@ -605,6 +605,12 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
         if (tid == 0) {
             own_cnt[q] = 0u;
             reff[q] = Re;
+            if (tcut) {  // no owned row
+                tcut[4u * q] = 0u;
+                tcut[4u * q + 1u] = 0u;
+                tcut[4u * q + 2u] = 0u;
+                tcut[4u * q + 3u] = 2u;
+            }
         }
         return;
     }
@@ -622,12 +628,32 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
     __syncthreads();
     const uint32_t T = s_T, need = Re - s_lt, tb = s_tb, mine = hist(me)[T];
     const uint32_t quota = need > tb ? min(need - tb, mine) : 0u;  // this rank's tied rows in the top-R
+    if (tcut) {
+        // the certified phase 2 only needs the rule: member iff d < T, or d == T and fewer than
+        // `quota` of the member list's rows tied at T lie below it (the list holds the shard's first
+        // tied rows by row; k_deep_certify counts, for the few listed rows it asks about) -- no radix
+        // select, no compaction (own_cnt = the owned count)
+        if (tid < 64) {
+            uint32_t below = 0u;  // members with d < T: the prefix of this rank's histogram
+            const uint32_t* hm = hist(me);
+            for (uint32_t t = tid; t < T; t += 64) below += hm[t];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) below += (uint32_t)__shfl_xor((int)below, off);
+            if (tid == 0) own_cnt[q] = min(below + quota, n);
+        }
+        if (tid == 0) {
+            reff[q] = Re;
+            tcut[4u * q] = T;
+            tcut[4u * q + 1u] = 0u;
+            tcut[4u * q + 2u] = quota;
+            tcut[4u * q + 3u] = quota ? 3u : 2u;
+        }
+        return;
+    }
     // the quota-th smallest row among this rank's members at d == T: 11 + 11 + 10 bits
     uint32_t cut = 0u;
     const bool all_ties = quota == mine, no_ties = quota == 0u;
-    // tcut (the certified phase 2): the rule for ANY row of the shard, so the cut is the
-    // quota-th tied row even when every listed tie is owned (the list may stop inside T)
-    if ((!all_ties || tcut) && !no_ties) {
+    if (!all_ties && !no_ties) {
         uint32_t left = quota, prefix = 0u, pmask = 0u;
         const uint32_t* rw = m_rows + (uint64_t)q * Rl;
         const uint32_t* dd = m_dist + (uint64_t)q * Rl;
@@ -656,12 +682,6 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
             __syncthreads();
         }
         cut = prefix;
-    }
-    if (tcut && tid == 0) {  // member iff d < T, or d == T and row <= cut (mode 2: no tied row)
-        tcut[4u * q] = T;
-        tcut[4u * q + 1u] = cut;
-        tcut[4u * q + 2u] = 0u;
-        tcut[4u * q + 3u] = no_ties ? 2u : 0u;
     }
     // order-preserving compaction into the owned lists
     const uint32_t* rw = m_rows + (uint64_t)q * Rl;
@@ -800,21 +820,28 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
         uint32_t* reff = own_cnt + B;
         uint32_t* tcut = (uint32_t*)m_cos;  // the certified form's rule [B][4] (the cosines are not written then)
         const uint32_t Rl = usable ? (uint32_t)std::min<uint64_t>(R, si.n) : 0u;
-        const bool try_cert = usable && Rl > 0 && B * 4 <= BR;
-        hipError_t e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
-                                             (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist,
-                                             own_cnt, reff, s, try_cert ? tcut : nullptr);
-        if (e == hipSuccess && try_cert) {
+        const bool try_cert = usable && Rl > 0 && B * 4 <= BR && shard_certified_eligible(shard, dim, k);
+        hipError_t e = hipSuccess;
+        if (try_cert) {
             // the certified form: the rank's exact cosine top-32 / 64 filtered by its owned-row rule
+            e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
+                                      (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist, own_cnt,
+                                      reff, s, tcut);
             bool done = false;
-            const gvdb_status st = shard_certified_phase2(shard, d_queries, B, dim, k, tcut, own_cnt, reff, d_block2,
-                                                          s, &done);
-            if (st != GVDB_OK) return st;
+            if (e == hipSuccess) {
+                const gvdb_status st = shard_certified_phase2(shard, d_queries, B, dim, k, tcut, own_cnt, reff,
+                                                              m_rows, m_dist, Rl, d_block2, s, &done);
+                if (st != GVDB_OK) return st;
+            }
             if (done) {
                 index_track_use(shard, s);
                 return GVDB_OK;
             }
         }
+        if (e == hipSuccess)
+            e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
+                                      (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist, own_cnt,
+                                      reff, s);
         if (e == hipSuccess && Rl > 0) {
             RerankArgs rr{};
             rr.rows = si.rows;
