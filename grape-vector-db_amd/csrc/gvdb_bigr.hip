@@ -184,7 +184,9 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
                                                               const uint32_t* __restrict__ qpc,
                                                               uint32_t* __restrict__ s1_rows,
                                                               uint32_t* __restrict__ s1_dist,
-                                                              uint32_t* __restrict__ tcut, int lazy) {
+                                                              uint32_t* __restrict__ tcut, int lazy,
+                                                              uint32_t* __restrict__ mhist,
+                                                              uint32_t* __restrict__ mcount) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
     uint32_t* bins = hist + ((D + 4u) & ~3u);
     __shared__ uint32_t s_T, s_lt, s_n, s_cut, s_below;
@@ -222,6 +224,11 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
     }
     __syncthreads();
     const uint32_t T = s_T, need = R - s_lt;
+    if (mhist) {  // the members' histogram: every bin below T, `need` at T (the exchange-1 block)
+        uint32_t* out = mhist + (uint64_t)q * (D + 1u);
+        for (uint32_t t = tid; t <= D; t += nt) out[t] = t < T ? hist[t] : t == T ? need : 0u;
+        if (tid == 0) mcount[q] = R;
+    }
     if (tcut && lazy) {
         if (tid == 0) {
             const bool cut_needed = hist[T] > need;
@@ -292,7 +299,8 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
     hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
                        a.qpc + g0, a.tcut ? nullptr : a.s1_rows + (uint64_t)g0 * a.R,
                        a.tcut ? nullptr : a.s1_dist + (uint64_t)g0 * a.R, a.tcut ? a.tcut + 4ull * g0 : nullptr,
-                       a.tcut_lazy);
+                       a.tcut_lazy, a.mhist ? a.mhist + (uint64_t)g0 * (a.D + 1u) : nullptr,
+                       a.mcount ? a.mcount + g0 : nullptr);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -355,15 +363,16 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     if (nt && mode == 3u) {  // block-uniform: the member list's rows tied at T below each listed tied row
         const uint32_t* mr = m_rows + (uint64_t)q * mlen;
         const uint32_t* md = m_dist + (uint64_t)q * mlen;
-        for (uint32_t i0 = 0; i0 < mlen; i0 += kCertThreads * kCertU) {
-            uint32_t dv[kCertU];
+        constexpr uint32_t kU = 32;  // 4-B loads in flight per thread (a 1M-entry list: 32 rounds)
+        for (uint32_t i0 = 0; i0 < mlen; i0 += kCertThreads * kU) {
+            uint32_t dv[kU];
 #pragma unroll
-            for (uint32_t u = 0; u < kCertU; ++u) {
+            for (uint32_t u = 0; u < kU; ++u) {
                 const uint32_t i = i0 + u * kCertThreads + tid;
                 dv[u] = i < mlen ? md[i] : ~0u;
             }
 #pragma unroll
-            for (uint32_t u = 0; u < kCertU; ++u) {
+            for (uint32_t u = 0; u < kU; ++u) {
                 if (dv[u] != T) continue;
                 const uint32_t r = mr[i0 + u * kCertThreads + tid];
                 for (uint32_t i = 0; i < nt; ++i)

@@ -2276,8 +2276,14 @@ gvdb_status gvdb::shard_stage1_members(const gvdb_index* ix, const float* d_q, u
     s1.qcodes = ws.qcodes.as<uint4>();
     s1.s1_rows = m_rows;
     s1.s1_dist = m_dist;
+    if (s1.dense_sel) {  // k_select_dense writes the members' histogram itself (it holds the full one)
+        s1.mhist = block1;
+        s1.mcount = block1 + (uint64_t)B * (dim + 1u);
+    }
     HIP_TRY(launch_stage1_fast(s1, s), "deep sharded stage 1");
-    HIP_TRY(launch_shard_member_hist(m_dist, (uint32_t)B, Rl, dim + 1u, block1, s), "deep sharded stage 1 histogram");
+    if (!s1.dense_sel)
+        HIP_TRY(launch_shard_member_hist(m_dist, (uint32_t)B, Rl, dim + 1u, block1, s),
+                "deep sharded stage 1 histogram");
     return GVDB_OK;
 }
 

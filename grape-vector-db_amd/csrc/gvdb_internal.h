@@ -101,6 +101,8 @@ struct Stage1Args {
     uint32_t* tcut;          // optional, dense_sel: [B][4] the membership rule (T, cut, need, lazy) instead of
                              // the lists
     int tcut_lazy;           //   skip the tie-cut passes (the dense block stays valid for k_deep_certify)
+    uint32_t* mhist;         // optional, dense_sel: [B][H = D+1] the members' Hamming histogram (deep sharded
+    uint32_t* mcount;        //   exchange-1 block) and [B] their count, written by k_select_dense
 };
 // ---- large rescore depth (gvdb_bigr.hip): R up to 2^20, D < 4096, k <= 1024 --------
 constexpr uint32_t kBigRMax = 1u << 20;
