@@ -169,50 +169,60 @@ hipError_t launch_select_big(const Stage1Args& a, hipStream_t s) {
 // f16 dots (k_scan_mx7<DENSE>): the Hamming distance of row n is |q| - dot; the
 // members are every row with d < T plus the first R - count(< T) rows tied at
 // T in row order -- k_select_big's rule, with every distance known (no
-// candidate buffer, nothing to certify).  With `tcut` set the block writes only
-// the membership rule itself, tcut[q] = (T, cut, need, lazy) -- row n is a member
-// iff d_n < T or (d_n == T and n <= cut) -- for the certified search below, and
-// no list; with `lazy` it stops after the histogram (lazy = 1 when the tie cut is
-// needed at all: the certify pass counts the ties below the few rows it asks
-// about instead of three radix passes over every row).
+// candidate buffer, nothing to certify).  One pass: wave w histograms its own
+// contiguous 1/16 of the rows (private LDS histogram: no atomics shared across
+// waves), the sum gives T, and the per-segment counts at T locate the segment
+// holding the cut, which alone is rescanned in row order (a block prefix of the
+// tied rows) -- instead of three radix passes over every row.  With `tcut` set
+// the block writes only the rule, tcut[q] = (T, cut, need, 0): row n is a member
+// iff d_n < T or (d_n == T and n <= cut); `mhist` / `mcount`: the members'
+// histogram (the deep sharded exchange-1 block).
 __device__ __forceinline__ uint32_t dense_d(uint32_t h16, float pc) {
     return (uint32_t)(int)(pc - (float)__builtin_bit_cast(_Float16, (uint16_t)h16));
 }
 
+constexpr uint32_t kSdWaves = kBigThreads / 64;
 __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __restrict__ dense, uint32_t np,
                                                               uint32_t N, uint32_t D, uint32_t R,
                                                               const uint32_t* __restrict__ qpc,
                                                               uint32_t* __restrict__ s1_rows,
                                                               uint32_t* __restrict__ s1_dist,
-                                                              uint32_t* __restrict__ tcut, int lazy,
+                                                              uint32_t* __restrict__ tcut,
                                                               uint32_t* __restrict__ mhist,
                                                               uint32_t* __restrict__ mcount) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-    uint32_t* bins = hist + ((D + 4u) & ~3u);
-    __shared__ uint32_t s_T, s_lt, s_n, s_cut, s_below;
-    const uint32_t q = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-    const uint16_t* dq = dense + (uint64_t)q * np;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t H4 = (D + 4u) & ~3u;
+    uint32_t* hist = lds;        // [H4] the query's histogram
+    uint32_t* whist = lds + H4;  // [kSdWaves][H4] per wave: its row segment's
+    __shared__ uint32_t s_T, s_lt, s_n, s_cut, s_seg, s_left, wsum[kSdWaves];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);  // 8 rows per 16-B load (np % 32 == 0)
     const float pc = (float)qpc[q];
-    uint32_t* orow = s1_rows + (uint64_t)q * R;
-    uint32_t* odist = s1_dist + (uint64_t)q * R;
-    const uint32_t nv = (N + 7u) / 8u;  // 8 rows per 16-B load (the row stride is a multiple of 32)
-    // visit(fn): fn(row, d) for every row, 16-B coalesced loads
-    auto visit = [&](auto fn) __attribute__((always_inline)) {
-        for (uint32_t v = tid; v < nv; v += nt) {
-            const uint4 w = ((const uint4*)dq)[v];
-            const uint32_t n0 = 8u * v;
-            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (n0 + 2u * j < N) fn(n0 + 2u * j, dense_d(ws[j] & 0xffffu, pc));
-                if (n0 + 2u * j + 1u < N) fn(n0 + 2u * j + 1u, dense_d(ws[j] >> 16, pc));
-            }
-        }
-    };
-    for (uint32_t i = tid; i <= D; i += nt) hist[i] = 0u;
+    const uint32_t nv = (N + 7u) / 8u;
+    const uint32_t segv = (nv + kSdWaves - 1u) / kSdWaves;  // 16-B words per wave segment
+    for (uint32_t i = tid; i < (kSdWaves + 1u) * H4; i += nt) lds[i] = 0u;
     if (tid == 0) s_n = 0u;
     __syncthreads();
-    visit([&](uint32_t, uint32_t d) { atomicAdd(&hist[min(d, D)], 1u); });
+    {
+        uint32_t* wh = whist + wv * H4;
+        const uint32_t v1 = min(nv, (wv + 1u) * segv);
+        for (uint32_t v = wv * segv + lane; v < v1; v += 64u) {
+            const uint4 w = dq[v];
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (8u * v + (uint32_t)j < N)
+                    atomicAdd(&wh[min(dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc), D)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t <= D; t += nt) {
+        uint32_t c = 0u;
+#pragma unroll
+        for (uint32_t w = 0; w < kSdWaves; ++w) c += whist[w * H4 + t];
+        hist[t] = c;
+    }
     __syncthreads();
     if (tid < 64) {
         const uint32_t t = wave_find_cum(hist, D + 1u, R);
@@ -229,43 +239,59 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
         for (uint32_t t = tid; t <= D; t += nt) out[t] = t < T ? hist[t] : t == T ? need : 0u;
         if (tid == 0) mcount[q] = R;
     }
-    if (tcut && lazy) {
-        if (tid == 0) {
-            const bool cut_needed = hist[T] > need;
-            tcut[4u * q] = T;
-            tcut[4u * q + 1u] = ~0u;
-            tcut[4u * q + 2u] = need;
-            tcut[4u * q + 3u] = cut_needed ? 1u : 0u;
-        }
-        return;
-    }
     uint32_t cut = ~0u;  // tied rows with row <= cut are members
     if (hist[T] > need) {
-        uint32_t left = need, prefix = 0u, pmask = 0u;
-        for (int pass = 0; pass < 3; ++pass) {
-            const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
-            const uint32_t nb = pass == 2 ? 1024u : 2048u, dm = nb - 1u;
-            for (uint32_t i = tid; i < nb; i += nt) bins[i] = 0u;
+        if (tid == 0) {  // the segment holding the need-th tied row, and its rank there
+            uint32_t c = 0u, sg = 0u;
+            for (; sg + 1u < kSdWaves; ++sg) {
+                const uint32_t ws = whist[sg * H4 + T];
+                if (c + ws >= need) break;
+                c += ws;
+            }
+            s_seg = sg;
+            s_left = need - c;
+            s_cut = ~0u;
+        }
+        __syncthreads();
+        const uint32_t sv0 = s_seg * segv, sv1 = min(nv, sv0 + segv), left = s_left;
+        uint32_t base = 0u;  // tied rows of the segment before this round
+        for (uint32_t it = sv0; it < sv1; it += nt) {  // block-uniform rounds, rows in order
+            const uint32_t v = it + tid;
+            uint32_t tm = 0u;  // this thread's 8 rows tied at T (bit j)
+            if (v < sv1) {
+                const uint4 w = dq[v];
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (8u * v + (uint32_t)j < N && dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) == T)
+                        tm |= 1u << j;
+            }
+            const uint32_t cnt = (uint32_t)__popc(tm);
+            uint32_t incl = cnt;  // wave-inclusive prefix
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+                if ((int)lane >= off) incl += y;
+            }
+            if (lane == 63u) wsum[wv] = incl;
             __syncthreads();
-            visit([&](uint32_t n, uint32_t d) {
-                if (d == T && (n & pmask) == prefix) atomicAdd(&bins[(n >> shift) & dm], 1u);
-            });
-            __syncthreads();
-            if (tid < 64) {
-                const uint32_t bin = wave_find_cum(bins, nb, left);
-                const uint32_t below = wave_sum_below(bins, bin);
-                if (tid == 0) {
-                    s_cut = bin;
-                    s_below = below;
-                }
+            uint32_t offs = 0u, total = 0u;
+            for (uint32_t w = 0; w < kSdWaves; ++w) {
+                const uint32_t c = wsum[w];
+                if (w < wv) offs += c;
+                total += c;
+            }
+            const uint32_t excl = base + offs + incl - cnt;
+            if (cnt && excl < left && left <= excl + cnt) {  // the left-th tied row is one of this thread's
+                uint32_t r = left - excl, bits = tm;
+                while (--r) bits &= bits - 1u;
+                s_cut = 8u * v + (uint32_t)__builtin_ctz(bits);
             }
             __syncthreads();
-            left -= s_below;
-            prefix |= s_cut << shift;
-            pmask |= dm << shift;
-            __syncthreads();
+            base += total;
+            if (base >= left) break;
         }
-        cut = prefix;
+        cut = s_cut;
     }
     if (tcut) {
         if (tid == 0) {
@@ -280,14 +306,14 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
     for (uint32_t v0 = 0; v0 < nv; v0 += nt) {
         const uint32_t v = v0 + tid;
         uint4 w = make_uint4(0u, 0u, 0u, 0u);
-        if (v < nv) w = ((const uint4*)dq)[v];
+        if (v < nv) w = dq[v];
         const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint32_t n = 8u * v + (uint32_t)j;
             const uint32_t d = dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc);
             const bool keep = v < nv && n < N && (d < T || (d == T && n <= cut));
-            big_append(keep, n, d, &s_n, orow, odist, R);
+            big_append(keep, n, d, &s_n, s1_rows + (uint64_t)q * R, s1_dist + (uint64_t)q * R, R);
         }
     }
 }
@@ -295,12 +321,12 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
 hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hipStream_t s) {
     if (bg == 0) return hipSuccess;
     if (a.R > a.N || !a.dense) return hipErrorInvalidValue;  // every list slot must be filled
-    const size_t lds = (size_t)((a.D + 4u) & ~3u) * 4u + 2048u * 4u;
+    const size_t lds = (size_t)(kSdWaves + 1u) * ((a.D + 4u) & ~3u) * 4u;
+    if (lds > 160u * 1024u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
                        a.qpc + g0, a.tcut ? nullptr : a.s1_rows + (uint64_t)g0 * a.R,
                        a.tcut ? nullptr : a.s1_dist + (uint64_t)g0 * a.R, a.tcut ? a.tcut + 4ull * g0 : nullptr,
-                       a.tcut_lazy, a.mhist ? a.mhist + (uint64_t)g0 * (a.D + 1u) : nullptr,
-                       a.mcount ? a.mcount + g0 : nullptr);
+                       a.mhist ? a.mhist + (uint64_t)g0 * (a.D + 1u) : nullptr, a.mcount ? a.mcount + g0 : nullptr);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -315,18 +341,16 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
 // candidates (quantization.rs:165-190) -- are the query's result whenever the
 // min(k, R)-th of them scores STRICTLY above the list's last entry: every
 // member scoring that high is then in the list, ties included.  Otherwise the
-// query fails and the caller reranks the batch the regular way.  A lazy rule
-// (cut not computed) resolves a listed row tied at T by counting the rows tied
-// at T below it in the query's dense f16 block (member iff fewer than `need`):
-// one pass over at most the query's block, only for queries with such a row.
-// One block per query; wave 0 holds the list, one lane per entry (K2 <= 64).
+// query fails and the caller reranks the batch the regular way.  The deep
+// sharded phase 2 passes a rule without a cut (mode 3): a listed row tied at T
+// is then resolved by counting the rank's member-list rows tied at T below it
+// (member iff fewer than `need`), only for queries with such a row.  One block
+// per query; wave 0 holds the list, one lane per entry (K2 <= 64).
 constexpr uint32_t kCertThreads = 1024;
-constexpr uint32_t kCertU = 8;  // 16-B loads in flight per thread (the count pass is latency-bound otherwise)
 __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     const uint64_t* __restrict__ frow, const float* __restrict__ fsc, const uint32_t* __restrict__ fn, uint32_t K2,
     const uint32_t* __restrict__ tcut, const uint4* __restrict__ codes, uint64_t cap, uint32_t W4,
-    const uint4* __restrict__ qcodes, const uint16_t* __restrict__ dense, uint32_t np,
-    const uint32_t* __restrict__ qpc, uint32_t k, uint32_t R, const uint64_t* __restrict__ ids,
+    const uint4* __restrict__ qcodes, uint32_t k, uint32_t R, const uint64_t* __restrict__ ids,
     uint64_t* __restrict__ out_ids, float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
     uint32_t* __restrict__ fail, const uint32_t* __restrict__ kcnt, uint32_t* __restrict__ block2,
     const uint32_t* __restrict__ reff, const uint32_t* __restrict__ m_rows, const uint32_t* __restrict__ m_dist,
@@ -336,9 +360,9 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
     const uint32_t n = min(fn[q], K2);
     const uint32_t T = tcut[4u * q], cut = tcut[4u * q + 1u], need = tcut[4u * q + 2u];
-    // 0: cut, 1: lazy, counted in the dense block, 2: no tied member, 3: lazy, counted in the member list
+    // 0: cut, 2: no tied member, 3: the tie rank counted in the member list (deep sharded phase 2)
     const uint32_t mode = tcut[4u * q + 3u];
-    const bool lazy = (mode == 1u && dense) || (mode == 3u && m_rows);
+    const bool lazy = mode == 3u && m_rows;
     bool mem = false, tied = false;
     uint32_t row = 0u, d = 0u, o = ~0u;  // o: ascending = cosine descending
     if (tid < 64u) {
@@ -377,32 +401,6 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
                 const uint32_t r = mr[i0 + u * kCertThreads + tid];
                 for (uint32_t i = 0; i < nt; ++i)
                     if (r < s_trow[i]) atomicAdd(&s_cnt[i], 1u);
-            }
-        }
-        __syncthreads();
-    } else if (nt) {  // block-uniform: count the rows tied at T below each listed tied row
-        uint32_t maxr = 0u;
-        for (uint32_t i = 0; i < nt; ++i) maxr = max(maxr, s_trow[i]);
-        const float pc = (float)qpc[q];
-        const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);
-        for (uint32_t v0 = 0; 8u * v0 < maxr; v0 += kCertThreads * kCertU) {
-            uint4 w[kCertU];
-#pragma unroll
-            for (uint32_t u = 0; u < kCertU; ++u) {
-                const uint32_t v = v0 + u * kCertThreads + tid;
-                w[u] = 8u * v < maxr ? dq[v] : make_uint4(0u, 0u, 0u, 0u);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kCertU; ++u) {
-                const uint32_t v = v0 + u * kCertThreads + tid;
-                const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t r = 8u * v + (uint32_t)j;
-                    if (r < maxr && dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) == T)
-                        for (uint32_t i = 0; i < nt; ++i)
-                            if (r < s_trow[i]) atomicAdd(&s_cnt[i], 1u);
-                }
             }
         }
         __syncthreads();
@@ -455,15 +453,15 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
 
 hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uint32_t* fn, uint32_t K2,
                                const uint32_t* tcut, const uint4* codes, uint64_t cap, uint32_t W4,
-                               const uint4* qcodes, const uint16_t* dense, uint32_t np, const uint32_t* qpc,
-                               uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
+                               const uint4* qcodes, uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids,
+                               uint64_t* out_ids,
                                float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
                                const uint32_t* kcnt, uint32_t* block2, const uint32_t* reff,
                                const uint32_t* m_rows, const uint32_t* m_dist, uint32_t mlen) {
     if (B == 0) return hipSuccess;
     if (K2 == 0 || K2 > 64u || (block2 && !reff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(kCertThreads), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4,
-                       qcodes, dense, np, qpc, k, R, ids, out_ids, out_scores, out_n, fail, kcnt, block2, reff, m_rows,
+                       qcodes, k, R, ids, out_ids, out_scores, out_n, fail, kcnt, block2, reff, m_rows,
                        m_dist, mlen);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;

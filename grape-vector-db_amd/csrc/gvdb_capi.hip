@@ -1326,8 +1326,6 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     s1.qcodes = ws.qcodes.as<uint4>();
     s1.ev = nullptr;
     s1.tcut = tcut;
-    // one 256-query group: its dense block outlives stage 1, so the tie cut is resolved lazily (certify pass)
-    s1.tcut_lazy = B <= 256u ? 1 : 0;
     HIP_TRY(launch_stage1_fast(s1, s), "certified depth: stage 1");
     bool cert = false;
     gvdb_status st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, ws, s, true, &cert, true);
@@ -1338,9 +1336,8 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     }
     if (cert) {
         HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
-        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(),
-                                    s1.tcut_lazy ? s1.dense : nullptr, s1.dense_np, s1.qpc, B, k, R, ix->ids, d_ids,
-                                    d_scores, d_n, dfail, s),
+        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), B, k, R,
+                                    ix->ids, d_ids, d_scores, d_n, dfail, s),
                 "certified depth: certify");
         HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
         HIP_TRY(hipStreamSynchronize(s), "sync");
@@ -2330,9 +2327,9 @@ gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q,
     }
     if (cert) {
         HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
-        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), nullptr, 0,
-                                    nullptr, (uint32_t)B, (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s,
-                                    own_cnt, block2, reff, m_rows, m_dist, Rl),
+        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(),
+                                    (uint32_t)B, (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s, own_cnt,
+                                    block2, reff, m_rows, m_dist, Rl),
                 "certified deep phase 2");
         HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
         HIP_TRY(hipStreamSynchronize(s), "sync");

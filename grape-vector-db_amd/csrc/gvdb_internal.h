@@ -98,9 +98,8 @@ struct Stage1Args {
     uint32_t dense_np;       //   row stride (N rounded up to 32)
     const float* qf32;       // mfma_scan: the f32 queries [B][D] -- k_qprep packs qcodes itself
     float qthr;              //   (packing threshold)
-    uint32_t* tcut;          // optional, dense_sel: [B][4] the membership rule (T, cut, need, lazy) instead of
+    uint32_t* tcut;          // optional, dense_sel: [B][4] the membership rule (T, cut, need, 0) instead of
                              // the lists
-    int tcut_lazy;           //   skip the tie-cut passes (the dense block stays valid for k_deep_certify)
     uint32_t* mhist;         // optional, dense_sel: [B][H = D+1] the members' Hamming histogram (deep sharded
     uint32_t* mcount;        //   exchange-1 block) and [B] their count, written by k_select_dense
 };
@@ -113,14 +112,12 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
 // list (rows + scores, (cos desc, row) order, fn[q] entries) under the membership rule tcut; fail[0] |= 1
 // for a query the list cannot certify
 constexpr uint32_t kDeepK2 = 64;  // exact cosine list length (one lane per entry)
-// (dense / np / qpc: the stage-1 dense block of the batch, for a lazy rule; nullptr = every rule resolved)
 // (kcnt: per-query member counts instead of R; block2 / reff: write the exchange-2 block of the deep sharded
 // form -- {cos bits, Hamming, id lo, id hi} [B][k] + meta -- instead of out_ids / out_scores / out_n)
 hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uint32_t* fn, uint32_t K2,
                                const uint32_t* tcut, const uint4* codes, uint64_t cap, uint32_t W4,
-                               const uint4* qcodes, const uint16_t* dense, uint32_t np, const uint32_t* qpc,
-                               uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids, uint64_t* out_ids,
-                               float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
+                               const uint4* qcodes, uint32_t B, uint32_t k, uint32_t R, const uint64_t* ids,
+                               uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
                                const uint32_t* kcnt = nullptr, uint32_t* block2 = nullptr,
                                const uint32_t* reff = nullptr, const uint32_t* m_rows = nullptr,
                                const uint32_t* m_dist = nullptr, uint32_t mlen = 0);
