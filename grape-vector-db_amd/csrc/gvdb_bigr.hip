@@ -205,15 +205,22 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
     if (tid == 0) s_n = 0u;
     __syncthreads();
     {
+        constexpr uint32_t kU = 4;  // 16-B loads in flight per lane
         uint32_t* wh = whist + wv * H4;
         const uint32_t v1 = min(nv, (wv + 1u) * segv);
-        for (uint32_t v = wv * segv + lane; v < v1; v += 64u) {
-            const uint4 w = dq[v];
-            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        for (uint32_t v = wv * segv + lane; v < v1; v += 64u * kU) {
+            uint4 w[kU];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (8u * v + (uint32_t)j < N)
-                    atomicAdd(&wh[min(dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc), D)], 1u);
+            for (uint32_t u = 0; u < kU; ++u) w[u] = v + 64u * u < v1 ? dq[v + 64u * u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (uint32_t u = 0; u < kU; ++u) {
+                const uint32_t vv = v + 64u * u;
+                const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (vv < v1 && 8u * vv + (uint32_t)j < N)
+                        atomicAdd(&wh[min(dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc), D)], 1u);
+            }
         }
     }
     __syncthreads();
@@ -255,16 +262,21 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
         __syncthreads();
         const uint32_t sv0 = s_seg * segv, sv1 = min(nv, sv0 + segv), left = s_left;
         uint32_t base = 0u;  // tied rows of the segment before this round
-        for (uint32_t it = sv0; it < sv1; it += nt) {  // block-uniform rounds, rows in order
-            const uint32_t v = it + tid;
-            uint32_t tm = 0u;  // this thread's 8 rows tied at T (bit j)
-            if (v < sv1) {
-                const uint4 w = dq[v];
-                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        constexpr uint32_t kR = 4;  // 16-B words per thread per round: 32 consecutive rows
+        for (uint32_t it = sv0; it < sv1; it += nt * kR) {  // block-uniform rounds, rows in order
+            const uint32_t v = it + tid * kR;
+            uint32_t tm = 0u;  // this thread's 32 rows tied at T (bit 8 u + j)
+            uint4 w[kR];
+#pragma unroll
+            for (uint32_t u = 0; u < kR; ++u) w[u] = v + u < sv1 ? dq[v + u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (uint32_t u = 0; u < kR; ++u) {
+                const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    if (8u * v + (uint32_t)j < N && dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) == T)
-                        tm |= 1u << j;
+                    if (v + u < sv1 && 8u * (v + u) + (uint32_t)j < N &&
+                        dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) == T)
+                        tm |= 1u << (8u * u + (uint32_t)j);
             }
             const uint32_t cnt = (uint32_t)__popc(tm);
             uint32_t incl = cnt;  // wave-inclusive prefix
