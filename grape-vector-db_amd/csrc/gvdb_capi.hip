@@ -1326,13 +1326,37 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     s1.qcodes = ws.qcodes.as<uint4>();
     s1.ev = nullptr;
     s1.tcut = tcut;
+    // the flat pass runs on a second workspace's stream, concurrently with stage 1 (they share
+    // nothing until the certify pass): ordered after the caller's queries, joined before certify
+    struct Ev {
+        hipEvent_t e = nullptr;
+        ~Ev() {
+            if (e) (void)hipEventDestroy(e);
+        }
+    } e_in, e_flat;
+    WsGuard g2(ix->device);
+    Workspace* ws2 = &ws;
+    hipStream_t s2 = s;
+    if (g2.w && hipEventCreateWithFlags(&e_in.e, hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&e_flat.e, hipEventDisableTiming) == hipSuccess) {
+        ws2 = g2.w;
+        s2 = g2.w->stream;
+        g2.begin(s2);
+        HIP_TRY(hipEventRecord(e_in.e, s), "event");
+        HIP_TRY(hipStreamWaitEvent(s2, e_in.e, 0), "stream wait");
+    }
+    UseGuard ug2{ix, s2};
     HIP_TRY(launch_stage1_fast(s1, s), "certified depth: stage 1");
     bool cert = false;
-    gvdb_status st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, ws, s, true, &cert, true);
+    gvdb_status st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, true, &cert, true);
     if (st != GVDB_OK) return st;
     if (!cert) {
-        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, ws, s, false, &cert, true);
+        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, false, &cert, true);
         if (st != GVDB_OK) return st;
+    }
+    if (s2 != s) {
+        HIP_TRY(hipEventRecord(e_flat.e, s2), "event");
+        HIP_TRY(hipStreamWaitEvent(s, e_flat.e, 0), "stream wait");
     }
     if (cert) {
         HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
