@@ -189,7 +189,9 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
                                                               uint32_t* __restrict__ s1_dist,
                                                               uint32_t* __restrict__ tcut,
                                                               uint32_t* __restrict__ mhist,
-                                                              uint32_t* __restrict__ mcount) {
+                                                              uint32_t* __restrict__ mcount,
+                                                              const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t H4 = (D + 4u) & ~3u;
     uint32_t* hist = lds;        // [H4] the query's histogram
@@ -338,7 +340,8 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
     hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
                        a.qpc + g0, a.tcut ? nullptr : a.s1_rows + (uint64_t)g0 * a.R,
                        a.tcut ? nullptr : a.s1_dist + (uint64_t)g0 * a.R, a.tcut ? a.tcut + 4ull * g0 : nullptr,
-                       a.mhist ? a.mhist + (uint64_t)g0 * (a.D + 1u) : nullptr, a.mcount ? a.mcount + g0 : nullptr);
+                       a.mhist ? a.mhist + (uint64_t)g0 * (a.D + 1u) : nullptr, a.mcount ? a.mcount + g0 : nullptr,
+                       a.gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -366,10 +369,14 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     uint64_t* __restrict__ out_ids, float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
     uint32_t* __restrict__ fail, const uint32_t* __restrict__ kcnt, uint32_t* __restrict__ block2,
     const uint32_t* __restrict__ reff, const uint32_t* __restrict__ m_rows, const uint32_t* __restrict__ m_dist,
-    uint32_t mlen) {
+    uint32_t mlen, const uint32_t* __restrict__ list_fail) {
     __shared__ uint32_t s_trow[64], s_cnt[64];
     __shared__ uint32_t s_nt;
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
+    if (list_fail && *list_fail != 0u) {  // the exact list itself was not certified: nothing to certify
+        if (tid == 0) atomicOr(fail, 1u);
+        return;
+    }
     const uint32_t n = min(fn[q], K2);
     const uint32_t T = tcut[4u * q], cut = tcut[4u * q + 1u], need = tcut[4u * q + 2u];
     // 0: cut, 2: no tied member, 3: the tie rank counted in the member list (deep sharded phase 2)
@@ -469,12 +476,13 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                uint64_t* out_ids,
                                float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
                                const uint32_t* kcnt, uint32_t* block2, const uint32_t* reff,
-                               const uint32_t* m_rows, const uint32_t* m_dist, uint32_t mlen) {
+                               const uint32_t* m_rows, const uint32_t* m_dist, uint32_t mlen,
+                               const uint32_t* list_fail) {
     if (B == 0) return hipSuccess;
     if (K2 == 0 || K2 > 64u || (block2 && !reff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(kCertThreads), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4,
                        qcodes, k, R, ids, out_ids, out_scores, out_n, fail, kcnt, block2, reff, m_rows,
-                       m_dist, mlen);
+                       m_dist, mlen, list_fail);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -628,7 +636,9 @@ __global__ __launch_bounds__(kBigThreads) void k_topk_big(const float* __restric
                                                           const uint64_t* __restrict__ ids, uint64_t row_offset,
                                                           uint64_t* __restrict__ out_ids,
                                                           float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
-                                                          uint32_t* __restrict__ nan_flag) {
+                                                          uint32_t* __restrict__ nan_flag,
+                                                          const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     __shared__ TopkLds L;
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
     const float* sc = scores + (uint64_t)q * R;
@@ -672,7 +682,9 @@ __global__ __launch_bounds__(kBigThreads) void k_shard_deep_topk(const float* __
                                                                  const uint32_t* __restrict__ reff, uint32_t B,
                                                                  uint32_t Rl, uint32_t kout,
                                                                  const uint64_t* __restrict__ ids, uint32_t err,
-                                                                 uint32_t* __restrict__ block2) {
+                                                                 uint32_t* __restrict__ block2,
+                                                                 const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     __shared__ TopkLds L;
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
     const uint64_t base = (uint64_t)q * Rl;
@@ -699,11 +711,12 @@ __global__ __launch_bounds__(kBigThreads) void k_shard_deep_topk(const float* __
 
 hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,
-                                  const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s) {
+                                  const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s,
+                                  const uint32_t* gate) {
     if (B == 0) return hipSuccess;
     if (k > kTopkBigMax || Rl > kBigRMax) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_shard_deep_topk, dim3(B), dim3(kBigThreads), 0, s, m_cos, m_rows, m_dist, own_cnt, reff, B,
-                       Rl, k, ids, err, block2);
+                       Rl, k, ids, err, block2, gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -712,7 +725,7 @@ hipError_t launch_topk_big(const FinalArgs& a, const uint32_t* s1_dist, hipStrea
     if (a.B == 0) return hipSuccess;
     if (a.kout > kTopkBigMax) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_topk_big, dim3(a.B), dim3(kBigThreads), 0, s, a.scores, a.s1_rows, s1_dist, a.R, a.kout,
-                       a.descending, a.ids, a.row_offset, a.out_ids, a.out_scores, a.out_n, a.nan_flag);
+                       a.descending, a.ids, a.row_offset, a.out_ids, a.out_scores, a.out_n, a.nan_flag, a.gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

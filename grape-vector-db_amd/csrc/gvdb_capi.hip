@@ -87,6 +87,11 @@ std::atomic<uint64_t>& flat_fallbacks_i8() {
     static std::atomic<uint64_t> n{0};
     return n;
 }
+// certified default-depth searches: [0] certified batches, [1] batches sent to bq_search
+std::atomic<uint64_t>& deep_cert_count(int which) {
+    static std::atomic<uint64_t> c[2];
+    return c[which & 1];
+}
 
 enum { kTimSampleHist = 0, kTimScan = 1, kTimSelect = 2, kTimRerank = 3, kTimFinal = 4, kTimFlatEmit = 5, kTimFlat = 6,
        kTimFlatEmitI8 = 7, kTimFlatI8 = 8, kTimN = 9 };
@@ -178,8 +183,11 @@ struct WsPool {
     std::vector<std::unique_ptr<Workspace>> free;
     Workspace* acquire(int device) {
         {
+            // LIFO: a call that nests a second workspace (deep_cert_search's flat pass)
+            // releases the inner one first, so the next call gets the same pair in the
+            // same roles (their buffers stay sized for one role each)
             std::lock_guard<std::mutex> g(mu);
-            for (size_t i = 0; i < free.size(); ++i) {
+            for (size_t i = free.size(); i-- > 0;) {
                 if (free[i]->device == device) {
                     Workspace* w = free[i].release();
                     free.erase(free.begin() + i);
@@ -370,6 +378,7 @@ struct BqSearchArgs {
     uint32_t* d_out_dist;   // candidates mode: stage-1 order, no final sort
     uint64_t out_stride;    // candidates mode: output row stride (0 = R)
     const uint32_t* row_map;  // filtered search: v's codes are the compacted allowed rows; subset row -> index row
+    const uint32_t* gate;     // device-side fallback (deep_cert_search): runs iff *gate != 0 (large-R dense path)
 };
 
 // Stage-1 + stage-2 timing without a host round trip: events are recorded
@@ -576,6 +585,8 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     const ShardView& v = a.v;
     const uint32_t B = a.B, R = a.R;
     if (B == 0) return GVDB_OK;
+    if (a.gate && (R <= kSelectLdsCap || !a.dims_match || a.d_out_dist || a.row_map))
+        return fail(GVDB_ERR_INVALID_ARGUMENT, "gated search: the large-R path only");
     if (R == 0) {
         if (a.d_out_n) HIP_TRY(hipMemsetAsync(a.d_out_n, 0, (size_t)B * 4, s), "memset out_n");
         return GVDB_OK;
@@ -636,7 +647,8 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         } else if (big) {
             // R beyond the LDS select (the reference's default ratio 0.1): the
             // batched stage 1 with k_select_big (exact top-R membership)
-            if (timed) ev = timing_events();
+            if (timed && !a.gate) ev = timing_events();
+            s1.gate = a.gate;
             s1.codes = v.codes;
             s1.cap = v.cap;
             s1.N = v.N;
@@ -671,6 +683,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     rr.R = R;
     rr.kind = a.kind;
     rr.scores = ws.scores.as<float>();
+    rr.gate = a.gate;
     HIP_TRY(launch_rerank(rr, s), "rerank");
     if (a.d_out_dist) {
         const uint64_t ostr = a.out_stride ? a.out_stride : R;
@@ -691,6 +704,7 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
         fa.out_scores = a.d_out_scores;
         fa.out_n = a.d_out_n;
         fa.nan_flag = d_flags + 1;
+        fa.gate = a.gate;
         if (big) {
             HIP_TRY(launch_topk_big(fa, ws.s1_dist.as<uint32_t>(), s), "final top-k (large R)");
         } else if (R <= kSortLdsCap) {
@@ -718,6 +732,37 @@ gvdb_status check_poisoned(const uint32_t* h_n, uint64_t B) {
 }
 
 }  // namespace
+
+// ============================================================================
+// tier outcomes of the host-sync-free searches
+// ============================================================================
+// The _device entry points decide their fallback tiers on the device (gated
+// launches, gvdb_device.h gate_closed).  What the host keeps from a tier's
+// outcome -- the adaptive i8 skip and the diagnostics counters -- arrives
+// through a pinned word copied behind the search on its stream and read once
+// the search's event has completed (tier_poll, at the next search): never
+// waited for (the diagnostics getters wait, a destroyed index's records are
+// dropped).  One process-wide log.
+enum TierKind : int { kTierFlatI8 = 0, kTierFlatBf16 = 1, kTierDeepCert = 2 };
+struct FlagLog {
+    static constexpr uint32_t kSlots = 256;
+    std::mutex mu;
+    uint32_t* h = nullptr;  // pinned [kSlots]
+    struct Rec {
+        hipEvent_t ev;
+        uint32_t slot;
+        int kind;
+        const gvdb_index* ix;  // the adaptive i8 skip's owner (nullptr once destroyed)
+    };
+    std::vector<Rec> pend;  // oldest first
+    std::vector<hipEvent_t> spare;
+    uint32_t next = 0;
+    ~FlagLog() {
+        for (auto& r : pend) (void)hipEventDestroy(r.ev);
+        for (auto e : spare) (void)hipEventDestroy(e);
+        if (h) (void)hipHostFree(h);
+    }
+};
 
 // ============================================================================
 // index object
@@ -934,6 +979,71 @@ uint32_t effective_R(const gvdb_index* ix, const gvdb_search_params* sp, uint64_
     return (uint32_t)R;
 }
 
+FlagLog& tier_log() {
+    static FlagLog* L = new FlagLog();  // never destroyed: records may outlive static destructors
+    return *L;
+}
+void tier_apply(const FlagLog::Rec& r, uint32_t failed) {
+    if (r.kind == kTierFlatI8) {
+        if (!failed) return;
+        flat_fallbacks_i8().fetch_add(1);
+        flat_fallbacks().fetch_add(1);  // the async form's next tier is the exact scan
+        const char* fk = getenv("GVDB_FLAT");
+        if (r.ix && !(fk && strcmp(fk, "i8") == 0)) r.ix->i8_skip.store(16);
+    } else if (r.kind == kTierFlatBf16) {
+        if (failed) flat_fallbacks().fetch_add(1);
+    } else {
+        deep_cert_count(failed ? 1 : 0).fetch_add(1);
+    }
+}
+// the completed outcomes, oldest first (wait = true: every pending one)
+void tier_poll(bool wait = false) {
+    FlagLog& L = tier_log();
+    std::lock_guard<std::mutex> g(L.mu);
+    size_t done = 0;
+    for (; done < L.pend.size(); ++done) {
+        const FlagLog::Rec& r = L.pend[done];
+        if (wait ? hipEventSynchronize(r.ev) != hipSuccess : hipEventQuery(r.ev) != hipSuccess) break;
+        tier_apply(r, L.h[r.slot]);
+        L.spare.push_back(r.ev);
+    }
+    L.pend.erase(L.pend.begin(), L.pend.begin() + done);
+}
+// an index being destroyed: its pending records keep their counters, lose their owner
+void tier_forget(const gvdb_index* ix) {
+    FlagLog& L = tier_log();
+    std::lock_guard<std::mutex> g(L.mu);
+    for (auto& r : L.pend)
+        if (r.ix == ix) r.ix = nullptr;
+}
+// copy the tier's device outcome word (non-zero = not certified) behind the search
+gvdb_status tier_record(const gvdb_index* ix, const uint32_t* d_word, int kind, hipStream_t s) {
+    tier_poll();
+    FlagLog& L = tier_log();
+    std::lock_guard<std::mutex> g(L.mu);
+    if (!L.h) HIP_TRY(hipHostMalloc((void**)&L.h, FlagLog::kSlots * 4, hipHostMallocDefault), "alloc tier log");
+    if (L.pend.size() >= FlagLog::kSlots) {  // a full log drops its oldest record (diagnostics only)
+        L.spare.push_back(L.pend.front().ev);
+        L.pend.erase(L.pend.begin());
+    }
+    hipEvent_t ev = nullptr;
+    if (!L.spare.empty()) {
+        ev = L.spare.back();
+        L.spare.pop_back();
+    } else {
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "tier event");
+    }
+    const uint32_t slot = L.next++ % FlagLog::kSlots;
+    hipError_t e = hipMemcpyAsync(L.h + slot, d_word, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(ev, s);
+    if (e != hipSuccess) {
+        L.spare.push_back(ev);
+        return dev_fail(e, "tier record");
+    }
+    L.pend.push_back({ev, slot, kind, ix});
+    return GVDB_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -995,6 +1105,7 @@ gvdb_status gvdb_index_create(const gvdb_params* params, gvdb_index** out) {
 void gvdb_index_destroy(gvdb_index* ix) {
     if (!ix) return;
     (void)quiesce(ix);
+    tier_forget(ix);
     for (auto& p : ix->use_ev) (void)hipEventDestroy(p.second);
     ix->free_all();
     (void)hipStreamDestroy(ix->stream);
@@ -1107,14 +1218,26 @@ static void zero_past_counts(uint64_t* ids, float* scores, const uint32_t* n, ui
     }
 }
 
+// fail_out != nullptr: the host-sync-free form -- nothing is read back; *fail_out
+// points at the device word that is non-zero when the batch is NOT certified (the
+// gate of the caller's device-side fallback), and *certified stays false.
 static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32_t B, uint32_t dim, uint32_t k, int kind,
                            int descending, uint64_t* d_ids, float* d_scores, uint32_t* d_n, Workspace& ws,
-                           hipStream_t s, bool i8, bool* certified, bool rows_out = false) {
+                           hipStream_t s, bool i8, bool* certified, bool rows_out = false,
+                           uint32_t** fail_out = nullptr) {
     *certified = false;
     gvdb_status st = i8 ? ensure_rowsq(ix, ws, s) : ensure_rowsb(ix, ws, s);
     if (st != GVDB_OK) return st;
+    HIP_TRY(ws.zero.ensure((kFxQ + 4) * 4), "alloc counts");
+    uint32_t* fail = ws.zero.as<uint32_t>();
+    if (fail_out) *fail_out = fail;
+    // a tier that cannot run at all is a failed tier (async form: its gate word says so)
+    auto uncertified = [&]() -> gvdb_status {
+        if (fail_out) HIP_TRY(hipMemsetD32Async(fail, 1u, 1, s), "mark tier failed");
+        return GVDB_OK;
+    };
     // the exact scan reproduces the reference's NaN behaviour
-    if (i8 ? ix->rows_nonfinite : ix->rows_have_nan) return GVDB_OK;
+    if (i8 ? ix->rows_nonfinite : ix->rows_have_nan) return uncertified();
     const uint32_t N = (uint32_t)ix->n, KC = i8 ? fx_kc_i8(dim) : fx_kc(dim);
     const uint32_t ntiles = (N + kFxRows - 1) / kFxRows;
     static const uint32_t every = [] {  // GVDB_FLAT_EVERY: sample-pass tile stride (A/B timing)
@@ -1139,7 +1262,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
             ++mk;
         }
     }
-    if (mk > S) return GVDB_OK;
+    if (mk > S) return uncertified();
     const uint32_t cc = kFxCandCap;
     HIP_TRY(ws.qnorm.ensure(kFxQ * 4), "alloc qnorm");
     HIP_TRY(ws.fx_qb.ensure((size_t)KC * kFxQ * 128 + kFxQ * 12), "alloc converted queries");
@@ -1151,12 +1274,10 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
     HIP_TRY(ws.fx_cand.ensure((size_t)kFxQ * cc * 8), "alloc candidates");  // rows, then their approx scores
     HIP_TRY(ws.fx_scores.ensure((size_t)kFxQ * cc * 4), "alloc candidate scores");
     HIP_TRY(ws.thr.ensure(kFxQ * 4), "alloc thresholds");
-    HIP_TRY(ws.zero.ensure((kFxQ + 4) * 4), "alloc counts");
     char* qx = ws.fx_qb.as<char>();
     float* qinv = (float*)(qx + (size_t)KC * kFxQ * 128);
     float* qa = qinv + kFxQ;
     float* qd = qa + kFxQ;
-    uint32_t* fail = ws.zero.as<uint32_t>();
     uint32_t* counts = fail + 4;
     bool timed;
     {
@@ -1271,6 +1392,7 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
             timing().n[sg] += 1;
         }
     }
+    if (fail_out) return GVDB_OK;
     HIP_TRY(hipMemcpyAsync(ws.h_flags, fail, 4, hipMemcpyDeviceToHost, s), "fail flag");
     HIP_TRY(hipStreamSynchronize(s), "sync");
     *certified = ws.h_flags[0] == 0;
@@ -1286,17 +1408,19 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
 // reference's (cosine desc, Hamming, row) order when the list certifies them
 // (gvdb_bigr.hip).  Any query it cannot certify (members below the list's last
 // score, a flat tier that cannot certify, non-finite rows) sends the whole batch
-// to bq_search; *done tells the caller which.  Shards with orphan rows (the
-// reference truncates before dropping them) and metrics other than cosine take
-// bq_search directly.  Synchronises the host, as GVDB_SEARCH_FLAT does.
-static std::atomic<uint64_t>& deep_cert_count(int which) {  // [0] certified batches, [1] batches sent to bq_search
-    static std::atomic<uint64_t> c[2];
-    return c[which & 1];
-}
-
+// to bq_search.  Shards with orphan rows (the reference truncates before
+// dropping them) and metrics other than cosine take bq_search directly
+// (*eligible = false).
+// sync = true (host-buffer entry points): the flat tiers and the certificate are
+//   read back on the host; *done tells the caller whether bq_search must run.
+// sync = false (the _device entry points): nothing is read back -- the flat pass
+//   runs one tier, k_deep_certify folds that tier's failure word into its own,
+//   and the B x R rerank (bq_search) is enqueued behind it GATED by that word, so
+//   it runs on the device only for a batch that did not certify (*done = true:
+//   the caller has nothing left to do).
 static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint32_t B, uint32_t dim, uint32_t k,
                                     uint32_t R, int kind, uint64_t* d_ids, float* d_scores, uint32_t* d_n,
-                                    Workspace& ws, hipStream_t s, bool* done) {
+                                    Workspace& ws, hipStream_t s, bool* done, bool sync) {
     *done = false;
     const uint32_t N = (uint32_t)ix->n, W4 = code_w4(dim);
     const char* env = getenv("GVDB_DEEP_CERT");
@@ -1313,6 +1437,12 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     const uint32_t K2 = k <= 16u ? 32u : kDeepK2;
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
     HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 20 + 16), "alloc certified-depth lists");
+    if (!sync) {  // the gated fallback's buffers, sized before anything is enqueued (no reallocation under it)
+        HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
+        HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
+        HIP_TRY(ws.scores.ensure((size_t)B * R * 4), "alloc scores");
+        HIP_TRY(ws.qnorm.ensure((size_t)B * 4), "alloc qnorm");
+    }
     char* p = ws.deep.as<char>();
     uint64_t* frow = (uint64_t*)p;
     float* fsc = (float*)(p + (size_t)B * K2 * 8);
@@ -1348,33 +1478,99 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     UseGuard ug2{ix, s2};
     HIP_TRY(launch_stage1_fast(s1, s), "certified depth: stage 1");
     bool cert = false;
-    gvdb_status st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, true, &cert, true);
-    if (st != GVDB_OK) return st;
-    if (!cert) {
-        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, false, &cert, true);
+    uint32_t* flat_fail = nullptr;
+    gvdb_status st;
+    if (sync) {
+        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, true, &cert, true);
+        if (st != GVDB_OK) return st;
+        if (!cert) {
+            st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, false, &cert, true);
+            if (st != GVDB_OK) return st;
+        }
+    } else {  // one tier (i8, or bf16 while the index skips i8), its failure word read on the device
+        const bool i8 = ix->i8_skip.load() == 0;
+        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, i8, &cert, true, &flat_fail);
         if (st != GVDB_OK) return st;
     }
     if (s2 != s) {
         HIP_TRY(hipEventRecord(e_flat.e, s2), "event");
         HIP_TRY(hipStreamWaitEvent(s, e_flat.e, 0), "stream wait");
     }
-    if (cert) {
-        HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
-        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), B, k, R,
-                                    ix->ids, d_ids, d_scores, d_n, dfail, s),
-                "certified depth: certify");
+    if (sync && !cert) {
+        deep_cert_count(1).fetch_add(1);
+        return GVDB_OK;
+    }
+    HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
+    HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), B, k, R,
+                                ix->ids, d_ids, d_scores, d_n, dfail, s, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                0, flat_fail),
+            "certified depth: certify");
+    if (sync) {
         HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
         HIP_TRY(hipStreamSynchronize(s), "sync");
         cert = ws.h_flags[0] == 0;
+        deep_cert_count(cert ? 0 : 1).fetch_add(1);
+        *done = cert;
+        return GVDB_OK;
     }
-    deep_cert_count(cert ? 0 : 1).fetch_add(1);
-    *done = cert;
+    // the B x R rerank, run by the device only if the certify pass failed
+    BqSearchArgs a{};
+    a.v = ShardView{ix->rows, dim, ix->norms, ix->codes, ix->cap, N, dim, ix->ids, 0};
+    a.d_q = d_q;
+    a.qlen = dim;
+    a.B = B;
+    a.thr = ix->thr;
+    a.dims_match = true;
+    a.R = R;
+    a.kout = k;
+    a.kind = kind;
+    a.descending = 1;
+    a.d_out_ids = d_ids;
+    a.d_out_scores = d_scores;
+    a.d_out_n = d_n;
+    a.gate = dfail;
+    st = bq_search(a, ws, s);
+    if (st != GVDB_OK) return st;
+    if ((st = tier_record(ix, dfail, kTierDeepCert, s)) != GVDB_OK) return st;
+    *done = true;
     return GVDB_OK;
 }
 
+// FLAT mode's exact tier: the exact scan + one-launch top-k, in query groups whose
+// dense score block stays within kFlatScoreBytes (1 GiB: 26 queries per group at
+// 10M rows) instead of one B x N block (10 GB at B = 256).  gate: the device-side
+// fallback form (runs only if *gate != 0; k <= 1024).
+static gvdb_status flat_exact(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k, int kind,
+                              int descending, uint64_t* d_ids, float* d_scores, uint32_t* d_n, Workspace& ws,
+                              hipStream_t s, const uint32_t* gate) {
+    const uint64_t per_q = std::max<uint64_t>(ix->n * 4, 1);
+    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(B, kFlatScoreBytes / per_q));
+    HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
+    HIP_TRY(ws.scores.ensure(G * per_q), "alloc flat scores");
+    HIP_TRY(ws.flags.ensure(16), "alloc flags");
+    HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
+    HIP_TRY(launch_row_norms(d_q, B, dim, ws.qnorm.as<float>(), s, gate), "qnorm");
+    if (!gate) HIP_TRY(ws.sort_tmp.ensure(flat_select_bytes((uint32_t)ix->n)), "alloc sort tmp");
+    for (uint64_t g0 = 0; g0 < B; g0 += G) {
+        const uint32_t bg = (uint32_t)std::min<uint64_t>(G, B - g0);
+        HIP_TRY(launch_flat_scores(d_q + g0 * dim, bg, ws.qnorm.as<float>() + g0, ix->rows, (uint32_t)ix->n, dim,
+                                   ix->norms, kind, nullptr, ws.scores.as<float>(), s, gate),
+                "flat scores");
+        HIP_TRY(launch_flat_select(ws.scores.as<float>(), bg, (uint32_t)ix->n, (uint32_t)k, descending, 0, 0.0f, ix->ids,
+                                   d_ids + g0 * k, d_scores + g0 * k, d_n ? d_n + g0 : nullptr, ws.sort_tmp.p,
+                                   ws.sort_tmp.n, ws.flags.as<uint32_t>() + 1, s, gate),
+                "flat select");
+    }
+    return GVDB_OK;
+}
+
+// sync: the host-buffer entry points (they synchronise anyway) decide the flat
+// tiers and the certified default depth on the host; the _device entry points
+// (sync = false) return after enqueueing: every fallback tier is enqueued behind
+// the tier it backs up and gated on the device by that tier's failure word.
 static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                      const gvdb_search_params* sp_in, uint64_t* d_ids, float* d_scores, uint32_t* d_n,
-                                     Workspace& ws, hipStream_t s) {
+                                     Workspace& ws, hipStream_t s, bool sync) {
     gvdb_search_params sp{};
     sp.mode = GVDB_SEARCH_BQ_RERANK;
     sp.metric = GVDB_METRIC_COSINE;
@@ -1384,6 +1580,7 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
                      : sp.metric == GVDB_METRIC_COSINE_DISTANCE ? kScoreCosineDistance
                                                                  : kScoreCosine;
     const int descending = kind == kScoreCosine;
+    tier_poll();  // earlier async searches' tier outcomes (adaptive i8 skip)
     if (sp.mode == GVDB_SEARCH_FLAT && kind != kScoreL2 && ix->n >= kFxMinN && k >= 1 && k <= 256 &&
         !getenv_flag("GVDB_FLAT_EXACT_ONLY")) {
         // Tiers: i8 candidates first (half the bytes of bf16, twice the MFMA
@@ -1393,7 +1590,9 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
         // adaptive -- after an i8 batch fails to certify, this index skips the
         // i8 tier for its next 16 batches (bounding the wasted pass on data
         // whose i8 candidate sets overflow).  GVDB_FLAT=i8 / bf16 forces the
-        // first tier.
+        // first tier.  The async form runs the first tier, then the exact scan
+        // gated by its failure word (no bf16 retry: that tier's mirror is built
+        // only once a synchronous search or the skip asks for it).
         const char* fk = getenv("GVDB_FLAT");
         const bool force_i8 = fk && strcmp(fk, "i8") == 0;
         const bool force_bf16 = fk && strcmp(fk, "bf16") == 0;
@@ -1405,6 +1604,15 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
             try_i8 = skip == 0;
         }
         bool certified = false;
+        if (!sync) {
+            uint32_t* fail = nullptr;
+            gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
+                                            d_n, ws, s, try_i8, &certified, false, &fail);
+            if (st != GVDB_OK) return st;
+            if ((st = flat_exact(ix, d_q, B, dim, k, kind, descending, d_ids, d_scores, d_n, ws, s, fail)) != GVDB_OK)
+                return st;
+            return tier_record(ix, fail, try_i8 ? kTierFlatI8 : kTierFlatBf16, s);
+        }
         if (try_i8) {
             gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
                                             d_n, ws, s, true, &certified);
@@ -1417,37 +1625,13 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
         if (st != GVDB_OK || certified) return st;
         flat_fallbacks().fetch_add(1);
     }
-    if (sp.mode == GVDB_SEARCH_FLAT) {
-        // exact scan + radix select, in query groups whose dense score block
-        // stays within kFlatScoreBytes (1 GiB: 26 queries per group at 10M rows)
-        // instead of one B x N block (10 GB at B = 256)
-        const uint64_t per_q = std::max<uint64_t>(ix->n * 4, 1);
-        const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(B, kFlatScoreBytes / per_q));
-        HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
-        HIP_TRY(ws.scores.ensure(G * per_q), "alloc flat scores");
-        HIP_TRY(ws.flags.ensure(16), "alloc flags");
-        HIP_TRY(hipMemsetAsync(ws.flags.p, 0, 16, s), "memset flags");
-        HIP_TRY(launch_row_norms(d_q, B, dim, ws.qnorm.as<float>(), s), "qnorm");
-        const size_t need = flat_select_bytes((uint32_t)ix->n);
-        HIP_TRY(ws.sort_tmp.ensure(need), "alloc sort tmp");
-        for (uint64_t g0 = 0; g0 < B; g0 += G) {
-            const uint32_t bg = (uint32_t)std::min<uint64_t>(G, B - g0);
-            HIP_TRY(launch_flat_scores(d_q + g0 * dim, bg, ws.qnorm.as<float>() + g0, ix->rows, (uint32_t)ix->n, dim,
-                                       ix->norms, kind, nullptr, ws.scores.as<float>(), s),
-                    "flat scores");
-            HIP_TRY(launch_flat_select(ws.scores.as<float>(), bg, (uint32_t)ix->n, (uint32_t)k, descending, 0, 0.0f,
-                                       ix->ids, d_ids + g0 * k, d_scores + g0 * k, d_n ? d_n + g0 : nullptr,
-                                       ws.sort_tmp.p, ws.sort_tmp.n, ws.flags.as<uint32_t>() + 1, s),
-                    "flat select");
-        }
-        HIP_TRY(hipStreamSynchronize(s), "sync");
-        return GVDB_OK;
-    }
+    if (sp.mode == GVDB_SEARCH_FLAT)
+        return flat_exact(ix, d_q, B, dim, k, kind, descending, d_ids, d_scores, d_n, ws, s, nullptr);
     const uint32_t R = effective_R(ix, &sp, k);
     if (sp.mode == GVDB_SEARCH_BQ_RERANK) {  // the reference's default depth: certified, no B x R rerank
         bool done = false;
         gvdb_status st = deep_cert_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, R, kind, d_ids, d_scores, d_n, ws, s,
-                                          &done);
+                                          &done, sync);
         if (st != GVDB_OK || done) return st;
     }
     BqSearchArgs a{};
@@ -1499,7 +1683,7 @@ gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64
         return GVDB_OK;
     }
     st = index_search_impl(ix, ws.q.as<float>(), B, dim, k, sp, ws.out_ids.as<uint64_t>(), ws.out_scores.as<float>(),
-                           ws.out_n.as<uint32_t>(), ws, s);
+                           ws.out_n.as<uint32_t>(), ws, s, true);
     if (st != GVDB_OK) return st;
     HIP_TRY(hipMemcpyAsync(out_ids, ws.out_ids.p, B * k * 8, hipMemcpyDeviceToHost, s), "download ids");
     HIP_TRY(hipMemcpyAsync(out_scores, ws.out_scores.p, B * k * 4, hipMemcpyDeviceToHost, s), "download scores");
@@ -1637,7 +1821,7 @@ gvdb_status gvdb_index_search_device(const gvdb_index* ix, const float* d_querie
     hipStream_t s = (hipStream_t)stream;  // NULL = the legacy default stream (orders with the caller's work)
     g.begin(s);
     UseGuard ug{ix, s};
-    return index_search_impl(ix, d_queries, B, dim, k, sp, d_out_ids, d_out_scores, d_out_n, *g.w, s);
+    return index_search_impl(ix, d_queries, B, dim, k, sp, d_out_ids, d_out_scores, d_out_n, *g.w, s, false);
 }
 
 gvdb_status gvdb_index_bq_topr_device(const gvdb_index* ix, const float* d_queries, uint64_t B, uint32_t dim, uint64_t R,
@@ -2156,8 +2340,15 @@ gvdb_status gvdb_topk_merge_device(const uint64_t* d_ids, const float* d_scores,
     return GVDB_OK;
 }
 
-uint64_t gvdb_flat_fallback_count(void) { return flat_fallbacks().load(); }
-uint64_t gvdb_flat_i8_fallback_count(void) { return flat_fallbacks_i8().load(); }
+// (diagnostics: they wait for the tier outcomes of the async searches still in flight)
+uint64_t gvdb_flat_fallback_count(void) {
+    tier_poll(true);
+    return flat_fallbacks().load();
+}
+uint64_t gvdb_flat_i8_fallback_count(void) {
+    tier_poll(true);
+    return flat_fallbacks_i8().load();
+}
 
 }  // extern "C"
 
@@ -2177,6 +2368,7 @@ extern "C" int gvdb_debug_stage1_thresholds(uint32_t* out, uint32_t B) {
 // tests only: 1 if a query of the last GVDB_DEBUG_THR=1 batch took the all-rows rescan
 extern "C" int gvdb_debug_deep_cert(uint64_t* out) {  // [0] certified batches, [1] sent to the rerank path
     if (!out) return 1;
+    tier_poll(true);
     out[0] = deep_cert_count(0).load();
     out[1] = deep_cert_count(1).load();
     return 0;
@@ -2312,8 +2504,11 @@ gvdb_status gvdb::shard_stage1_members(const gvdb_index* ix, const float* d_q, u
 // top-K2 over its shard (flat_mx_search, rows), filtered by the rule of its owned
 // rows that k_shard_deep_own wrote (tcut), gives its local top-min(k, own) entries
 // whenever the list certifies them (k_deep_certify) -- instead of reranking
-// ~R / G owned rows per query.  Shards with orphan rows, k > 32 or fewer than
-// kFxMinN rows, and batches the list cannot certify, leave *done = false.
+// ~R / G owned rows per query.  No host sync: the flat tier's failure word is
+// folded into the certificate's, *dfail (a device word that must outlive the call:
+// the caller's scratch), which gates the caller's rerank fallback on the device.
+// Shards with orphan rows, k > 32 or fewer than kFxMinN rows are not eligible
+// (*enqueued = false: the caller reranks ungated).
 bool gvdb::shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t k) {
     const char* env = getenv("GVDB_DEEP_CERT");
     return !(env && env[0] == '0') && ix && k >= 1 && k <= 32 && ix->n >= kFxMinN && ix->n <= 0xFFFFFFFFull &&
@@ -2323,8 +2518,8 @@ bool gvdb::shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t
 gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                          const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
                                          const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl,
-                                         uint32_t* block2, hipStream_t s, bool* done) {
-    *done = false;
+                                         uint32_t* block2, uint32_t* dfail, hipStream_t s, bool* enqueued) {
+    *enqueued = false;
     if (!shard_certified_eligible(ix, dim, k) || B == 0 || B > 0xFFFFFFFFull) return GVDB_OK;
     gvdb_status st = set_device(ix->device);
     if (st != GVDB_OK) return st;
@@ -2333,6 +2528,7 @@ gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q,
     Workspace& ws = *g.w;
     g.begin(s);
     UseGuard ug{ix, s};
+    tier_poll();
     const uint32_t W4 = code_w4(dim), K2 = k <= 16 ? 32u : kDeepK2;
     HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc qcodes");
     HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 4 + 16), "alloc certified lists");
@@ -2340,26 +2536,19 @@ gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q,
     uint64_t* frow = (uint64_t*)p;
     float* fsc = (float*)(p + (size_t)B * K2 * 8);
     uint32_t* fn = (uint32_t*)(p + (size_t)B * K2 * 12);
-    uint32_t* dfail = fn + B;
     HIP_TRY(launch_pack(d_q, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
     bool cert = false;
-    st = flat_mx_search(ix, d_q, (uint32_t)B, dim, K2, kScoreCosine, 1, frow, fsc, fn, ws, s, true, &cert, true);
+    uint32_t* flat_fail = nullptr;
+    const bool i8 = ix->i8_skip.load() == 0;
+    st = flat_mx_search(ix, d_q, (uint32_t)B, dim, K2, kScoreCosine, 1, frow, fsc, fn, ws, s, i8, &cert, true,
+                        &flat_fail);
     if (st != GVDB_OK) return st;
-    if (!cert) {
-        st = flat_mx_search(ix, d_q, (uint32_t)B, dim, K2, kScoreCosine, 1, frow, fsc, fn, ws, s, false, &cert, true);
-        if (st != GVDB_OK) return st;
-    }
-    if (cert) {
-        HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
-        HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(),
-                                    (uint32_t)B, (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s, own_cnt,
-                                    block2, reff, m_rows, m_dist, Rl),
-                "certified deep phase 2");
-        HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
-        HIP_TRY(hipStreamSynchronize(s), "sync");
-        cert = ws.h_flags[0] == 0;
-    }
-    deep_cert_count(cert ? 0 : 1).fetch_add(1);
-    *done = cert;
+    HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
+    HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), (uint32_t)B,
+                                (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s, own_cnt, block2, reff,
+                                m_rows, m_dist, Rl, flat_fail),
+            "certified deep phase 2");
+    if ((st = tier_record(ix, dfail, kTierDeepCert, s)) != GVDB_OK) return st;
+    *enqueued = true;
     return GVDB_OK;
 }

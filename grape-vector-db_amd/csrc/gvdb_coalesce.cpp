@@ -74,11 +74,16 @@ void run_batch(gvdb_coalescer* c, const std::vector<Req*>& reqs) {
     const gvdb_status st =
         gvdb_index_search(c->ix, q.data(), B, c->dim, c->k, &c->sp, ids.data(), sc.data(), n.data());
     const std::string err = st == GVDB_OK ? std::string() : std::string(gvdb_last_error());
+    // A NaN score fails only the queries it poisoned: gvdb_index_search has
+    // downloaded every query's results and counts before it reports
+    // GVDB_ERR_QUANTIZATION, and each caller gets exactly its own serial result.
+    const bool per_query = st == GVDB_ERR_QUANTIZATION;
     for (size_t i = 0; i < B; ++i) {
         Req* r = reqs[i];
-        r->st = st;
-        r->err = err;
-        if (st == GVDB_OK) {
+        const bool ok = st == GVDB_OK || (per_query && n[i] != GVDB_N_POISONED);
+        r->st = ok ? GVDB_OK : st;
+        r->err = ok ? std::string() : err;
+        if (ok) {
             memcpy(r->ids, ids.data() + i * c->k, c->k * 8);
             memcpy(r->scores, sc.data() + i * c->k, c->k * 4);
             if (r->n) *r->n = n[i];

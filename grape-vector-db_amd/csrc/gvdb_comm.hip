@@ -167,6 +167,17 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
     hipError_t he = hipSetDevice(c->device);
     if (he != hipSuccess) return report_status(GVDB_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(he));
     hipStream_t s = (hipStream_t)stream;
+    // the next call (possibly on another stream) and gvdb_comm_destroy wait for
+    // everything enqueued here: `done` is recorded on EVERY return path below
+    struct DoneGuard {
+        gvdb_comm* c;
+        hipStream_t s;
+        ~DoneGuard() {
+            if (!c->done) (void)hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+            c->pending = c->done && hipEventRecord(c->done, s) == hipSuccess;
+            c->last = s;
+        }
+    } done_guard{c, s};
     uint64_t w1 = 0, w2 = 0, scratch = 0;
     gvdb_shard_sizes(B, R, k, dim, &w1, &w2, &scratch);
     const uint64_t wf = shard_words_flat(B, k);
@@ -235,11 +246,6 @@ gvdb_status gvdb_index_search_sharded_device(const gvdb_index* shard, gvdb_comm*
         if (st == GVDB_OK) st = gvdb_shard_final_device(recv2, G, B, k, d_out_ids, d_out_scores, d_out_n, stream);
         if (st == GVDB_OK && local != GVDB_OK) report_status(local, local_err);
     }
-    // the next call (possibly on another stream) waits for everything enqueued here,
-    // error paths included
-    if (!c->done) (void)hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
-    c->pending = c->done && hipEventRecord(c->done, s) == hipSuccess;
-    c->last = s;
     return st != GVDB_OK ? st : local;
 }
 

@@ -11,6 +11,13 @@ namespace gvdb {
         if (e__ != hipSuccess) return e__;  \
     } while (0)
 
+// Device-side tier gate of the host-sync-free searches: a fallback tier is
+// enqueued unconditionally behind the tier it backs up, with that tier's
+// failure word as its gate; while the word is 0 (the earlier tier certified
+// its batch) every block of the fallback returns at once.  nullptr = ungated.
+// (Written by an earlier kernel of the same stream: visible at kernel start.)
+__device__ __forceinline__ bool gate_closed(const uint32_t* gate) { return gate && *gate == 0u; }
+
 // Total order key for f32 scores: -0.0 == +0.0 (Rust partial_cmp), ascending.
 __device__ __forceinline__ uint32_t f32_order(float f) {
     uint32_t u = __float_as_uint(f);

@@ -52,7 +52,10 @@ hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, uint64_t n, 
                                 hipStream_t s);
 
 // ---- exact sequential norms (bit-identical to the reference's fold) -----------
-hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t D, float* out, hipStream_t s);
+// gate (optional): a device-side tier gate (gvdb_device.h gate_closed): the launch does
+// nothing while *gate == 0 -- the host-sync-free fallback tiers take one everywhere below
+hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t D, float* out, hipStream_t s,
+                            const uint32_t* gate = nullptr);
 
 // ---- K2 stage 1: BQ Hamming top-R -----------------------------------------------
 struct Stage1Args {
@@ -102,6 +105,7 @@ struct Stage1Args {
                              // the lists
     uint32_t* mhist;         // optional, dense_sel: [B][H = D+1] the members' Hamming histogram (deep sharded
     uint32_t* mcount;        //   exchange-1 block) and [B] their count, written by k_select_dense
+    const uint32_t* gate;    // optional tier gate (dense_sel + FP4 scan only): the stage runs iff *gate != 0
 };
 // ---- large rescore depth (gvdb_bigr.hip): R up to 2^20, D < 4096, k <= 1024 --------
 constexpr uint32_t kBigRMax = 1u << 20;
@@ -120,7 +124,9 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                uint64_t* out_ids, float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
                                const uint32_t* kcnt = nullptr, uint32_t* block2 = nullptr,
                                const uint32_t* reff = nullptr, const uint32_t* m_rows = nullptr,
-                               const uint32_t* m_dist = nullptr, uint32_t mlen = 0);
+                               const uint32_t* m_dist = nullptr, uint32_t mlen = 0,
+                               const uint32_t* list_fail = nullptr);  // != 0: the list is not certified
+                                                                      // (every query fails)
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
@@ -198,6 +204,7 @@ struct RerankArgs {
     float* scores;           // [B][R]
     const uint32_t* counts;  // optional [B]: only the first counts[q] entries are valid
     int short_lists;         // counts are mostly <= 16 (sharded owned rows): k_rerank_small
+    const uint32_t* gate;    // optional tier gate: the rerank runs iff *gate != 0
 };
 hipError_t launch_rerank(const RerankArgs& a, hipStream_t s);
 
@@ -216,6 +223,7 @@ struct FinalArgs {
     uint32_t* out_n;         // [B] or nullptr
     uint32_t* nan_flag;      // [0] set to 1 if a NaN score would make the reference panic;
                              // [1] per-query scratch of the global sort (zero on entry)
+    const uint32_t* gate;    // optional tier gate (launch_topk_big only): runs iff *gate != 0
 };
 hipError_t launch_final_sort(const FinalArgs& a, hipStream_t s);
 size_t final_sort_global_bytes(uint32_t R);
@@ -229,7 +237,7 @@ hipError_t launch_topk_big(const FinalArgs& a, const uint32_t* s1_dist, hipStrea
 // (filtered search); scores stay indexed by scan position.
 hipError_t launch_flat_scores(const float* q, uint32_t B, const float* qnorm, const float* rows, uint32_t N,
                               uint32_t D, const float* norms, int kind, const uint32_t* list,
-                              float* scores /*[B][N]*/, hipStream_t s);
+                              float* scores /*[B][N]*/, hipStream_t s, const uint32_t* gate = nullptr);
 size_t flat_select_bytes(uint32_t N);
 // per query: keep score >= threshold when has_threshold (cosine), stable sort,
 // first `limit`.
@@ -237,7 +245,7 @@ size_t flat_select_bytes(uint32_t N);
 hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint32_t limit, int descending,
                               int has_threshold, float threshold, const uint64_t* ids, uint64_t* out_idx,
                               float* out_scores, uint32_t* out_n, void* tmp, size_t tmp_bytes, uint32_t* nan_flag,
-                              hipStream_t s);
+                              hipStream_t s, const uint32_t* gate = nullptr);  // gated: limit <= 1024
 
 // ---- K4 flat exact search on bf16 MFMA (gvdb_flat.hip) ---------------------------
 // Candidate pass on bf16 MFMA + exact rerank + per-query certificate; see
@@ -383,7 +391,8 @@ hipError_t launch_shard_phase2(const uint32_t* gathered1, uint64_t words1, uint3
 //   block 1 deep: hist u32 [B][dim+1] (Hamming histogram of the local top-min(R, n)
 //                 membership) | counts u32 [B] | err u32 | pad
 //   scratch deep: member rows u32 [B][R] | member dist u32 [B][R] | owned rows u32 [B][R] |
-//                 owned dist u32 [B][R] | cosines f32 [B][R] | own count u32 [B] | reff u32 [B]
+//                 owned dist u32 [B][R] | cosines f32 [B][R] | own count u32 [B] | reff u32 [B] |
+//                 certify word u32 (the certified phase 2's gate)
 //                 (lists dense with stride Rl = min(R, n); phase 2 reads the members only)
 inline bool shard_deep(uint64_t R) { return R > kSelectLdsCap; }
 inline uint64_t shard_words1_deep(uint64_t B, uint32_t dim) { return (B * (dim + 1ull) + B + 1 + 1) & ~1ull; }
@@ -394,19 +403,21 @@ hipError_t launch_shard_member_hist(const uint32_t* m_dist, uint32_t B, uint32_t
 hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
                                  uint32_t R, uint32_t Rl, uint32_t H, const uint32_t* m_rows, const uint32_t* m_dist,
                                  uint32_t* o_rows, uint32_t* o_dist, uint32_t* own_cnt, uint32_t* reff,
-                                 hipStream_t s, uint32_t* tcut = nullptr);
+                                 hipStream_t s, uint32_t* tcut = nullptr, const uint32_t* gate = nullptr);
 // the certified deep phase 2 (gvdb_capi.hip): this rank's local top-k of its owned rows (rule tcut [B][4],
-// counts own_cnt) from its exact cosine top-K2 list, into the exchange-2 block; *done = false: the caller
-// reranks the owned lists instead (nothing written that it relies on)
+// counts own_cnt) from its exact cosine top-K2 list, into the exchange-2 block, with no host sync; *dfail
+// (a device word that outlives the call) becomes non-zero when the batch is not certified: it gates the
+// caller's rerank of the owned lists on the device.  *enqueued = false: not eligible, nothing enqueued
 bool shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t k);
 gvdb_status shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                    const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
                                    const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl, uint32_t* block2,
-                                   hipStream_t s, bool* done);
+                                   uint32_t* dfail, hipStream_t s, bool* enqueued);
 // gvdb_bigr.hip: the owned entries' local top-k (k <= 1024) -> the exchange-2 block
 hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,
-                                  const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s);
+                                  const uint64_t* ids, uint32_t err, uint32_t* block2, hipStream_t s,
+                                  const uint32_t* gate = nullptr);
 // sharded FLAT: gathered blocks of the ranks' exact top-k -> merged top-k
 //   block F (sharded FLAT): ids u64 [B][k] | scores f32 [B][k] | counts [B] | err | pad
 inline uint64_t shard_words_flat(uint64_t B, uint64_t k) { return (3 * B * k + B + 1 + 1) & ~1ull; }

@@ -203,7 +203,8 @@ __device__ __forceinline__ void stage_tile(float* tile, const float* __restrict_
 
 // sqrt(sum x*x) per row, bit-identical to `a.iter().map(|x| x*x).sum::<f32>().sqrt()`.
 __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ rows, uint64_t n, uint32_t D,
-                                                   float* __restrict__ out) {
+                                                   float* __restrict__ out, const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     __shared__ __attribute__((aligned(16))) float tiles[4][64 * kTileLd];
     __shared__ uint64_t bases[4][64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -242,7 +243,9 @@ __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ row
 // (all loads in flight), then lane r < RB folds row r from -0.0 in order.
 constexpr uint32_t kRnSmallFloats = 16384;  // LDS floats per block (64 KiB)
 __global__ __launch_bounds__(256) void k_row_norms_few(const float* __restrict__ rows, uint64_t n, uint32_t D,
-                                                       uint32_t RB, float* __restrict__ out) {
+                                                       uint32_t RB, float* __restrict__ out,
+                                                       const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     extern __shared__ __attribute__((aligned(16))) float stage[];  // [RB][D + 1]
     const uint64_t r0 = (uint64_t)blockIdx.x * RB;
     const uint32_t nr = (uint32_t)min((uint64_t)RB, n - r0), ld = D + 1u;
@@ -257,18 +260,19 @@ __global__ __launch_bounds__(256) void k_row_norms_few(const float* __restrict__
     }
 }
 
-hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t D, float* out, hipStream_t s) {
+hipError_t launch_row_norms(const float* rows, uint64_t n, uint32_t D, float* out, hipStream_t s,
+                            const uint32_t* gate) {
     if (n == 0) return hipSuccess;
     const uint32_t rb = kRnSmallFloats / (D + 1u);
     if (n <= 4096 && rb >= 1) {  // few rows: one staging round trip per block
         const uint32_t RB = std::min<uint32_t>(rb, 16u);
         hipLaunchKernelGGL(k_row_norms_few, dim3((uint32_t)((n + RB - 1) / RB)), dim3(256),
-                           (size_t)RB * (D + 1u) * 4u, s, rows, n, D, RB, out);
+                           (size_t)RB * (D + 1u) * 4u, s, rows, n, D, RB, out, gate);
         GVDB_LAUNCH_CHECK();
         return hipSuccess;
     }
     const uint64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(k_row_norms, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, D, out);
+    hipLaunchKernelGGL(k_row_norms, dim3((uint32_t)blocks), dim3(256), 0, s, rows, n, D, out, gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -964,7 +968,9 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
 template <int W4>
 __global__ __launch_bounds__(256) void k_qfrag(const uint32_t* __restrict__ qwords, uint32_t B, uint32_t ngroups,
                                                v4i_t* __restrict__ qfrag, uint32_t* __restrict__ qpc,
-                                               uint32_t* __restrict__ zero, uint32_t nzero) {
+                                               uint32_t* __restrict__ zero, uint32_t nzero,
+                                               const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     constexpr int KW = 4 * W4, KS = KW / 2, QT = 8;
     constexpr uint32_t kPer = QT * KS * 64;
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -1022,7 +1028,8 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
                                                            const uint32_t* __restrict__ thr, uint32_t B,
                                                            uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
                                                            uint32_t bufcap, uint16_t* __restrict__ dense,
-                                                           uint32_t dense_np) {
+                                                           uint32_t dense_np, const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     constexpr int KW = 4 * W4;  // 32-bit code words per row
     constexpr int KS = KW / 2;  // k-steps of 64 bits
     constexpr int QT = 8;       // query tiles of 32
@@ -1323,17 +1330,26 @@ template <int W4>
 __global__ __launch_bounds__(64) void k_qprep(const float* __restrict__ qf, uint32_t D, float thr, uint32_t B,
                                               uint32_t* __restrict__ qwords, v4i_t* __restrict__ qfrag,
                                               uint32_t* __restrict__ qpc, uint32_t* __restrict__ zero,
-                                              uint32_t nzero) {
+                                              uint32_t nzero, const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     constexpr int KW = 4 * W4, KS = KW / 2, QT = 8;
     constexpr uint32_t kPer = QT * KS * 64;
     __shared__ uint32_t w[KW];
     const uint32_t slot = blockIdx.x, lane = threadIdx.x;
     for (uint32_t i = slot * 64u + lane; i < nzero; i += gridDim.x * 64u) zero[i] = 0u;
     const bool live = slot < B;
-    for (uint32_t c = 0; c < (uint32_t)KW / 2; ++c) {  // 64 dims per ballot = 2 words
-        const uint32_t d = 64u * c + lane;
-        const bool bit = live && d < D && qf[(uint64_t)slot * D + d] > thr;
-        const uint64_t m = __ballot(bit);
+    // every load of the query row in flight at once (a load -> ballot chain per
+    // 64 dims serialised 12 HBM round trips at D = 768)
+    float v[KW / 2];
+#pragma unroll
+    for (int c = 0; c < KW / 2; ++c) {
+        const uint32_t d = 64u * (uint32_t)c + lane;
+        v[c] = live && d < D ? qf[(uint64_t)slot * D + d] : 0.0f;
+    }
+#pragma unroll
+    for (int c = 0; c < KW / 2; ++c) {  // 64 dims per ballot = 2 words
+        const uint32_t d = 64u * (uint32_t)c + lane;
+        const uint64_t m = __ballot(live && d < D && v[c] > thr);
         if (lane == 0) {
             w[2 * c] = msb0_word((uint32_t)m);
             w[2 * c + 1] = msb0_word((uint32_t)(m >> 32));
@@ -1361,14 +1377,14 @@ static void launch_qfrag_t(const Stage1Args& a, hipStream_t s) {
     if (a.qf32) {
         const uint32_t ng = (a.B + 255u) / 256u;
         hipLaunchKernelGGL((k_qprep<W4>), dim3(ng * 256u), dim3(64), 0, s, a.qf32, a.D, a.qthr, a.B,
-                           (uint32_t*)a.qcodes, (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero);
+                           (uint32_t*)a.qcodes, (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero, a.gate);
         return;
     }
     constexpr uint32_t kPer = 8u * (2u * W4) * 64u;
     const uint32_t ng = (a.B + 255u) / 256u;
     const uint32_t n = std::max<uint32_t>(ng * kPer, a.nzero);
     hipLaunchKernelGGL((k_qfrag<W4>), dim3((n + 255u) / 256u), dim3(256), 0, s, (const uint32_t*)a.qcodes, a.B, ng,
-                       (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero);
+                       (v4i_t*)a.qfrag, a.qpc, a.zero, a.nzero, a.gate);
 }
 
 template <int W4>
@@ -1379,14 +1395,14 @@ static hipError_t launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
         if (a.dense_sel) {  // every distance of the group, then its members (the dense block is reused per group)
             hipLaunchKernelGGL((k_scan_mx7<W4, true>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap, a.N,
                                (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                               a.buf, a.bufcap, a.dense, a.dense_np);
+                               a.buf, a.bufcap, a.dense, a.dense_np, a.gate);
             GVDB_LAUNCH_CHECK();
             const hipError_t e = launch_select_dense(a, g, bg, s);
             if (e != hipSuccess) return e;
         } else {
             hipLaunchKernelGGL((k_scan_mx7<W4, false>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap,
                                a.N, (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                               a.buf + (uint64_t)g * a.bufcap, a.bufcap, nullptr, 0u);
+                               a.buf + (uint64_t)g * a.bufcap, a.bufcap, nullptr, 0u, a.gate);
             GVDB_LAUNCH_CHECK();
         }
     }
@@ -2088,6 +2104,8 @@ size_t stage1_plan(Stage1Args& a) {
 
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     const uint32_t W4 = code_w4(a.D);
+    // a tier gate is carried by the dense FP4 form's kernels only (the deep fallback)
+    if (a.gate && !(a.dense_sel && a.mfma_scan)) return hipErrorInvalidValue;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     if (a.mfma_scan) {
         switch (W4) {
@@ -2305,7 +2323,9 @@ __global__ __launch_bounds__(kRrThreads, 2) void k_rerank(const float* __restric
                                                           const float* __restrict__ norms, const float* __restrict__ q,
                                                           uint64_t qlen, const uint32_t* __restrict__ s1_rows,
                                                           uint32_t B, uint32_t R, const uint32_t* __restrict__ counts,
-                                                          int kind, float* __restrict__ scores) {
+                                                          int kind, float* __restrict__ scores,
+                                                          const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     __shared__ __attribute__((aligned(16))) float tiles[2][kRrRows * kRrLd];
     __shared__ __attribute__((aligned(16))) float qs[2][kRrCh];
     __shared__ uint64_t bases[kRrRows];
@@ -2463,7 +2483,9 @@ __global__ __launch_bounds__(kRr2Threads, 4) void k_rerank2(const float* __restr
                                                             const float* __restrict__ q, uint64_t qlen,
                                                             const uint32_t* __restrict__ s1_rows, uint32_t B,
                                                             uint32_t R, const uint32_t* __restrict__ counts, int kind,
-                                                            float* __restrict__ scores) {
+                                                            float* __restrict__ scores,
+                                                            const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     __shared__ __attribute__((aligned(16))) float tiles[kRr2Threads / 64][64 * kRr2Ld];
     __shared__ uint64_t bases[kRr2Threads / 64][64];
     __shared__ uint32_t pre[kRrMaxB + 1];  // work items before query i
@@ -2692,7 +2714,9 @@ __global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __rest
                                                             const float* __restrict__ q, uint64_t qlen,
                                                             const uint32_t* __restrict__ s1_rows, uint32_t B,
                                                             uint32_t R, const uint32_t* __restrict__ counts, int kind,
-                                                            float* __restrict__ scores) {
+                                                            float* __restrict__ scores,
+                                                            const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     __shared__ float4 tile4[kRsRows * (kRsMaxLen / 4 + 1)];
     __shared__ float4 qs4[kRsMaxLen / 4];
     __shared__ uint32_t rowid[kRsRows];
@@ -2737,7 +2761,7 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
     if ((small_slots <= rerank_small_max() || (a.short_lists && a.counts)) && std::min(a.qlen, a.clen) <= kRsMaxLen &&
         small_slots < (1ull << 31)) {
         hipLaunchKernelGGL(k_rerank_small, dim3((uint32_t)small_slots), dim3(kRsThreads), 0, s, a.rows, a.clen,
-                           a.norms, a.q, a.qlen, a.s1_rows, a.B, a.R, a.counts, a.kind, a.scores);
+                           a.norms, a.q, a.qlen, a.s1_rows, a.B, a.R, a.counts, a.kind, a.scores, a.gate);
         GVDB_LAUNCH_CHECK();
         return hipSuccess;
     }
@@ -2760,12 +2784,12 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
             const uint32_t grid = (uint32_t)std::min<uint64_t>(blocks, 4ull * cus);
             hipLaunchKernelGGL(k_rerank2, dim3(grid), dim3(kRr2Threads), 0, s, a.rows, a.clen, a.norms,
                                a.q + (uint64_t)b0 * a.qlen, a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
-                               a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R);
+                               a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R, a.gate);
         } else {
             const uint32_t grid = (uint32_t)std::min<uint64_t>(max_items, 2ull * cus);
             hipLaunchKernelGGL(k_rerank, dim3(grid), dim3(kRrThreads), 0, s, a.rows, a.clen, a.norms,
                                a.q + (uint64_t)b0 * a.qlen, a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
-                               a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R);
+                               a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R, a.gate);
         }
         GVDB_LAUNCH_CHECK();
     }
@@ -2919,72 +2943,83 @@ constexpr int kFlatQT = 16;
 __global__ __launch_bounds__(256) void k_flat_scores(const float* __restrict__ q, uint32_t B,
                                                      const float* __restrict__ qnorm, const float* __restrict__ rows,
                                                      uint32_t N, uint32_t D, const float* __restrict__ norms, int kind,
-                                                     const uint32_t* __restrict__ list, float* __restrict__ scores) {
+                                                     const uint32_t* __restrict__ list, float* __restrict__ scores,
+                                                     const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     __shared__ __attribute__((aligned(16))) float tiles[4][64 * kTileLd];
     __shared__ __attribute__((aligned(16))) float qs[kFlatQT][kCh];
     __shared__ uint64_t bases[4][64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    // row: position in the scan (scores column); src: the shard row it reads
-    // (list[row] for a filtered scan, else row itself)
-    const uint64_t row = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    const uint64_t src = row < N ? (list ? (uint64_t)list[row] : row) : 0;
-    const uint32_t q0 = blockIdx.y * kFlatQT;
-    const uint32_t qn = (B - q0) < (uint32_t)kFlatQT ? (B - q0) : (uint32_t)kFlatQT;
-    bases[wv][lane] = row < N ? src * D : ~0ull;
-    float* tile = tiles[wv];
-    const bool vec4 = (D & 3u) == 0;
-    float acc[kFlatQT];
+    // grid-stride over 256-row tiles (a bounded grid: a gated launch exits cheaply)
+    for (uint32_t tile_i = blockIdx.x; tile_i < (N + 255u) / 256u; tile_i += gridDim.x) {
+        // row: position in the scan (scores column); src: the shard row it reads
+        // (list[row] for a filtered scan, else row itself)
+        const uint64_t row = (uint64_t)tile_i * 256u + threadIdx.x;
+        const uint64_t src = row < N ? (list ? (uint64_t)list[row] : row) : 0;
+        const uint32_t q0 = blockIdx.y * kFlatQT;
+        const uint32_t qn = (B - q0) < (uint32_t)kFlatQT ? (B - q0) : (uint32_t)kFlatQT;
+        bases[wv][lane] = row < N ? src * D : ~0ull;
+        float* tile = tiles[wv];
+        const bool vec4 = (D & 3u) == 0;
+        float acc[kFlatQT];
 #pragma unroll
-    for (int i = 0; i < kFlatQT; ++i) acc[i] = -0.0f;
-    __syncthreads();
-    for (uint64_t c0 = 0; c0 < D; c0 += kCh) {
-        stage_tile(tile, rows, bases[wv], c0, D, vec4, lane);
-        for (uint32_t t = threadIdx.x; t < kFlatQT * kCh; t += 256) {
-            const uint32_t qi = t / kCh, j = t % kCh;
-            qs[qi][j] = (qi < qn && c0 + j < D) ? q[(uint64_t)(q0 + qi) * D + c0 + j] : 0.0f;
-        }
+        for (int i = 0; i < kFlatQT; ++i) acc[i] = -0.0f;
         __syncthreads();
-        const uint32_t m = (uint32_t)((D - c0) < (uint64_t)kCh ? (D - c0) : kCh);
-        const float* tr = tile + lane * kTileLd;
-        for (uint32_t j = 0; j < m; ++j) {
-            const float x = tr[j];
-            if (kind == kScoreL2) {
+        for (uint64_t c0 = 0; c0 < D; c0 += kCh) {
+            stage_tile(tile, rows, bases[wv], c0, D, vec4, lane);
+            for (uint32_t t = threadIdx.x; t < kFlatQT * kCh; t += 256) {
+                const uint32_t qi = t / kCh, j = t % kCh;
+                qs[qi][j] = (qi < qn && c0 + j < D) ? q[(uint64_t)(q0 + qi) * D + c0 + j] : 0.0f;
+            }
+            __syncthreads();
+            const uint32_t m = (uint32_t)((D - c0) < (uint64_t)kCh ? (D - c0) : kCh);
+            const float* tr = tile + lane * kTileLd;
+            for (uint32_t j = 0; j < m; ++j) {
+                const float x = tr[j];
+                if (kind == kScoreL2) {
 #pragma unroll
-                for (int i = 0; i < kFlatQT; ++i) {
-                    const float d = qs[i][j] - x;
-                    acc[i] = acc[i] + d * d;
+                    for (int i = 0; i < kFlatQT; ++i) {
+                        const float d = qs[i][j] - x;
+                        acc[i] = acc[i] + d * d;
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < kFlatQT; ++i) acc[i] = acc[i] + qs[i][j] * x;
                 }
-            } else {
+            }
+            __syncthreads();
+        }
+        if (row < N) {
+            const float nb = norms ? norms[src] : 0.0f;
 #pragma unroll
-                for (int i = 0; i < kFlatQT; ++i) acc[i] = acc[i] + qs[i][j] * x;
+            for (int i = 0; i < kFlatQT; ++i) {
+                if ((uint32_t)i >= qn) break;
+                float score;
+                if (kind == kScoreL2) {
+                    score = sqrtf(acc[i]);
+                } else {
+                    const float na = qnorm[q0 + i];
+                    if (kind == kScoreCosine)
+                        score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc[i] / (na * nb);
+                    else
+                        score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc[i] / (na * nb));
+                }
+                scores[(uint64_t)(q0 + i) * N + row] = score;
             }
         }
-        __syncthreads();
-    }
-    if (row >= N) return;
-    const float nb = norms ? norms[src] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < kFlatQT; ++i) {
-        if ((uint32_t)i >= qn) break;
-        float score;
-        if (kind == kScoreL2) {
-            score = sqrtf(acc[i]);
-        } else {
-            const float na = qnorm[q0 + i];
-            if (kind == kScoreCosine)
-                score = (na == 0.0f || nb == 0.0f) ? 0.0f : acc[i] / (na * nb);
-            else
-                score = (na == 0.0f || nb == 0.0f) ? __builtin_inff() : 1.0f - (acc[i] / (na * nb));
-        }
-        scores[(uint64_t)(q0 + i) * N + row] = score;
+        __syncthreads();  // bases[] is rewritten by the next tile
     }
 }
 
 hipError_t launch_flat_scores(const float* q, uint32_t B, const float* qnorm, const float* rows, uint32_t N, uint32_t D,
-                              const float* norms, int kind, const uint32_t* list, float* scores, hipStream_t s) {
+                              const float* norms, int kind, const uint32_t* list, float* scores, hipStream_t s,
+                              const uint32_t* gate) {
     if (B == 0 || N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_flat_scores, dim3((N + 255) / 256, (B + kFlatQT - 1) / kFlatQT), dim3(256), 0, s, q, B, qnorm,
-                       rows, N, D, norms, kind, list, scores);
+    const uint32_t qg = (B + kFlatQT - 1) / kFlatQT;
+    // about 8 blocks per CU over all query groups; each block walks its row tiles
+    const uint32_t gx = std::max<uint32_t>(1u, std::min<uint32_t>((N + 255) / 256, (8u * cu_count() + qg - 1) / qg));
+    hipLaunchKernelGGL(k_flat_scores, dim3(gx, qg), dim3(256), 0, s, q, B, qnorm, rows, N, D, norms, kind, list,
+                       scores, gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -3041,7 +3076,9 @@ __global__ __launch_bounds__(kFlatTopkThreads) void k_flat_topk(const float* __r
                                                    int descending, int has_threshold, float threshold,
                                                    const uint64_t* __restrict__ ids, uint64_t* __restrict__ out_idx,
                                                    float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
-                                                   uint32_t* __restrict__ nan_flag) {
+                                                   uint32_t* __restrict__ nan_flag,
+                                                   const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     constexpr uint32_t kKeys = STAGED ? kFlatTopkStage : 1u;
     __shared__ uint32_t s_key[kKeys];
     __shared__ uint32_t s_kept[STAGED ? kFlatTopkStage / 32 : 1u];
@@ -3198,18 +3235,21 @@ __global__ __launch_bounds__(kFlatTopkThreads) void k_flat_topk(const float* __r
 hipError_t launch_flat_select(const float* scores, uint32_t B, uint32_t N, uint32_t limit, int descending,
                               int has_threshold, float threshold, const uint64_t* ids, uint64_t* out_idx,
                               float* out_scores, uint32_t* out_n, void* tmp, size_t tmp_bytes, uint32_t* nan_flag,
-                              hipStream_t s) {
+                              hipStream_t s, const uint32_t* gate) {
     if (B == 0) return hipSuccess;
-    if (limit <= kFlatTopkCap && N <= kFlatTopkMaxN && !getenv("GVDB_FLAT_SORT")) {
+    // a gated (device-decided fallback) select takes the one-launch form at any N:
+    // the per-query radix sorts below are B launches each
+    if (limit <= kFlatTopkCap && (gate || (N <= kFlatTopkMaxN && !getenv("GVDB_FLAT_SORT")))) {
         if (N <= kFlatTopkStage)
             hipLaunchKernelGGL(k_flat_topk<true>, dim3(B), dim3(kFlatTopkThreads), 0, s, scores, N, limit, descending,
-                               has_threshold, threshold, ids, out_idx, out_scores, out_n, nan_flag);
+                               has_threshold, threshold, ids, out_idx, out_scores, out_n, nan_flag, gate);
         else
             hipLaunchKernelGGL(k_flat_topk<false>, dim3(B), dim3(kFlatTopkThreads), 0, s, scores, N, limit, descending,
-                               has_threshold, threshold, ids, out_idx, out_scores, out_n, nan_flag);
+                               has_threshold, threshold, ids, out_idx, out_scores, out_n, nan_flag, gate);
         GVDB_LAUNCH_CHECK();
         return hipSuccess;
     }
+    if (gate) return hipErrorInvalidValue;  // a gated select needs limit <= kFlatTopkCap
     char* p = (char*)tmp;
     const size_t al = align256((size_t)N * 4);
     uint32_t* k0 = (uint32_t*)p;

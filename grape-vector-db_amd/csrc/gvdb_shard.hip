@@ -583,7 +583,9 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
                                                                  uint32_t* __restrict__ o_dist,
                                                                  uint32_t* __restrict__ own_cnt,
                                                                  uint32_t* __restrict__ reff,
-                                                                 uint32_t* __restrict__ tcut) {
+                                                                 uint32_t* __restrict__ tcut,
+                                                                 const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t tot[];  // [H] global histogram, then bins [2048]
     uint32_t* bins = tot + ((H + 3u) & ~3u);
     __shared__ uint32_t s_S, s_T, s_lt, s_tb, s_cut, s_below, wcnt[kDeepThreads / 64];
@@ -714,12 +716,12 @@ __global__ __launch_bounds__(kDeepThreads) void k_shard_deep_own(const uint32_t*
 hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uint32_t G, uint32_t me, uint32_t B,
                                  uint32_t R, uint32_t Rl, uint32_t H, const uint32_t* m_rows, const uint32_t* m_dist,
                                  uint32_t* o_rows, uint32_t* o_dist, uint32_t* own_cnt, uint32_t* reff,
-                                 hipStream_t s, uint32_t* tcut) {
+                                 hipStream_t s, uint32_t* tcut, const uint32_t* gate) {
     if (B == 0) return hipSuccess;
     const size_t lds = (size_t)((H + 3u) & ~3u) * 4u + 2048u * 4u;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_shard_deep_own, dim3(B), dim3(kDeepThreads), lds, s, gathered1, words1, G, me, B, R, Rl, H,
-                       m_rows, m_dist, o_rows, o_dist, own_cnt, reff, tcut);
+                       m_rows, m_dist, o_rows, o_dist, own_cnt, reff, tcut, gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -822,26 +824,26 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
         const uint32_t Rl = usable ? (uint32_t)std::min<uint64_t>(R, si.n) : 0u;
         const bool try_cert = usable && Rl > 0 && B * 4 <= BR && shard_certified_eligible(shard, dim, k);
         hipError_t e = hipSuccess;
+        // the certified form: the rank's exact cosine top-32 / 64 filtered by its owned-row rule; the
+        // rerank of the owned lists below is then gated on the device by its failure word (scratch)
+        uint32_t* dfail = reff + B;
+        const uint32_t* gate = nullptr;
         if (try_cert) {
-            // the certified form: the rank's exact cosine top-32 / 64 filtered by its owned-row rule
             e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
                                       (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist, own_cnt,
                                       reff, s, tcut);
-            bool done = false;
+            bool enqueued = false;
             if (e == hipSuccess) {
                 const gvdb_status st = shard_certified_phase2(shard, d_queries, B, dim, k, tcut, own_cnt, reff,
-                                                              m_rows, m_dist, Rl, d_block2, s, &done);
+                                                              m_rows, m_dist, Rl, d_block2, dfail, s, &enqueued);
                 if (st != GVDB_OK) return st;
             }
-            if (done) {
-                index_track_use(shard, s);
-                return GVDB_OK;
-            }
+            if (enqueued) gate = dfail;
         }
         if (e == hipSuccess)
             e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
                                       (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist, own_cnt,
-                                      reff, s);
+                                      reff, s, nullptr, gate);
         if (e == hipSuccess && Rl > 0) {
             RerankArgs rr{};
             rr.rows = si.rows;
@@ -855,11 +857,12 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
             rr.kind = kScoreCosine;
             rr.scores = m_cos;
             rr.counts = own_cnt;
+            rr.gate = gate;
             e = launch_rerank(rr, s);
         }
         if (e == hipSuccess)
             e = launch_shard_deep_topk(m_cos, o_rows, o_dist, own_cnt, reff, (uint32_t)B, Rl, (uint32_t)k,
-                                       usable ? si.ids : nullptr, 0u, d_block2, s);
+                                       usable ? si.ids : nullptr, 0u, d_block2, s, gate);
         if (e != hipSuccess)
             return report_status(GVDB_ERR_DEVICE, std::string("deep shard phase 2: ") + hipGetErrorString(e));
         if (usable) index_track_use(shard, s);

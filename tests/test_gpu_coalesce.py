@@ -71,3 +71,59 @@ def test_coalescer_errors(g):
     with pytest.raises(g.DimensionMismatch):
         co.search(np.zeros(D + 1, np.float32))
     co.close()
+
+
+@pytest.mark.parametrize("ratio", [None, 0.1])
+def test_nan_query_fails_only_its_caller(g, ratio):
+    """A query with a NaN poisons only its own result: the other callers batched
+    with it still get exactly their serial results (one
+    QuantizationError used to fail the whole coalesced batch).  ratio=0.1 is the
+    reference's default depth (the certified path, sent to the B x R rerank by the
+    poisoned query)."""
+    N, D, k = 100_000, 256, 10  # R = 0.1 N = 10000 > 8192: the certified default depth
+    r = np.random.default_rng(11)
+    x = r.standard_normal((N, D)).astype(np.float32)
+    Q = r.standard_normal((48, D)).astype(np.float32)
+    bad = {5, 17, 40}
+    for i in bad:
+        Q[i, 3] = np.nan
+    ix = g.GpuVectorIndex(dimension=D)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    sp = g.SearchParams(rescore_count=100) if ratio is None else g.SearchParams(rescore_ratio=ratio)
+    ser = {}
+    for i in range(len(Q)):
+        if i in bad:
+            with pytest.raises(g.QuantizationError):
+                ix.search_batch(Q[i:i + 1], k, sp)
+        else:
+            ser[i] = ix.search_batch(Q[i:i + 1], k, sp)
+    co = g.RequestCoalescer(ix, D, k, sp)
+    got, errs = [None] * len(Q), [None] * len(Q)
+    threads = 16
+    barrier = threading.Barrier(threads)
+
+    def worker(t):
+        barrier.wait()
+        for i in range(t, len(Q), threads):
+            try:
+                got[i] = co.search(Q[i])
+            except g.VectorDbError as e:
+                errs[i] = e
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    batches, queries, _ = co.stats()
+    co.close()
+    assert batches < len(Q), "no query was coalesced"
+    for i in range(len(Q)):
+        if i in bad:
+            assert isinstance(errs[i], g.QuantizationError), i
+        else:
+            assert errs[i] is None, (i, errs[i])
+            ids, sc, n = got[i]
+            si, ss, sn = ser[i]
+            assert n == sn[0] == k
+            assert (ids == si[0]).all() and sc.tobytes() == ss[0].tobytes(), i
