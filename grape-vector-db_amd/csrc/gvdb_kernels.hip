@@ -1018,6 +1018,21 @@ __global__ __launch_bounds__(256) void k_qfrag(const uint32_t* __restrict__ qwor
 // query tile) units of KS MFMAs spread over all waves.
 // Same emit contract as mx5: (d << 32 | row) for every row with d <= thr[q].
 constexpr int kMx7Threads = 512;  // 8 waves per CU, 2 per SIMD
+#ifdef GVDB_MX7_CLK
+// timing study (variant builds only, scripts/build_variant.sh -DGVDB_MX7_CLK): per wave
+// of the last non-dense launch, s_memrealtime (100 MHz) at kernel start, after the
+// prologue, after the full rounds, after the tail units, at the end; and the number
+// of tile tests that took the hit path
+__device__ unsigned long long g_mx7_clk[4096][6];
+#define MX7_CLK(i)                                                                              \
+    do {                                                                                        \
+        if (!DENSE && lane == 0 && gw < 4096u) g_mx7_clk[gw][i] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define MX7_CLK(i) \
+    do {           \
+    } while (0)
+#endif
 // DENSE (the reference's default depth, R/N >= 1/64): no threshold test; every
 // tile's 16 dots per lane go to dense[q][row] as f16 (exact: |dot| <= 768),
 // four consecutive rows per 8-byte store; the select reads d = |q| - dot.
@@ -1034,6 +1049,9 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     constexpr int KS = KW / 2;  // k-steps of 64 bits
     constexpr int QT = 8;       // query tiles of 32
     constexpr int NM = KS * QT;  // MFMAs per sub-tile
+#ifdef GVDB_MX7_CLK
+    uint32_t n_hit = 0;
+#endif
     constexpr uint32_t kWaveStage = 256;  // ~90 emits per wave at 10M x 768 x 256 (overflow: global atomics)
     constexpr int NW = kMx7Threads / 64;
     constexpr int PF = 4;  // A-fragment ring depth (in MFMAs; 8: same time)
@@ -1052,6 +1070,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     const uint32_t W = gridDim.x * NW;        // waves in the grid
     const uint32_t nround = nsub / W;         // full rounds (every wave the same count)
     const uint32_t gw = blockIdx.x * NW + wv;
+    MX7_CLK(0);
     uint2 ring[2][W4];
     auto load = [&](uint32_t sb, uint2 (&c)[W4]) __attribute__((always_inline)) {
         const uint32_t n = min(sb * 32u + (lane & 31u), N - 1u);  // clamped: branch-free ring
@@ -1133,6 +1152,9 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         const float c = cq[qt];
         const bool ok = qt < nqt;  // padded query tile: no emits (a query past B has cq = 1e9)
         if (__ballot(ok && mx >= c)) {
+#ifdef GVDB_MX7_CLK
+            ++n_hit;
+#endif
             float* sc = tscr[wv];
 #pragma unroll
             for (int r = 0; r < 16; ++r) sc[r * 64 + lane] = A[r];
@@ -1182,6 +1204,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
             }
         }
     };
+    MX7_CLK(1);
     const v4i_t* qf = qfrag + lane;
     // A fragment mm of the sub-tile: two base registers, one per 64 KiB of
     // fragments (a ds_read offset is 16 bits; without the split hipcc keeps one
@@ -1277,6 +1300,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
 #pragma unroll
             for (int p = 0; p < W4; ++p) asm volatile("s_waitcnt vmcnt(0)" : "+v"(ring[k][p]));
     }
+    MX7_CLK(2);
     // the partial last round: (sub-tile, query tile) units of KS MFMAs over all waves
     const uint32_t sb0 = nround * W;
     const uint32_t nunits = (nsub - sb0) * nqt;
@@ -1302,10 +1326,22 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         asm volatile("s_nop 15\n\ts_nop 15" : "+v"(A));
         test(A, qt, sb * 32u);
     }
+    MX7_CLK(3);
     if constexpr (!DENSE)
         flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase,
                                           counts, buf, bufcap);
+    MX7_CLK(4);
+#ifdef GVDB_MX7_CLK
+    if (!DENSE && lane == 0 && gw < 4096u) g_mx7_clk[gw][5] = n_hit;
+#endif
 }
+
+#ifdef GVDB_MX7_CLK
+extern "C" int gvdb_debug_mx7_clock(unsigned long long* out, uint32_t n) {  // [n][6]
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mx7_clk), (size_t)std::min(n, 4096u) * 48) == hipSuccess ? 0 : -2;
+}
+#endif
 
 // CUs of the current device (cached per device: read on every launch)
 static uint32_t cu_count() {

@@ -210,6 +210,12 @@ class TwoExchangeSearch:
 
 
 class ShardedBQSearch:
+    """TEST-ONLY legacy one-exchange form (each rank's top-R with its exact
+    cosines, one all-gather of B*R*16 B, gvdb_bq_shard_merge_packed_device):
+    kept as a second, independent orchestration the tests compare the
+    two-exchange protocol against.  Production sharding is
+    gvdb_index_search_sharded_device / RcclShardedSearch / TwoExchangeSearch."""
+
     def __init__(self, candidates_fn: CandidatesFn, shard_rows: Sequence[int], B: int, R: int, k: int,
                  device: torch.device, group=None):
         self.cand = candidates_fn

@@ -219,9 +219,12 @@ _STOP_WORDS = {
 
 
 class SimpleTokenizer:
-    """sparse.rs:257-359.  Host-side text processing that produces the term
-    lists the GPU index consumes.  Vocabulary ids are assigned in sorted term
-    order (the reference enumerates a HashSet: arbitrary order)."""
+    """sparse.rs:257-359.  NOT part of the GPU path: SURVEY §2 row 10 marks text
+    processing out of scope; this host-side helper only turns the hybrid mirror's
+    and the tests' text queries into the term lists the GPU BM25 index consumes
+    (a deployment passes its own SparseVector terms).  Vocabulary ids are
+    assigned in sorted term order (the reference enumerates a HashSet: arbitrary
+    order)."""
 
     def __init__(self):
         self.stop_words = set(_STOP_WORDS)

@@ -74,9 +74,26 @@ public:
         const uint64_t u = intern(id);
         check(gvdb_index_add(h_, v.data(), 1, (uint32_t)v.size(), &u));
     }
-    // index.rs:187-210: rows before a dimension mismatch stay added.
+    // index.rs:187-210: rows before a dimension mismatch stay added.  Each run of
+    // equal-length rows is ONE gvdb_index_add (one H2D copy); the C ABI checks the
+    // run's length, so the first row of another length fails where the reference's
+    // per-row check does.
     void add_vectors(std::vector<std::pair<std::string, std::vector<float>>> vs) override {
-        for (auto& kv : vs) add_vector(std::move(kv.first), std::move(kv.second));
+        for (size_t i = 0; i < vs.size();) {
+            const size_t d = vs[i].second.size();
+            size_t j = i;
+            while (j < vs.size() && vs[j].second.size() == d) ++j;
+            std::vector<float> flat;
+            flat.reserve((j - i) * d);
+            std::vector<uint64_t> ids;
+            ids.reserve(j - i);
+            for (size_t r = i; r < j; ++r) {
+                ids.push_back(intern(vs[r].first));
+                flat.insert(flat.end(), vs[r].second.begin(), vs[r].second.end());
+            }
+            check(gvdb_index_add(h_, flat.data(), j - i, (uint32_t)d, ids.data()));
+            i = j;
+        }
     }
     std::vector<std::pair<std::string, float>> search(const std::vector<float>& q, size_t k) const override {
         std::vector<uint64_t> ids(k ? k : 1);

@@ -120,6 +120,9 @@ for t in "${TASKS[@]}"; do
                 GVDB_SAMPLE_FLOOR=$f run 600 gpurun_out/c3floor_$f.log python3 scripts/c3_emulate.py --oracle-queries 0 --steps 20
                 echo "== floor $f"; grep '^\[c3\]' gpurun_out/c3floor_$f.log | tail -2
             done ;;
+        mx7clk)  # k_scan_mx7 per-wave phase clocks (variant build abl/libgvdb_mx7clk.so) at 1.25M and 10M rows
+            GVDB_LIB_PATH=$PWD/grape-vector-db_amd/abl/libgvdb_mx7clk.so run 600 gpurun_out/mx7clk.log python3 -u scripts/mx7_clock.py
+            grep '^\[mx7clk\]' gpurun_out/mx7clk.log ;;
         c3clk)
             run 600 gpurun_out/c3clk.log python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10 --p2clk
             grep '^\[c3\]' gpurun_out/c3clk.log ;;
