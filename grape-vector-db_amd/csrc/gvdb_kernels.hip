@@ -1052,17 +1052,27 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
 #ifdef GVDB_MX7_CLK
     uint32_t n_hit = 0;
 #endif
-    constexpr uint32_t kWaveStage = 256;  // ~90 emits per wave at 10M x 768 x 256 (overflow: global atomics)
     constexpr int NW = kMx7Threads / 64;
     constexpr int PF = 4;  // A-fragment ring depth (in MFMAs; 8: same time)
     static_assert(NM % PF == 0, "the A ring's slot of MFMA m must not depend on the sub-tile");
+    // Hit records (the threshold scan): a tile test that hits appends, per hitting LANE,
+    // its 16 dots as f16 (exact: |dot| <= 768) + (first row, query) to the wave's LDS
+    // record list -- two ds_write_b128 and one ds_write_b64, no read-back -- and the
+    // per-value tests, keys and buffer slots are worked out once, at the end (the
+    // round-4 hit path staged all 16 values, read them back and emitted per value inside
+    // the MFMA stream: ~0.4 us per hit, ~20 % of the scan at the 1.25M-row shard where
+    // 29 % of the tile tests hit).  A full list drains to the global buffer.
+    constexpr uint32_t kRec = 176;  // records per wave (10M x 768 x 256: ~105 used on average)
     __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
     __shared__ float cq_lds[QT * 32];  // |q| - thr (a query past B: never reached)
     __shared__ float pc_lds[QT * 32];  // |q|
-    __shared__ uint64_t st_key[NW][kWaveStage];
-    __shared__ uint8_t st_q[NW][kWaveStage];
     __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
-    __shared__ float tscr[NW][16 * 64];  // a hit tile's 16 values per lane ([r][lane]: conflict-free)
+    constexpr uint32_t kRecBytes = NW * kRec * 40u, kTscrBytes = NW * 16u * 64u * 4u;
+    __shared__ __attribute__((aligned(16))) char scr_raw[DENSE ? kTscrBytes : kRecBytes];
+    // DENSE: a tile's transposed f16 dots per wave; else the hit records: dots [NW][kRec][16] f16 | meta [NW][kRec]
+    float(*tscr)[16 * 64] = (float(*)[16 * 64])scr_raw;
+    uint4(*rec_v)[kRec][2] = (uint4(*)[kRec][2])scr_raw;
+    uint2(*rec_m)[kRec] = (uint2(*)[kRec])(scr_raw + NW * kRec * 32u);
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t h = lane >> 5;
@@ -1101,8 +1111,59 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) cq[qt] = cq_lds[qt * 32 + (lane & 31u)];
     const uint32_t nqt = (B + 31u) / 32u;
-    uint32_t wcnt = 0;  // this wave's staged emits (wave-uniform)
+    uint32_t wrec = 0;  // this wave's hit records (wave-uniform)
     v16f_t acc[QT];
+    // global (address space 1) pointers: a flat atomic / store in the stream would count in
+    // lgkmcnt too and make every later LDS wait of the stream a full lgkmcnt(0)
+    typedef __attribute__((address_space(1))) uint32_t g_u32;
+    typedef __attribute__((address_space(1))) uint64_t g_u64;
+    // a record's hits: value r is row nb + 8 (r / 4) + (r % 4) of query qi; hit iff dot >= cq[qi], row < N
+    auto rec_hits = [&](uint32_t e, uint32_t& qi, uint32_t& nb, float (&v)[16]) __attribute__((always_inline)) {
+        const uint2 m = rec_m[wv][e];
+        nb = m.x;
+        qi = m.y;
+        const uint4 a0 = rec_v[wv][e][0], a1 = rec_v[wv][e][1];
+        const uint32_t w[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float c = cq_lds[qi];
+        uint32_t hm = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            v[r] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[r >> 1] >> (16 * (r & 1))));
+            const uint32_t n = nb + 8u * (uint32_t)(r >> 2) + (uint32_t)(r & 3);
+            hm |= (v[r] >= c && n < N) ? 1u << r : 0u;
+        }
+        return hm;
+    };
+    // the wave's full list -> the global buffer, one atomic per emit (rare: a burst of hits)
+    auto drain = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the lanes' record writes before the reads
+        g_u32* cnt = (g_u32*)counts;
+        g_u64* bf = (g_u64*)buf;
+        uint32_t bcap = bufcap;
+        asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
+#pragma unroll 1
+        for (uint32_t e = lane; e < wrec; e += 64u) {
+            uint32_t qi, nb;
+            float v[16];
+            uint32_t hm = rec_hits(e, qi, nb, v);
+            const float pcl = pc_lds[qi];
+#pragma unroll 1
+            while (hm) {
+                const uint32_t r = __builtin_ctz(hm);
+                hm &= hm - 1u;
+                float vr = v[0];
+#pragma unroll
+                for (int j = 1; j < 16; ++j) vr = (uint32_t)j == r ? v[j] : vr;
+                const uint32_t pos = __hip_atomic_fetch_add(cnt + qi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t n = nb + 8u * (r >> 2) + (r & 3u);
+                if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = ((uint64_t)(uint32_t)(int)(pcl - vr) << 32) | n;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        wrec = 0;
+    };
     const int scale1 = 0x7f7f7f7f;
     // threshold test of one query tile (a hit: dot >= cq).  Common path: the max
     // of the lane's 16 dots against its cq and one ballot.  Rare hit path, kept
@@ -1151,57 +1212,31 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         const float mx = max3f(max3f(m0, m1, m2), m3, max3f(m4, A[15], A[15]));
         const float c = cq[qt];
         const bool ok = qt < nqt;  // padded query tile: no emits (a query past B has cq = 1e9)
-        if (__ballot(ok && mx >= c)) {
+        const bool hit = ok && mx >= c;
+        const uint64_t hb = __ballot(hit);
+        if (hb) {
 #ifdef GVDB_MX7_CLK
             ++n_hit;
 #endif
-            float* sc = tscr[wv];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sc[r * 64 + lane] = A[r];
-            uint32_t gm = 0;  // groups of 4 with a hit (wave-uniform)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float gx = max3f(A[4 * g], A[4 * g + 1], max3f(A[4 * g + 2], A[4 * g + 3], A[4 * g + 3]));
-                gm |= __ballot(ok && gx >= c) ? (1u << g) : 0u;
+            const uint32_t nh = (uint32_t)__popcll(hb);
+            if (wrec + nh > kRec) drain();
+            if (hit) {
+                const uint32_t e = wrec + __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
+                uint4 a0, a1;
+                a0.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[0], A[1]));
+                a0.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[2], A[3]));
+                a0.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[4], A[5]));
+                a0.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[6], A[7]));
+                a1.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[8], A[9]));
+                a1.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[10], A[11]));
+                a1.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[12], A[13]));
+                a1.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(A[14], A[15]));
+                rec_v[wv][e][0] = a0;
+                rec_v[wv][e][1] = a1;
+                rec_m[wv][e] = make_uint2(n0 + 4u * h, qt * 32u + (lane & 31u));
             }
-            // global (address space 1) pointers: a flat atomic / store here would count in
-            // lgkmcnt too and make every later LDS wait of the stream a full lgkmcnt(0)
-            typedef __attribute__((address_space(1))) uint32_t g_u32;
-            typedef __attribute__((address_space(1))) uint64_t g_u64;
-            g_u32* cnt = (g_u32*)counts;
-            g_u64* bf = (g_u64*)buf;
-            uint32_t bcap = bufcap;
-            asm volatile("" : "+s"(cnt), "+s"(bf), "+s"(bcap));
-            const uint32_t qi = qt * 32u + (lane & 31u);
-            const float pcl = pc_lds[qi];
-#pragma unroll 1
-            while (gm) {
-                const uint32_t g = __builtin_ctz(gm);
-                gm &= gm - 1u;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t r = 4u * g + (uint32_t)j;
-                    const float v = sc[r * 64u + lane];
-                    const uint32_t n = n0 + 8u * g + 4u * h + (uint32_t)j;
-                    const bool hit = ok && v >= c && n < N;
-                    const uint64_t m = __ballot(hit);
-                    if (hit) {
-                        const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
-                                                       (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        const uint32_t d = (uint32_t)(int)(pcl - v);
-                        const uint64_t key = ((uint64_t)d << 32) | n;
-                        if (sp < kWaveStage) {
-                            st_key[wv][sp] = key;
-                            st_q[wv][sp] = (uint8_t)qi;
-                        } else {
-                            const uint32_t pos = __hip_atomic_fetch_add(cnt + qi, 1u, __ATOMIC_RELAXED,
-                                                                        __HIP_MEMORY_SCOPE_AGENT);
-                            if (pos < bcap) bf[(uint64_t)qi * bcap + pos] = key;
-                        }
-                    }
-                    wcnt += (uint32_t)__popcll(m);
-                }
-            }
+            wrec += nh;
         }
     };
     MX7_CLK(1);
@@ -1327,9 +1362,49 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         test(A, qt, sb * 32u);
     }
     MX7_CLK(3);
-    if constexpr (!DENSE)
-        flush_stage_block<NW, kWaveStage>(st_key, st_q, wv, lane, wcnt, min(B, (uint32_t)QT * 32u), qcnt, qbase,
-                                          counts, buf, bufcap);
+    if constexpr (!DENSE) {
+        // the records' emits, block-aggregated: per record its hit count ranks it within
+        // (block, query) by one LDS atomic, ONE global atomicAdd per (block, query)
+        // reserves the block's slots, then every record writes its keys
+        constexpr uint32_t kPer = (kRec + 63u) / 64u;
+        uint32_t rk[kPer];
+        __syncthreads();  // qcnt zeroed in the prologue; every wave's records complete
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t e = lane + 64u * i;
+            rk[i] = 0u;
+            if (e < wrec) {
+                uint32_t qi, nb;
+                float v[16];
+                const uint32_t hm = rec_hits(e, qi, nb, v);
+                if (hm) rk[i] = atomicAdd(&qcnt[qi], (uint32_t)__popc(hm));
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < min(B, (uint32_t)QT * 32u); q += kMx7Threads) {
+            const uint32_t c = qcnt[q];
+            if (c) qbase[q] = atomicAdd(&counts[q], c);
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t e = lane + 64u * i;
+            if (e < wrec) {
+                uint32_t qi, nb;
+                float v[16];
+                const uint32_t hm = rec_hits(e, qi, nb, v);
+                uint32_t pos = qbase[qi] + rk[i];
+                const float pcl = pc_lds[qi];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    if (!((hm >> r) & 1u)) continue;
+                    const uint32_t n = nb + 8u * (uint32_t)(r >> 2) + (uint32_t)(r & 3);
+                    if (pos < bufcap) buf[(uint64_t)qi * bufcap + pos] = ((uint64_t)(uint32_t)(int)(pcl - v[r]) << 32) | n;
+                    ++pos;
+                }
+            }
+        }
+    }
     MX7_CLK(4);
 #ifdef GVDB_MX7_CLK
     if (!DENSE && lane == 0 && gw < 4096u) g_mx7_clk[gw][5] = n_hit;

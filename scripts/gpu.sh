@@ -92,6 +92,12 @@ for t in "${TASKS[@]}"; do
                 GVDB_LIB_PATH=$lib SHARD_N=10000000 SCANS="" REPS=2 run 300 gpurun_out/ablscan_$v.log python3 -u scripts/scan_ab.py
                 echo "$v $(grep '^\[scan_ab\]' gpurun_out/ablscan_$v.log | tail -1)"
             done ;;
+        scanvar)  # k_scan timing of build variants at 10M and the 1.25M shard (VARIANTS, "base" = product), one box
+            for v in ${VARIANTS:-base}; do
+                lib=""; [ "$v" != base ] && lib=grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib SHARD_N=10000000,1250000 SCANS="" REPS=2 run 400 gpurun_out/scanvar_$v.log python3 -u scripts/scan_ab.py
+                grep '^\[scan_ab\]' gpurun_out/scanvar_$v.log | sed "s/^/$v /"
+            done ;;
         scanab)  # stage-1 scan timing at 10M and the 1.25M shard (same box, alternating SCANS)
             SHARD_N=10000000,1250000 SCANS="${SCANS:-,}" REPS=3 run 900 gpurun_out/scanab.log python3 -u scripts/scan_ab.py
             grep '^\[scan_ab\]' gpurun_out/scanab.log ;;
