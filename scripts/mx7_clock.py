@@ -42,6 +42,8 @@ for n in [int(x) for x in os.environ.get("SHARD_N", "1250000,10000000").split(",
     buf = (C.c_ulonglong * (waves * 6))()
     assert fn(buf, waves) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(waves, 6).astype(np.float64)
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.save(f"gpurun_out/mx7clk_{n}.npy", a)  # raw per-wave clocks (wave gw = 8 * block + wave)
     t0 = a[:, 0].min()
     us = (a[:, :5] - t0) / 100.0  # 100 MHz ticks -> us
     ph = np.diff(us, axis=1)
