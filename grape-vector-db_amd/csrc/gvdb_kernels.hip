@@ -1067,6 +1067,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     __shared__ float cq_lds[QT * 32];  // |q| - thr (a query past B: never reached)
     __shared__ float pc_lds[QT * 32];  // |q|
     __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
+    __shared__ uint32_t blk_next;  // the block's sub-tile pool: next free slot
     constexpr uint32_t kRecBytes = NW * kRec * 40u, kTscrBytes = NW * 16u * 64u * 4u;
     __shared__ __attribute__((aligned(16))) char scr_raw[DENSE ? kTscrBytes : kRecBytes];
     // DENSE: a tile's transposed f16 dots per wave; else the hit records: dots [NW][kRec][16] f16 | meta [NW][kRec]
@@ -1106,6 +1107,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         pc_lds[q] = (float)pc;
         qcnt[q] = 0u;
     }
+    if (tid == 0) blk_next = 2u * NW;  // slots wv and NW + wv: the prologue's loads
     __syncthreads();
     float cq[QT];  // this lane's query of each tile
 #pragma unroll
@@ -1252,19 +1254,37 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         const uint32_t ad = mm < 64 ? qf_lo + (uint32_t)mm * 1024u : qf_hi + (uint32_t)(mm - 64) * 1024u;
         return *(lds_v4i_t*)ad;
     };
+    // The full rounds are shared out DYNAMICALLY inside the block: the block owns the
+    // sub-tiles b*NW + w + r*W (r < nround, w < NW) -- pool slot j = r*NW + w -- and a
+    // wave takes the next free slot (an LDS atomic, issued a whole sub-tile ahead of
+    // its use) for each ring refill.  With a static share the second wave of every
+    // SIMD (waves 4..7, lower MFMA-issue priority) finished its rounds 39 % after the
+    // first (601 vs 432 us at 10M x 768 x 256, profiles/r05/mx7clk) and the kernel
+    // ended with it.
+    const uint32_t npool = nround * (uint32_t)NW;
+    auto slot_sb = [&](uint32_t j) { return (j / NW) * W + blockIdx.x * NW + (j % NW); };
+    const uint32_t blk_addr = (uint32_t)(uintptr_t)&blk_next;  // LDS byte address
     if (nround > 0) {
         v4i_t ar[PF];
 #pragma unroll
         for (int m = 0; m < PF; ++m) ar[m] = afrag(m);
         // one sub-tile of the stream: slot c holds its codes; tile qt of the
         // previous sub-tile (rows of sub-tile sbp) is tested just before its
-        // first MFMA here; the slot is refilled with sub-tile sb + 2W after its
-        // last expansion
-        auto step = [&](uint2 (&c)[W4], uint32_t sb, bool prev, uint32_t sbp) __attribute__((always_inline)) {
+        // first MFMA here; the slot is refilled with the next pool sub-tile (nx,
+        // valid iff nv; else a clamped dummy) after its last expansion
+        auto step = [&](uint2 (&c)[W4], uint32_t sb, bool prev, uint32_t sbp, uint32_t& nx, bool& nv)
+                        __attribute__((always_inline)) {
             const uint32_t np = sbp * 32u;  // the previous sub-tile's first row
 #pragma unroll
             for (int p = 0; p < W4; ++p)  // this slot's loads are the older of the two in flight
                 asm volatile("s_waitcnt vmcnt(%1)" : "+v"(c[p]) : "n"(W4));
+            // the pool grab through asm: the compiler's atomic (wave-reduced by its atomic
+            // optimizer) waited lgkmcnt(0) right here, draining the A ring at every step;
+            // this one is waited at the refill (LDS ops complete in order, so the
+            // compiler's own counted waits only get stricter)
+            uint32_t jn = 0;
+            if (lane == 0)
+                asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(jn) : "v"(blk_addr), "v"(1u) : "memory");
             v4i_t bcur = fp4_row01(c[0].x);
             v4i_t bnext;
             // k-step 0, peeled (its control flow would stop the k-loop unroll):
@@ -1313,17 +1333,30 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
                 }
                 bcur = bnext;
             }
-            load(sb + 2u * W, c);  // every expansion of this slot is done
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(jn)::"memory");
+            jn = __builtin_amdgcn_readfirstlane(jn);
+            nv = jn < npool;
+            nx = nv ? slot_sb(jn) : nsub;  // nsub: rows past N, clamped (a dummy refill)
+            load(nx, c);  // every expansion of this slot is done
         };
         // two inlined copies of step() (one per ring slot); the first sub-tile
-        // has no predecessor to test, an odd count ends after slot 0
-        for (uint32_t i = 0; i < nround; i += 2) {
-            const uint32_t sb = gw + i * W;
-            step(ring[0], sb, i > 0, sb - W);
-            if (i + 1 < nround) step(ring[1], sb + W, true, sb);
+        // has no predecessor to test
+        uint32_t s0 = gw, s1 = gw + W, sbp = 0, nx;
+        bool v0 = true, v1 = nround > 1, prev = false, nv;
+        while (v0) {
+            step(ring[0], s0, prev, sbp, nx, nv);
+            prev = true;
+            sbp = s0;
+            s0 = nx;
+            v0 = nv;
+            if (!v1) break;
+            step(ring[1], s1, true, sbp, nx, nv);
+            sbp = s1;
+            s1 = nx;
+            v1 = nv;
         }
         asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
-        const uint32_t nl = (gw + (nround - 1u) * W) * 32u;
+        const uint32_t nl = sbp * 32u;
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             asm volatile("" : "+v"(acc[qt]));
