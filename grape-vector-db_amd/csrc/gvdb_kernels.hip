@@ -2152,6 +2152,173 @@ __global__ __launch_bounds__(kSsThreads) void k_sample_select(const uint16_t* __
     if (tid == 0) thr[q] = min(s_T, D);
 }
 
+// k_sample_prep: k_qprep and k_sample_dense in ONE launch (the large-batch
+// stage 1 with the dense sample; round 5).  k_qprep (one 64-thread block per
+// query slot, ~4.6 us) only fed k_sample_dense, whose every block then copied the
+// whole group's 96 KiB of FP4 query fragments into LDS to run one sub-tile per
+// wave at the 1.25M-row shard: two launches of mostly latency.  Here block
+// f = 8 s + qt (32 slices s x 8 query tiles qt of one 256-query group; the 32
+// blocks of a tile share blockIdx % 8) packs its tile's 32 queries itself (a
+// ballot per 64 dims, as k_qprep: Msb0 words, pad bits 0), keeps the tile's 2*W4
+// FP4 A fragments in REGISTERS (no LDS reads in the MFMA stream), and computes
+// the dense sample of its slice for those 32 queries: per wave a contiguous run of
+// sample sub-tiles, two accumulator chains at a time (acc = -|q| + dot =
+// -Hamming), then the minimum of every 16 rows per query through the wave's LDS
+// transpose -> dsm[q][S/16], the layout k_sample_select reads (the same values
+// as k_sample_dense's, so the same thresholds).  The slice-0 block of each tile
+// also writes what the scan and the select read: the query words [B][4 W4], |q|
+// per slot and the tile's fragments in the scan's layout (slots past B: zero
+// words); and the blocks zero the stage-1 flags / counts (k_qprep's duty).
+template <int W4>
+__global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
+    const float* __restrict__ qf, uint32_t D, float qthr, uint32_t B, uint32_t* __restrict__ qwords,
+    v4i_t* __restrict__ qfrag, uint32_t* __restrict__ qpc, uint32_t* __restrict__ zero, uint32_t nzero,
+    const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t stride, uint32_t nsub, uint32_t pw,
+    uint16_t* __restrict__ dsm, uint32_t S) {
+    constexpr int KW = 4 * W4, KS = KW / 2, QT = 8, NW = kMx5Threads / 64;
+    constexpr uint32_t kSlices = 32;
+    __shared__ uint32_t qw_lds[32][KW + 1];
+    __shared__ uint32_t pc_lds[32];
+    __shared__ __attribute__((aligned(16))) uint16_t tr_lds[NW][32 * 32];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t f = blockIdx.x, qt = f % QT, sl = f / QT, h = lane >> 5;
+    for (uint32_t i = f * kMx5Threads + tid; i < nzero; i += gridDim.x * kMx5Threads) zero[i] = 0u;
+    // 1. the tile's 32 queries: wave wv packs queries 4 wv .. 4 wv + 3, every load in flight
+    {
+        float v[4][KW / 2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t q = qt * 32u + wv * 4u + (uint32_t)u;
+#pragma unroll
+            for (int c = 0; c < KW / 2; ++c) {
+                const uint32_t d = 64u * (uint32_t)c + lane;
+                v[u][c] = q < B && d < D ? qf[(uint64_t)q * D + d] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t x = wv * 4u + (uint32_t)u, q = qt * 32u + x;
+#pragma unroll
+            for (int c = 0; c < KW / 2; ++c) {
+                const uint32_t d = 64u * (uint32_t)c + lane;
+                const uint64_t m = __ballot(q < B && d < D && v[u][c] > qthr);
+                if (lane == 0) {
+                    qw_lds[x][2 * c] = msb0_word((uint32_t)m);
+                    qw_lds[x][2 * c + 1] = msb0_word((uint32_t)(m >> 32));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 32) {
+        uint32_t pc = 0;
+#pragma unroll
+        for (int i = 0; i < KW; ++i) pc += __popc(qw_lds[tid][i]);
+        pc_lds[tid] = pc;  // 0 past B (zero words)
+    }
+    __syncthreads();
+    if (sl == 0) {  // the scan's and the select's operands for this tile
+        for (uint32_t i = tid; i < 32u * KW; i += kMx5Threads) {
+            const uint32_t x = i / KW, w = i % KW, q = qt * 32u + x;
+            if (q < B) qwords[(uint64_t)q * KW + w] = qw_lds[x][w];
+        }
+        if (tid < 32) qpc[qt * 32u + tid] = pc_lds[tid];
+        for (uint32_t i = tid; i < (uint32_t)KS * 64u; i += kMx5Threads) {
+            const uint32_t sk = i >> 6, l = i & 63u;
+            const uint32_t wi = 4u * (sk >> 1) + 2u * (l >> 5) + (sk & 1u);
+            qfrag[(sk * QT + qt) * 64u + l] = fp4_query_pm(qw_lds[l & 31u][wi]);
+        }
+    }
+    // this lane's A fragments (query l & 31, k-half h) and the accumulator seeds -|q|
+    v4i_t A[KS];
+#pragma unroll
+    for (int sk = 0; sk < KS; ++sk) A[sk] = fp4_query_pm(qw_lds[lane & 31u][4 * (sk >> 1) + 2 * (int)h + (sk & 1)]);
+    float seed[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t x = 8u * (uint32_t)(r >> 2) + 4u * h + (uint32_t)(r & 3);
+        seed[r] = qt * 32u + x < B ? -(float)pc_lds[x] : -1.0e6f;
+    }
+    if (qt * 32u >= B) return;  // a tile past B: fragments written, nothing to sample
+    // 2. the slice's sample sub-tiles: wave (sl, wv) takes the contiguous run [wg * pw, +pw)
+    const uint32_t wg = sl * NW + wv;
+    const uint32_t j0 = min(wg * pw, nsub), j1 = min(j0 + pw, nsub);
+    uint16_t* tw = tr_lds[wv];
+    const int scale1 = 0x7f7f7f7f;
+    auto rown = [&](uint32_t j) { const uint32_t s0 = j * 32u; return (s0 >> 12) * stride + (s0 & 4095u) + (lane & 31u); };
+    auto epi = [&](const v16f_t& acc, uint32_t j) __attribute__((always_inline)) {
+        // rows past N (an unsampled small shard's last chunk) read as 0xffff
+        const uint32_t n = rown(j);
+        const float lim = n < N ? 65535.0f : -1.0f;
+        const uint32_t jj = lane & 31u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t qo = 8u * (uint32_t)(r >> 2) + 4u * h + (uint32_t)(r & 3);
+            const float dv = -acc[r];
+            tw[qo * 32u + jj] = lim < 0.0f ? (uint16_t)0xffffu : (uint16_t)min(dv, lim);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // lane L: query L / 2 of the tile, rows 16 (L % 2) .. +15 -> their minimum
+        const uint32_t qo = lane >> 1, rh = lane & 1u;
+        const uint4 v0 = *(const uint4*)(tw + qo * 32u + rh * 16u);
+        const uint4 v1 = *(const uint4*)(tw + qo * 32u + rh * 16u + 8u);
+        uint32_t mn = 0xffffu;
+        const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mn = min(mn, min(w[e] & 0xffffu, w[e] >> 16));
+        const uint32_t qg = qt * 32u + qo;
+        if (qg < B) dsm[(uint64_t)qg * (S >> 4) + 2u * j + rh] = (uint16_t)mn;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    };
+    for (uint32_t j = j0; j < j1; j += 2) {  // two independent accumulator chains
+        const bool two = j + 1 < j1;
+        uint2 c0[W4], c1[W4];
+        const uint32_t n0 = min(rown(j), N - 1u), n1 = min(rown(two ? j + 1 : j), N - 1u);
+#pragma unroll
+        for (int p = 0; p < W4; ++p) {
+            c0[p] = ((const uint2*)(codes + (uint64_t)p * cap + n0))[h];
+            c1[p] = ((const uint2*)(codes + (uint64_t)p * cap + n1))[h];
+        }
+        v16f_t acc[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            acc[0][r] = seed[r];
+            acc[1][r] = seed[r];
+        }
+#pragma unroll
+        for (int sk = 0; sk < KS; ++sk) {
+            const v4i_t b0 = fp4_row01((sk & 1) ? c0[sk >> 1].y : c0[sk >> 1].x);
+            const v4i_t b1 = fp4_row01((sk & 1) ? c1[sk >> 1].y : c1[sk >> 1].x);
+            mfma_fp4_acc_nop(acc[0], A[sk], b0, scale1);
+            mfma_fp4_acc_nop(acc[1], A[sk], b1, scale1);
+        }
+        mfma_fp4_drain_acc(acc);
+        epi(acc[0], j);
+        if (two) epi(acc[1], j + 1);
+    }
+}
+
+template <int W4>
+static void launch_sample_prep_t(const Stage1Args& a, hipStream_t s) {
+    const uint32_t S = a.sample_chunks * 4096u;
+    const uint32_t nsub = S / 32u;
+    constexpr uint32_t kBlocks = 32u * 8u, kWaves = kBlocks / 8u * (kMx5Threads / 64u);  // per query tile: 256 waves
+    const uint32_t pw = (nsub + kWaves - 1u) / kWaves;
+    constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
+    for (uint32_t g = 0; g < a.B; g += 256) {
+        const uint32_t bg = min(256u, a.B - g);
+        hipLaunchKernelGGL((k_sample_prep<W4>), dim3(kBlocks), dim3(kMx5Threads), 0, s, a.qf32 + (uint64_t)g * a.D,
+                           a.D, a.qthr, bg, (uint32_t*)a.qcodes + (uint64_t)g * 4u * W4,
+                           (v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, g == 0 ? a.zero : nullptr,
+                           g == 0 ? a.nzero : 0u, a.codes, a.cap, a.N, a.sample_stride, nsub, pw,
+                           a.smp + (uint64_t)g * (S / 16u), S);
+    }
+    hipLaunchKernelGGL(k_sample_select, dim3(a.B), dim3(kSsThreads), 0, s, a.smp, S / 16u, a.D, a.target, a.thr);
+}
+
 template <int W4>
 static void launch_sample_dense_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t S = a.sample_chunks * 4096u;
@@ -2246,12 +2413,20 @@ size_t stage1_plan(Stage1Args& a) {
     return bytes;
 }
 
+// GVDB_PREP=0: k_qprep + k_sample_dense instead of the fused k_sample_prep (A/B, tests)
+static bool prep_enabled() {
+    const char* e = getenv("GVDB_PREP");
+    return !(e && e[0] == '0');
+}
+
 hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     const uint32_t W4 = code_w4(a.D);
     // a tier gate is carried by the dense FP4 form's kernels only (the deep fallback)
     if (a.gate && !(a.dense_sel && a.mfma_scan)) return hipErrorInvalidValue;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    if (a.mfma_scan) {
+    // the query packing fused into the dense sample (one launch instead of two)
+    const bool prep = a.mfma_scan && !a.dense_sel && a.sample_mode == kSampleDense && a.qf32 && prep_enabled();
+    if (a.mfma_scan && !prep) {
         switch (W4) {
             case 2: launch_qfrag_t<2>(a, s); break;
             case 3: launch_qfrag_t<3>(a, s); break;
@@ -2277,7 +2452,14 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
         }
         return hipSuccess;
     }
-    if (a.sample_mode == kSampleDense) {
+    if (prep) {
+        switch (W4) {
+            case 2: launch_sample_prep_t<2>(a, s); break;
+            case 3: launch_sample_prep_t<3>(a, s); break;
+            case 4: launch_sample_prep_t<4>(a, s); break;
+            default: launch_sample_prep_t<6>(a, s); break;
+        }
+    } else if (a.sample_mode == kSampleDense) {
         switch (W4) {
             case 2: launch_sample_dense_t<2>(a, s); break;
             case 3: launch_sample_dense_t<3>(a, s); break;

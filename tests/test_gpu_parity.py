@@ -920,3 +920,56 @@ def test_sample_histogram_mfma_thresholds_equal_valu(g, N, D, B, R):
     for mode in ("mfma", "dense"):
         assert max(out[mode][0]) < D  # a real estimate, not the no-pruning fallback
         assert (out[mode][1] == out["valu"][1]).all() and (out[mode][2] == out["valu"][2]).all(), mode
+
+
+@pytest.mark.parametrize("N,D,B,R", [(1_250_000, 768, 256, 100), (400_000, 256, 300, 100), (200_000, 768, 100, 100),
+                                     (70_003, 512, 256, 300), (300_001, 384, 160, 64)])
+def test_fused_sample_prep_equals_separate_kernels(g, oracle_mod, N, D, B, R):
+    """k_sample_prep (query packing + dense sample in one launch, round 5) against
+    k_qprep + k_sample_dense (GVDB_PREP=0): the same group minima, so the same
+    per-query thresholds, and the same search results; B = 300 spans two 256-query
+    groups, N <= 262144 makes the "sample" the whole (ragged) shard.  A query
+    equal to a row and two equal queries check the packing."""
+    import ctypes as C
+    import os
+
+    import torch
+
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(N + 3 * D)
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    x0 = None
+    for c0 in range(0, N, 1 << 19):
+        n = min(1 << 19, N - c0)
+        xc = torch.randn((n, D), generator=gen, device=dev)
+        if c0 == 0:
+            x0 = xc[:4].clone()
+        ix.add_device(xc, torch.arange(c0, c0 + n, device=dev))
+    q = torch.randn((B, D), generator=gen, device=dev)
+    q[1] = x0[3]
+    q[B - 1] = q[B - 2]
+    L = g.lib()
+    L.gvdb_debug_stage1_thresholds.argtypes = [C.POINTER(C.c_uint32), C.c_uint32]
+    sp = g.SearchParams(rescore_count=R)
+    out = {}
+    os.environ["GVDB_DEBUG_THR"] = "1"
+    try:
+        for mode in ("fused", "separate"):
+            if mode == "separate":
+                os.environ["GVDB_PREP"] = "0"
+            oi = torch.zeros((B, 10), dtype=torch.int64, device=dev)
+            osc = torch.zeros((B, 10), dtype=torch.float32, device=dev)
+            on = torch.zeros(B, dtype=torch.int32, device=dev)
+            ix.search_device(q, 10, oi, osc, on, sp)
+            torch.cuda.synchronize()
+            thr = (C.c_uint32 * B)()
+            assert L.gvdb_debug_stage1_thresholds(thr, B) == 0
+            out[mode] = (list(thr), oi.cpu().numpy(), osc.cpu().numpy(), on.cpu().numpy())
+    finally:
+        os.environ.pop("GVDB_DEBUG_THR", None)
+        os.environ.pop("GVDB_PREP", None)
+    assert out["fused"][0] == out["separate"][0]
+    assert max(out["fused"][0]) < D
+    for i in (1, 2, 3):
+        assert out["fused"][i].tobytes() == out["separate"][i].tobytes()
+    assert out["fused"][1][1, 0] == 3
