@@ -2088,7 +2088,7 @@ __global__ __launch_bounds__(kSsThreads) void k_sample_select(const uint16_t* __
     uint32_t base = red[0];
 #pragma unroll
     for (int w = 1; w < kSsThreads / 64; ++w) base = min(base, red[w]);
-    uint32_t win = 16;
+    uint32_t win = 64;  // one round in the common case: the target-th minimum lies within ~40 of the minimum
     while (true) {
         for (uint32_t i = tid; i < win; i += kSsThreads) hist[i] = 0u;
         __syncthreads();
