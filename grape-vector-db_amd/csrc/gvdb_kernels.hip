@@ -2184,6 +2184,23 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t f = blockIdx.x, qt = f % QT, sl = f / QT, h = lane >> 5;
     for (uint32_t i = f * kMx5Threads + tid; i < nzero; i += gridDim.x * kMx5Threads) zero[i] = 0u;
+    // the slice's sample sub-tiles: wave (sl, wv) takes the contiguous run [wg * pw, +pw), two
+    // at a time (two accumulator chains); the codes of the next pair load under the current
+    // pair's MFMAs, the first pair's under the query packing
+    const uint32_t wg = sl * NW + wv;
+    const uint32_t j0 = min(wg * pw, nsub), j1 = min(j0 + pw, nsub);
+    auto rown = [&](uint32_t j) { const uint32_t s0 = j * 32u; return (s0 >> 12) * stride + (s0 & 4095u) + (lane & 31u); };
+    uint2 cc[2][2][W4];  // [buffer][chain][plane]
+    auto load_pair = [&](uint32_t j, uint2 (&c)[2][W4]) __attribute__((always_inline)) {
+        const uint32_t n0 = min(rown(j), N - 1u), n1 = min(rown(j + 1 < j1 ? j + 1 : j), N - 1u);
+#pragma unroll
+        for (int p = 0; p < W4; ++p) {
+            c[0][p] = ((const uint2*)(codes + (uint64_t)p * cap + n0))[h];
+            c[1][p] = ((const uint2*)(codes + (uint64_t)p * cap + n1))[h];
+        }
+    };
+    const bool live_tile = qt * 32u < B;
+    if (live_tile && j0 < j1) load_pair(j0, cc[0]);
     // 1. the tile's 32 queries: wave wv packs queries 4 wv .. 4 wv + 3, every load in flight
     {
         float v[4][KW / 2];
@@ -2240,13 +2257,10 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
         const uint32_t x = 8u * (uint32_t)(r >> 2) + 4u * h + (uint32_t)(r & 3);
         seed[r] = qt * 32u + x < B ? -(float)pc_lds[x] : -1.0e6f;
     }
-    if (qt * 32u >= B) return;  // a tile past B: fragments written, nothing to sample
-    // 2. the slice's sample sub-tiles: wave (sl, wv) takes the contiguous run [wg * pw, +pw)
-    const uint32_t wg = sl * NW + wv;
-    const uint32_t j0 = min(wg * pw, nsub), j1 = min(j0 + pw, nsub);
+    if (!live_tile) return;  // a tile past B: fragments written, nothing to sample
+    // 2. the sample
     uint16_t* tw = tr_lds[wv];
     const int scale1 = 0x7f7f7f7f;
-    auto rown = [&](uint32_t j) { const uint32_t s0 = j * 32u; return (s0 >> 12) * stride + (s0 & 4095u) + (lane & 31u); };
     auto epi = [&](const v16f_t& acc, uint32_t j) __attribute__((always_inline)) {
         // rows past N (an unsampled small shard's last chunk) read as 0xffff
         const uint32_t n = rown(j);
@@ -2273,15 +2287,10 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     };
-    for (uint32_t j = j0; j < j1; j += 2) {  // two independent accumulator chains
+    auto pair = [&](uint32_t j, const uint2 (&cb)[2][W4]) __attribute__((always_inline)) {
         const bool two = j + 1 < j1;
-        uint2 c0[W4], c1[W4];
-        const uint32_t n0 = min(rown(j), N - 1u), n1 = min(rown(two ? j + 1 : j), N - 1u);
-#pragma unroll
-        for (int p = 0; p < W4; ++p) {
-            c0[p] = ((const uint2*)(codes + (uint64_t)p * cap + n0))[h];
-            c1[p] = ((const uint2*)(codes + (uint64_t)p * cap + n1))[h];
-        }
+        const uint2(&c0)[W4] = cb[0];
+        const uint2(&c1)[W4] = cb[1];
         v16f_t acc[2];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -2298,6 +2307,14 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
         mfma_fp4_drain_acc(acc);
         epi(acc[0], j);
         if (two) epi(acc[1], j + 1);
+    };
+    // two inlined copies (one per code buffer)
+    for (uint32_t j = j0; j < j1; j += 4) {
+        if (j + 2 < j1) load_pair(j + 2, cc[1]);
+        pair(j, cc[0]);
+        if (j + 2 >= j1) break;
+        if (j + 4 < j1) load_pair(j + 4, cc[0]);
+        pair(j + 2, cc[1]);
     }
 }
 
