@@ -2169,6 +2169,21 @@ __global__ __launch_bounds__(kSsThreads) void k_sample_select(const uint16_t* __
 // also writes what the scan and the select read: the query words [B][4 W4], |q|
 // per slot and the tile's fragments in the scan's layout (slots past B: zero
 // words); and the blocks zero the stage-1 flags / counts (k_qprep's duty).
+#ifdef GVDB_PREP_CLK
+__device__ unsigned long long g_prep_clk[256 * 8][5];  // timing study (variant builds): per wave phase clocks
+#define PREP_CLK(i)                                                                                  \
+    do {                                                                                             \
+        if (lane == 0) g_prep_clk[blockIdx.x * 8u + wv][i] = __builtin_amdgcn_s_memrealtime();      \
+    } while (0)
+extern "C" int gvdb_debug_prep_clock(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prep_clk), sizeof(g_prep_clk)) == hipSuccess ? 0 : -2;
+}
+#else
+#define PREP_CLK(i) \
+    do {            \
+    } while (0)
+#endif
 template <int W4>
 __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
     const float* __restrict__ qf, uint32_t D, float qthr, uint32_t B, uint32_t* __restrict__ qwords,
@@ -2176,13 +2191,13 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
     const uint4* __restrict__ codes, uint64_t cap, uint32_t N, uint32_t stride, uint32_t nsub, uint32_t pw,
     uint16_t* __restrict__ dsm, uint32_t S) {
     constexpr int KW = 4 * W4, KS = KW / 2, QT = 8, NW = kMx5Threads / 64;
-    constexpr uint32_t kSlices = 32;
     __shared__ uint32_t qw_lds[32][KW + 1];
     __shared__ uint32_t pc_lds[32];
     __shared__ __attribute__((aligned(16))) uint16_t tr_lds[NW][32 * 32];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t f = blockIdx.x, qt = f % QT, sl = f / QT, h = lane >> 5;
+    PREP_CLK(0);
     for (uint32_t i = f * kMx5Threads + tid; i < nzero; i += gridDim.x * kMx5Threads) zero[i] = 0u;
     // the slice's sample sub-tiles: wave (sl, wv) takes the contiguous run [wg * pw, +pw), two
     // at a time (two accumulator chains); the codes of the next pair load under the current
@@ -2228,6 +2243,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
         }
     }
     __syncthreads();
+    PREP_CLK(1);
     if (tid < 32) {
         uint32_t pc = 0;
 #pragma unroll
@@ -2257,6 +2273,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
         const uint32_t x = 8u * (uint32_t)(r >> 2) + 4u * h + (uint32_t)(r & 3);
         seed[r] = qt * 32u + x < B ? -(float)pc_lds[x] : -1.0e6f;
     }
+    PREP_CLK(2);
     if (!live_tile) return;  // a tile past B: fragments written, nothing to sample
     // 2. the sample
     uint16_t* tw = tr_lds[wv];
@@ -2316,6 +2333,7 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
         if (j + 4 < j1) load_pair(j + 4, cc[0]);
         pair(j + 2, cc[1]);
     }
+    PREP_CLK(3);
 }
 
 template <int W4>

@@ -129,6 +129,9 @@ for t in "${TASKS[@]}"; do
         mx7clk)  # k_scan_mx7 per-wave phase clocks (variant build abl/libgvdb_mx7clk.so) at 1.25M and 10M rows
             GVDB_LIB_PATH=$PWD/grape-vector-db_amd/abl/libgvdb_mx7clk.so run 600 gpurun_out/mx7clk.log python3 -u scripts/mx7_clock.py
             grep '^\[mx7clk\]' gpurun_out/mx7clk.log ;;
+        prepclk)  # k_sample_prep per-wave phase clocks (variant build abl/libgvdb_prepclk.so)
+            GVDB_LIB_PATH=$PWD/grape-vector-db_amd/abl/libgvdb_prepclk.so run 300 gpurun_out/prepclk.log python3 -u scripts/prep_clock.py
+            grep '^\[prepclk\]' gpurun_out/prepclk.log ;;
         c3clk)
             run 600 gpurun_out/c3clk.log python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10 --p2clk
             grep '^\[c3\]' gpurun_out/c3clk.log ;;
