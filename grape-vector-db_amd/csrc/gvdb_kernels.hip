@@ -2215,7 +2215,6 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
         }
     };
     const bool live_tile = qt * 32u < B;
-    if (live_tile && j0 < j1) load_pair(j0, cc[0]);
     // 1. the tile's 32 queries: wave wv packs queries 4 wv .. 4 wv + 3, every load in flight
     {
         float v[4][KW / 2];
@@ -2228,6 +2227,9 @@ __global__ __launch_bounds__(kMx5Threads, 1) void k_sample_prep(
                 v[u][c] = q < B && d < D ? qf[(uint64_t)q * D + d] : 0.0f;
             }
         }
+        // the first pair's codes: issued after the query loads, so the ballots wait only for
+        // those (vector loads complete in order)
+        load_pair(j0, cc[0]);  // unconditional (clamped rows): a branch here made the ballots wait for it
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t x = wv * 4u + (uint32_t)u, q = qt * 32u + x;
