@@ -2515,34 +2515,138 @@ bool gvdb::shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t
            ix->n == ix->id_row.size() && dim == ix->dim && dim > 0;
 }
 
+// The deep sharded form's exact cosine list, computed EARLY: enqueued by the
+// stage-1 call on a second pooled stream, concurrently with the dense stage 1 --
+// it reads nothing stage 1 writes -- into the caller's scratch (`list`: rows u64
+// [B][K2] | scores f32 [B][K2] | counts u32 [B] | tier failure word), then joined
+// by phase 2 through an event kept per scratch list.  K2 = 32 (phase 2's k is not
+// known yet; k <= 16 certifies on it like the single-index search).
+namespace {
+constexpr uint32_t kEarlyK2 = 32;
+struct EarlyFlat {
+    std::mutex mu;
+    std::unordered_map<const void*, hipEvent_t> ev;  // scratch list -> the list's completion
+};
+EarlyFlat& early_flat() {
+    static EarlyFlat* e = new EarlyFlat();  // never destroyed: events may outlive static destructors
+    return *e;
+}
+}  // namespace
+
+size_t gvdb::shard_early_list_bytes(uint64_t B) { return (size_t)B * kEarlyK2 * 12 + (size_t)B * 4 + 16; }
+
+gvdb_status gvdb::shard_deep_flat_early(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, void* list,
+                                        hipStream_t s) {
+    {  // a list an earlier search left here unjoined is stale from now on
+        std::lock_guard<std::mutex> lk(early_flat().mu);
+        auto it = early_flat().ev.find(list);
+        if (it != early_flat().ev.end()) {
+            (void)hipEventDestroy(it->second);
+            early_flat().ev.erase(it);
+        }
+    }
+    if (!shard_certified_eligible(ix, dim, 1) || B == 0 || B > 0xFFFFFFFFull) return GVDB_OK;
+    gvdb_status st = set_device(ix->device);
+    if (st != GVDB_OK) return st;
+    tier_poll();
+    WsGuard g(ix->device);
+    if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
+    Workspace& ws = *g.w;
+    hipStream_t s2 = ws.stream;
+    hipEvent_t e_in = nullptr, e_done = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e_in, hipEventDisableTiming), "event");
+    HIP_TRY(hipEventCreateWithFlags(&e_done, hipEventDisableTiming), "event");
+    struct EvDel {
+        hipEvent_t& e;
+        ~EvDel() {
+            if (e) (void)hipEventDestroy(e);
+        }
+    } del_in{e_in}, del_done{e_done};
+    HIP_TRY(hipEventRecord(e_in, s), "event");  // after the caller's queries
+    g.begin(s2);
+    HIP_TRY(hipStreamWaitEvent(s2, e_in, 0), "stream wait");
+    UseGuard ug{ix, s2};
+    char* p = (char*)list;
+    uint64_t* frow = (uint64_t*)p;
+    float* fsc = (float*)(p + (size_t)B * kEarlyK2 * 8);
+    uint32_t* fn = (uint32_t*)(p + (size_t)B * kEarlyK2 * 12);
+    uint32_t* lfail = fn + B;
+    bool cert = false;
+    uint32_t* flat_fail = nullptr;
+    const bool i8 = ix->i8_skip.load() == 0;
+    st = flat_mx_search(ix, d_q, (uint32_t)B, dim, kEarlyK2, kScoreCosine, 1, frow, fsc, fn, ws, s2, i8, &cert, true,
+                        &flat_fail);
+    if (st != GVDB_OK) return st;
+    // the tier's failure word into the list (the pooled workspace may serve another call next)
+    HIP_TRY(hipMemcpyAsync(lfail, flat_fail, 4, hipMemcpyDeviceToDevice, s2), "list failure word");
+    HIP_TRY(hipEventRecord(e_done, s2), "event");
+    std::lock_guard<std::mutex> lk(early_flat().mu);
+    early_flat().ev[list] = e_done;
+    e_done = nullptr;  // owned by the map now
+    return GVDB_OK;
+}
+
 gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                          const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
                                          const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl,
-                                         uint32_t* block2, uint32_t* dfail, hipStream_t s, bool* enqueued) {
+                                         uint32_t* block2, uint32_t* dfail, void* early_list, hipStream_t s,
+                                         bool* enqueued) {
     *enqueued = false;
     if (!shard_certified_eligible(ix, dim, k) || B == 0 || B > 0xFFFFFFFFull) return GVDB_OK;
     gvdb_status st = set_device(ix->device);
     if (st != GVDB_OK) return st;
+    // the early list of this scratch (shard_deep_flat_early), if the stage-1 call made one
+    hipEvent_t early = nullptr;
+    if (early_list) {
+        std::lock_guard<std::mutex> lk(early_flat().mu);
+        auto it = early_flat().ev.find(early_list);
+        if (it != early_flat().ev.end()) {
+            early = it->second;
+            early_flat().ev.erase(it);
+        }
+    }
+    struct EvDel {
+        hipEvent_t& e;
+        ~EvDel() {
+            if (e) (void)hipEventDestroy(e);
+        }
+    } del_early{early};
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
     g.begin(s);
     UseGuard ug{ix, s};
     tier_poll();
-    const uint32_t W4 = code_w4(dim), K2 = k <= 16 ? 32u : kDeepK2;
+    const uint32_t W4 = code_w4(dim);
+    uint32_t K2 = k <= 16 ? 32u : kDeepK2;
     HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc qcodes");
-    HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 4 + 16), "alloc certified lists");
-    char* p = ws.deep.as<char>();
-    uint64_t* frow = (uint64_t*)p;
-    float* fsc = (float*)(p + (size_t)B * K2 * 8);
-    uint32_t* fn = (uint32_t*)(p + (size_t)B * K2 * 12);
     HIP_TRY(launch_pack(d_q, B, dim, ix->thr, ws.qcodes.p, kPackWordsAoS, 0, 0, s), "pack queries");
-    bool cert = false;
-    uint32_t* flat_fail = nullptr;
-    const bool i8 = ix->i8_skip.load() == 0;
-    st = flat_mx_search(ix, d_q, (uint32_t)B, dim, K2, kScoreCosine, 1, frow, fsc, fn, ws, s, i8, &cert, true,
-                        &flat_fail);
-    if (st != GVDB_OK) return st;
+    const uint64_t* frow;
+    const float* fsc;
+    const uint32_t* fn;
+    const uint32_t* flat_fail = nullptr;
+    if (early) {  // joined here: the list ran beside stage 1 and the exchange
+        K2 = kEarlyK2;
+        HIP_TRY(hipStreamWaitEvent(s, early, 0), "stream wait");
+        const char* p = (const char*)early_list;
+        frow = (const uint64_t*)p;
+        fsc = (const float*)(p + (size_t)B * K2 * 8);
+        fn = (const uint32_t*)(p + (size_t)B * K2 * 12);
+        flat_fail = fn + B;
+    } else {
+        HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 4 + 16), "alloc certified lists");
+        char* p = ws.deep.as<char>();
+        bool cert = false;
+        uint32_t* ff = nullptr;
+        const bool i8 = ix->i8_skip.load() == 0;
+        st = flat_mx_search(ix, d_q, (uint32_t)B, dim, K2, kScoreCosine, 1, (uint64_t*)p, (float*)(p + (size_t)B * K2 * 8),
+                            (uint32_t*)(p + (size_t)B * K2 * 12), ws, s, i8, &cert, true, &ff);
+        if (st != GVDB_OK) return st;
+        frow = (const uint64_t*)p;
+        fsc = (const float*)(p + (size_t)B * K2 * 8);
+        fn = (const uint32_t*)(p + (size_t)B * K2 * 12);
+        flat_fail = ff;
+    }
     HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
     HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), (uint32_t)B,
                                 (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s, own_cnt, block2, reff,

@@ -412,7 +412,13 @@ bool shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t k);
 gvdb_status shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                    const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
                                    const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl, uint32_t* block2,
-                                   uint32_t* dfail, hipStream_t s, bool* enqueued);
+                                   uint32_t* dfail, void* early_list, hipStream_t s, bool* enqueued);
+// the certified phase 2's exact cosine list, enqueued EARLY by the stage-1 call on a second
+// stream (concurrent with stage 1 and the exchange) into `list` (shard_early_list_bytes(B) bytes
+// of the caller's scratch); phase 2 joins it by the list's address.  Not eligible: nothing.
+size_t shard_early_list_bytes(uint64_t B);
+gvdb_status shard_deep_flat_early(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, void* list,
+                                  hipStream_t s);
 // gvdb_bigr.hip: the owned entries' local top-k (k <= 1024) -> the exchange-2 block
 hipError_t launch_shard_deep_topk(const float* m_cos, const uint32_t* m_rows, const uint32_t* m_dist,
                                   const uint32_t* own_cnt, const uint32_t* reff, uint32_t B, uint32_t Rl, uint32_t k,

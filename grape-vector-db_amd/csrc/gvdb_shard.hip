@@ -772,6 +772,12 @@ gvdb_status gvdb_shard_stage1_device(const gvdb_index* shard, const float* d_que
     if (deep) {
         uint32_t* m_rows = (uint32_t*)d_scratch;
         const uint64_t hw = B * (dim + 1ull);  // histogram words before the counts
+        // the certified phase 2's exact cosine list, beside stage 1 (into the owned-rows region,
+        // which only the rerank fallback writes, after the certify pass has read the list)
+        if (shard_early_list_bytes(B) <= B * R * 4) {  // (it checks the shard's eligibility itself)
+            st = shard_deep_flat_early(shard, d_queries, B, dim, m_rows + 2 * BR, s);
+            if (st != GVDB_OK) return st;
+        }
         st = shard_stage1_members(shard, d_queries, B, dim, R, m_rows, m_rows + BR, d_block1, s);
         if (st != GVDB_OK || si.n == 0) {
             if (hipMemsetD32Async(d_block1, 0, hw + B, s) != hipSuccess ||
@@ -835,7 +841,8 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
             bool enqueued = false;
             if (e == hipSuccess) {
                 const gvdb_status st = shard_certified_phase2(shard, d_queries, B, dim, k, tcut, own_cnt, reff,
-                                                              m_rows, m_dist, Rl, d_block2, dfail, s, &enqueued);
+                                                              m_rows, m_dist, Rl, d_block2, dfail, o_rows, s,
+                                                              &enqueued);
                 if (st != GVDB_OK) return st;
             }
             if (enqueued) gate = dfail;
