@@ -1036,7 +1036,9 @@ __device__ unsigned long long g_mx7_clk[4096][6];
 // DENSE (the reference's default depth, R/N >= 1/64): no threshold test; every
 // tile's 16 dots per lane go to dense[q][row] as f16 (exact: |dot| <= 768),
 // four consecutive rows per 8-byte store; the select reads d = |q| - dot.
-template <int W4, bool DENSE>
+// QT: query tiles of 32 per launch (8 = a full 256-query group; smaller batches take
+// 1 / 2 / 4 instead of multiplying padded slots: the MFMAs per row scale with QT).
+template <int W4, bool DENSE, int QT = 8>
 __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const v4i_t* __restrict__ qfrag_g,
                                                            const uint32_t* __restrict__ qpc,
@@ -1047,13 +1049,12 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     if (gate_closed(gate)) return;
     constexpr int KW = 4 * W4;  // 32-bit code words per row
     constexpr int KS = KW / 2;  // k-steps of 64 bits
-    constexpr int QT = 8;       // query tiles of 32
     constexpr int NM = KS * QT;  // MFMAs per sub-tile
 #ifdef GVDB_MX7_CLK
     uint32_t n_hit = 0;
 #endif
     constexpr int NW = kMx7Threads / 64;
-    constexpr int PF = 4;  // A-fragment ring depth (in MFMAs; 8: same time)
+    constexpr int PF = NM % 4 == 0 ? 4 : NM % 3 == 0 ? 3 : 2;  // A-fragment ring depth (in MFMAs; 8: same time)
     static_assert(NM % PF == 0, "the A ring's slot of MFMA m must not depend on the sub-tile");
     // Hit records (the threshold scan): a tile test that hits appends, per hitting LANE,
     // its 16 dots as f16 (exact: |dot| <= 768) + (first row, query) to the wave's LDS
@@ -1097,8 +1098,10 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
         load(gw, ring[0]);
         load(gw + W, ring[1]);
     }
+    // the group's fragments are laid out for 8 tiles: (k-step, tile, lane) at (s * 8 + qt) * 64 + l
 #pragma unroll 4
-    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx7Threads) qfrag[i] = qfrag_g[i];
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx7Threads)
+        qfrag[i] = QT == 8 ? qfrag_g[i] : qfrag_g[((i >> 6) / QT * 8u + (i >> 6) % QT) * 64u + (i & 63u)];
     constexpr uint32_t kPadBits = 32u * KW;
     if (tid < QT * 32) {
         const uint32_t q = tid;
@@ -1306,14 +1309,14 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
                     bnext = fp4_row01(v.y);                                    \
                 }                                                              \
             }
-            GVDB_MX7_POS0(0)
-            GVDB_MX7_POS0(1)
-            GVDB_MX7_POS0(2)
-            GVDB_MX7_POS0(3)
-            GVDB_MX7_POS0(4)
-            GVDB_MX7_POS0(5)
-            GVDB_MX7_POS0(6)
-            GVDB_MX7_POS0(7)
+            if constexpr (QT > 0) GVDB_MX7_POS0(0)
+            if constexpr (QT > 1) GVDB_MX7_POS0(1)
+            if constexpr (QT > 2) GVDB_MX7_POS0(2)
+            if constexpr (QT > 3) GVDB_MX7_POS0(3)
+            if constexpr (QT > 4) GVDB_MX7_POS0(4)
+            if constexpr (QT > 5) GVDB_MX7_POS0(5)
+            if constexpr (QT > 6) GVDB_MX7_POS0(6)
+            if constexpr (QT > 7) GVDB_MX7_POS0(7)
 #undef GVDB_MX7_POS0
             bcur = bnext;
 #pragma unroll
@@ -1536,17 +1539,24 @@ static hipError_t launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
     constexpr uint64_t kPer = 8u * (2u * W4) * 64u;
     for (uint32_t g = 0; g < a.B; g += 256) {
         const uint32_t bg = min(256u, a.B - g);
+        const v4i_t* qf = (const v4i_t*)a.qfrag + (g / 256u) * kPer;
+        // the query tiles this group needs (a batch of 64 pays 2 tiles' MFMAs, not 8)
+        const uint32_t qt = bg <= 32u ? 1u : bg <= 64u ? 2u : bg <= 128u ? 4u : 8u;
         if (a.dense_sel) {  // every distance of the group, then its members (the dense block is reused per group)
-            hipLaunchKernelGGL((k_scan_mx7<W4, true>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap, a.N,
-                               (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                               a.buf, a.bufcap, a.dense, a.dense_np, a.gate);
+            auto kern = qt == 1 ? k_scan_mx7<W4, true, 1> : qt == 2 ? k_scan_mx7<W4, true, 2>
+                      : qt == 4 ? k_scan_mx7<W4, true, 4> : k_scan_mx7<W4, true, 8>;
+            // few tiles: little MFMA work per code load, two blocks per CU keep more loads in flight
+            hipLaunchKernelGGL(kern, dim3(cu_count() * (qt <= 2u ? 2u : 1u)), dim3(kMx7Threads), 0, s, a.codes, a.cap,
+                               a.N, qf, a.qpc + g, a.thr + g, bg, a.counts + g, a.buf, a.bufcap, a.dense, a.dense_np,
+                               a.gate);
             GVDB_LAUNCH_CHECK();
             const hipError_t e = launch_select_dense(a, g, bg, s);
             if (e != hipSuccess) return e;
         } else {
-            hipLaunchKernelGGL((k_scan_mx7<W4, false>), dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap,
-                               a.N, (const v4i_t*)a.qfrag + (g / 256u) * kPer, a.qpc + g, a.thr + g, bg, a.counts + g,
-                               a.buf + (uint64_t)g * a.bufcap, a.bufcap, nullptr, 0u, a.gate);
+            auto kern = qt <= 4 ? k_scan_mx7<W4, false, 4> : k_scan_mx7<W4, false, 8>;
+            hipLaunchKernelGGL(kern, dim3(cu_count()), dim3(kMx7Threads), 0, s, a.codes, a.cap, a.N, qf, a.qpc + g,
+                               a.thr + g, bg, a.counts + g, a.buf + (uint64_t)g * a.bufcap, a.bufcap, nullptr, 0u,
+                               a.gate);
             GVDB_LAUNCH_CHECK();
         }
     }
