@@ -946,9 +946,13 @@ constexpr int kI8qSpread = 2;       // a row piece of the sub-tile two ahead eve
 constexpr uint32_t kI8qSub = 2;     // 32-row groups per LDS sub-tile
 constexpr uint32_t kI8qBufs = 3;    // LDS sub-tile buffers (kI8qBufs - 1 sub-tiles in flight)
 constexpr uint32_t kI8qCl = 1024;  // block nomination list, u32 entries + scores (flushed at a barrier once half full)
-template <int KC>
+// SPLIT (batches of <= 128 queries, round 5): the 4 live query tiles take two waves
+// each, wave w tile w % 4 and row group w / 4 of every sub-tile -- half the MFMAs and
+// B-fragment reads per wave instead of 4 waves computing padded slots.
+template <int KC, bool SPLIT>
 __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     constexpr int KS = 4 * KC;                          // k-steps of 32 per row group
+    constexpr uint32_t NGI = SPLIT ? 1u : kI8qSub;      // row groups per wave and sub-tile
     constexpr uint32_t kPieces = kI8qSub * KC * 4;      // 1 KiB pieces per sub-tile
     constexpr uint32_t kPerWave = kPieces / 8;          // row DMAs per wave per sub-tile
     constexpr uint32_t kSubBytes = kPieces * 1024u;
@@ -967,6 +971,8 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[kFxQ];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t qtile = SPLIT ? (wv & 3u) : wv;   // this wave's 32 query slots
+    const uint32_t gi0 = SPLIT ? (wv >> 2) : 0u;     // its first row group of a sub-tile
     const uint32_t N = a.N, G = gridDim.x;
     const uint32_t nsub_all = ((N + kFxRows - 1) / kFxRows) * (kFxRows / 32u / kI8qSub);
     const uint32_t ns = blockIdx.x < nsub_all ? (nsub_all - blockIdx.x + G - 1) / G : 0u;  // sub-tiles b, b+G, ...
@@ -1016,7 +1022,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         const char* qx = (const char*)a.qx;
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-            A[s] = *(const fx_v4i*)(qx + (((uint32_t)(s >> 2) * 8u + wv) * 4u + (uint32_t)(s & 3)) * 1024u + lane * 16u);
+            A[s] = *(const fx_v4i*)(qx + (((uint32_t)(s >> 2) * 8u + qtile) * 4u + (uint32_t)(s & 3)) * 1024u + lane * 16u);
         // landed here, once: otherwise the waitcnt pass defers these waits into the
         // loop, where its counts (blind to the asm DMAs) drain the row prefetch
 #pragma unroll
@@ -1032,7 +1038,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     if (ns)
 #pragma unroll
         for (uint32_t j = 0; j + 1 < kI8qBufs; ++j) stage(j);
-    fx_v16i acc[kI8qSub];
+    fx_v16i acc[NGI];
     auto row_of = [&](uint32_t e) {  // a list entry's row
         const uint32_t v = blockIdx.x + ((e >> 6) & 0x3ffffu) * G;
         return (v / kSubPerTile) * kFxRows + (kI8qSub * (v % kSubPerTile) + ((e >> 5) & 1u)) * 32u + (e & 31u);
@@ -1052,11 +1058,12 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     auto epilogue = [&](uint32_t i, uint32_t t, uint32_t u, const float* rv, const float* rh)
                         __attribute__((always_inline)) {
 #pragma unroll
-        for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
+        for (uint32_t ga = 0; ga < NGI; ++ga) {
+            const uint32_t gi = gi0 + ga;
             const uint32_t n = t * kFxRows + (kI8qSub * u + gi) * 32u + (lane & 31u);
-            const float rinv = n < N ? rv[gi] : 0.0f, rho = n < N ? rh[gi] : 0.0f;
+            const float rinv = n < N ? rv[ga] : 0.0f, rho = n < N ? rh[ga] : 0.0f;
             // this lane's 16 slots: qb0 + (e & 3) + 8 (e >> 2)
-            uint32_t qb0 = wv * 32u + 4u * (lane >> 5);
+            uint32_t qb0 = qtile * 32u + 4u * (lane >> 5);
             asm volatile("" : "+v"(qb0));  // keep the per-slot addresses out of the loop
             float qs[16], ts[16];
 #pragma unroll
@@ -1075,13 +1082,13 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             }
             float mx = -__builtin_inff();
 #pragma unroll
-            for (int e = 0; e < 16; ++e) mx = fmaxf(mx, (float)acc[gi][e] * qs[e] - ts[e]);
+            for (int e = 0; e < 16; ++e) mx = fmaxf(mx, (float)acc[ga][e] * qs[e] - ts[e]);
             if (!__ballot(mx >= 0.0f && n < N)) continue;
             // rare: a candidate in this fragment (thr = +inf for slots >= B)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const uint32_t q = qb0 + (e & 3) + 8u * (e >> 2);
-                const float v = (float)acc[gi][e] * qs[e];
+                const float v = (float)acc[ga][e] * qs[e];
                 if (n < N && v >= ts[e]) {
                     const uint32_t li = atomicAdd(&cl_n, 1u);
                     if (li < kI8qCl) {
@@ -1102,7 +1109,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     // barrier of step i, before step i's MFMAs: on every SIMD one wave's candidate test
     // overlaps the other wave's MFMAs instead of both testing while the matrix core idles.
     const bool late = wv >= 4;
-    float lrv[kI8qSub] = {}, lrh[kI8qSub] = {};  // step i-1's row operands (late waves)
+    float lrv[NGI] = {}, lrh[NGI] = {};  // step i-1's row operands (late waves)
     for (uint32_t i = 0; i < ns; ++i) {
         // stage i landed (stages i+1 .. i+kI8qBufs-2 are the younger ops), then every wave's part
         if (wv < kOpsWaves)
@@ -1131,24 +1138,25 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             epilogue(i - 1, tp, up, lrv, lrh);
         }
 #pragma unroll
-        for (uint32_t gi = 0; gi < kI8qSub; ++gi)
+        for (uint32_t ga = 0; ga < NGI; ++ga)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[gi][e] = 0;
+            for (int e = 0; e < 16; ++e) acc[ga][e] = 0;
         // B fragments from LDS, kI8qBr k-steps ahead of their MFMAs (LDS latency > the
         // ~64 cycles of one k-step's two MFMAs)
         constexpr int BR = kI8qBr;
-        fx_v4i bf[BR][kI8qSub];
+        fx_v4i bf[BR][NGI];
 #pragma unroll
         for (int s = 0; s < BR - 1; ++s)
 #pragma unroll
-            for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-                bf[s][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)s) * 1024u);
+            for (uint32_t ga = 0; ga < NGI; ++ga)
+                bf[s][ga] = *(const fx_v4i*)(Bb + ((gi0 + ga) * KC * 4u + (uint32_t)s) * 1024u);
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             if (s + BR - 1 < KS) {
 #pragma unroll
-                for (uint32_t gi = 0; gi < kI8qSub; ++gi)
-                    bf[(s + BR - 1) % BR][gi] = *(const fx_v4i*)(Bb + (gi * KC * 4u + (uint32_t)(s + BR - 1)) * 1024u);
+                for (uint32_t ga = 0; ga < NGI; ++ga)
+                    bf[(s + BR - 1) % BR][ga] =
+                        *(const fx_v4i*)(Bb + ((gi0 + ga) * KC * 4u + (uint32_t)(s + BR - 1)) * 1024u);
             }
             __builtin_amdgcn_sched_barrier(0);  // the reads stay BR - 1 k-steps ahead (no sinking)
             // the row pieces of sub-tile i + kI8qBufs - 1 spread over the MFMAs rather than
@@ -1158,24 +1166,24 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             if (s % kI8qSpread == 0 && (uint32_t)(s / kI8qSpread) < kPerWave)
                 piece(i + kI8qBufs - 1u, (uint32_t)(s / kI8qSpread));
 #pragma unroll
-            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
-                acc[gi] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][gi], acc[gi], 0, 0, 0);
+            for (uint32_t ga = 0; ga < NGI; ++ga) {
+                acc[ga] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][ga], acc[ga], 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
         if (!late) {
-            float rv[kI8qSub], rh[kI8qSub];
+            float rv[NGI], rh[NGI];
 #pragma unroll
-            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
-                rv[gi] = ops[gi * 32u + (lane & 31u)];
-                rh[gi] = ops[kRows + gi * 32u + (lane & 31u)];
+            for (uint32_t ga = 0; ga < NGI; ++ga) {
+                rv[ga] = ops[(gi0 + ga) * 32u + (lane & 31u)];
+                rh[ga] = ops[kRows + (gi0 + ga) * 32u + (lane & 31u)];
             }
             epilogue(i, t, u, rv, rh);
         } else {  // this step's operands to registers: buffer i % 3 is refilled after the next barrier
 #pragma unroll
-            for (uint32_t gi = 0; gi < kI8qSub; ++gi) {
-                lrv[gi] = ops[gi * 32u + (lane & 31u)];
-                lrh[gi] = ops[kRows + gi * 32u + (lane & 31u)];
+            for (uint32_t ga = 0; ga < NGI; ++ga) {
+                lrv[ga] = ops[(gi0 + ga) * 32u + (lane & 31u)];
+                lrh[ga] = ops[kRows + (gi0 + ga) * 32u + (lane & 31u)];
             }
         }
     }
@@ -1217,7 +1225,10 @@ hipError_t launch_flat_mx_emit(const FlatMxArgs& a, hipStream_t s) {
     const uint64_t nsub = (uint64_t)tiles * (kFxRows / 32u / kI8qSub);
     const uint32_t g = fx_grid((uint32_t)std::min<uint64_t>(nsub, 0xffffffffull));
     if (a.i8 && a.KC == 6 && i8r && nsub < (uint64_t)g << 18) {  // one block per CU over the 64-row sub-tiles
-        hipLaunchKernelGGL((k_flat_i8q<6>), dim3(g), dim3(kFxThreads), 0, s, a);
+        if (a.B <= 128u)  // 4 live query tiles: two waves per tile, one row group each
+            hipLaunchKernelGGL((k_flat_i8q<6, true>), dim3(g), dim3(kFxThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_flat_i8q<6, false>), dim3(g), dim3(kFxThreads), 0, s, a);
     } else if (a.i8)
         hipLaunchKernelGGL((k_flat_mx<false, true>), dim3(fx_grid(tiles)), dim3(kFxThreads), 0, s, a);
     else

@@ -159,7 +159,7 @@ for t in "${TASKS[@]}"; do
             IFS=',' read -ra VARS <<< "${t#flatvar:}"
             for v in "${VARS[@]}"; do
                 lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
-                GVDB_FLAT=i8 GVDB_LIB_PATH=$lib BS=256 FLAT_REPS=10 run 600 gpurun_out/flatvar_$v.log python3 scripts/flat_timing.py
+                GVDB_FLAT=i8 GVDB_LIB_PATH=$lib BS=${FBS:-256} FLAT_REPS=10 run 600 gpurun_out/flatvar_$v.log python3 scripts/flat_timing.py
                 echo "== $v"; grep -E "B=|emit" gpurun_out/flatvar_$v.log | tail -2
             done ;;
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
