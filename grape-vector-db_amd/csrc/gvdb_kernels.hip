@@ -1055,6 +1055,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
 #endif
     constexpr int NW = kMx7Threads / 64;
     constexpr int PF = NM % 4 == 0 ? 4 : NM % 3 == 0 ? 3 : 2;  // A-fragment ring depth (in MFMAs; 8: same time)
+    constexpr int kExpandAt = QT > 1 ? 1 : 0;  // the next k-step's row fragment is expanded after this tile's MFMA
     static_assert(NM % PF == 0, "the A ring's slot of MFMA m must not depend on the sub-tile");
     // Hit records (the threshold scan): a tile test that hits appends, per hitting LANE,
     // its 16 dots as f16 (exact: |dot| <= 768) + (first row, query) to the wave's LDS
@@ -1304,7 +1305,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
                 const v4i_t a = ar[(qt) % PF];                                 \
                 ar[(qt) % PF] = afrag(((qt) + PF) % NM);                        \
                 mfma_fp4_first_nop(acc[qt], bcur, a, scale1);                 \
-                if ((qt) == 1) {                                               \
+                if ((qt) == kExpandAt) {                                       \
                     const uint2 v = c[0];                                      \
                     bnext = fp4_row01(v.y);                                    \
                 }                                                              \
@@ -1329,7 +1330,7 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
                     const v4i_t a = ar[m % PF];
                     ar[m % PF] = afrag((m + PF) % NM);  // the ring runs on into the next sub-tile
                     mfma_fp4_acc(acc[qt], bcur, a, scale1);
-                    if (qt == 1 && s + 1 < KS) {  // next k-step's row fragment under this one's MFMAs
+                    if (qt == kExpandAt && s + 1 < KS) {  // next k-step's row fragment under this one's MFMAs
                         const uint2 v = c[(s + 1) >> 1];
                         bnext = fp4_row01(((s + 1) & 1) ? v.y : v.x);
                     }

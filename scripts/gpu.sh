@@ -113,6 +113,9 @@ for t in "${TASKS[@]}"; do
         c3)
             run 900 gpurun_out/c3.log python -u scripts/c3_emulate.py
             grep '^{' gpurun_out/c3.log > gpurun_out/c3.json; grep '^\[c3\]' gpurun_out/c3.log | tail -4 ;;
+        c4prof)  # kernel trace of config 4's per-rank step (8 shards of 1.25M x 3072, batch 256)
+            run 900 gpurun_out/c4prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o run -- python3 scripts/c3_emulate.py --dim 3072 --no-single --oracle-queries 0 --steps 5
+            python3 scripts/trace_summary.py gpurun_out/prof_c4/run_kernel_trace.csv > gpurun_out/c4_kernels.txt; head -20 gpurun_out/c4_kernels.txt ;;
         c3prof)
             run 600 gpurun_out/c3prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10
             python3 scripts/trace_summary.py gpurun_out/prof_c3/run_kernel_trace.csv | grep gvdb | head -12 ;;
