@@ -332,9 +332,173 @@ __global__ __launch_bounds__(kBigThreads) void k_select_dense(const uint16_t* __
     }
 }
 
+// ---- the rule form of the dense select in parallel (round 5): k_select_dense runs one
+// block per query over its whole dense row (a batch of 64 at a 1.25M-row shard: 64
+// blocks reading 2.5 MB each, 0.5 ms).  Here the rows are cut into S segments of L
+// rows: k_dense_seg_hist (one block per (segment, query)) writes each segment's
+// Hamming histogram, seg_hist[q][s][0..D]; k_dense_rule (one block per query) sums
+// them, finds T and the tie quota, and rescans only the segment that holds the
+// quota-th tied row.  The per-segment histograms stay in memory: the deep sharded
+// phase 2 counts a row's tied predecessors from them (k_deep_certify) and k_dense_own
+// compacts owned rows from the dense block without member lists.
+constexpr uint32_t kSegThreads = 256;
+__global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist(const uint16_t* __restrict__ dense, uint32_t np,
+                                                                uint32_t N, uint32_t D, const uint32_t* __restrict__ qpc,
+                                                                uint32_t S, uint32_t L,
+                                                                uint32_t* __restrict__ seg_hist,
+                                                                const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t wh_all[];  // [4][H4] one histogram per wave
+    const uint32_t sg = blockIdx.x, q = blockIdx.y, tid = threadIdx.x, H = D + 1u, H4 = (H + 3u) & ~3u;
+    const uint32_t wv = tid >> 6;
+    for (uint32_t i = tid; i < 4u * H4; i += kSegThreads) wh_all[i] = 0u;
+    __syncthreads();
+    const float pc = (float)qpc[q];
+    const uint32_t r0 = sg * L, r1 = min(N, r0 + L);  // L % 8 == 0
+    const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);
+    uint32_t* wh = wh_all + wv * H4;
+    const uint32_t v0 = r0 / 8u, v1 = (r1 + 7u) / 8u;
+    constexpr uint32_t kU = 4;  // 16-B loads in flight per thread
+    for (uint32_t v = v0 + tid; v < v1; v += kSegThreads * kU) {
+        uint4 w[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t vv = v + kSegThreads * u;
+            w[u] = vv < v1 ? dq[vv] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t vv = v + kSegThreads * u;
+            const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (vv < v1 && 8u * vv + (uint32_t)j < r1)
+                    atomicAdd(&wh[min(dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc), D)], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* out = seg_hist + ((uint64_t)q * S + sg) * H;
+    for (uint32_t t = tid; t < H; t += kSegThreads) out[t] = wh_all[t] + wh_all[H4 + t] + wh_all[2 * H4 + t] + wh_all[3 * H4 + t];
+}
+
+// the rule of query q from its segment histograms: (T, cut, need, 0) into tcut; optional
+// mhist / mcount (the deep exchange-1 block: members below T, `need` at T)
+__global__ __launch_bounds__(kBigThreads) void k_dense_rule(const uint32_t* __restrict__ seg_hist, uint32_t S,
+                                                            uint32_t L, const uint16_t* __restrict__ dense,
+                                                            uint32_t np, uint32_t N, uint32_t D, uint32_t R,
+                                                            const uint32_t* __restrict__ qpc,
+                                                            uint32_t* __restrict__ tcut, uint32_t* __restrict__ mhist,
+                                                            uint32_t* __restrict__ mcount,
+                                                            uint32_t* __restrict__ pc_out,
+                                                            const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [H]
+    __shared__ uint32_t s_T, s_lt, s_seg, s_left, s_cut, wsum[kBigThreads / 64];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, H = D + 1u;
+    const uint32_t wv = tid >> 6, lane = tid & 63u;
+    const uint32_t* sh = seg_hist + (uint64_t)q * S * H;
+    for (uint32_t t = tid; t < H; t += kBigThreads) {
+        uint32_t c = 0u;
+        for (uint32_t sg = 0; sg < S; ++sg) c += sh[(uint64_t)sg * H + t];
+        hist[t] = c;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t t = wave_find_cum(hist, H, R);
+        const uint32_t lt = wave_sum_below(hist, t);
+        if (tid == 0) {
+            s_T = t;
+            s_lt = lt;
+        }
+    }
+    __syncthreads();
+    const uint32_t T = s_T, need = R - s_lt;
+    if (mhist) {
+        uint32_t* out = mhist + (uint64_t)q * H;
+        for (uint32_t t = tid; t < H; t += kBigThreads) out[t] = t < T ? hist[t] : t == T ? need : 0u;
+        if (tid == 0) mcount[q] = R;
+    }
+    uint32_t cut = ~0u;
+    if (hist[T] > need) {  // block-uniform
+        if (tid == 0) {  // the segment holding the need-th tied row, and its rank there
+            uint32_t c = 0u, sg = 0u;
+            for (; sg + 1u < S; ++sg) {
+                const uint32_t w = sh[(uint64_t)sg * H + T];
+                if (c + w >= need) break;
+                c += w;
+            }
+            s_seg = sg;
+            s_left = need - c;
+            s_cut = ~0u;
+        }
+        __syncthreads();
+        const float pc = (float)qpc[q];
+        const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);
+        const uint32_t r0 = s_seg * L, r1 = min(N, r0 + L), left = s_left;
+        const uint32_t sv0 = r0 / 8u, sv1 = (r1 + 7u) / 8u;
+        uint32_t base = 0u;
+        for (uint32_t it = sv0; it < sv1; it += kBigThreads) {  // block-uniform rounds, rows in order
+            const uint32_t v = it + tid;
+            uint32_t tm = 0u;  // this thread's 8 rows tied at T
+            if (v < sv1) {
+                const uint4 w = dq[v];
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (8u * v + (uint32_t)j < r1 && dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) == T)
+                        tm |= 1u << j;
+            }
+            uint32_t total;
+            const uint32_t excl = base + block_scan_u32((uint32_t)__popc(tm), wsum, &total);
+            const uint32_t cnt = (uint32_t)__popc(tm);
+            if (cnt && excl < left && left <= excl + cnt) {
+                uint32_t r = left - excl, bits = tm;
+                while (--r) bits &= bits - 1u;
+                s_cut = 8u * v + (uint32_t)__builtin_ctz(bits);
+            }
+            base += total;
+            if (base >= left) break;
+        }
+        __syncthreads();
+        cut = s_cut;
+    }
+    (void)wv;
+    (void)lane;
+    if (tid == 0) {
+        if (pc_out) pc_out[q] = qpc[q];  // |q| for the deep sharded phase 2 (the stage-1 operands do not outlive it)
+        tcut[4u * q] = T;
+        tcut[4u * q + 1u] = cut;
+        tcut[4u * q + 2u] = need;
+        tcut[4u * q + 3u] = 0u;
+    }
+}
+
+// segments of a dense row: S segments of L rows (L % 256 == 0), S <= smax
+void dense_segments(uint32_t N, uint32_t smax, uint32_t* S, uint32_t* L) {
+    const uint32_t s0 = std::max<uint32_t>(1u, std::min<uint32_t>(smax, kDenseSegs));
+    uint32_t l = ((N + s0 - 1u) / s0 + 255u) & ~255u;
+    if (l == 0) l = 256u;
+    *L = l;
+    *S = std::max<uint32_t>(1u, (N + l - 1u) / l);
+}
+
 hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hipStream_t s) {
     if (bg == 0) return hipSuccess;
     if (a.R > a.N || !a.dense) return hipErrorInvalidValue;  // every list slot must be filled
+    if (a.seg_hist && a.tcut) {  // the parallel rule form
+        const uint32_t H = a.D + 1u;
+        const uint16_t* dn = a.dense + (a.dense_keep ? (uint64_t)g0 * a.dense_np : 0ull);
+        uint32_t* sh = a.seg_hist + (uint64_t)g0 * a.seg_n * H;
+        hipLaunchKernelGGL(k_dense_seg_hist, dim3(a.seg_n, bg), dim3(kSegThreads), (size_t)4u * ((H + 3u) & ~3u) * 4u,
+                           s, dn, a.dense_np, a.N, a.D, a.qpc + g0, a.seg_n, a.seg_len, sh, a.gate);
+        GVDB_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_dense_rule, dim3(bg), dim3(kBigThreads), (size_t)H * 4u, s, sh, a.seg_n, a.seg_len, dn,
+                           a.dense_np, a.N, a.D, a.R, a.qpc + g0, a.tcut + 4ull * g0,
+                           a.mhist ? a.mhist + (uint64_t)g0 * H : nullptr, a.mcount ? a.mcount + g0 : nullptr,
+                           a.pc_out ? a.pc_out + g0 : nullptr, a.gate);
+        GVDB_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     const size_t lds = (size_t)(kSdWaves + 1u) * ((a.D + 4u) & ~3u) * 4u;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_select_dense, dim3(bg), dim3(kBigThreads), lds, s, a.dense, a.dense_np, a.N, a.D, a.R,
@@ -369,7 +533,8 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     uint64_t* __restrict__ out_ids, float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
     uint32_t* __restrict__ fail, const uint32_t* __restrict__ kcnt, uint32_t* __restrict__ block2,
     const uint32_t* __restrict__ reff, const uint32_t* __restrict__ m_rows, const uint32_t* __restrict__ m_dist,
-    uint32_t mlen, const uint32_t* __restrict__ list_fail) {
+    uint32_t mlen, const uint32_t* __restrict__ list_fail, const uint32_t* __restrict__ seg_hist, uint32_t seg_n,
+    uint32_t seg_len, uint32_t seg_h, const uint16_t* __restrict__ dense, uint32_t dense_np) {
     __shared__ uint32_t s_trow[64], s_cnt[64];
     __shared__ uint32_t s_nt;
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
@@ -381,7 +546,7 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     const uint32_t T = tcut[4u * q], cut = tcut[4u * q + 1u], need = tcut[4u * q + 2u];
     // 0: cut, 2: no tied member, 3: the tie rank counted in the member list (deep sharded phase 2)
     const uint32_t mode = tcut[4u * q + 3u];
-    const bool lazy = mode == 3u && m_rows;
+    const bool lazy = mode == 3u && (m_rows || seg_hist);
     bool mem = false, tied = false;
     uint32_t row = 0u, d = 0u, o = ~0u;  // o: ascending = cosine descending
     if (tid < 64u) {
@@ -403,7 +568,33 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     }
     __syncthreads();
     const uint32_t nt = s_nt;
-    if (nt && mode == 3u) {  // block-uniform: the member list's rows tied at T below each listed tied row
+    if (nt && mode == 3u && seg_hist) {  // block-uniform: the shard's rows tied at T below each listed tied row,
+        // from the segment histograms (whole segments) and the dense block (the row's own segment)
+        uint32_t pcq = 0u;
+        for (uint32_t w = 0; w < W4; ++w) {
+            const uint4 c = qcodes[(uint64_t)q * W4 + w];
+            pcq += (uint32_t)(__popc(c.x) + __popc(c.y) + __popc(c.z) + __popc(c.w));
+        }
+        const float pc = (float)pcq;
+        const uint32_t* sh = seg_hist + (uint64_t)q * seg_n * seg_h;
+        const uint4* dq = (const uint4*)(dense + (uint64_t)q * dense_np);
+        for (uint32_t i = 0; i < nt; ++i) {
+            const uint32_t r = s_trow[i], sg = r / seg_len;
+            uint32_t c = 0u;
+            for (uint32_t t = tid; t < sg; t += kCertThreads) c += sh[(uint64_t)t * seg_h + T];
+            const uint32_t v0 = sg * seg_len / 8u, v1 = (r + 7u) / 8u;
+            for (uint32_t v = v0 + tid; v < v1; v += kCertThreads) {
+                const uint4 w = dq[v];
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    c += (8u * v + (uint32_t)j < r && dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) == T) ? 1u
+                                                                                                                 : 0u;
+            }
+            if (c) atomicAdd(&s_cnt[i], c);
+        }
+        __syncthreads();
+    } else if (nt && mode == 3u) {  // block-uniform: the member list's rows tied at T below each listed tied row
         const uint32_t* mr = m_rows + (uint64_t)q * mlen;
         const uint32_t* md = m_dist + (uint64_t)q * mlen;
         constexpr uint32_t kU = 32;  // 4-B loads in flight per thread (a 1M-entry list: 32 rounds)
@@ -477,12 +668,86 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                float* out_scores, uint32_t* out_n, uint32_t* fail, hipStream_t s,
                                const uint32_t* kcnt, uint32_t* block2, const uint32_t* reff,
                                const uint32_t* m_rows, const uint32_t* m_dist, uint32_t mlen,
-                               const uint32_t* list_fail) {
+                               const uint32_t* list_fail, const uint32_t* seg_hist, uint32_t seg_n,
+                               uint32_t seg_len, uint32_t seg_h, const uint16_t* dense, uint32_t dense_np) {
     if (B == 0) return hipSuccess;
     if (K2 == 0 || K2 > 64u || (block2 && !reff)) return hipErrorInvalidValue;
+    if (seg_hist && (!dense || seg_n == 0 || seg_len == 0 || seg_len % 8u || seg_h == 0)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_deep_certify, dim3(B), dim3(kCertThreads), 0, s, frow, fsc, fn, K2, tcut, codes, cap, W4,
                        qcodes, k, R, ids, out_ids, out_scores, out_n, fail, kcnt, block2, reff, m_rows,
-                       m_dist, mlen, list_fail);
+                       m_dist, mlen, list_fail, seg_hist, seg_n, seg_len, seg_h, dense, dense_np);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// The deep sharded fallback's owned rows without member lists (round 5): one block per
+// query walks the dense row in order, 8 rows per thread per round; a row is owned iff
+// d < T, or d == T and fewer than `quota` tied rows precede it (tcut[q] = (T, -, quota,
+// mode) from k_shard_deep_own's rule form) -- the member-list compaction's set, in row
+// order.  Gated like the rerank it feeds.
+__global__ __launch_bounds__(kBigThreads) void k_dense_own(const uint16_t* __restrict__ dense, uint32_t np, uint32_t N,
+                                                           const uint32_t* __restrict__ tcut,
+                                                           const uint32_t* __restrict__ qpc,
+                                                           uint32_t* __restrict__ o_rows, uint32_t* __restrict__ o_dist,
+                                                           uint32_t ostride, const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    __shared__ uint32_t wsum[kBigThreads / 64];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    const uint32_t T = tcut[4u * q], quota = tcut[4u * q + 2u], mode = tcut[4u * q + 3u];
+    const float pc = (float)qpc[q];
+    // mode 2 with quota 0 and T = 0 marks "no owned row" (k_shard_deep_own: an empty rank / list)
+    const bool none = mode == 2u && quota == 0u && T == 0u;
+    const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);
+    uint32_t* orw = o_rows + (uint64_t)q * ostride;
+    uint32_t* odd = o_dist + (uint64_t)q * ostride;
+    const uint32_t nv = (N + 7u) / 8u;
+    uint32_t ties = 0u, o = 0u;  // tied rows seen, rows written (block-uniform)
+    for (uint32_t it = 0; it < nv && !none; it += kBigThreads) {
+        const uint32_t v = it + tid;
+        uint32_t dv[8];
+        uint32_t lt = 0u, tm = 0u;
+        if (v < nv) {
+            const uint4 w = dq[v];
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t d = 8u * v + (uint32_t)j < N ? dense_d((ws[j >> 1] >> (16 * (j & 1))) & 0xffffu, pc) : ~0u;
+                dv[j] = d;
+                lt |= (d < T ? 1u : 0u) << j;
+                tm |= (d == T ? 1u : 0u) << j;
+            }
+        }
+        uint32_t tt;
+        const uint32_t tex = ties + block_scan_u32((uint32_t)__popc(tm), wsum, &tt);
+        // this thread's tied rows ranked tex, tex + 1, ...: owned while the rank < quota
+        const uint32_t take = quota > tex ? min((uint32_t)__popc(tm), quota - tex) : 0u;
+        uint32_t keep = lt, tk = tm;
+        for (uint32_t c = 0; c < take; ++c) {
+            keep |= tk & (0u - tk);  // lowest remaining tied row
+            tk &= tk - 1u;
+        }
+        uint32_t tot;
+        uint32_t pos = o + block_scan_u32((uint32_t)__popc(keep), wsum, &tot);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if ((keep >> j) & 1u) {
+                orw[pos] = 8u * v + (uint32_t)j;
+                odd[pos] = dv[j];
+                ++pos;
+            }
+        }
+        ties += tt;
+        o += tot;
+    }
+}
+
+hipError_t launch_dense_own(const uint16_t* dense, uint32_t np, uint32_t N, const uint32_t* tcut, const uint32_t* qpc,
+                            uint32_t B, uint32_t* o_rows, uint32_t* o_dist, uint32_t ostride, const uint32_t* gate,
+                            hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (!dense || np % 8u || np < N) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_dense_own, dim3(B), dim3(kBigThreads), 0, s, dense, np, N, tcut, qpc, o_rows, o_dist, ostride,
+                       gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -153,7 +153,7 @@ struct Workspace {
     hipStream_t stream = nullptr;
     DBuf q, qnorm, qcodes, zero, thr, buf, s1_rows, s1_dist, scores, out_ids, out_scores, out_n, slow, sort_tmp, flags,
         rows, norms, codes, misc, fx_qb, fx_smp, fx_cand, fx_scores, fx_probe, flt_rows, flt_ids, flt_codes, s1_mx,
-        deep;
+        deep, seg;
     uint32_t* h_flags = nullptr;  // pinned [4]: any_fail / nan
     EvSet ev;                     // timing events (created on first timed call)
     // Searches return without a host sync: the workspace goes back to the pool
@@ -171,7 +171,7 @@ struct Workspace {
         if (done) (void)hipEventDestroy(done);
         for (DBuf* b : {&q, &qnorm, &qcodes, &zero, &thr, &buf, &s1_rows, &s1_dist, &scores, &out_ids, &out_scores,
                         &out_n, &slow, &sort_tmp, &flags, &rows, &norms, &codes, &misc, &fx_qb, &fx_smp, &fx_probe, &fx_cand,
-                        &fx_scores, &flt_rows, &flt_ids, &flt_codes, &s1_mx, &deep, &b1})
+                        &fx_scores, &flt_rows, &flt_ids, &flt_codes, &s1_mx, &deep, &seg, &b1})
             b->release();
         if (h_flags) (void)hipHostFree(h_flags);
         if (stream) (void)hipStreamDestroy(stream);
@@ -333,7 +333,7 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
             p += ng * 256u * 4u;
         }
         if (s1.sample_mode == kSampleDense) s1.smp = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
-        if (s1.dense_sel) s1.dense = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+        if (s1.dense_sel && !s1.dense_keep) s1.dense = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
     }
     HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
     if (s1.dense_sel) s1.bufcap = 1;  // no candidate buffer: every distance goes to the dense block
@@ -1456,6 +1456,12 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     s1.qcodes = ws.qcodes.as<uint4>();
     s1.ev = nullptr;
     s1.tcut = tcut;
+    {  // the rule in parallel over row segments (k_dense_seg_hist + k_dense_rule)
+        dense_segments(N, kDenseSegs, &s1.seg_n, &s1.seg_len);
+        const size_t gq = std::min<uint32_t>(B, 256u);  // one 256-query group at a time
+        HIP_TRY(ws.seg.ensure(gq * s1.seg_n * (dim + 1u) * 4 * ((B + 255u) / 256u)), "alloc segment histograms");
+        s1.seg_hist = ws.seg.as<uint32_t>();
+    }
     // the flat pass runs on a second workspace's stream, concurrently with stage 1 (they share
     // nothing until the certify pass): ordered after the caller's queries, joined before certify
     struct Ev {
@@ -2475,9 +2481,13 @@ gvdb_status gvdb::shard_stage1_members(const gvdb_index* ix, const float* d_q, u
     UseGuard ug{ix, s};
     const uint32_t W4 = code_w4(dim);
     HIP_TRY(ws.qcodes.ensure(B * W4 * 16), "alloc qcodes");
+    ShardDenseLayout lay;
+    const ShardDenseLayout* dl = shard_dense_layout(ix, B, R, dim, m_rows, &lay) ? &lay : nullptr;
     Stage1Args s1{};
+    s1.dense_keep = dl ? 1 : 0;  // (before the plan: no workspace dense block)
     st = prepare_stage1(ws, s1, (uint32_t)B, dim, Rl, (uint32_t)ix->n, s, true, false);
     if (st != GVDB_OK) return st;
+    if (dl && !s1.dense_sel) return fail(GVDB_ERR_DEVICE, "deep sharded stage 1: dense layout without a dense scan");
     if (s1.mfma_scan) {
         s1.qf32 = d_q;  // packed by k_qprep
         s1.qthr = ix->thr;
@@ -2493,11 +2503,58 @@ gvdb_status gvdb::shard_stage1_members(const gvdb_index* ix, const float* d_q, u
         s1.mhist = block1;
         s1.mcount = block1 + (uint64_t)B * (dim + 1u);
     }
+    if (dl) {  // the dense block, the rule, |q| and the segment histograms stay in the scratch
+        s1.dense = dl->dense;
+        s1.dense_keep = 1;
+        s1.tcut = dl->rule;
+        s1.pc_out = dl->qpc;
+        s1.seg_hist = dl->seg;
+        s1.seg_n = dl->S;
+        s1.seg_len = dl->L;
+        s1.s1_rows = nullptr;
+        s1.s1_dist = nullptr;
+    }
     HIP_TRY(launch_stage1_fast(s1, s), "deep sharded stage 1");
     if (!s1.dense_sel)
         HIP_TRY(launch_shard_member_hist(m_dist, (uint32_t)B, Rl, dim + 1u, block1, s),
                 "deep sharded stage 1 histogram");
     return GVDB_OK;
+}
+
+// stage1_plan's dense_sel decision for (D, R, N) under the current GVDB_SCAN / GVDB_DENSE_SEL
+static bool plan_dense_sel(uint32_t D, uint32_t R, uint32_t N) {
+    const char* scan = getenv("GVDB_SCAN");
+    if (scan && strcmp(scan, "valu") == 0) return false;
+    const char* ds = getenv("GVDB_DENSE_SEL");
+    if (ds && strcmp(ds, "0") == 0) return false;
+    return R > kSelectLdsCap && mfma_scan_supported(code_w4(D)) && (uint64_t)R * 64u >= N;
+}
+
+bool gvdb::shard_dense_layout(const gvdb_index* ix, uint64_t B, uint64_t R, uint32_t dim, void* scratch,
+                              ShardDenseLayout* dl) {
+    const char* env = getenv("GVDB_DEEP_DENSE");  // =0: the member-list form (A/B, tests)
+    if (env && env[0] == '0') return false;
+    if (!ix || !scratch || !dl || ix->n == 0 || ix->n > 0xFFFFFFFFull || B == 0 || dim != ix->dim || dim == 0 ||
+        dim >= 4096 || R > kBigRMax)
+        return false;
+    const uint32_t n = (uint32_t)ix->n, Rl = (uint32_t)std::min<uint64_t>(R, n);
+    if (!plan_dense_sel(dim, Rl, n)) return false;
+    const uint64_t np = ((uint64_t)n + 31u) & ~31ull, H = dim + 1ull;
+    if (2 * np > 8 * R || R < 12 + H) return false;  // the row within m_rows | m_dist; one segment at least
+    uint32_t S = 0, L = 0;
+    dense_segments(n, (uint32_t)std::min<uint64_t>(kDenseSegs, (R - 12) / H), &S, &L);
+    if ((uint64_t)S * H + 12 > R) return false;
+    uint32_t* base = (uint32_t*)scratch;
+    uint32_t* m_cos = base + 4 * B * R;
+    dl->S = S;
+    dl->L = L;
+    dl->np = (uint32_t)np;
+    dl->n = n;
+    dl->dense = (uint16_t*)base;
+    dl->rule = m_cos + 4 * B;
+    dl->qpc = m_cos + 8 * B;
+    dl->seg = m_cos + 12 * B;
+    return true;
 }
 
 // The certified deep phase 2 (gvdb_shard.hip, R > 8192): this rank's exact cosine
@@ -2590,7 +2647,7 @@ gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q,
                                          const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
                                          const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl,
                                          uint32_t* block2, uint32_t* dfail, void* early_list, hipStream_t s,
-                                         bool* enqueued) {
+                                         bool* enqueued, const ShardDenseLayout* dl) {
     *enqueued = false;
     if (!shard_certified_eligible(ix, dim, k) || B == 0 || B > 0xFFFFFFFFull) return GVDB_OK;
     gvdb_status st = set_device(ix->device);
@@ -2650,7 +2707,8 @@ gvdb_status gvdb::shard_certified_phase2(const gvdb_index* ix, const float* d_q,
     HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
     HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), (uint32_t)B,
                                 (uint32_t)k, 0u, ix->ids, nullptr, nullptr, nullptr, dfail, s, own_cnt, block2, reff,
-                                m_rows, m_dist, Rl, flat_fail),
+                                dl ? nullptr : m_rows, dl ? nullptr : m_dist, Rl, flat_fail, dl ? dl->seg : nullptr,
+                                dl ? dl->S : 0u, dl ? dl->L : 0u, dim + 1u, dl ? dl->dense : nullptr, dl ? dl->np : 0u),
             "certified deep phase 2");
     if ((st = tier_record(ix, dfail, kTierDeepCert, s)) != GVDB_OK) return st;
     *enqueued = true;

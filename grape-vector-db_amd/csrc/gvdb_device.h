@@ -111,4 +111,27 @@ __device__ __forceinline__ uint32_t big_prefix(bool f, uint32_t* wcnt, uint32_t*
     return pre;
 }
 
+// Block-wide exclusive prefix of a per-thread count in thread order; *total = the block sum.
+// wsum: [blockDim.x / 64] LDS words.
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+        if ((int)lane >= off) incl += y;
+    }
+    if (lane == 63u) wsum[w] = incl;
+    __syncthreads();
+    uint32_t pre = incl - v, tot = 0;
+    for (uint32_t i = 0; i < nw; ++i) {
+        const uint32_t c = wsum[i];
+        if (i < w) pre += c;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre;
+}
+
 }  // namespace gvdb

@@ -106,7 +106,22 @@ struct Stage1Args {
     uint32_t* mhist;         // optional, dense_sel: [B][H = D+1] the members' Hamming histogram (deep sharded
     uint32_t* mcount;        //   exchange-1 block) and [B] their count, written by k_select_dense
     const uint32_t* gate;    // optional tier gate (dense_sel + FP4 scan only): the stage runs iff *gate != 0
+    uint32_t* seg_hist;      // optional, dense_sel + tcut: [B][seg_n][D+1] per-segment Hamming histograms (the
+    uint32_t seg_n;          //   parallel rule form: k_dense_seg_hist + k_dense_rule); seg_n segments of
+    uint32_t seg_len;        //   seg_len rows (dense_segments)
+    int dense_keep;          // dense_sel: `dense` holds every query's row ([B][dense_np], caller memory) instead
+                             // of one 256-query group's
+    uint32_t* pc_out;        // optional, the parallel rule form: |q| per query [B] (kept for a later call)
 };
+constexpr uint32_t kDenseSegs = 64;  // row segments of the parallel dense rule
+// S segments of L rows (L % 256 == 0) covering N rows, S <= min(smax, kDenseSegs)
+void dense_segments(uint32_t N, uint32_t smax, uint32_t* S, uint32_t* L);
+// the deep sharded fallback without member lists: this rank's owned rows under tcut's rule (T, -, quota)
+// -- every row with d < T, then the first `quota` rows with d == T in row order -- compacted in row
+// order from the dense block into o_rows / o_dist [B][ostride]
+hipError_t launch_dense_own(const uint16_t* dense, uint32_t np, uint32_t N, const uint32_t* tcut, const uint32_t* qpc,
+                            uint32_t B, uint32_t* o_rows, uint32_t* o_dist, uint32_t ostride, const uint32_t* gate,
+                            hipStream_t s);
 // ---- large rescore depth (gvdb_bigr.hip): R up to 2^20, D < 4096, k <= 1024 --------
 constexpr uint32_t kBigRMax = 1u << 20;
 hipError_t launch_select_big(const Stage1Args& a, hipStream_t s);
@@ -125,8 +140,11 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                const uint32_t* kcnt = nullptr, uint32_t* block2 = nullptr,
                                const uint32_t* reff = nullptr, const uint32_t* m_rows = nullptr,
                                const uint32_t* m_dist = nullptr, uint32_t mlen = 0,
-                               const uint32_t* list_fail = nullptr);  // != 0: the list is not certified
-                                                                      // (every query fails)
+                               const uint32_t* list_fail = nullptr,  // != 0: the list is not certified
+                                                                     // (every query fails)
+                               const uint32_t* seg_hist = nullptr, uint32_t seg_n = 0, uint32_t seg_len = 0,
+                               uint32_t seg_h = 0, const uint16_t* dense = nullptr, uint32_t dense_np = 0);  // mode 3 from the
+                                                                     // dense block instead of m_rows / m_dist
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
 enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
@@ -409,10 +427,29 @@ hipError_t launch_shard_deep_own(const uint32_t* gathered1, uint64_t words1, uin
 // (a device word that outlives the call) becomes non-zero when the batch is not certified: it gates the
 // caller's rerank of the owned lists on the device.  *enqueued = false: not eligible, nothing enqueued
 bool shard_certified_eligible(const gvdb_index* ix, uint32_t dim, uint64_t k);
+// (dl: the dense-block form below -- the tied rows are counted from its segment histograms, not the lists)
+struct ShardDenseLayout;
 gvdb_status shard_certified_phase2(const gvdb_index* ix, const float* d_q, uint64_t B, uint32_t dim, uint64_t k,
                                    const uint32_t* tcut, const uint32_t* own_cnt, const uint32_t* reff,
                                    const uint32_t* m_rows, const uint32_t* m_dist, uint32_t Rl, uint32_t* block2,
-                                   uint32_t* dfail, void* early_list, hipStream_t s, bool* enqueued);
+                                   uint32_t* dfail, void* early_list, hipStream_t s, bool* enqueued,
+                                   const ShardDenseLayout* dl = nullptr);
+// The deep form without member lists (round 5): when the shard's stage 1 is the dense FP4
+// scan and its dense block fits the scratch's member-list regions, stage 1 keeps the block
+// there ([B][np] f16 dots over m_rows | m_dist) and writes, in the m_cos region (words from
+// m_cos): [4B, 8B) its own rule, [8B, 9B) |q|, [12B, ...) the segment histograms [B][S][dim+1]
+// -- the exchange-1 histograms come from the same pass.  Phase 2 certifies from them and its
+// fallback compacts the owned rows from the block (k_dense_own).  Both calls derive the
+// layout from (shard, B, R, dim) alone.
+struct ShardDenseLayout {
+    uint32_t S = 0, L = 0, np = 0, n = 0;
+    uint16_t* dense = nullptr;
+    uint32_t* rule = nullptr;
+    uint32_t* qpc = nullptr;
+    uint32_t* seg = nullptr;
+};
+bool shard_dense_layout(const gvdb_index* ix, uint64_t B, uint64_t R, uint32_t dim, void* scratch,
+                        ShardDenseLayout* dl);
 // the certified phase 2's exact cosine list, enqueued EARLY by the stage-1 call on a second
 // stream (concurrent with stage 1 and the exchange) into `list` (shard_early_list_bytes(B) bytes
 // of the caller's scratch); phase 2 joins it by the list's address.  Not eligible: nothing.

@@ -1547,8 +1547,9 @@ static hipError_t launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
             auto kern = qt == 1 ? k_scan_mx7<W4, true, 1> : qt == 2 ? k_scan_mx7<W4, true, 2>
                       : qt == 4 ? k_scan_mx7<W4, true, 4> : k_scan_mx7<W4, true, 8>;
             // few tiles: little MFMA work per code load, two blocks per CU keep more loads in flight
+            uint16_t* dn = a.dense + (a.dense_keep ? (uint64_t)g * a.dense_np : 0ull);
             hipLaunchKernelGGL(kern, dim3(cu_count() * (qt <= 2u ? 2u : 1u)), dim3(kMx7Threads), 0, s, a.codes, a.cap,
-                               a.N, qf, a.qpc + g, a.thr + g, bg, a.counts + g, a.buf, a.bufcap, a.dense, a.dense_np,
+                               a.N, qf, a.qpc + g, a.thr + g, bg, a.counts + g, a.buf, a.bufcap, dn, a.dense_np,
                                a.gate);
             GVDB_LAUNCH_CHECK();
             const hipError_t e = launch_select_dense(a, g, bg, s);
@@ -2457,7 +2458,7 @@ size_t stage1_plan(Stage1Args& a) {
         bytes += ng * (8u * 2u * W4 * 64u * 16u + 256u * 4u);
     }
     if (a.sample_mode == kSampleDense) bytes += (size_t)a.B * (S / 16u) * 2u + 256u;
-    if (a.dense_sel) bytes += (size_t)std::min<uint32_t>(a.B, 256u) * a.dense_np * 2u + 256u;
+    if (a.dense_sel && !a.dense_keep) bytes += (size_t)std::min<uint32_t>(a.B, 256u) * a.dense_np * 2u + 256u;
     return bytes;
 }
 

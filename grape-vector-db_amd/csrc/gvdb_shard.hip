@@ -830,6 +830,49 @@ gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_que
         const uint32_t Rl = usable ? (uint32_t)std::min<uint64_t>(R, si.n) : 0u;
         const bool try_cert = usable && Rl > 0 && B * 4 <= BR && shard_certified_eligible(shard, dim, k);
         hipError_t e = hipSuccess;
+        ShardDenseLayout lay;
+        if (usable && Rl > 0 && shard_dense_layout(shard, B, R, dim, d_scratch, &lay)) {
+            // stage 1 kept the dense block: the rule (T, quota) from the exchange, then the certified
+            // form, then -- gated by its failure word -- the owned rows compacted from the block
+            uint32_t* dfail = reff + B;
+            const uint32_t* gate = nullptr;
+            e = launch_shard_deep_own(d_gathered1, shard_words1_deep(B, dim), (uint32_t)G, (uint32_t)rank,
+                                      (uint32_t)B, (uint32_t)R, Rl, dim + 1u, m_rows, m_dist, o_rows, o_dist, own_cnt,
+                                      reff, s, tcut);
+            if (e == hipSuccess && try_cert) {
+                bool enqueued = false;
+                const gvdb_status st = shard_certified_phase2(shard, d_queries, B, dim, k, tcut, own_cnt, reff,
+                                                              nullptr, nullptr, Rl, d_block2, dfail, o_rows, s,
+                                                              &enqueued, &lay);
+                if (st != GVDB_OK) return st;
+                if (enqueued) gate = dfail;
+            }
+            if (e == hipSuccess)
+                e = launch_dense_own(lay.dense, lay.np, lay.n, tcut, lay.qpc, (uint32_t)B, o_rows, o_dist, Rl, gate, s);
+            if (e == hipSuccess) {
+                RerankArgs rr{};
+                rr.rows = si.rows;
+                rr.clen = dim;
+                rr.norms = si.norms;
+                rr.q = d_queries;
+                rr.qlen = dim;
+                rr.s1_rows = o_rows;
+                rr.B = (uint32_t)B;
+                rr.R = Rl;
+                rr.kind = kScoreCosine;
+                rr.scores = m_cos;
+                rr.counts = own_cnt;
+                rr.gate = gate;
+                e = launch_rerank(rr, s);
+            }
+            if (e == hipSuccess)
+                e = launch_shard_deep_topk(m_cos, o_rows, o_dist, own_cnt, reff, (uint32_t)B, Rl, (uint32_t)k, si.ids,
+                                           0u, d_block2, s, gate);
+            if (e != hipSuccess)
+                return report_status(GVDB_ERR_DEVICE, std::string("deep shard phase 2: ") + hipGetErrorString(e));
+            index_track_use(shard, s);
+            return GVDB_OK;
+        }
         // the certified form: the rank's exact cosine top-32 / 64 filtered by its owned-row rule; the
         // rerank of the owned lists below is then gated on the device by its failure word (scratch)
         uint32_t* dfail = reff + B;

@@ -225,18 +225,21 @@ def deep_cert_counts(g):
     return int(out[0]), int(out[1])
 
 
-@pytest.mark.parametrize("plant", [False, True])
-def test_deep_certified_phase2_equals_single_index_and_oracle(g, oracle_mod, plant):
+@pytest.mark.parametrize("plant,R", [(False, 16_000), (True, 16_000), (False, 24_000), (True, 24_000)])
+def test_deep_certified_phase2_equals_single_index_and_oracle(g, oracle_mod, plant, R):
     """The certified deep phase 2 (shards of >= 65536 rows, k <= 32): each rank's
     local top-k comes from its exact cosine top-32 filtered by the owned-row rule
     k_shard_deep_own writes, not from reranking its ~R / G owned rows.  Equal rows
     across the shard boundary make cross-shard cosine ties.  plant: 70 rows of
     cosine ~0.85 but Hamming 400 (> T) in shard 1 for query 0 fill that rank's list,
     so rank 1 cannot certify and reranks its owned rows while rank 0 certifies;
-    the merged results are the same either way."""
+    the merged results are the same either way.  R = 16000: the member-list form
+    (a 90K-row shard's dense block exceeds the scratch's list regions); R = 24000:
+    stage 1 keeps the dense block and its segment histograms in the scratch, ties at
+    T are counted from them and the fallback compacts from the block (k_dense_own)."""
     import torch
 
-    sizes, D, B, R, k = (70_000, 90_000), 768, 48, 16_000, 10
+    sizes, D, B, k = (70_000, 90_000), 768, 48, 10
     N = sum(sizes)
     x = rows(733, N, D, dup=100)
     x[sizes[0]] = x[5]
