@@ -3109,6 +3109,59 @@ __global__ __launch_bounds__(kRsThreads) void k_rerank_small(const float* __rest
     if (tid < nr) scores[(uint64_t)qi * R + r0 + tid] = sc;
 }
 
+// k_rerank_small over device-side counts (round 5): a fixed grid of blocks walks the
+// (query, 16-candidate) items of the prefix of min(counts, R) / 16 -- every row load
+// of an item in flight at once, instead of k_rerank2's 64-row wave items whose 24
+// chunk gathers are serial (at ~900 candidates per query the items are fewer than
+// the waves and the kernel is one item's latency: 130 us for 58K rows).
+__global__ __launch_bounds__(kRsThreads) void k_rerank_small_items(
+    const float* __restrict__ rows, uint64_t clen, const float* __restrict__ norms, const float* __restrict__ q,
+    uint64_t qlen, const uint32_t* __restrict__ s1_rows, uint32_t B, uint32_t R, const uint32_t* __restrict__ counts,
+    int kind, float* __restrict__ scores, const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    __shared__ float4 tile4[kRsRows * (kRsMaxLen / 4 + 1)];
+    __shared__ float4 qs4[kRsMaxLen / 4];
+    __shared__ uint32_t rowid[kRsRows];
+    __shared__ uint32_t pre[kRrMaxB + 1];  // items before query i
+    __shared__ uint32_t part[kRsThreads];
+    const uint32_t tid = threadIdx.x;
+    {
+        const uint32_t per = (B + kRsThreads - 1) / kRsThreads, b0 = tid * per;
+        uint32_t loc = 0;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) loc += (min(counts[b0 + i], R) + kRsRows - 1) / kRsRows;
+        part[tid] = loc;
+        __syncthreads();
+        for (uint32_t o = 1; o < kRsThreads; o <<= 1) {
+            const uint32_t v = tid >= o ? part[tid - o] : 0u;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        uint32_t run = part[tid] - loc;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) {
+            pre[b0 + i] = run;
+            run += (min(counts[b0 + i], R) + kRsRows - 1) / kRsRows;
+        }
+        if (tid == kRsThreads - 1) pre[B] = part[tid];
+        __syncthreads();
+    }
+    const uint32_t items = pre[B];
+    for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {  // block-uniform
+        uint32_t lo = 0, hi = B;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= item) lo = mid; else hi = mid;
+        }
+        const uint32_t qi = lo, r0 = (item - pre[qi]) * kRsRows;
+        const uint32_t Rq = min(counts[qi], R), nr = min((uint32_t)kRsRows, Rq - r0);
+        if (tid < kRsRows) rowid[tid] = tid < nr ? s1_rows[(uint64_t)qi * R + r0 + tid] : 0u;
+        __syncthreads();
+        const float sc = rerank16(rows, clen, norms, q + (uint64_t)qi * qlen, qlen, kind, rowid, nr, tile4, qs4);
+        if (tid < nr) scores[(uint64_t)qi * R + r0 + tid] = sc;
+        __syncthreads();  // rowid / the tiles are rewritten by the next item
+    }
+}
+
 // GVDB_RERANK=v1: always the block-synchronous k_rerank (A/B)
 static bool rerank_v2() {
     static const bool v = [] {
@@ -3138,6 +3191,25 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_rerank_small, dim3((uint32_t)small_slots), dim3(kRsThreads), 0, s, a.rows, a.clen,
                            a.norms, a.q, a.qlen, a.s1_rows, a.B, a.R, a.counts, a.kind, a.scores, a.gate);
         GVDB_LAUNCH_CHECK();
+        return hipSuccess;
+    }
+    // device-counted lists (D <= 1024): the item-walking k_rerank_small (flat candidates at the 8-GPU
+    // shard, k 32, batch 64: 132 -> 84 us; neutral at 10M, batch 256); GVDB_RERANK=v2 / v1: the
+    // 64-row wave items / the block-synchronous form (A/B)
+    static const bool counted = [] {
+        const char* e = getenv("GVDB_RERANK");
+        return !(e && (strcmp(e, "v2") == 0 || strcmp(e, "v1") == 0));
+    }();
+    if (a.counts && std::min(a.qlen, a.clen) <= kRsMaxLen && counted) {
+        for (uint32_t b0 = 0; b0 < a.B; b0 += kRrMaxB) {
+            const uint32_t nb = std::min<uint32_t>(kRrMaxB, a.B - b0);
+            const uint64_t slots = (uint64_t)nb * ((a.R + kRsRows - 1) / kRsRows);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, 2ull * cus);
+            hipLaunchKernelGGL(k_rerank_small_items, dim3(grid), dim3(kRsThreads), 0, s, a.rows, a.clen, a.norms,
+                               a.q + (uint64_t)b0 * a.qlen, a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
+                               a.counts + b0, a.kind, a.scores + (uint64_t)b0 * a.R, a.gate);
+            GVDB_LAUNCH_CHECK();
+        }
         return hipSuccess;
     }
     for (uint32_t b0 = 0; b0 < a.B; b0 += kRrMaxB) {

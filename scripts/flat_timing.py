@@ -13,6 +13,7 @@ import gvdb  # noqa: E402
 
 N = int(os.environ.get("N", 10_000_000))
 D = int(os.environ.get("D", 768))
+K = int(os.environ.get("K", 10))
 dev = torch.device("cuda", 0)
 ix = gvdb.GpuVectorIndex(dimension=D, capacity_hint=N)
 g = torch.Generator(device=dev).manual_seed(7)
@@ -24,23 +25,23 @@ L = gvdb.lib()
 p = gvdb.SearchParams(mode=1, metric=0)
 for B in [int(b) for b in os.environ.get("BS", "256,64,1").split(",")]:
     q = torch.randn((B, D), generator=g, device=dev)
-    oi = torch.zeros((B, 10), dtype=torch.int64, device=dev)
-    osc = torch.zeros((B, 10), device=dev)
+    oi = torch.zeros((B, K), dtype=torch.int64, device=dev)
+    osc = torch.zeros((B, K), device=dev)
     for _ in range(2):
-        ix.search_device(q, 10, oi, osc, None, p)
+        ix.search_device(q, K, oi, osc, None, p)
     torch.cuda.synchronize()
     f0 = L.gvdb_flat_fallback_count()
     f8 = L.gvdb_flat_i8_fallback_count()
     reps = int(os.environ.get("FLAT_REPS", 10 if B > 1 else 20))
     t = time.perf_counter()
     for _ in range(reps):
-        ix.search_device(q, 10, oi, osc, None, p)
+        ix.search_device(q, K, oi, osc, None, p)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) * 1e3 / reps
     L.gvdb_timing_reset()
     L.gvdb_timing_enable(1)
     for _ in range(3):
-        ix.search_device(q, 10, oi, osc, None, p)
+        ix.search_device(q, K, oi, osc, None, p)
     L.gvdb_timing_enable(0)
     import ctypes as C
     em, en, tm, tn = C.c_double(), C.c_uint64(), C.c_double(), C.c_uint64()

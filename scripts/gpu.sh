@@ -165,6 +165,45 @@ for t in "${TASKS[@]}"; do
                 GVDB_FLAT=i8 GVDB_LIB_PATH=$lib BS=${FBS:-256} FLAT_REPS=10 run 600 gpurun_out/flatvar_$v.log python3 scripts/flat_timing.py
                 echo "== $v"; grep -E "B=|emit" gpurun_out/flatvar_$v.log | tail -2
             done ;;
+        flatshard)  # the flat pass at the 8-GPU shard (1.25M x 768), batch 64, k = 10 and 32, kernel trace
+            for kk in 10 32; do
+                N=1250000 K=$kk GVDB_FLAT=i8 BS=64 FLAT_REPS=10 run 600 gpurun_out/flatshard_$kk.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flatshard_$kk -o run -- python3 scripts/flat_timing.py
+                echo "== k $kk"; grep -E "B=|emit" gpurun_out/flatshard_$kk.log | tail -2
+                python3 scripts/trace_summary.py gpurun_out/prof_flatshard_$kk/run_kernel_trace.csv | head -14
+            done ;;
+        flatshardab)  # the flat pass at the 8-GPU shard, batch 64, k = 32: sample stride and prune variants
+            for v in e64 e16 e4 noprune; do
+                case $v in
+                    e64) ENVV="GVDB_FLAT_EVERY=64" ;;
+                    e16) ENVV="GVDB_FLAT_EVERY=16" ;;
+                    e4) ENVV="GVDB_FLAT_EVERY=4" ;;
+                    noprune) ENVV="GVDB_FLAT_PRUNE=0" ;;
+                esac
+                env $ENVV N=1250000 K=32 GVDB_FLAT=i8 BS=64 FLAT_REPS=10 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fsab_$v -o run -- python3 scripts/flat_timing.py > gpurun_out/fsab_$v.log 2>&1 || { echo "FAILED $v"; exit 1; }
+                echo "== $v"; grep -E "B=|emit" gpurun_out/fsab_$v.log | tail -2
+                python3 scripts/trace_summary.py gpurun_out/prof_fsab_$v/run_kernel_trace.csv | head -12
+            done ;;
+        flatstats)  # candidate counts of the flat pass (variant build abl/libgvdb_fstats.so), 1.25M and 10M rows
+            for nn in 1250000 10000000; do
+                GVDB_LIB_PATH=$PWD/grape-vector-db_amd/abl/libgvdb_fstats.so N=$nn K=32 GVDB_FLAT=i8 BS=64 FLAT_REPS=2 run 600 gpurun_out/fstats_$nn.log python3 scripts/flat_timing.py
+                grep flatstats gpurun_out/fstats_$nn.log | tail -2
+            done ;;
+        flatrr)  # flat pass rerank variants (GVDB_RERANK = default | items) at the shard (k 32, B 64) and 10M (k 10, B 256)
+            for v in def items; do
+                ENVV="GVDB_RERANK=$v"
+                env $ENVV N=1250000 K=32 GVDB_FLAT=i8 BS=64 FLAT_REPS=10 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_frr_$v -o run -- python3 scripts/flat_timing.py > gpurun_out/frr_$v.log 2>&1 || { echo "FAILED $v"; exit 1; }
+                echo "== shard $v"; grep -E "B=|emit" gpurun_out/frr_$v.log | tail -2
+                python3 scripts/trace_summary.py gpurun_out/prof_frr_$v/run_kernel_trace.csv | grep -E "rerank|i8q"
+                env $ENVV N=10000000 K=10 GVDB_FLAT=i8 BS=256 FLAT_REPS=10 timeout -k 10 600 python3 scripts/flat_timing.py > gpurun_out/frr10_$v.log 2>&1 || { echo "FAILED 10M $v"; exit 1; }
+                echo "== 10M $v"; grep -E "B=|emit" gpurun_out/frr10_$v.log | tail -2
+            done ;;
+        flatevery2)  # flat sample stride A/B at the shard (k 32, B 64) and 10M (k 10, B 256)
+            for v in 64 32 16; do
+                GVDB_FLAT_EVERY=$v N=1250000 K=32 GVDB_FLAT=i8 BS=64 FLAT_REPS=10 run 600 gpurun_out/fe2s_$v.log python3 scripts/flat_timing.py
+                echo "== shard every $v"; grep -E "B=|emit" gpurun_out/fe2s_$v.log | tail -2
+                GVDB_FLAT_EVERY=$v N=10000000 K=10 GVDB_FLAT=i8 BS=256 FLAT_REPS=10 run 600 gpurun_out/fe2l_$v.log python3 scripts/flat_timing.py
+                echo "== 10M every $v"; grep -E "B=|emit" gpurun_out/fe2l_$v.log | tail -2
+            done ;;
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
             BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
             grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;
