@@ -320,7 +320,8 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
     const size_t extra = stage1_plan(s1);
     const size_t nb = (size_t)D + 1u;
     // the dense sample needs no histogram: only flags | counts | fail are zeroed
-    const size_t words = 4 + 2 * (size_t)B + (s1.sample_mode == kSampleDense ? 0 : (size_t)B * nb);
+    const size_t words =
+        4 + 2 * (size_t)B + (s1.sample_mode == kSampleDense || s1.sample_mode == kSampleWide ? 0 : (size_t)B * nb);
     HIP_TRY(ws.zero.ensure(words * 4 + 16), "alloc stage-1 state");
     if (extra) {
         HIP_TRY(ws.s1_mx.ensure(extra), "alloc stage-1 MFMA operands");
@@ -332,7 +333,8 @@ gvdb_status prepare_stage1(Workspace& ws, Stage1Args& s1, uint32_t B, uint32_t D
             s1.qpc = (uint32_t*)p;
             p += ng * 256u * 4u;
         }
-        if (s1.sample_mode == kSampleDense) s1.smp = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+        if (s1.sample_mode == kSampleDense || s1.sample_mode == kSampleWide)
+            s1.smp = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
         if (s1.dense_sel && !s1.dense_keep) s1.dense = (uint16_t*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
     }
     HIP_TRY(ws.thr.ensure((size_t)B * 4), "alloc thr");
@@ -1272,10 +1274,11 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
     HIP_TRY(ws.qnorm.ensure(kFxQ * 4), "alloc qnorm");
     HIP_TRY(ws.fx_qb.ensure((size_t)KC * kFxQ * 128 + kFxQ * 12), "alloc converted queries");
     HIP_TRY(ws.fx_smp.ensure((size_t)kFxQ * S * 4), "alloc sample scores");
-    HIP_TRY(ws.fx_probe.ensure((size_t)kFxQ * 33 * 4), "alloc probes");
+    HIP_TRY(ws.fx_probe.ensure((size_t)kFxQ * 34 * 4 + (size_t)kFxQ * kFxProbeParts * 16 * 8), "alloc probes");
     uint32_t* probes = ws.fx_probe.as<uint32_t>();
     float* pscores = (float*)(probes + kFxQ * 16);
     uint32_t* pcount = probes + kFxQ * 32;
+    uint64_t* ppart = (uint64_t*)(probes + kFxQ * 34);  // partial top-16 lists of the probe selection
     HIP_TRY(ws.fx_cand.ensure((size_t)kFxQ * cc * 8), "alloc candidates");  // rows, then their approx scores
     HIP_TRY(ws.fx_scores.ensure((size_t)kFxQ * cc * 4), "alloc candidate scores");
     HIP_TRY(ws.thr.ensure(kFxQ * 4), "alloc thresholds");
@@ -1336,7 +1339,8 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         HIP_TRY(launch_flat_mx_sample(a, s), "flat sample pass");
         DBG_SYNC(s, "dbg: flat sample pass");
         // tau from exactly re-scored probes (the 16 best sampled rows per query)
-        HIP_TRY(launch_flat_probes(a.smp, Bg, S, every, N, ix->ids, probes, pcount, s), "flat probes");
+        HIP_TRY(launch_flat_probes(a.smp, Bg, S, every, N, ix->n != ix->id_row.size() ? ix->ids : nullptr, probes,
+                                   pcount, ppart, s), "flat probes");
         {
             RerankArgs pr{};
             pr.rows = ix->rows;

@@ -623,11 +623,15 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
 // Orphan rows (an id re-added elsewhere, ids[row] == kOrphan) are never probes:
 // tau must be reached by mk LIVE rows, or the certificate would fail whenever
 // a shadowed row of a query's own neighbourhood falls into the sample.
+// gridDim.y > 1 (A/B, GVDB_PROBE_PARTS): a query's sample split over P blocks, each
+// writing its top-16 keys to `part` [B][P][16]; k_flat_probes_merge picks the query's 16.
 __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ smp, uint32_t S, uint32_t every,
                                                       uint32_t N, const uint64_t* __restrict__ ids,
-                                                      uint32_t* __restrict__ probes, uint32_t* __restrict__ pcount) {
+                                                      uint32_t* __restrict__ probes, uint32_t* __restrict__ pcount,
+                                                      uint64_t* __restrict__ part, uint32_t chunk) {
     __shared__ uint64_t keys[256];
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t P = gridDim.y, s0 = blockIdx.y * chunk, s1 = min(S, s0 + chunk);
     // wave-cooperative top-16: lanes 0..15 hold the wave's best keys, descending
     // ((order(score) << 32) | sample position; 0 = empty); a batch of 64 values
     // costs one compare + ballot unless a lane beats the current 16th key
@@ -640,12 +644,12 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const uint32_t i = i0 + u * 1024u + lane;
-            v[u] = i < S ? src[i] : -__builtin_inff();
+            v[u] = i < s1 ? src[i] : -__builtin_inff();
         }
     };
     float vc[kU], vn[kU];
-    load(wv * 64u, vn);
-    for (uint32_t i0 = wv * 64u; i0 < S; i0 += 1024u * kU) {
+    load(s0 + wv * 64u, vn);
+    for (uint32_t i0 = s0 + wv * 64u; i0 < s1; i0 += 1024u * kU) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) vc[u] = vn[u];
         load(i0 + 1024u * kU, vn);
@@ -676,10 +680,34 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
     if (lane < 16) keys[wv * 16 + lane] = ~mine;  // ascending sort of ~key = descending key
     __syncthreads();
     bitonic_sort_lds(keys, 256);  // merge the 16 wave lists
+    if (P > 1) {
+        if (tid < 16) part[((uint64_t)q * P + blockIdx.y) * 16u + tid] = ~keys[tid];
+        return;
+    }
     if (tid < 16) {
         const uint64_t key = ~keys[tid];
         const uint32_t sp = (uint32_t)key;
         const uint32_t row = ((sp >> 8) * every << 8) | (sp & 255u);  // sample position -> row
+        const bool ok = key != 0 && row < N;
+        probes[q * 16u + tid] = ok ? row : 0u;
+        const uint32_t valid = (uint32_t)__ballot(ok) & 0xffffu;
+        if (tid == 0) pcount[q] = __popc(valid);
+    }
+}
+
+// the query's 16 best of its P partial top-16 lists (k_flat_probes with P > 1)
+__global__ __launch_bounds__(256) void k_flat_probes_merge(const uint64_t* __restrict__ part, uint32_t P, uint32_t every,
+                                                           uint32_t N, uint32_t* __restrict__ probes,
+                                                           uint32_t* __restrict__ pcount) {
+    __shared__ uint64_t keys[256];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    keys[tid] = tid < P * 16u ? ~part[(uint64_t)q * P * 16u + tid] : ~0ull;
+    __syncthreads();
+    bitonic_sort_lds(keys, 256);
+    if (tid < 16) {
+        const uint64_t key = ~keys[tid];
+        const uint32_t sp = (uint32_t)key;
+        const uint32_t row = ((sp >> 8) * every << 8) | (sp & 255u);
         const bool ok = key != 0 && row < N;
         probes[q * 16u + tid] = ok ? row : 0u;
         const uint32_t valid = (uint32_t)__ballot(ok) & 0xffffu;
@@ -1248,10 +1276,24 @@ hipError_t launch_flat_prune(uint32_t* counts, uint32_t* cand, const float* csco
 }
 
 hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, const uint64_t* ids,
-                              uint32_t* probes, uint32_t* pcount, hipStream_t s) {
+                              uint32_t* probes, uint32_t* pcount, uint64_t* part, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_flat_probes, dim3(B), dim3(1024), 0, s, smp, S, every, N, ids, probes, pcount);
+    // GVDB_PROBE_PARTS: blocks per query (A/B).  Default 1: every block starts from an empty
+    // top-16 and its first insertions dominate (10M, batch 256: 86 / 169 / 336 us at 1 / 4 / 10
+    // blocks per query; the 1.25M shard with K2 = 32: 0.517 / 0.519 / 0.544 ms per batch)
+    static const uint32_t P_env = [] {
+        const char* e = getenv("GVDB_PROBE_PARTS");
+        return e ? (uint32_t)atoi(e) : 1u;
+    }();
+    uint32_t P = P_env;
+    P = part ? std::max<uint32_t>(1u, std::min<uint32_t>(kFxProbeParts, P)) : 1u;
+    const uint32_t chunk = (((S + P - 1u) / P) + 63u) & ~63u;
+    hipLaunchKernelGGL(k_flat_probes, dim3(B, P), dim3(1024), 0, s, smp, S, every, N, ids, probes, pcount, part, chunk);
     GVDB_LAUNCH_CHECK();
+    if (P > 1) {
+        hipLaunchKernelGGL(k_flat_probes_merge, dim3(B), dim3(256), 0, s, part, P, every, N, probes, pcount);
+        GVDB_LAUNCH_CHECK();
+    }
     return hipSuccess;
 }
 

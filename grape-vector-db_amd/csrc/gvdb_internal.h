@@ -146,7 +146,7 @@ hipError_t launch_deep_certify(const uint64_t* frow, const float* fsc, const uin
                                uint32_t seg_h = 0, const uint16_t* dense = nullptr, uint32_t dense_np = 0);  // mode 3 from the
                                                                      // dense block instead of m_rows / m_dist
 constexpr uint32_t kMfmaMinB = 96;  // batch size from which k_scan_mfma replaces k_scan
-enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2 };
+enum SampleMode : int { kSampleValu = 0, kSampleMxHist = 1, kSampleDense = 2, kSampleWide = 3 };
 // Decide sample_mode / mfma_scan for a prepared Stage1Args (use_mfma, B, D, N,
 // sample_chunks, target set) and return the workspace bytes of qfrag + qpc +
 // smp it needs (0 = none).
@@ -273,6 +273,7 @@ constexpr uint32_t kFxQ = 256;         // query slots per launch group
 constexpr uint32_t kFxCandCap = 8192;  // candidates per query (LDS sort capacity)
 constexpr uint32_t kFxMinN = 65536;    // smaller shards use the exact full scan
 constexpr uint32_t kFxSampleEvery = 64;  // sample pass: every 64th row tile
+constexpr uint32_t kFxProbeParts = 16;   // probe selection: blocks per query (partial top-16 lists)
 __host__ __device__ inline uint32_t fx_kc(uint32_t D) { return (D + 63u) / 64u; }        // bf16 chunks
 __host__ __device__ inline uint32_t fx_kc_i8(uint32_t D) { return (D + 127u) / 128u; }  // i8 chunks
 // Fragment-major flat mirror: per 256-row tile and 128-B chunk, 8 groups of
@@ -331,7 +332,7 @@ hipError_t launch_flat_prune(uint32_t* counts, uint32_t* cand, const float* csco
                              hipStream_t s);
 // probes[q][16] = rows of the 16 largest sampled MFMA scores, pcount[q] valid
 hipError_t launch_flat_probes(const float* smp, uint32_t B, uint32_t S, uint32_t every, uint32_t N, const uint64_t* ids,
-                              uint32_t* probes, uint32_t* pcount, hipStream_t s);
+                              uint32_t* probes, uint32_t* pcount, uint64_t* part, hipStream_t s);  // part: [B][16][16]
 // thr[q] = (mk-th largest exact probe score) - qd[q] (mk <= 16); +inf for q >= B.
 // distance: pscores hold 1 - cos (the index metric's rerank output).
 hipError_t launch_flat_tau(const float* pscores, const uint32_t* pcount, uint32_t B, uint32_t mk, int distance,

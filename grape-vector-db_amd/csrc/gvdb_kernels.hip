@@ -1742,6 +1742,109 @@ static void launch_scan_mx4_t(const Stage1Args& a, hipStream_t s) {
 
 
 
+// The stage-1 sample of WIDE codes on the FP4 matrix cores (round 5): the
+// VALU k_sample_hist re-read every 4096-row chunk once per query tile and spent
+// 2 x W4 x 4 xor/popcount per (row, query) -- 0.30 ms of the 0.93 ms per-rank
+// step of config 4 (10M x 3072, 8 shards of 1.25M rows, batch 256).  Here a block
+// holds QT query tiles' fragments (k_scan_mx4's operands and layout: A = queries
+// from LDS, B = the row's code words), a wave takes 32 sample positions at a time
+// (position p is row (p / 4096) * stride + p % 4096: plan_sampling's chunks), and
+// every Hamming distance d = (32 KW - dot) / 2 (exact) goes to dsm[q][p] as u16;
+// k_sample_thr then takes T[q] = the smallest t with #{d <= t} >= target from a
+// per-query histogram -- k_sample_hist + k_threshold's T, bit for bit (positions past
+// the shard's last row, in a shard of <= kExactN rows, are written as 0xffff: not counted).
+template <int W4, int QT>
+__global__ __launch_bounds__(kMx3Threads, 1) void k_sample_wide(const uint4* __restrict__ codes, uint64_t cap,
+                                                               uint32_t N, uint32_t S, uint32_t stride,
+                                                               const uint32_t* __restrict__ qwords, uint32_t B,
+                                                               uint16_t* __restrict__ dsm) {
+    constexpr int KW = 4 * W4;  // 32-bit code words per row
+    constexpr int KS = KW / 2;  // k-steps of 64 bits
+    __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, h = lane >> 5;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t q0 = blockIdx.y * 32u * QT;
+    for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx3Threads) {
+        const uint32_t l = i & 63u, st = i >> 6, qs = st % KS, qt = st / KS;
+        const uint32_t q = q0 + qt * 32u + (l & 31u);
+        qfrag[i] = fp4_x32(q < B ? qwords[(uint64_t)q * KW + 2u * qs + (l >> 5)] : 0u);
+    }
+    __syncthreads();
+    constexpr float kPadF = (float)(32 * KW);
+    const int scale1 = 0x7f7f7f7f;
+    const uint32_t nsub = (S + 31u) / 32u, W = gridDim.x * (kMx3Threads / 64);
+    for (uint32_t sb = blockIdx.x * (kMx3Threads / 64) + wv; sb < nsub; sb += W) {
+        const uint32_t p = sb * 32u + (lane & 31u), pc = min(p, S - 1u);
+        const uint32_t raw = (pc >> 12) * stride + (pc & 4095u), row = min(raw, N - 1u);
+        const bool live = raw < N;  // a shard of <= kExactN rows: its last chunk runs past N
+        uint4 c[W4];
+#pragma unroll
+        for (int w = 0; w < W4; ++w) c[w] = codes[(uint64_t)w * cap + row];
+        v16f_t acc[QT];
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+            const uint4 v = c[st >> 1];
+            const v4i_t b = fp4_x32((st & 1) ? (h ? v.w : v.z) : (h ? v.y : v.x));
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const v4i_t a = qfrag[(qt * KS + st) * 64 + lane];
+                if (st == 0)
+                    mfma_fp4_first_nop(acc[qt], a, b, scale1);
+                else
+                    mfma_fp4_acc_nop(acc[qt], a, b, scale1);
+            }
+        }
+        mfma_fp4_drain_acc(acc);
+        if (p < S) {
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t q = q0 + (uint32_t)qt * 32u + 4u * h + (uint32_t)(r & 3) + 8u * (uint32_t)(r >> 2);
+                    if (q < B)
+                        dsm[(uint64_t)q * S + p] = live ? (uint16_t)((uint32_t)(kPadF - acc[qt][r]) >> 1) : (uint16_t)0xffffu;
+                }
+        }
+    }
+}
+
+// T[q] from the query's S sampled distances (k_sample_wide): smallest t with
+// #{d <= t} >= target, D if never -- k_threshold's rule on the same counts
+__global__ __launch_bounds__(256) void k_sample_thr(const uint16_t* __restrict__ dsm, uint32_t S, uint32_t D,
+                                                    uint32_t target, uint32_t* __restrict__ thr) {
+    extern __shared__ uint32_t sh[];  // [D + 1]
+    const uint32_t q = blockIdx.x, tid = threadIdx.x;
+    for (uint32_t t = tid; t <= D; t += 256u) sh[t] = 0u;
+    __syncthreads();
+    const uint4* src = (const uint4*)(dsm + (uint64_t)q * S);  // S % 8 == 0 (4096-row chunks)
+    const uint32_t nv = S / 8u;
+    for (uint32_t v = tid; v < nv; v += 256u) {
+        const uint4 w = src[v];
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t d = (ws[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            if (d <= D) atomicAdd(&sh[d], 1u);  // 0xffff: a position past the shard's rows
+        }
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t t = wave_find_cum(sh, D + 1u, target);
+        if (tid == 0) thr[q] = t;
+    }
+}
+
+template <int W4, int QT>
+static void launch_sample_wide_t(const Stage1Args& a, hipStream_t s) {
+    const uint32_t S = a.sample_chunks * 4096u;
+    const uint32_t npairs = (a.B + 32u * QT - 1u) / (32u * QT);
+    const uint32_t bx = std::max<uint32_t>(1u, std::min<uint32_t>(cu_count() / std::max<uint32_t>(1u, npairs),
+                                                                  (S / 32u + 7u) / 8u));
+    hipLaunchKernelGGL((k_sample_wide<W4, QT>), dim3(bx, npairs), dim3(kMx3Threads), 0, s, a.codes, a.cap, a.N, S,
+                       a.sample_stride, (const uint32_t*)a.qcodes, a.B, a.smp);
+    hipLaunchKernelGGL(k_sample_thr, dim3(a.B), dim3(256), (size_t)(a.D + 1u) * 4u, s, a.smp, S, a.D, a.target, a.thr);
+}
+
 template <int W4, int CPL>
 static void launch_scan_t(const Stage1Args& a, hipStream_t s) {
     const uint64_t per_block = 256ull * CPL;
@@ -2422,6 +2525,10 @@ size_t stage1_plan(Stage1Args& a) {
     const bool big = a.use_mfma == 1 && a.B >= kMfmaMinB && mfma_scan_supported(W4);
     a.mfma_scan = big;
     a.sample_mode = kSampleValu;
+    // wide codes (k_scan_mx4): the FP4 sample when the scan is the FP4 one (GVDB_SAMPLE=valu: the VALU form)
+    if (a.use_mfma == 1 && a.B >= kMfmaMinB && mx4_scan_supported(W4) && !getenv_flag_eq("GVDB_SAMPLE", "valu") &&
+        (uint64_t)a.B * a.sample_chunks * 4096u * 2u <= (1ull << 30))
+        a.sample_mode = kSampleWide;
     // GVDB_SAMPLE=valu / =mx / =dense force a sample form (tests, A/B).  Default
     // for large batches: the dense FP4 sample (any shard size: for N <= kExactN
     // the "sample" is the whole shard and T is the exact R-th distance); the
@@ -2458,6 +2565,7 @@ size_t stage1_plan(Stage1Args& a) {
         bytes += ng * (8u * 2u * W4 * 64u * 16u + 256u * 4u);
     }
     if (a.sample_mode == kSampleDense) bytes += (size_t)a.B * (S / 16u) * 2u + 256u;
+    if (a.sample_mode == kSampleWide) bytes += (size_t)a.B * S * 2u + 256u;
     if (a.dense_sel && !a.dense_keep) bytes += (size_t)std::min<uint32_t>(a.B, 256u) * a.dense_np * 2u + 256u;
     return bytes;
 }
@@ -2515,6 +2623,14 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 4: launch_sample_dense_t<4>(a, s); break;
             default: launch_sample_dense_t<6>(a, s); break;
         }
+    } else if (a.sample_mode == kSampleWide) {
+        switch (W4) {
+            case 8: launch_sample_wide_t<8, 4>(a, s); break;
+            case 12: launch_sample_wide_t<12, 4>(a, s); break;
+            case 16: launch_sample_wide_t<16, 3>(a, s); break;
+            case 24: launch_sample_wide_t<24, 2>(a, s); break;
+            default: launch_sample_wide_t<32, 1>(a, s); break;
+        }
     } else if (a.sample_mode == kSampleMxHist) {
         switch (W4) {
             case 2: launch_sample_mx_t<2>(a, s); break;
@@ -2543,7 +2659,7 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
                                a.N, a.D, W4, a.sample_stride, a.qcodes, a.B, a.hist);
     }
     GVDB_LAUNCH_CHECK();
-    if (a.sample_mode != kSampleDense) {
+    if (a.sample_mode != kSampleDense && a.sample_mode != kSampleWide) {
         hipLaunchKernelGGL(k_threshold, dim3((a.B + 3) / 4), dim3(256), 0, s, a.hist, a.B, a.D, a.target, a.thr);
         GVDB_LAUNCH_CHECK();
     }

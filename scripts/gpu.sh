@@ -204,6 +204,14 @@ for t in "${TASKS[@]}"; do
                 GVDB_FLAT_EVERY=$v N=10000000 K=10 GVDB_FLAT=i8 BS=256 FLAT_REPS=10 run 600 gpurun_out/fe2l_$v.log python3 scripts/flat_timing.py
                 echo "== 10M every $v"; grep -E "B=|emit" gpurun_out/fe2l_$v.log | tail -2
             done ;;
+        probeab)  # flat pass probe selection blocks per query (GVDB_PROBE_PARTS 1 / 4 / default) at 10M B 256 k 10 and the shard
+            for v in 1 4 0; do
+                GVDB_PROBE_PARTS=$v N=10000000 K=10 GVDB_FLAT=i8 BS=256 FLAT_REPS=10 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pab_$v -o run -- python3 scripts/flat_timing.py > gpurun_out/pab_$v.log 2>&1 || { echo "FAILED $v"; exit 1; }
+                echo "== 10M parts $v"; grep -E "B=|emit" gpurun_out/pab_$v.log | tail -2
+                python3 scripts/trace_summary.py gpurun_out/prof_pab_$v/run_kernel_trace.csv | grep -E "i8q|rerank|k_flat" | head -10
+                GVDB_PROBE_PARTS=$v N=1250000 K=32 GVDB_FLAT=i8 BS=64 FLAT_REPS=10 run 600 gpurun_out/pabs_$v.log python3 scripts/flat_timing.py
+                echo "== shard parts $v"; grep -E "B=|emit" gpurun_out/pabs_$v.log | tail -2
+            done ;;
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
             BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
             grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;

@@ -3,6 +3,7 @@
 for a repeated step, the per-step timeline (kernel start offsets and the idle
 gaps between consecutive kernels).  Usage: trace_summary.py run_kernel_trace.csv [first_kernel_substring]"""
 import csv
+import re
 import sys
 from collections import defaultdict
 
@@ -11,7 +12,9 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 anchor = sys.argv[2] if len(sys.argv) > 2 else None
 dur = defaultdict(list)
 for r in rows:
-    dur[r["Kernel_Name"].split("(")[0][:70]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    m = re.search(r"(k_\w+)", r["Kernel_Name"])  # anonymous-namespace kernels by their own name
+    dur[m.group(1) if m else r["Kernel_Name"].split("(")[0][:70]].append(
+        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 print(f"{'kernel':70s} {'calls':>6s} {'avg us':>9s}")
 for k, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
     print(f"{k:70s} {len(v):6d} {sum(v) / len(v):9.1f}")
