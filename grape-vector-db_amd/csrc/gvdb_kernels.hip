@@ -1576,13 +1576,29 @@ static hipError_t launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
 // wave's NEXT sub-tile as soon as chunk c has been consumed, so NC - 1 chunks
 // of MFMA work cover each chunk's HBM latency.  The QT accumulators live
 // across the chunks; threshold epilogue and emits are those of k_scan_mx3.
+//
+// Round 5: ONE launch covers every query tile group ("pair" of QT tiles) of the batch.
+// Block L runs on XCD L % 8; its slot L / 8 on that XCD names (pair, row block), with
+// the row block's npairs blocks on the SAME XCD -- they stream the same code rows at
+// about the same time, so 3 of 4 row reads hit that XCD's L2 instead of HBM (the
+// launch-per-pair form read the planes ceil(B / 32QT) times from HBM: 4 x 480 MB per
+// batch-256 step at the 1.25M-row shard of config 4).
 template <int W4, int CH, int QT>
 __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
-                                                           const uint32_t* __restrict__ qwords,
-                                                           const uint32_t* __restrict__ thr, uint32_t B,
-                                                           uint32_t* __restrict__ counts, uint64_t* __restrict__ buf,
-                                                           uint32_t bufcap) {
+                                                           const uint32_t* __restrict__ qwords_all,
+                                                           const uint32_t* __restrict__ thr_all, uint32_t Bt,
+                                                           uint32_t* __restrict__ counts_all,
+                                                           uint64_t* __restrict__ buf_all, uint32_t bufcap,
+                                                           uint32_t npairs) {
     constexpr int KW = 4 * W4;  // 32-bit code words per row
+    const uint32_t xcd = blockIdx.x % 8u, slot = blockIdx.x / 8u;
+    const uint32_t pair = slot % npairs, rb = (slot / npairs) * 8u + xcd, nrb = gridDim.x / npairs;
+    const uint32_t qg0 = pair * 32u * QT;
+    const uint32_t B = min(32u * QT, Bt - qg0);
+    const uint32_t* __restrict__ qwords = qwords_all + (uint64_t)qg0 * KW;
+    const uint32_t* __restrict__ thr = thr_all + qg0;
+    uint32_t* __restrict__ counts = counts_all + qg0;
+    uint64_t* __restrict__ buf = buf_all + (uint64_t)qg0 * bufcap;
     constexpr int KS = KW / 2;  // k-steps of 64 bits
     constexpr int NC = W4 / CH;
     constexpr int KC = 2 * CH;  // k-steps per chunk
@@ -1614,7 +1630,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
     }
     __syncthreads();
     const uint32_t nsub = (N + kMx3Rows - 1) / kMx3Rows;
-    const uint32_t W = gridDim.x * (kMx3Threads / 64);
+    const uint32_t W = nrb * (kMx3Threads / 64);
     const uint32_t h = lane >> 5;
     uint4 cr[NC][CH];
     auto load = [&](uint32_t sb, int c) __attribute__((always_inline)) {
@@ -1703,7 +1719,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
             }
         }
     };
-    uint32_t sb = blockIdx.x * (kMx3Threads / 64) + wv;
+    uint32_t sb = rb * (kMx3Threads / 64) + wv;
 #pragma unroll
     for (int c = 0; c < NC; ++c) load(sb, c);
     for (; sb < nsub; sb += W) {
@@ -1724,19 +1740,17 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
 
 template <int W4, int CH, int QT>
 static void launch_scan_mx4_t(const Stage1Args& a, hipStream_t s) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t cus = cu_count();
     const uint32_t nsub = (a.N + kMx3Rows - 1) / kMx3Rows;
     const uint32_t wpb = kMx3Threads / 64;
-    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus, (nsub + wpb - 1) / wpb));
-    constexpr uint32_t QB = 32u * QT;  // queries per launch
-    for (uint32_t g = 0; g < a.B; g += QB) {
-        const uint32_t bg = min(QB, a.B - g);
-        hipLaunchKernelGGL((k_scan_mx4<W4, CH, QT>), dim3(grid), dim3(kMx3Threads), 0, s, a.codes, a.cap, a.N,
-                           (const uint32_t*)a.qcodes + (uint64_t)g * 4u * W4, a.thr + g, bg, a.counts + g,
-                           a.buf + (uint64_t)g * a.bufcap, a.bufcap);
-    }
+    constexpr uint32_t QB = 32u * QT;  // queries per tile group
+    const uint32_t npairs = (a.B + QB - 1u) / QB;
+    // row blocks: a multiple of 8 (one per XCD per slot row), all resident (one block per CU)
+    uint32_t nrbl = std::max<uint32_t>(1u, cus / (8u * npairs));                    // row blocks per XCD
+    nrbl = std::min<uint32_t>(nrbl, std::max<uint32_t>(1u, (nsub + 8u * wpb - 1u) / (8u * wpb)));
+    const uint32_t grid = 8u * nrbl * npairs;
+    hipLaunchKernelGGL((k_scan_mx4<W4, CH, QT>), dim3(grid), dim3(kMx3Threads), 0, s, a.codes, a.cap, a.N,
+                       (const uint32_t*)a.qcodes, a.thr, a.B, a.counts, a.buf, a.bufcap, npairs);
 }
 
 
