@@ -2629,7 +2629,12 @@ gvdb_status gvdb::shard_deep_flat_early(const gvdb_index* ix, const float* d_q, 
             early_flat().ev.erase(it);
         }
     }
-    if (!shard_certified_eligible(ix, dim, 1) || B == 0 || B > 0xFFFFFFFFull) return GVDB_OK;
+    // GVDB_DEEP_EARLY=1: enqueue the list early (A/B).  Off by default: with the dense stage 1
+    // down to ~0.13 ms the second stream's event traffic costs more than the overlap gains
+    // (10M, 8 shards, batch 64: 0.788 ms per rank with it, 0.720 without; stage-1 host
+    // enqueue 81 vs 34 us per call)
+    const char* env = getenv("GVDB_DEEP_EARLY");
+    if (!(env && env[0] == '1') || !shard_certified_eligible(ix, dim, 1) || B == 0 || B > 0xFFFFFFFFull) return GVDB_OK;
     gvdb_status st = set_device(ix->device);
     if (st != GVDB_OK) return st;
     tier_poll();

@@ -221,6 +221,11 @@ for t in "${TASKS[@]}"; do
             run 1100 gpurun_out/deep_10M.log python3 -u scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --steps 2 --oracle-queries 2
             grep '^{' gpurun_out/deep_10M.log > gpurun_out/deep_10M.json
             grep '\[c3\]' gpurun_out/deep_1M.log gpurun_out/deep_10M.log ;;
+        deepearly)  # deep 10M with / without the early flat list (GVDB_DEEP_EARLY=0), same box
+            for v in 1 0; do
+                GVDB_DEEP_EARLY=$v run 900 gpurun_out/deepearly_$v.log python3 -u scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --steps 3 --oracle-queries 0 --no-single
+                echo "== early $v"; grep '\[c3\]' gpurun_out/deepearly_$v.log | tail -2
+            done ;;
         c4x2)  # config 4 (10M x 3072, 8 shards) on the TWO-exchange protocol, vs one 10M x 3072 index
             run 1100 gpurun_out/c4x2.log python -u scripts/c3_emulate.py --dim 3072 --oracle-queries 0 --steps 10
             grep '^{' gpurun_out/c4x2.log > gpurun_out/c4x2.json; grep '^\[c3\]' gpurun_out/c4x2.log | tail -4 ;;
