@@ -16,7 +16,7 @@ import bench  # noqa: E402
 import gvdb  # noqa: E402
 
 n = int(os.environ.get("SHARD_N", 10_000_000))
-D, B, R, k = 768, 256, 100, 10
+D, B, R, k = int(os.environ.get("DIM", 768)), 256, 100, 10
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
 q = bench.gen_queries(B, D, dev)

@@ -118,7 +118,7 @@ for t in "${TASKS[@]}"; do
             python3 scripts/trace_summary.py gpurun_out/prof_c4/run_kernel_trace.csv > gpurun_out/c4_kernels.txt; head -20 gpurun_out/c4_kernels.txt ;;
         c3prof)
             run 600 gpurun_out/c3prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o run -- python3 scripts/c3_emulate.py --no-single --oracle-queries 0 --steps 10
-            python3 scripts/trace_summary.py gpurun_out/prof_c3/run_kernel_trace.csv | grep gvdb | head -12 ;;
+            python3 scripts/trace_summary.py gpurun_out/prof_c3/run_kernel_trace.csv | head -16 ;;
         deepprof)  # kernel trace of the deep form (1M, R = 100K, batch 256; 10M, R = 1M, batch 64)
             run 600 gpurun_out/deepprof_1M.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_deep1M -o run -- python3 scripts/c3_emulate.py --n 1000000 --R 100000 --no-single --oracle-queries 0 --steps 2
             python3 scripts/trace_summary.py gpurun_out/prof_deep1M/run_kernel_trace.csv > gpurun_out/deep1M_kernels.txt
