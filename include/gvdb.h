@@ -346,7 +346,9 @@ gvdb_status gvdb_comm_info(const gvdb_comm* comm, int32_t* world, int32_t* rank)
  * world * k <= 8192, dim <= 8192; R > 8192 (the reference's default ratio at
  * scale) runs the deep form of the protocol (exchange 1 = Hamming histograms,
  * below) with R <= 2^20, dim < 4096, k <= 1024.  Results land on every rank, on
- * `stream`; no host sync in BQ mode.  An empty shard contributes nothing; a
+ * `stream`, with no host sync in either mode: the deep form's certified phase 2
+ * and every fallback tier (the owned-row rerank, FLAT's exact scan) are chosen on
+ * the device by the failing tier's flag.  An empty shard contributes nothing; a
  * rank whose local part fails still joins both collectives (no deadlock),
  * returns its error, and poisons every query of the merge (out_n =
  * GVDB_N_POISONED on every rank), as does a NaN score.  Calls on one comm are
