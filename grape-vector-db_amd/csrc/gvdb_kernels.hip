@@ -1606,21 +1606,33 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
     constexpr uint32_t kWaveStage = 512;
     __shared__ __attribute__((aligned(16))) v4i_t qfrag[QT * KS * 64];
     __shared__ __attribute__((aligned(16))) float tf_lds[QT * 32];
+    __shared__ float pc_lds[QT * 32];  // |q|
     __shared__ float tmin_lds[QT * 2];
     __shared__ uint64_t st_key[kMx3Threads / 64][kWaveStage];
     __shared__ uint8_t st_q[kMx3Threads / 64][kWaveStage];
     __shared__ uint32_t qcnt[QT * 32], qbase[QT * 32];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr float kPadF = (float)(32 * KW);
     const int scale1 = 0x7f7f7f7f;
+    // round 5: mx7's {0,1} x {+-1} operands (fp4_row01 / fp4_query_pm: dot = 2 pop(q & x) - |x|,
+    // Hamming = |q| - dot) and its word map (k-step s, lane half h: word 4 (s / 2) + 2 h + s % 2,
+    // one uint2 per plane and half) -- 5 VALU per row fragment and no word select, instead of
+    // fp4_x32's 8 plus a select on the uint4 (7.7 VALU per MFMA by PMC at 10M x 3072)
     for (uint32_t i = tid; i < (uint32_t)(QT * KS * 64); i += kMx3Threads) {
         const uint32_t l = i & 63u, st = i >> 6, qs = st % KS, qt = st / KS;
         const uint32_t q = qt * 32u + (l & 31u);
-        qfrag[i] = fp4_x32(q < B ? qwords[(uint64_t)q * KW + 2u * qs + (l >> 5)] : 0u);
+        const uint32_t wi = 4u * (qs >> 1) + 2u * (l >> 5) + (qs & 1u);
+        qfrag[i] = fp4_query_pm(q < B ? qwords[(uint64_t)q * KW + wi] : 0u);
     }
-    if (tid < QT * 32) tf_lds[tid] = tid < B ? kPadF - 2.0f * (float)thr[tid] : __builtin_inff();
-    if (tid < QT * 32) qcnt[tid] = 0u;
+    if (tid < QT * 32) {
+        uint32_t pc = 0;
+        if (tid < B)
+            for (int w = 0; w < KW; ++w) pc += __popc(qwords[(uint64_t)tid * KW + w]);
+        pc_lds[tid] = (float)pc;
+        // a hit: d = |q| - dot <= thr  <=>  dot >= |q| - thr
+        tf_lds[tid] = tid < B ? (float)pc - (float)thr[tid] : __builtin_inff();
+        qcnt[tid] = 0u;
+    }
     __syncthreads();
     if (tid < QT * 2) {
         const float* tq = tf_lds + (tid >> 1) * 32 + 4u * (tid & 1u);
@@ -1632,15 +1644,15 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
     const uint32_t nsub = (N + kMx3Rows - 1) / kMx3Rows;
     const uint32_t W = nrb * (kMx3Threads / 64);
     const uint32_t h = lane >> 5;
-    uint4 cr[NC][CH];
+    uint2 cr[NC][CH];  // this lane half's two words of each plane
     auto load = [&](uint32_t sb, int c) __attribute__((always_inline)) {
         const uint32_t n = min(sb * (uint32_t)kMx3Rows + (lane & 31u), N - 1u);  // clamped: branch-free ring
 #pragma unroll
-        for (int p = 0; p < CH; ++p) cr[c][p] = codes[(uint64_t)(c * CH + p) * cap + n];
+        for (int p = 0; p < CH; ++p) cr[c][p] = ((const uint2*)(codes + (uint64_t)(c * CH + p) * cap))[2u * n + h];
     };
     auto word = [&](int c, int s) __attribute__((always_inline)) {
-        const uint4 v = cr[c][(2 * s) >> 2];
-        return (2 * s) & 3 ? (h ? v.w : v.z) : (h ? v.y : v.x);
+        const uint2 v = cr[c][s >> 1];
+        return (s & 1) ? v.y : v.x;
     };
     uint32_t wcnt = 0;
     v16f_t acc[QT];
@@ -1656,7 +1668,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
 #pragma unroll
         for (int s = 0; s < KC; ++s) {
             __builtin_amdgcn_sched_barrier(0);
-            const v4i_t b = fp4_x32(word(c, s));
+            const v4i_t b = fp4_row01(word(c, s));
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
                 const int m = s * QT + qt;
@@ -1704,7 +1716,7 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
                         const uint32_t sp = wcnt + __builtin_amdgcn_mbcnt_hi(
                             (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                         const uint32_t qi = rb + (r & 3) + 8 * (r >> 2);
-                        const uint32_t d = (uint32_t)(kPadF - acc[qt][r]) >> 1;
+                        const uint32_t d = (uint32_t)(int)(pc_lds[qi] - acc[qt][r]);  // exact: integers
                         const uint64_t key = ((uint64_t)d << 32) | n;
                         if (sp < kWaveStage) {
                             st_key[wv][sp] = key;
@@ -1738,6 +1750,9 @@ __global__ __launch_bounds__(kMx3Threads, 1) void k_scan_mx4(const uint4* __rest
                                                      qbase, counts, buf, bufcap);
 }
 
+#ifndef GVDB_MX4_CH24
+#define GVDB_MX4_CH24 6  // code planes per chunk at W4 = 24 (variant builds: -DGVDB_MX4_CH24=N)
+#endif
 template <int W4, int CH, int QT>
 static void launch_scan_mx4_t(const Stage1Args& a, hipStream_t s) {
     const uint32_t cus = cu_count();
@@ -2685,7 +2700,7 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
             case 8: launch_scan_mx4_t<8, 4, 4>(a, s); break;
             case 12: launch_scan_mx4_t<12, 6, 4>(a, s); break;
             case 16: launch_scan_mx4_t<16, 8, 3>(a, s); break;
-            case 24: launch_scan_mx4_t<24, 6, 2>(a, s); break;
+            case 24: launch_scan_mx4_t<24, GVDB_MX4_CH24, 2>(a, s); break;
             default: launch_scan_mx4_t<32, 8, 1>(a, s); break;
         }
     } else if (mfma) {  // FP4 block-scaled MFMA, {0,1} x {+-1} operands (default for large batches)
