@@ -226,6 +226,13 @@ for t in "${TASKS[@]}"; do
                 GVDB_DEEP_EARLY=$v run 900 gpurun_out/deepearly_$v.log python3 -u scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --steps 3 --oracle-queries 0 --no-single
                 echo "== early $v"; grep '\[c3\]' gpurun_out/deepearly_$v.log | tail -2
             done ;;
+        mx4var:*)  # k_scan_mx4 build variants at 10M x 3072 (b256_timing, one box): mx4var:base,ch8,...
+            IFS=',' read -ra VARS <<< "${t#mx4var:}"
+            for v in "${VARS[@]}"; do
+                lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
+                DIM=3072 GVDB_LIB_PATH=$lib TAG=$v run 600 gpurun_out/mx4var_$v.log python3 -u scripts/b256_timing.py
+                grep "scan" gpurun_out/mx4var_$v.log | tail -1
+            done ;;
         c4x2)  # config 4 (10M x 3072, 8 shards) on the TWO-exchange protocol, vs one 10M x 3072 index
             run 1100 gpurun_out/c4x2.log python -u scripts/c3_emulate.py --dim 3072 --oracle-queries 0 --steps 10
             grep '^{' gpurun_out/c4x2.log > gpurun_out/c4x2.json; grep '^\[c3\]' gpurun_out/c4x2.log | tail -4 ;;
