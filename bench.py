@@ -392,7 +392,7 @@ def main():
         }
     roof.update({
         "frac": roof["achieved"] / peak,
-        "traffic": pmc_traffic("gvdb::k_scan_mx7<" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
+        "traffic": pmc_traffic("gvdb::k_scan_mx7<6, false" if variant == "fp4" else "gvdb::k_scan<", n_local, D) if mfma else None,
         "avg_launch_ms": scan_avg,
         "algorithmic_ops_per_launch": ops,
         "hbm_bytes_per_launch": n_local * w4 * 16 * scan_launches,
@@ -607,7 +607,7 @@ def main():
         dist.destroy_process_group()
 
 
-PMC_FILE = "profiles/r04/pmc_bench_10M.json"
+PMC_FILE = "profiles/r05/pmc_bench_10M.json"
 PMC_FLAT_FILE = PMC_FILE  # the same passes cover k_flat_i8q (bench.py operating points, 10M x 768, B = 256)
 
 
