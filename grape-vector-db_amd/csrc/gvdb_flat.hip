@@ -997,6 +997,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     __shared__ float cs[kI8qCl];  // their approx scores
     __shared__ uint32_t cl_n;
     __shared__ __attribute__((aligned(16))) float qinv_l[kFxQ], thr_l[kFxQ], qa_l[kFxQ];
+    __shared__ uint32_t fl_n[kFxQ], fl_b[kFxQ];  // flush: entries per query, their global base
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t qtile = SPLIT ? (wv & 3u) : wv;   // this wave's 32 query slots
@@ -1071,13 +1072,36 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         const uint32_t v = blockIdx.x + ((e >> 6) & 0x3ffffu) * G;
         return (v / kSubPerTile) * kFxRows + (kI8qSub * (v % kSubPerTile) + ((e >> 5) & 1u)) * 32u + (e & 31u);
     };
-    auto flush = [&](uint32_t m) {  // the block's list -> the per-query global lists
-        for (uint32_t x = tid; x < m; x += kFxThreads) {
-            const uint32_t e = cl[x], q = e >> 24;
-            const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-            if (pos < a.candcap) {
-                a.cand[(uint64_t)q * a.candcap + pos] = row_of(e);
-                if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = cs[x];
+    // the block's list -> the per-query global lists, block-aggregated (round 5): ranks within
+    // (block, query) by LDS atomics, ONE global atomic per (block, query) reserves the slots.
+    // One global atomic per entry put ~1000 serialised atomics on each query's counter at the
+    // end of a 1.25M-row shard's pass (K2 = 32: ~1000 nominations per query, all blocks
+    // flushing together).  Every thread calls it (block-uniform).
+    constexpr uint32_t kPerT = (kI8qCl + kFxThreads - 1) / kFxThreads;
+    auto flush = [&](uint32_t m) {
+        for (uint32_t q = tid; q < kFxQ; q += kFxThreads) fl_n[q] = 0u;
+        __syncthreads();
+        uint32_t rk[kPerT];
+#pragma unroll
+        for (uint32_t j = 0; j < kPerT; ++j) {
+            const uint32_t x = tid + j * kFxThreads;
+            rk[j] = x < m ? atomicAdd(&fl_n[cl[x] >> 24], 1u) : 0u;
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < kFxQ; q += kFxThreads) {
+            const uint32_t c = fl_n[q];
+            if (c) fl_b[q] = atomicAdd(&a.counts[q], c);
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kPerT; ++j) {
+            const uint32_t x = tid + j * kFxThreads;
+            if (x < m) {
+                const uint32_t e = cl[x], q = e >> 24, pos = fl_b[q] + rk[j];
+                if (pos < a.candcap) {
+                    a.cand[(uint64_t)q * a.candcap + pos] = row_of(e);
+                    if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = cs[x];
+                }
             }
         }
     };

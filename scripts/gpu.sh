@@ -233,6 +233,11 @@ for t in "${TASKS[@]}"; do
                 DIM=3072 GVDB_LIB_PATH=$lib TAG=$v run 600 gpurun_out/mx4var_$v.log python3 -u scripts/b256_timing.py
                 grep "scan" gpurun_out/mx4var_$v.log | tail -1
             done ;;
+        bm25clk)  # BM25 leg at 5M docs: timing, then the per-phase shader clocks (GVDB_BM25_ABL=8)
+            run 600 gpurun_out/bm25t.log python3 -u scripts/bm25_timing.py --check
+            tail -3 gpurun_out/bm25t.log
+            GVDB_BM25_ABL=8 run 600 gpurun_out/bm25clk.log python3 -u scripts/bm25_timing.py --steps 2
+            grep "bm25 prof" gpurun_out/bm25clk.log | tail -2 ;;
         c4x2)  # config 4 (10M x 3072, 8 shards) on the TWO-exchange protocol, vs one 10M x 3072 index
             run 1100 gpurun_out/c4x2.log python -u scripts/c3_emulate.py --dim 3072 --oracle-queries 0 --steps 10
             grep '^{' gpurun_out/c4x2.log > gpurun_out/c4x2.json; grep '^\[c3\]' gpurun_out/c4x2.log | tail -4 ;;

@@ -3,10 +3,19 @@
 for a repeated step, the per-step timeline (kernel start offsets and the idle
 gaps between consecutive kernels).  Usage: trace_summary.py run_kernel_trace.csv [first_kernel_substring]"""
 import csv
+import os
 import re
 import sys
 from collections import defaultdict
 
+def _quiet_pipe(exc_type, exc, tb):  # `| head` in a pipefail script: a closed pipe is not a failure
+    if exc_type is BrokenPipeError:
+        os.dup2(os.open(os.devnull, os.O_WRONLY), sys.stdout.fileno())
+        sys.exit(0)
+    sys.__excepthook__(exc_type, exc, tb)
+
+
+sys.excepthook = _quiet_pipe
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 anchor = sys.argv[2] if len(sys.argv) > 2 else None
