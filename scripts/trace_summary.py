@@ -10,8 +10,7 @@ from collections import defaultdict
 
 def _quiet_pipe(exc_type, exc, tb):  # `| head` in a pipefail script: a closed pipe is not a failure
     if exc_type is BrokenPipeError:
-        os.dup2(os.open(os.devnull, os.O_WRONLY), sys.stdout.fileno())
-        sys.exit(0)
+        os._exit(0)
     sys.__excepthook__(exc_type, exc, tb)
 
 
@@ -43,3 +42,7 @@ if anchor:
             prev_end = e
         span = int(rows[i1]["Start_Timestamp"]) - t0
         print(f"  step span {span / 1e3:.1f} us, kernels busy {busy / 1e3:.1f} us")
+try:
+    sys.stdout.flush()
+except BrokenPipeError:
+    os._exit(0)
