@@ -1247,11 +1247,10 @@ static gvdb_status flat_mx_search(const gvdb_index* ix, const float* d_q, uint32
         const int v = e ? atoi(e) : 0;
         return v > 0 ? (uint32_t)v : 0u;
     }();
-    // long lists (the certified default depth's K2 = 32 / 64): a 4x denser sample -- a tighter tau
-    // nominates ~3x fewer candidates, whose appends and reranks cost more than the sample pass
-    // (1.25M rows, k = 32, batch 64: 0.656 -> 0.568 ms per batch; 10M, k = 10, batch 256: stride 64
-    // stays best, 2.80 vs 2.85 / 2.97 ms at 32 / 16)
-    const uint32_t every = every_env ? every_env : k >= 24u ? kFxSampleEvery / 4u : kFxSampleEvery;
+    // (a 4x denser sample for K2 >= 24 lists paid off while k_flat_i8q flushed one global atomic per
+    // nomination: 0.656 -> 0.568 ms per batch at the 1.25M-row shard; with the aggregated flush the
+    // strides 64 / 32 / 16 measure 0.446 / 0.448 / 0.457 ms there, so the default stride stays)
+    const uint32_t every = every_env ? every_env : kFxSampleEvery;
     const uint32_t sampled = (ntiles + every - 1) / every;
     const uint32_t S = sampled * kFxRows;
 
