@@ -3307,6 +3307,139 @@ __global__ __launch_bounds__(kRsThreads) void k_rerank_small_items(
     }
 }
 
+// k_rerank_dma (round 5): k_rerank2's wave items (64 candidates of one query, one row
+// per lane, the reference's sequential fold) with the row gathers made asynchronous:
+// each 32-dimension chunk of the 64 rows (8 KiB) is DMA'd straight into LDS by eight
+// global_load_lds_dwordx4 (one 16-B piece per lane, any row address), kRdBufs - 1
+// chunks ahead of the fold -- k_rerank2 held two chunks in registers and waited on each
+// gather in turn (at ~850 candidates per query its 64-row items are fewer than the
+// waves, and the kernel was one item's serial latency).  A lane writes float4 f of row r
+// to slot f ^ ((r >> 1) & 7) of the row, so the fold's per-lane row reads hit 16 distinct
+// bank groups per 16 lanes.  The query is DMA'd once per item.  Cosine / cosine
+// distance, rows and queries of one length D % 32 == 0, D <= 1024, 16-B aligned.
+constexpr int kRdThreads = 256;  // 4 independent waves
+constexpr int kRdBufs = 4;       // chunk buffers per wave
+constexpr uint32_t kRdMaxD = 1024;
+__global__ __launch_bounds__(kRdThreads, 1) void k_rerank_dma(const float* __restrict__ rows, uint32_t D,
+                                                             const float* __restrict__ norms,
+                                                             const float* __restrict__ q,
+                                                             const uint32_t* __restrict__ s1_rows, uint32_t B,
+                                                             uint32_t R, const uint32_t* __restrict__ counts, int kind,
+                                                             float* __restrict__ scores,
+                                                             const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    __shared__ __attribute__((aligned(16))) float4 tile[kRdThreads / 64][kRdBufs][64 * 8];
+    __shared__ __attribute__((aligned(16))) float4 qs[kRdThreads / 64][kRdMaxD / 4];
+    __shared__ uint32_t pre[kRrMaxB + 1];
+    __shared__ uint32_t part[kRdThreads];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    {  // items (64 candidates of one query) before query i
+        const uint32_t per = (B + kRdThreads - 1) / kRdThreads, b0 = tid * per;
+        uint32_t loc = 0;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) loc += (min(counts[b0 + i], R) + 63u) / 64u;
+        part[tid] = loc;
+        __syncthreads();
+        for (uint32_t o = 1; o < kRdThreads; o <<= 1) {
+            const uint32_t v = tid >= o ? part[tid - o] : 0u;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        uint32_t run = part[tid] - loc;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) {
+            pre[b0 + i] = run;
+            run += (min(counts[b0 + i], R) + 63u) / 64u;
+        }
+        if (tid == kRdThreads - 1) pre[B] = part[tid];
+        __syncthreads();
+    }
+    const uint32_t items = pre[B], nch = D / 32u, L4 = D / 4u;
+    const uint32_t tb = (uint32_t)(uintptr_t)&tile[wv][0][0];  // LDS byte addresses
+    const uint32_t qb = (uint32_t)(uintptr_t)&qs[wv][0];
+    const uint32_t W = gridDim.x * (kRdThreads / 64);
+    // chunk c of the item's rows -> buffer c % kRdBufs: instruction s, lane l fills slot
+    // (8 s + l / 8, l % 8) with float4 (l % 8) ^ ((row >> 1) & 7) of row 8 s + l / 8
+    const uint32_t lr = lane >> 3, lp = lane & 7u;
+    for (uint32_t item = blockIdx.x * (kRdThreads / 64) + wv; item < items; item += W) {  // wave-uniform
+        uint32_t lo = 0, hi = B;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= item) lo = mid; else hi = mid;
+        }
+        const uint32_t qi = __builtin_amdgcn_readfirstlane(lo);
+        const uint32_t r0 = (item - pre[qi]) * 64u, Rq = min(counts[qi], R);
+        const uint32_t* srow = s1_rows + (uint64_t)qi * R;
+        const uint32_t my_r = r0 + lane;
+        const bool live = my_r < Rq;
+        // the source row of each of this lane's 8 DMA pieces: row 8 s + l / 8 of the item
+        uint64_t src[8];
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+            const uint32_t rr = r0 + 8u * (uint32_t)st + lr;
+            const uint32_t row = srow[rr < Rq ? rr : r0];  // past the list: a valid row, never used
+            const uint32_t f = lp ^ (((8u * (uint32_t)st + lr) >> 1) & 7u);
+            src[st] = (uint64_t)(uintptr_t)(rows + (uint64_t)row * D + 4u * f);
+        }
+        // the query (a piece per lane per 1 KiB), then the first chunks
+        const float* qv = q + (uint64_t)qi * D;
+        for (uint32_t k = 0; k * 64u < L4; ++k) {
+            const uint32_t idx = min(k * 64u + lane, L4 - 1u);
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(qv + 4u * idx),
+                         "s"(qb + k * 1024u)
+                         : "memory");
+        }
+        auto issue = [&](uint32_t c) __attribute__((always_inline)) {
+            const uint32_t b = tb + (c % kRdBufs) * 8192u;
+#pragma unroll
+            for (int st = 0; st < 8; ++st)
+                asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src[st] + 128ull * c),
+                             "s"(b + (uint32_t)st * 1024u)
+                             : "memory");
+        };
+#pragma unroll
+        for (int c = 0; c < kRdBufs - 1; ++c)
+            if ((uint32_t)c < nch) issue((uint32_t)c);
+        float acc = -0.0f, qq = -0.0f;
+        const uint32_t rsw = (lane >> 1) & 7u;  // this lane's row swizzle
+        for (uint32_t c = 0; c < nch; ++c) {
+            // chunk c (and the query) landed: the younger DMAs are the next kRdBufs - 2 chunks
+            if (c + kRdBufs - 2 < nch)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRdBufs - 2) * 8) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c + kRdBufs - 1 < nch) issue(c + kRdBufs - 1);  // into the buffer chunk c - 1 used
+            const float4* tr = (const float4*)&tile[wv][c % kRdBufs][8u * lane];
+            const float4* qc = &qs[wv][8u * c];
+#pragma unroll
+            for (uint32_t f = 0; f < 8u; ++f) {
+                const float4 x = tr[f ^ rsw];
+                const float4 w = qc[f];
+                acc = acc + w.x * x.x;
+                acc = acc + w.y * x.y;
+                acc = acc + w.z * x.z;
+                acc = acc + w.w * x.w;
+                qq = qq + w.x * w.x;
+                qq = qq + w.y * w.y;
+                qq = qq + w.z * w.z;
+                qq = qq + w.w * w.w;
+            }
+        }
+        if (live) {
+            const uint32_t row = srow[my_r];
+            const float na = sqrtf(qq), nb = norms[row];
+            scores[(uint64_t)qi * R + my_r] = kind == kScoreCosine
+                                                  ? ((na == 0.0f || nb == 0.0f) ? 0.0f : acc / (na * nb))
+                                                  : ((na == 0.0f || nb == 0.0f) ? __builtin_inff()
+                                                                               : 1.0f - (acc / (na * nb)));
+        }
+        // every lane's LDS reads of this item are done before the next item's DMAs land
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // GVDB_RERANK=v1: always the block-synchronous k_rerank (A/B)
 static bool rerank_v2() {
     static const bool v = [] {
@@ -3345,6 +3478,26 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
         const char* e = getenv("GVDB_RERANK");
         return !(e && (strcmp(e, "v2") == 0 || strcmp(e, "v1") == 0));
     }();
+    // device-counted lists at D % 32 == 0: k_rerank_dma (flat candidates at the 1.25M-row shard,
+    // k = 32, batch 64: 84 -> 38 us; 10M, batch 256: flat group 2.65 -> 2.53 ms); GVDB_RERANK_DMA=0:
+    // the item-walking k_rerank_small below (A/B)
+    static const bool dma = [] {
+        const char* e = getenv("GVDB_RERANK_DMA");
+        return !(e && e[0] == '0');
+    }();
+    if (dma && a.counts && a.qlen == a.clen && a.clen % 32u == 0 && a.clen <= kRdMaxD &&
+        (a.kind == kScoreCosine || a.kind == kScoreCosineDistance) && (((uintptr_t)a.q | (uintptr_t)a.rows) & 15u) == 0) {
+        for (uint32_t b0 = 0; b0 < a.B; b0 += kRrMaxB) {
+            const uint32_t nb = std::min<uint32_t>(kRrMaxB, a.B - b0);
+            const uint64_t waves = (uint64_t)nb * ((a.R + 63u) / 64u);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3u) / 4u, (uint64_t)cus);
+            hipLaunchKernelGGL(k_rerank_dma, dim3(grid), dim3(kRdThreads), 0, s, a.rows, (uint32_t)a.clen, a.norms,
+                               a.q + (uint64_t)b0 * a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R, a.counts + b0,
+                               a.kind, a.scores + (uint64_t)b0 * a.R, a.gate);
+            GVDB_LAUNCH_CHECK();
+        }
+        return hipSuccess;
+    }
     if (a.counts && std::min(a.qlen, a.clen) <= kRsMaxLen && counted) {
         for (uint32_t b0 = 0; b0 < a.B; b0 += kRrMaxB) {
             const uint32_t nb = std::min<uint32_t>(kRrMaxB, a.B - b0);

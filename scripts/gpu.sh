@@ -191,6 +191,7 @@ for t in "${TASKS[@]}"; do
         flatrr)  # flat pass rerank variants (GVDB_RERANK = default | items) at the shard (k 32, B 64) and 10M (k 10, B 256)
             for v in ${RRV:-def items}; do
                 ENVV="GVDB_RERANK=$v"
+                [ "$v" = dma ] && ENVV="GVDB_RERANK_DMA=1"
                 env $ENVV N=1250000 K=32 GVDB_FLAT=i8 BS=64 FLAT_REPS=10 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_frr_$v -o run -- python3 scripts/flat_timing.py > gpurun_out/frr_$v.log 2>&1 || { echo "FAILED $v"; exit 1; }
                 echo "== shard $v"; grep -E "B=|emit" gpurun_out/frr_$v.log | tail -2
                 python3 scripts/trace_summary.py gpurun_out/prof_frr_$v/run_kernel_trace.csv | grep -E "rerank|i8q"
