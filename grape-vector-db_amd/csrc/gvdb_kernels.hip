@@ -3337,7 +3337,7 @@ __global__ __launch_bounds__(kRdThreads, 1) void k_rerank_dma(const float* __res
     {  // items (64 candidates of one query) before query i
         const uint32_t per = (B + kRdThreads - 1) / kRdThreads, b0 = tid * per;
         uint32_t loc = 0;
-        for (uint32_t i = 0; i < per && b0 + i < B; ++i) loc += (min(counts[b0 + i], R) + 63u) / 64u;
+        for (uint32_t i = 0; i < per && b0 + i < B; ++i) loc += ((counts ? min(counts[b0 + i], R) : R) + 63u) / 64u;
         part[tid] = loc;
         __syncthreads();
         for (uint32_t o = 1; o < kRdThreads; o <<= 1) {
@@ -3349,7 +3349,7 @@ __global__ __launch_bounds__(kRdThreads, 1) void k_rerank_dma(const float* __res
         uint32_t run = part[tid] - loc;
         for (uint32_t i = 0; i < per && b0 + i < B; ++i) {
             pre[b0 + i] = run;
-            run += (min(counts[b0 + i], R) + 63u) / 64u;
+            run += ((counts ? min(counts[b0 + i], R) : R) + 63u) / 64u;
         }
         if (tid == kRdThreads - 1) pre[B] = part[tid];
         __syncthreads();
@@ -3368,7 +3368,7 @@ __global__ __launch_bounds__(kRdThreads, 1) void k_rerank_dma(const float* __res
             if (pre[mid] <= item) lo = mid; else hi = mid;
         }
         const uint32_t qi = __builtin_amdgcn_readfirstlane(lo);
-        const uint32_t r0 = (item - pre[qi]) * 64u, Rq = min(counts[qi], R);
+        const uint32_t r0 = (item - pre[qi]) * 64u, Rq = counts ? min(counts[qi], R) : R;
         const uint32_t* srow = s1_rows + (uint64_t)qi * R;
         const uint32_t my_r = r0 + lane;
         const bool live = my_r < Rq;
@@ -3478,22 +3478,22 @@ hipError_t launch_rerank(const RerankArgs& a, hipStream_t s) {
         const char* e = getenv("GVDB_RERANK");
         return !(e && (strcmp(e, "v2") == 0 || strcmp(e, "v1") == 0));
     }();
-    // device-counted lists at D % 32 == 0: k_rerank_dma (flat candidates at the 1.25M-row shard,
+    // lists at D % 32 == 0 (counted or full): k_rerank_dma (flat candidates at the 1.25M-row shard,
     // k = 32, batch 64: 84 -> 38 us; 10M, batch 256: flat group 2.65 -> 2.53 ms); GVDB_RERANK_DMA=0:
     // the item-walking k_rerank_small below (A/B)
     static const bool dma = [] {
         const char* e = getenv("GVDB_RERANK_DMA");
         return !(e && e[0] == '0');
     }();
-    if (dma && a.counts && a.qlen == a.clen && a.clen % 32u == 0 && a.clen <= kRdMaxD &&
+    if (dma && a.qlen == a.clen && a.clen % 32u == 0 && a.clen <= kRdMaxD &&
         (a.kind == kScoreCosine || a.kind == kScoreCosineDistance) && (((uintptr_t)a.q | (uintptr_t)a.rows) & 15u) == 0) {
         for (uint32_t b0 = 0; b0 < a.B; b0 += kRrMaxB) {
             const uint32_t nb = std::min<uint32_t>(kRrMaxB, a.B - b0);
             const uint64_t waves = (uint64_t)nb * ((a.R + 63u) / 64u);
             const uint32_t grid = (uint32_t)std::min<uint64_t>((waves + 3u) / 4u, (uint64_t)cus);
             hipLaunchKernelGGL(k_rerank_dma, dim3(grid), dim3(kRdThreads), 0, s, a.rows, (uint32_t)a.clen, a.norms,
-                               a.q + (uint64_t)b0 * a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R, a.counts + b0,
-                               a.kind, a.scores + (uint64_t)b0 * a.R, a.gate);
+                               a.q + (uint64_t)b0 * a.qlen, a.s1_rows + (uint64_t)b0 * a.R, nb, a.R,
+                               a.counts ? a.counts + b0 : nullptr, a.kind, a.scores + (uint64_t)b0 * a.R, a.gate);
             GVDB_LAUNCH_CHECK();
         }
         return hipSuccess;
