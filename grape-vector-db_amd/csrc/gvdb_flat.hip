@@ -629,17 +629,19 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
                                                       uint32_t N, const uint64_t* __restrict__ ids,
                                                       uint32_t* __restrict__ probes, uint32_t* __restrict__ pcount,
                                                       uint64_t* __restrict__ part, uint32_t chunk) {
-    __shared__ uint64_t keys[256];
+    // Round 5: each lane keeps its own two best keys ((order(score) << 32) | sample
+    // position; 0 = empty) in registers -- no cross-lane work in the scan -- and one LDS
+    // sort of the block's 2048 keys picks the 16.  (The wave-cooperative top-16 it replaces
+    // paid a chain of LDS shuffles per insertion, ~64 of them per wave at the start: 39 us
+    // for 64 queries x 19.5K sampled rows.)  A lane holding three of the block's best 16
+    // keeps two: the probes are then not the exact top 16, which only lowers tau (any 16
+    // real rows bound it) -- more candidates, never a wrong certificate.
+    __shared__ uint64_t keys[2048];
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t P = gridDim.y, s0 = blockIdx.y * chunk, s1 = min(S, s0 + chunk);
-    // wave-cooperative top-16: lanes 0..15 hold the wave's best keys, descending
-    // ((order(score) << 32) | sample position; 0 = empty); a batch of 64 values
-    // costs one compare + ballot unless a lane beats the current 16th key
-    uint64_t mine = 0, t16 = 0;
+    uint64_t k1 = 0, k2 = 0;
     const float* src = smp + (uint64_t)q * S;
-    // 8 values per lane per batch, the next batch loaded while this one is
-    // merged (the scan is latency-bound otherwise: one block per query)
-    constexpr int kU = 8;  // 16 / 32 measured the same (round 3)
+    constexpr int kU = 8;  // values per lane per batch, the next batch in flight
     auto load = [&](uint32_t i0, float (&v)[kU]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -657,29 +659,27 @@ __global__ __launch_bounds__(1024) void k_flat_probes(const float* __restrict__ 
         for (int u = 0; u < kU; ++u) {
             const uint32_t i = i0 + u * 1024u + lane;
             const uint64_t key = vc[u] > -__builtin_inff() ? (((uint64_t)f32_order(vc[u]) << 32) | i) : 0ull;  // NaN / padding -> empty
-            uint64_t m = __ballot(key > t16);
-            while (m) {
-                const uint32_t l = __builtin_ctzll(m);
-                m &= m - 1;
-                const uint64_t kk = __shfl(key, l);
-                if (kk <= t16) continue;
-                if (ids) {  // wave-uniform: one load per insertion (rare after the first batches)
-                    const uint32_t sp = (uint32_t)kk;
-                    const uint32_t row = ((sp >> 8) * every << 8) | (sp & 255u);
-                    if (row < N && ids[row] == kOrphan) continue;
+            if (key > k2) {
+                bool live = true;
+                if (ids) {  // orphan rows are never probes (only when the shard holds any)
+                    const uint32_t row = ((i >> 8) * every << 8) | (i & 255u);
+                    live = !(row < N && ids[row] == kOrphan);
                 }
-                // insert into lanes 0..15: lanes holding a smaller key shift down
-                const uint64_t up = __shfl_up(mine, 1);
-                const bool below = lane < 16 && kk > mine;
-                const bool first = below && (lane == 0 || up >= kk);
-                mine = first ? kk : (below ? up : mine);
-                t16 = __shfl(mine, 15);
+                if (live) {
+                    if (key > k1) {
+                        k2 = k1;
+                        k1 = key;
+                    } else {
+                        k2 = key;
+                    }
+                }
             }
         }
     }
-    if (lane < 16) keys[wv * 16 + lane] = ~mine;  // ascending sort of ~key = descending key
+    keys[2u * tid] = ~k1;  // ascending sort of ~key = descending key
+    keys[2u * tid + 1u] = ~k2;
     __syncthreads();
-    bitonic_sort_lds(keys, 256);  // merge the 16 wave lists
+    bitonic_sort_lds(keys, 2048);
     if (P > 1) {
         if (tid < 16) part[((uint64_t)q * P + blockIdx.y) * 16u + tid] = ~keys[tid];
         return;
