@@ -125,7 +125,7 @@ for t in "${TASKS[@]}"; do
             run 900 gpurun_out/deepprof_10M.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_deep10M -o run -- python3 scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --no-single --oracle-queries 0 --steps 2
             python3 scripts/trace_summary.py gpurun_out/prof_deep10M/run_kernel_trace.csv > gpurun_out/deep10M_kernels.txt ;;
         c3floor)  # c3 per-rank step with the default sample floor vs 131072 / 262144 sample rows (same box)
-            for f in 0 131072 262144; do
+            for f in ${FLOORS:-0 131072 262144}; do
                 GVDB_SAMPLE_FLOOR=$f run 600 gpurun_out/c3floor_$f.log python3 scripts/c3_emulate.py --oracle-queries 0 --steps 20
                 echo "== floor $f"; grep '^\[c3\]' gpurun_out/c3floor_$f.log | tail -2
             done ;;
@@ -238,7 +238,9 @@ for t in "${TASKS[@]}"; do
             run 600 gpurun_out/bm25t.log python3 -u scripts/bm25_timing.py --check
             tail -3 gpurun_out/bm25t.log
             GVDB_BM25_ABL=8 run 600 gpurun_out/bm25clk.log python3 -u scripts/bm25_timing.py --steps 2
-            grep "bm25 prof" gpurun_out/bm25clk.log | tail -2 ;;
+            grep "bm25 prof" gpurun_out/bm25clk.log | tail -2
+            GVDB_BM25_ABL=1 run 600 gpurun_out/bm25norounds.log python3 -u scripts/bm25_timing.py
+            echo "== no rounds (results invalid)"; tail -1 gpurun_out/bm25norounds.log ;;
         c4x2)  # config 4 (10M x 3072, 8 shards) on the TWO-exchange protocol, vs one 10M x 3072 index
             run 1100 gpurun_out/c4x2.log python -u scripts/c3_emulate.py --dim 3072 --oracle-queries 0 --steps 10
             grep '^{' gpurun_out/c4x2.log > gpurun_out/c4x2.json; grep '^\[c3\]' gpurun_out/c4x2.log | tail -4 ;;
