@@ -599,15 +599,35 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_mx(FlatMxArgs a) {
                 asm volatile("s_waitcnt vmcnt(0)" : "+v"(rf[k][0][s]), "+v"(rf[k][1][s]) : : "memory");
     }
     if constexpr (!SAMPLE) {
+        // block-aggregated (k_flat_i8q's flush): ranks within (block, query) by LDS atomics,
+        // one global atomic per (block, query) -- not one per nomination on a shared counter
+        __shared__ uint32_t fl_n[kFxQ], fl_b[kFxQ];
+        constexpr uint32_t kPerT = (kCl + kFxThreads - 1) / kFxThreads;
+        for (uint32_t q = tid; q < kFxQ; q += kFxThreads) fl_n[q] = 0u;
         __syncthreads();
         const uint32_t m = min(cl_n, kCl);
-        for (uint32_t i = tid; i < m; i += kFxThreads) {
-            const uint64_t v = cl[i];
-            const uint32_t q = (uint32_t)(v >> 32);
-            const uint32_t pos = atomicAdd(&a.counts[q], 1u);
-            if (pos < a.candcap) {
-                a.cand[(uint64_t)q * a.candcap + pos] = (uint32_t)v;
-                if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = cs[i];
+        uint32_t rk[kPerT];
+#pragma unroll
+        for (uint32_t j = 0; j < kPerT; ++j) {
+            const uint32_t i = tid + j * kFxThreads;
+            rk[j] = i < m ? atomicAdd(&fl_n[(uint32_t)(cl[i] >> 32)], 1u) : 0u;
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < kFxQ; q += kFxThreads) {
+            const uint32_t c = fl_n[q];
+            if (c) fl_b[q] = atomicAdd(&a.counts[q], c);
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kPerT; ++j) {
+            const uint32_t i = tid + j * kFxThreads;
+            if (i < m) {
+                const uint64_t v = cl[i];
+                const uint32_t q = (uint32_t)(v >> 32), pos = fl_b[q] + rk[j];
+                if (pos < a.candcap) {
+                    a.cand[(uint64_t)q * a.candcap + pos] = (uint32_t)v;
+                    if (a.cscore) a.cscore[(uint64_t)q * a.candcap + pos] = cs[i];
+                }
             }
         }
     }

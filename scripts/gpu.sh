@@ -213,6 +213,13 @@ for t in "${TASKS[@]}"; do
                 GVDB_PROBE_PARTS=$v N=1250000 K=32 GVDB_FLAT=i8 BS=64 FLAT_REPS=10 run 600 gpurun_out/pabs_$v.log python3 scripts/flat_timing.py
                 echo "== shard parts $v"; grep -E "B=|emit" gpurun_out/pabs_$v.log | tail -2
             done ;;
+        flatwide)  # flat pass at D = 3072 (k_flat_mx path) on the config-4 shard, variants: flatwide:base,prevflush
+            IFS=',' read -ra VARS <<< "${FWV:-base,prevflush}"
+            for v in "${VARS[@]}"; do
+                lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib N=1250000 D=3072 K=10 BS=256,64 FLAT_REPS=10 run 600 gpurun_out/flatwide_$v.log python3 scripts/flat_timing.py
+                echo "== $v"; grep -E "B=|emit" gpurun_out/flatwide_$v.log | tail -4
+            done ;;
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
             BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
             grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;
