@@ -797,6 +797,16 @@ struct gvdb_index {
     mutable bool rows_nonfinite = false;
     // adaptive flat tiers: batches left that skip the i8 tier after it failed
     mutable std::atomic<uint32_t> i8_skip{0};
+    // batches skipped after the next i8 failure: doubles per failure (16 .. 4096), back to 16
+    // after an i8 batch certifies -- data whose i8 candidate sets overflow (e.g. i.i.d. rows at
+    // D = 3072, where the spread of cosines is below the int8 margin) stop paying the i8 pass
+    // plus the exact scan every 17th async batch, whose outcome the host learns late
+    mutable std::atomic<uint32_t> i8_backoff{16};
+    void i8_failed() const {
+        const uint32_t b = i8_backoff.load();
+        i8_skip.store(b);
+        i8_backoff.store(std::min<uint32_t>(b * 2u, 4096u));
+    }
     // searches return before their kernels finish: each records an event on
     // its stream after its last read of this index; a mutation waits for those
     // events only (not for the whole device)
@@ -987,11 +997,14 @@ FlagLog& tier_log() {
 }
 void tier_apply(const FlagLog::Rec& r, uint32_t failed) {
     if (r.kind == kTierFlatI8) {
-        if (!failed) return;
+        if (!failed) {
+            if (r.ix) r.ix->i8_backoff.store(16);
+            return;
+        }
         flat_fallbacks_i8().fetch_add(1);
         flat_fallbacks().fetch_add(1);  // the async form's next tier is the exact scan
         const char* fk = getenv("GVDB_FLAT");
-        if (r.ix && !(fk && strcmp(fk, "i8") == 0)) r.ix->i8_skip.store(16);
+        if (r.ix && !(fk && strcmp(fk, "i8") == 0)) r.ix->i8_failed();
     } else if (r.kind == kTierFlatBf16) {
         if (failed) flat_fallbacks().fetch_add(1);
     } else {
@@ -1648,9 +1661,13 @@ static gvdb_status index_search_impl(const gvdb_index* ix, const float* d_q, uin
         if (try_i8) {
             gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
                                             d_n, ws, s, true, &certified);
-            if (st != GVDB_OK || certified) return st;
+            if (st != GVDB_OK) return st;
+            if (certified) {
+                ix->i8_backoff.store(16);
+                return st;
+            }
             flat_fallbacks_i8().fetch_add(1);
-            if (!force_i8) ix->i8_skip.store(16);
+            if (!force_i8) ix->i8_failed();
         }
         gvdb_status st = flat_mx_search(ix, d_q, (uint32_t)B, dim, (uint32_t)k, kind, descending, d_ids, d_scores,
                                         d_n, ws, s, false, &certified);

@@ -220,6 +220,13 @@ for t in "${TASKS[@]}"; do
                 GVDB_LIB_PATH=$lib N=1250000 D=3072 K=10 BS=256,64 FLAT_REPS=10 run 600 gpurun_out/flatwide_$v.log python3 scripts/flat_timing.py
                 echo "== $v"; grep -E "B=|emit" gpurun_out/flatwide_$v.log | tail -4
             done ;;
+        flatwidestats)  # candidate counts of the flat tiers at 1.25M x 3072 (variant abl/libgvdb_fstats.so)
+            for tier in i8 bf16; do
+                for b in 64 256; do
+                    GVDB_FLAT=$tier GVDB_LIB_PATH=$PWD/grape-vector-db_amd/abl/libgvdb_fstats.so N=1250000 D=3072 K=10 BS=$b FLAT_REPS=1 run 600 gpurun_out/fws_${tier}_$b.log python3 scripts/flat_timing.py
+                    echo "== $tier B=$b"; grep -E "flatstats|B=" gpurun_out/fws_${tier}_$b.log | sort | uniq -c | sort -rn | head -6
+                done
+            done ;;
         flatprof)  # exact flat search at 10M x 768, batch 256, per-dispatch kernel trace
             BS=256 FLAT_REPS=5 run 600 gpurun_out/flatprof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flat -o run -- python3 scripts/flat_timing.py
             grep -E "B=|emit" gpurun_out/flatprof.log | tail -3 ;;
