@@ -142,30 +142,65 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
     const uint64_t* mine = glist(me);
     // round A: every read that depends on nothing else, issued together -- the
     // counts, this rank's keys (d parked in opos), the other lists' distances,
-    // the query row
+    // the query row.  The first kP2Threads / 4 kP2Threads items of each go to
+    // registers before any LDS store, so their latencies overlap (a load-then-store
+    // loop waits out each load); the loops past them only run for large G / R / D
+    const uint32_t GR = G * R;
+    constexpr uint32_t kA = 4u;
+    // unpredicated loads (clamped indices, always in bounds; the unused values are masked
+    // at the stores): a predicated load sits in its own branch and the stores' waits
+    // interleave with the remaining loads
+    const uint32_t cg0 = gathered[(uint64_t)min(tid, G - 1u) * words1 + 2ull * B * R + q];
+    const uint64_t key0 = mine[min(tid, R - 1u)];
+    uint32_t dv[kA];
+    float qx[kA];
+    const float* qg = queries + (uint64_t)q * D;
+#pragma unroll
+    for (uint32_t u = 0; u < kA; ++u) {
+        const uint32_t x = min(tid + u * kP2Threads, GR - 1u), g = x / R;
+        // the distance is the key's high word
+        if constexpr (DSTAGED) dv[u] = gathered[(uint64_t)g * words1 + 2ull * ((uint64_t)q * R + (x - g * R)) + 1u];
+        qx[u] = qg[min(tid + u * kP2Threads, D - 1u)];
+    }
     if (tid == 0) {
         s_total = 0u;
         s_c = 0u;
         s_nan = 0u;
     }
     __syncthreads();
-    for (uint32_t g = tid; g < G; g += kP2Threads) {
-        const uint32_t c = min(gathered[(uint64_t)g * words1 + 2ull * B * R + q], R);
+    auto put_cg = [&](uint32_t g, uint32_t c) __attribute__((always_inline)) {
+        c = min(c, R);
         cg[g] = g == me && !rows ? 0u : c;  // a shard that cannot rerank sent nothing
         atomicAdd(&s_total, c);
-    }
-    for (uint32_t i = tid; i < R; i += kP2Threads) {  // the block holds R key slots per query
-        const uint64_t key = mine[i];
+    };
+    auto put_key = [&](uint32_t i, uint64_t key) __attribute__((always_inline)) {  // R key slots per query
         opos[i] = (uint32_t)(key >> 32);
         orow[i] = (uint32_t)key;
-    }
-    if constexpr (DSTAGED)
-        for (uint32_t x = tid; x < G * R; x += kP2Threads) {
+    };
+    if (tid < G) put_cg(tid, cg0);
+    if (tid < R) put_key(tid, key0);
+    for (uint32_t g = tid + kP2Threads; g < G; g += kP2Threads) put_cg(g, gathered[(uint64_t)g * words1 + 2ull * B * R + q]);
+    for (uint32_t i = tid + kP2Threads; i < R; i += kP2Threads) put_key(i, mine[i]);
+    if constexpr (DSTAGED) {
+#pragma unroll
+        for (uint32_t u = 0; u < kA; ++u) {
+            const uint32_t x = tid + u * kP2Threads;
+            if (x < GR && x / R != me) dist[x] = dv[u];
+        }
+        for (uint32_t x = tid + kA * kP2Threads; x < GR; x += kP2Threads) {
             const uint32_t g = x / R, i = x - g * R;
             if (g != me) dist[x] = (uint32_t)(glist(g)[i] >> 32);
         }
-    const float* qg = queries + (uint64_t)q * D;
-    for (uint32_t j = tid; j < D; j += kP2Threads) {
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kA; ++u) {
+        const uint32_t j = tid + u * kP2Threads;
+        if (j < D) {
+            qv[j] = qx[u];
+            qsq[j] = qx[u] * qx[u];
+        }
+    }
+    for (uint32_t j = tid + kA * kP2Threads; j < D; j += kP2Threads) {
         const float v = qg[j];
         qv[j] = v;
         qsq[j] = v * v;
@@ -188,22 +223,33 @@ __global__ __launch_bounds__(kP2Threads) void k_shard_phase2(const uint32_t* __r
     float4 xr[kP2F4];
     constexpr bool vec = VEC;  // D % 4 == 0: 16-B row loads and LDS folds (a compile-time choice: clean loads)
     auto load = [&](uint32_t r0, uint32_t nr, uint32_t ch) __attribute__((always_inline)) {
+        if constexpr (VEC) {
+            // unpredicated: rows past nr re-read row nr - 1 and dimensions past D the last
+            // float4 (no fold reads those slots), so every orow read and every row load is
+            // issued back to back instead of one branch (and one LDS wait) per load
+            if (nr == 0u) return;
+            uint32_t rr[kP2F4];
 #pragma unroll
-        for (uint32_t e = 0; e < kP2F4; ++e) {
-            const uint32_t L = tid + e * kP2Threads, r = L / (kP2Ch / 4), j = ch * kP2Ch + 4u * (L % (kP2Ch / 4));
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (r < nr && j < D) {
-                const float* src = rows + (uint64_t)orow[r0 + r] * D + j;
-                if constexpr (VEC) {
-                    v = *(const float4*)src;
-                } else {
+            for (uint32_t e = 0; e < kP2F4; ++e) rr[e] = orow[r0 + min((tid + e * kP2Threads) / (kP2Ch / 4), nr - 1u)];
+#pragma unroll
+            for (uint32_t e = 0; e < kP2F4; ++e) {
+                const uint32_t L = tid + e * kP2Threads, j = min(ch * kP2Ch + 4u * (L % (kP2Ch / 4)), D - 4u);
+                xr[e] = *(const float4*)(rows + (uint64_t)rr[e] * D + j);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t e = 0; e < kP2F4; ++e) {
+                const uint32_t L = tid + e * kP2Threads, r = L / (kP2Ch / 4), j = ch * kP2Ch + 4u * (L % (kP2Ch / 4));
+                float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (r < nr && j < D) {
+                    const float* src = rows + (uint64_t)orow[r0 + r] * D + j;
                     v.x = src[0];
                     if (j + 1 < D) v.y = src[1];
                     if (j + 2 < D) v.z = src[2];
                     if (j + 3 < D) v.w = src[3];
                 }
+                xr[e] = v;
             }
-            xr[e] = v;
         }
     };
     const uint32_t nr0 = min(cnt_me, kP2Rows);
