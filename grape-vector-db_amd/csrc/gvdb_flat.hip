@@ -762,6 +762,91 @@ __global__ __launch_bounds__(256) void k_flat_tau(const float* __restrict__ psco
     thr[q] = (c >= mk ? v[mk - 1] : -__builtin_inff()) - qd[q];
 }
 
+// Block-wide ranks of the kk smallest 64-bit keys (one key per thread of a
+// 1024-thread block, ~0ull = no key, the others distinct; kk <= 64).  Each wave
+// sorts its 64 keys in registers (bitonic over lane shuffles), the sorted runs go
+// to runs[]; the key at position p of run w has block rank p plus, over the other
+// live runs, the number of their keys below it (a 6-step binary search of a 64-key
+// run), one (w, p, run) triple per thread -- only p < kk can rank below kk.  On
+// return rk[64 w + p] is that rank for p < kk (~0u otherwise).
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
+    const uint32_t lo = __shfl_xor((uint32_t)x, m), hi = __shfl_xor((uint32_t)(x >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void block_rank_smallest(uint64_t key, uint32_t kk, uint32_t nw, uint64_t* runs,
+                                                    uint32_t* rk) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+#pragma unroll
+    for (uint32_t k2 = 2; k2 <= 64; k2 <<= 1)
+#pragma unroll
+        for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+            const uint64_t y = shfl_xor_u64(key, (int)j);
+            const bool keep_min = ((lane & j) == 0u) == ((lane & k2) == 0u);
+            key = keep_min ? (key < y ? key : y) : (key < y ? y : key);
+        }
+    runs[tid] = key;
+    rk[tid] = lane < kk && key != ~0ull ? lane : ~0u;
+    __syncthreads();
+    const uint32_t npairs = nw * kk * nw;
+    for (uint32_t t = tid; t < npairs; t += blockDim.x) {
+        const uint32_t v = t % nw, wp = t / nw, p = wp % kk, w = wp / kk;
+        if (v == w) continue;
+        const uint64_t x = runs[w * 64u + p];
+        if (x == ~0ull) continue;
+        const uint64_t* r = runs + v * 64u;
+        uint32_t pos = 0;
+#pragma unroll
+        for (uint32_t st = 32; st > 0; st >>= 1)
+            if (r[pos + st - 1u] < x) pos += st;
+        pos += r[pos] < x ? 1u : 0u;
+        if (pos) atomicAdd(&rk[w * 64u + p], pos);
+    }
+    __syncthreads();
+}
+
+// One LDS counter reservation per wave: the position of this lane's entry among
+// the keeping lanes (the caller's list is unordered).  Every lane of the wave calls it.
+__device__ __forceinline__ uint32_t wave_append(bool keep, uint32_t* ctr) {
+    const uint64_t m = __ballot(keep);
+    if (m == 0ull) return 0u;
+    const uint32_t lane = threadIdx.x & 63u, lead = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)lead);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// The kk smallest of up to 8 keys per thread (lists up to 8192 = kFxCandCap
+// entries): T = the kk-th smallest of the threads' own minima bounds the
+// kk-th smallest key from above (kk threads hold a key <= T), and only those kk
+// threads can hold keys <= T, so at most 8 kk <= 512 keys survive the filter; they
+// are compacted into surv[] and ranked again.  On return runs[] / rk[] are the
+// second pass's (rk[t] = the block rank of runs[t] for the kk smallest).
+template <int P>  // kk >= 1
+__device__ __forceinline__ void block_smallest_multi(const uint64_t (&key)[P], uint32_t kk, uint32_t c, uint64_t* runs,
+                                                     uint32_t* rk, uint64_t* surv, uint32_t* s_n, uint64_t* s_T) {
+    const uint32_t tid = threadIdx.x;
+    uint64_t m = key[0];
+#pragma unroll
+    for (int j = 1; j < P; ++j) m = key[j] < m ? key[j] : m;
+    if (tid == 0) {
+        *s_n = 0u;
+        *s_T = ~0ull - 1u;  // fewer than kk live minima: every live key survives
+    }
+    block_rank_smallest(m, kk, (min(c, blockDim.x) + 63u) / 64u, runs, rk);
+    if (rk[tid] == kk - 1u) *s_T = runs[tid];
+    __syncthreads();
+    const uint64_t T = *s_T;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const uint32_t pos = wave_append(key[j] <= T, s_n);
+        if (key[j] <= T) surv[pos] = key[j];
+    }
+    __syncthreads();
+    const uint32_t n = *s_n;
+    block_rank_smallest(tid < n ? surv[tid] : ~0ull, kk, (n + 63u) / 64u, runs, rk);
+}
+
 // Candidate pruning between the emit pass and the exact rerank.  Each
 // nomination carries its approx score v, and the emit pass's own bound puts the
 // exact f32 cosine in [v - m, v + m], m = qa*rho_x + qd (bf16: m = qd).  With L
@@ -861,19 +946,22 @@ __global__ __launch_bounds__(kPrThreads) void k_flat_prune(uint32_t* __restrict_
     // every entry is in registers: compact in place
 #pragma unroll
     for (uint32_t j = 0; j < kPrPer; ++j) {
-        if (ub[j] >= L) {  // -inf (orphans, empty slots) never passes a finite L; -inf L keeps the live rows
-            if (!(ub[j] == -__builtin_inff())) {
-                const uint32_t pos = atomicAdd(&out_n, 1u);
-                cand[(uint64_t)q * candcap + pos] = row[j];
-            }
-        }
+        // -inf (orphans, empty slots) never passes a finite L; -inf L keeps the live rows
+        const bool keep = ub[j] >= L && !(ub[j] == -__builtin_inff());
+        const uint32_t pos = wave_append(keep, &out_n);
+        if (keep) cand[(uint64_t)q * candcap + pos] = row[j];
     }
     __syncthreads();
     if (tid == 0) counts[q] = out_n;
 }
 
-// Per query: sort the reranked candidates (exact score, then row ascending),
-// certify, emit the first k live rows.
+// Per query: order the reranked candidates by (exact score, then row ascending),
+// certify, emit the first k live rows.  k <= 64: orphans become the ~0
+// sentinel (their ids loaded in parallel), block_smallest_multi ranks the first
+// k keys and a live key of rank r < k is output r (shard flat pass, k = 32:
+// 34.5 -> 25.0 us).  The first version sorted the keys bitonically and walked them
+// on thread 0, one dependent ids[] load per emitted row; k > 64 keeps that form.
+// (The same selection for k_flat_prune's L measured 27.7 -> 38.2 us: not used.)
 __global__ __launch_bounds__(1024) void k_flat_final(const uint32_t* __restrict__ counts,
                                                     const uint32_t* __restrict__ cand, uint32_t candcap,
                                                     const float* __restrict__ scores, const float* __restrict__ thr,
@@ -881,29 +969,74 @@ __global__ __launch_bounds__(1024) void k_flat_final(const uint32_t* __restrict_
                                                     const uint64_t* __restrict__ ids, uint64_t* __restrict__ out_ids,
                                                     float* __restrict__ out_scores, uint32_t* __restrict__ out_n,
                                                     uint32_t* __restrict__ fail) {
-    __shared__ uint64_t keys[kFxCandCap];
+    __shared__ __attribute__((aligned(16))) uint64_t keys[kFxCandCap];
+    __shared__ uint32_t s_live;
+    __shared__ float s_last;
     const uint32_t q = blockIdx.x, tid = threadIdx.x;
     const uint32_t c = counts[q];
     if (c > candcap) {  // overflow: not certifiable
         if (tid == 0) atomicOr(fail, 1u);
         return;
     }
-    const uint32_t P = next_pow2(c < 2u ? 2u : c);
-    for (uint32_t i = tid; i < P; i += blockDim.x) {
-        if (i < c) {
-            const float sc = scores[(uint64_t)q * candcap + i];
-            const uint32_t o = descending ? ~f32_order(sc) : f32_order(sc);
-            keys[i] = ((uint64_t)o << 32) | cand[(uint64_t)q * candcap + i];
-        } else {
-            keys[i] = ~0ull;
+    uint32_t got = 0;
+    float last = 0.0f;
+    if (k >= 1u && k <= 64u) {
+        constexpr int kFP = (int)(kFxCandCap / 1024u);
+        uint64_t mk[kFP];
+#pragma unroll
+        for (int j = 0; j < kFP; ++j) {
+            const uint32_t i = tid + (uint32_t)j * 1024u;
+            mk[j] = ~0ull;
+            if (i < c) {
+                const float sc = scores[(uint64_t)q * candcap + i];
+                const uint32_t row = cand[(uint64_t)q * candcap + i];
+                const uint32_t o = descending ? ~f32_order(sc) : f32_order(sc);
+                if (!(ids && ids[row] == kOrphan)) mk[j] = ((uint64_t)o << 32) | row;
+            }
         }
-    }
-    __syncthreads();
-    bitonic_sort_lds(keys, P);
-    if (tid == 0) {
+        if (tid == 0) {
+            s_live = 0;
+            s_last = 0.0f;
+        }
+        __syncthreads();
+        uint32_t nl = 0;
+#pragma unroll
+        for (int j = 0; j < kFP; ++j) nl += mk[j] != ~0ull ? 1u : 0u;
+        if (nl) atomicAdd(&s_live, nl);
+        uint32_t* rk = (uint32_t*)(keys + 1024);
+        uint64_t* surv = keys + 1536;
+        uint32_t* s_n = (uint32_t*)(keys + 2048);
+        uint64_t* s_T = keys + 2049;
+        block_smallest_multi<kFP>(mk, k, c, keys, rk, surv, s_n, s_T);  // its barriers publish s_live
+        got = min(k, s_live);
+        const uint32_t r = rk[tid];
+        if (r < got) {
+            const uint64_t x = keys[tid];
+            const uint32_t row = (uint32_t)x;
+            const uint32_t o = descending ? ~(uint32_t)(x >> 32) : (uint32_t)(x >> 32);
+            const float sc = __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+            out_ids[(uint64_t)q * k + r] = ids ? ids[row] : row;
+            out_scores[(uint64_t)q * k + r] = sc;
+            if (r + 1u == got) s_last = sc;
+        }
+        __syncthreads();
+        if (tid != 0) return;
+        last = s_last;
+    } else {
+        const uint32_t P = next_pow2(c);
+        for (uint32_t i = tid; i < P; i += blockDim.x) {
+            if (i < c) {
+                const float sc = scores[(uint64_t)q * candcap + i];
+                const uint32_t o = descending ? ~f32_order(sc) : f32_order(sc);
+                keys[i] = ((uint64_t)o << 32) | cand[(uint64_t)q * candcap + i];
+            } else {
+                keys[i] = ~0ull;
+            }
+        }
+        __syncthreads();
+        bitonic_sort_lds(keys, P);
+        if (tid != 0) return;
         // first k live rows; the k-th one's exact score certifies the list
-        uint32_t got = 0;
-        float last = 0.0f;
         for (uint32_t i = 0; i < c && got < k; ++i) {
             const uint32_t row = (uint32_t)keys[i];
             const uint64_t id = ids ? ids[row] : row;
@@ -915,13 +1048,13 @@ __global__ __launch_bounds__(1024) void k_flat_final(const uint32_t* __restrict_
             out_scores[(uint64_t)q * k + got] = last;
             ++got;
         }
-        // cosine (descending): rows never nominated score < T + eps.  Cosine
-        // distance (ascending): their distance > 1 - (T + eps) up to one rounding.
-        const float cos_k = descending ? last : 1.0f - last;
-        const bool ok = k == 0 || (got == k && cos_k >= thr[q] + qd[q]);  // thr + qd = tau
-        if (!ok) atomicOr(fail, 1u);
-        if (out_n) out_n[q] = got;  // out_n is optional (gvdb_index_search_device)
     }
+    // thread 0: cosine (descending): rows never nominated score < T + eps.  Cosine
+    // distance (ascending): their distance > 1 - (T + eps) up to one rounding.
+    const float cos_k = descending ? last : 1.0f - last;
+    const bool ok = k == 0 || (got == k && cos_k >= thr[q] + qd[q]);  // thr + qd = tau
+    if (!ok) atomicOr(fail, 1u);
+    if (out_n) out_n[q] = got;  // out_n is optional (gvdb_index_search_device)
 }
 
 }  // namespace

@@ -241,6 +241,12 @@ for t in "${TASKS[@]}"; do
                 GVDB_DEEP_EARLY=$v run 900 gpurun_out/deepearly_$v.log python3 -u scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --steps 3 --oracle-queries 0 --no-single
                 echo "== early $v"; grep '\[c3\]' gpurun_out/deepearly_$v.log | tail -2
             done ;;
+        deepab)  # deep 10M (R = 1M, batch 64) per-rank step, VARIANTS (abl/libgvdb_NAME.so, "base" = product), one box
+            for v in ${VARIANTS:-base}; do
+                lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib run 900 gpurun_out/deepab_$v.log python3 -u scripts/c3_emulate.py --n 10000000 --R 1000000 --batch 64 --steps 3 --oracle-queries 0 --no-single
+                echo "== $v $(grep 'per-rank step' gpurun_out/deepab_$v.log)"
+            done ;;
         mx4var:*)  # k_scan_mx4 build variants at 10M x 3072 (b256_timing, one box): mx4var:base,ch8,...
             IFS=',' read -ra VARS <<< "${t#mx4var:}"
             for v in "${VARS[@]}"; do
