@@ -267,14 +267,20 @@ void plan_sampling(uint32_t N, uint32_t R, uint32_t sample_div, uint32_t& chunks
         bufcap = std::min<uint64_t>(N, 8ull * R + 2048ull);
         return;
     }
-    // GVDB_SAMPLE_FLOOR: minimum sample rows (timing experiments).  Default kExactN / 4:
-    // at the 8-GPU shard (1.25M rows) 64K sample rows measured fastest (per-rank step
-    // 0.300 -> 0.282 ms; 131K / 32K / 16K slower: sample pass vs looser threshold)
-    static const uint64_t floor_rows = [] {
+    // GVDB_SAMPLE_FLOOR: minimum sample rows (timing experiments).  Default kExactN / 4
+    // (64K): at the 8-GPU shard (1.25M rows) the fastest in round 3 (per-rank step
+    // 0.300 -> 0.282 ms).  For R <= 1000, kExactN / 8: with round 5's fused FP4 sample
+    // pass and cheaper emits 32K is faster (config-3 per rank 0.1525 -> 0.1491 ms mean,
+    // 1M x 768 batch 256 0.161 -> 0.158 ms; twice each on one box,
+    // profiles/r05/c3/c3floor_r05.log).  Deeper R keeps 64K: its target-th sampled
+    // distance sits in a sparser histogram at 32K, so the dense form's 16-row group
+    // minima loosen the threshold more often (test_sample_histogram_mfma_thresholds_equal_valu)
+    static const uint64_t floor_env = [] {
         const char* e = getenv("GVDB_SAMPLE_FLOOR");
         const long long v = e ? atoll(e) : 0;
-        return v >= 4096 ? (uint64_t)v : (uint64_t)(kExactN / 4);
+        return v >= 4096 ? (uint64_t)v : 0ull;
     }();
+    const uint64_t floor_rows = floor_env ? floor_env : (uint64_t)(R <= 1000u ? kExactN / 8 : kExactN / 4);
     uint64_t S = std::max<uint64_t>(floor_rows, N / sample_div);
     chunks = (uint32_t)(S / 4096u);
     stride = N / chunks;  // >= 4096: chunks never overlap
