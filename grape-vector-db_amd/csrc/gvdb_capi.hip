@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -593,7 +594,12 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     const ShardView& v = a.v;
     const uint32_t B = a.B, R = a.R;
     if (B == 0) return GVDB_OK;
-    if (a.gate && (R <= kSelectLdsCap || !a.dims_match || a.d_out_dist || a.row_map))
+    // the batched large-R path (gvdb_bigr.hip): unordered exact top-R + k_topk_big
+    const bool big = R > kSelectLdsCap && a.dims_match && v.D > 0 && v.D < 4096 && R <= kBigRMax && a.kout <= 1024 &&
+                     !a.d_out_dist && !getenv_flag("GVDB_BIGR_OFF");
+    // a gated search (the device-side fallback of deep_cert_search) exists only on the large-R
+    // path: only its launches honour the gate
+    if (a.gate && (!big || a.row_map))
         return fail(GVDB_ERR_INVALID_ARGUMENT, "gated search: the large-R path only");
     if (R == 0) {
         if (a.d_out_n) HIP_TRY(hipMemsetAsync(a.d_out_n, 0, (size_t)B * 4, s), "memset out_n");
@@ -606,9 +612,6 @@ gvdb_status bq_search(const BqSearchArgs& a, Workspace& ws, hipStream_t s) {
     HIP_TRY(ws.qnorm.ensure((size_t)B * 4), "alloc qnorm");
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
     HIP_TRY(ws.scores.ensure((size_t)B * R * 4), "alloc scores");
-    // the batched large-R path (gvdb_bigr.hip): unordered exact top-R + k_topk_big
-    const bool big = R > kSelectLdsCap && a.dims_match && v.D > 0 && v.D < 4096 && R <= kBigRMax && a.kout <= 1024 &&
-                     !a.d_out_dist && !getenv_flag("GVDB_BIGR_OFF");
     Stage1Args s1{};
     gvdb_status pst =
         prepare_stage1(ws, s1, B, v.D, R, v.N, s, a.dims_match && v.D > 0 && (R <= kSelectLdsCap || big));
@@ -751,7 +754,9 @@ gvdb_status check_poisoned(const uint32_t* h_n, uint64_t B) {
 // the search's event has completed (tier_poll, at the next search): never
 // waited for (the diagnostics getters wait, a destroyed index's records are
 // dropped).  One process-wide log.
-enum TierKind : int { kTierFlatI8 = 0, kTierFlatBf16 = 1, kTierDeepCert = 2 };
+// kTierDeepFlatI8: the i8 flat pass inside the async certified default depth (its failure
+// drives the index's i8 skip and backoff like a FLAT-mode i8 batch; counters untouched)
+enum TierKind : int { kTierFlatI8 = 0, kTierFlatBf16 = 1, kTierDeepCert = 2, kTierDeepFlatI8 = 3 };
 struct FlagLog {
     static constexpr uint32_t kSlots = 256;
     std::mutex mu;
@@ -808,6 +813,12 @@ struct gvdb_index {
     // D = 3072, where the spread of cosines is below the int8 margin) stop paying the i8 pass
     // plus the exact scan every 17th async batch, whose outcome the host learns late
     mutable std::atomic<uint32_t> i8_backoff{16};
+    // concurrent batch-1 host-buffer searches (the reference's many readers of
+    // Arc<RwLock<dyn VectorIndex>>, lib.rs:238) share batched searches: see b1_coalesced
+    mutable std::mutex b1_mu;
+    mutable std::condition_variable b1_cv;
+    mutable std::vector<struct B1Req*> b1_pend;  // arrival order
+    mutable bool b1_exec = false;
     void i8_failed() const {
         const uint32_t b = i8_backoff.load();
         i8_skip.store(b);
@@ -1013,6 +1024,13 @@ void tier_apply(const FlagLog::Rec& r, uint32_t failed) {
         if (r.ix && !(fk && strcmp(fk, "i8") == 0)) r.ix->i8_failed();
     } else if (r.kind == kTierFlatBf16) {
         if (failed) flat_fallbacks().fetch_add(1);
+    } else if (r.kind == kTierDeepFlatI8) {
+        const char* fk = getenv("GVDB_FLAT");
+        if (!r.ix || (fk && strcmp(fk, "i8") == 0)) return;
+        if (failed)
+            r.ix->i8_failed();
+        else
+            r.ix->i8_backoff.store(16);
     } else {
         deep_cert_count(failed ? 1 : 0).fetch_add(1);
     }
@@ -1043,8 +1061,13 @@ gvdb_status tier_record(const gvdb_index* ix, const uint32_t* d_word, int kind, 
     FlagLog& L = tier_log();
     std::lock_guard<std::mutex> g(L.mu);
     if (!L.h) HIP_TRY(hipHostMalloc((void**)&L.h, FlagLog::kSlots * 4, hipHostMallocDefault), "alloc tier log");
-    if (L.pend.size() >= FlagLog::kSlots) {  // a full log drops its oldest record (diagnostics only)
-        L.spare.push_back(L.pend.front().ev);
+    if (L.pend.size() >= FlagLog::kSlots) {
+        // a full log: the oldest record's slot is the one the new record takes (slots are
+        // handed out in order), so its copy must have landed before the slot is reused --
+        // wait for it and apply it rather than dropping it
+        const FlagLog::Rec& r = L.pend.front();
+        if (hipEventSynchronize(r.ev) == hipSuccess) tier_apply(r, L.h[r.slot]);
+        L.spare.push_back(r.ev);
         L.pend.erase(L.pend.begin());
     }
     hipEvent_t ev = nullptr;
@@ -1471,8 +1494,8 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     const char* env = getenv("GVDB_DEEP_CERT");
     if ((env && env[0] == '0') || kind != kScoreCosine || k == 0 || k > 32 || B == 0 || N < kFxMinN ||
         R <= kSelectLdsCap || R > N || R > kBigRMax || dim == 0 || dim >= 4096 || !mfma_scan_supported(W4) ||
-        (uint64_t)R * 64u < N || ix->n != ix->id_row.size())
-        return GVDB_OK;
+        (uint64_t)R * 64u < N || ix->n != ix->id_row.size() || (!sync && getenv_flag("GVDB_BIGR_OFF")))
+        return GVDB_OK;  // (async: the gated fallback below needs bq_search's large-R path)
     Stage1Args s1{};
     gvdb_status pst = prepare_stage1(ws, s1, B, dim, R, N, s, true, false);
     if (pst != GVDB_OK) return pst;
@@ -1528,7 +1551,7 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     }
     UseGuard ug2{ix, s2};
     HIP_TRY(launch_stage1_fast(s1, s), "certified depth: stage 1");
-    bool cert = false;
+    bool cert = false, i8_tier = false;
     uint32_t* flat_fail = nullptr;
     gvdb_status st;
     if (sync) {
@@ -1539,9 +1562,15 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
             if (st != GVDB_OK) return st;
         }
     } else {  // one tier (i8, or bf16 while the index skips i8), its failure word read on the device
-        const bool i8 = ix->i8_skip.load() == 0;
-        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, i8, &cert, true, &flat_fail);
+        i8_tier = ix->i8_skip.load() == 0;
+        st = flat_mx_search(ix, d_q, B, dim, K2, kind, 1, frow, fsc, fn, *ws2, s2, i8_tier, &cert, true, &flat_fail);
         if (st != GVDB_OK) return st;
+    }
+    uint32_t* ffail = dfail + 1;  // the flat tier's failure word, copied into THIS call's workspace
+    if (!sync) {
+        // ws2 returns to the pool when this call returns and its next user may clear its words before
+        // the certify pass (on s) has read them: copy the word out on s2, ahead of the join event
+        HIP_TRY(hipMemcpyAsync(ffail, flat_fail, 4, hipMemcpyDeviceToDevice, s2), "flat failure word");
     }
     if (s2 != s) {
         HIP_TRY(hipEventRecord(e_flat.e, s2), "event");
@@ -1554,7 +1583,7 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     HIP_TRY(hipMemsetAsync(dfail, 0, 4, s), "memset certify flag");
     HIP_TRY(launch_deep_certify(frow, fsc, fn, K2, tcut, ix->codes, ix->cap, W4, ws.qcodes.as<uint4>(), B, k, R,
                                 ix->ids, d_ids, d_scores, d_n, dfail, s, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                0, flat_fail),
+                                0, sync ? nullptr : ffail),
             "certified depth: certify");
     if (sync) {
         HIP_TRY(hipMemcpyAsync(ws.h_flags, dfail, 4, hipMemcpyDeviceToHost, s), "certify flag");
@@ -1583,6 +1612,7 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     st = bq_search(a, ws, s);
     if (st != GVDB_OK) return st;
     if ((st = tier_record(ix, dfail, kTierDeepCert, s)) != GVDB_OK) return st;
+    if (i8_tier && (st = tier_record(ix, ffail, kTierDeepFlatI8, s)) != GVDB_OK) return st;
     *done = true;
     return GVDB_OK;
 }
@@ -1715,13 +1745,12 @@ static gvdb_status check_search(const gvdb_index* ix, uint32_t dim, uint64_t B, 
     return GVDB_OK;
 }
 
-gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64_t B, uint32_t dim, uint64_t k,
-                              const gvdb_search_params* sp, uint64_t* out_ids, float* out_scores, uint32_t* out_n) {
-    gvdb_status st = check_search(ix, dim, B, k);
+// one host-buffer search of B queries (arguments already checked)
+static gvdb_status index_search_host(const gvdb_index* ix, const float* queries, uint64_t B, uint32_t dim,
+                                     uint64_t k, const gvdb_search_params* sp, uint64_t* out_ids, float* out_scores,
+                                     uint32_t* out_n) {
+    gvdb_status st = set_device(ix->device);
     if (st != GVDB_OK) return st;
-    if (B == 0) return GVDB_OK;
-    if (!queries || !out_n || (k && (!out_ids || !out_scores))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
-    if ((st = set_device(ix->device)) != GVDB_OK) return st;
     WsGuard g(ix->device);
     if (!g.w) return fail(GVDB_ERR_DEVICE, "workspace");
     Workspace& ws = *g.w;
@@ -1746,6 +1775,125 @@ gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64
     HIP_TRY(hipStreamSynchronize(s), "sync");
     zero_past_counts(out_ids, out_scores, out_n, B, k);
     return check_poisoned(out_n, B);
+}
+
+// Built-in coalescing of concurrent batch-1 host-buffer searches.  The reference
+// serves single-query searches from many concurrent readers of
+// Arc<RwLock<dyn VectorIndex>> (lib.rs:238), each running
+// HnswVectorIndex::search(q, k) (index.rs:212-231).  On the GPU a batch-1 search
+// reads the whole code array once (k_b1_scan, HBM-bound), and independent batch-1
+// searches from many threads each take a pooled workspace with its own stream --
+// 64 callers put 64 streams on the 4 hardware queues (2.1K QPS, p99 92 ms in round 5).
+// So a B = 1 call joins the index's pending list; whenever no coalesced batch is
+// executing, the first waiting caller takes the oldest pending request and every
+// later one with the same (k, params) (up to kB1MaxBatch) and runs them as ONE
+// index_search_host, then hands each caller its own results.  No timer: a lone
+// caller leads its own batch of one at once; batches grow with the load.  Every
+// search mode is exact, so a query's answer does not depend on its batch
+// (tests/test_gpu_concurrent.py, test_gpu_coalesce.py).  GVDB_B1_COALESCE=0 turns
+// it off (every call runs alone).
+struct B1Req {
+    const float* q;
+    uint64_t k;
+    bool has_sp;
+    gvdb_search_params sp;
+    uint64_t* ids;
+    float* scores;
+    uint32_t* n;
+    gvdb_status st = GVDB_OK;
+    std::string err;
+    bool taken = false, done = false;
+    bool same_batch(const B1Req& o) const {
+        return k == o.k && has_sp == o.has_sp &&
+               (!has_sp || (sp.mode == o.sp.mode && sp.metric == o.sp.metric &&
+                            sp.rescore_count == o.sp.rescore_count && sp.rescore_ratio == o.sp.rescore_ratio &&
+                            sp.reserved == o.sp.reserved));
+    }
+};
+constexpr size_t kB1MaxBatch = 256;
+std::atomic<uint64_t> g_b1_batches{0}, g_b1_queries{0}, g_b1_max{0};  // gvdb_debug_b1_coalesce
+
+static void b1_run_batch(const gvdb_index* ix, uint32_t dim, const std::vector<B1Req*>& reqs) {
+    const size_t B = reqs.size();
+    const uint64_t k = reqs[0]->k;
+    std::vector<float> q(B * (size_t)dim);
+    for (size_t i = 0; i < B; ++i) memcpy(q.data() + i * dim, reqs[i]->q, (size_t)dim * 4);
+    std::vector<uint64_t> ids(B * k);
+    std::vector<float> sc(B * k);
+    std::vector<uint32_t> n(B);
+    const gvdb_status st = index_search_host(ix, q.data(), B, dim, k, reqs[0]->has_sp ? &reqs[0]->sp : nullptr,
+                                             ids.data(), sc.data(), n.data());
+    const std::string err = st == GVDB_OK ? std::string() : t_err;
+    // a NaN score fails only the queries it poisoned: index_search_host downloads every
+    // query's results and counts before it reports GVDB_ERR_QUANTIZATION
+    const bool per_query = st == GVDB_ERR_QUANTIZATION;
+    for (size_t i = 0; i < B; ++i) {
+        B1Req* r = reqs[i];
+        const bool poisoned = n[i] == GVDB_N_POISONED;
+        const bool ok = st == GVDB_OK || (per_query && !poisoned);
+        r->st = ok ? GVDB_OK : st;
+        r->err = ok ? std::string() : err;
+        if (ok || (per_query && poisoned)) {  // a poisoned query's slots as the serial call leaves them
+            memcpy(r->ids, ids.data() + i * k, k * 8);
+            memcpy(r->scores, sc.data() + i * k, k * 4);
+            *r->n = n[i];
+        }
+    }
+}
+
+static gvdb_status b1_coalesced(const gvdb_index* ix, const float* query, uint32_t dim, uint64_t k,
+                                const gvdb_search_params* sp, uint64_t* out_ids, float* out_scores, uint32_t* out_n) {
+    B1Req r;
+    r.q = query;
+    r.k = k;
+    r.has_sp = sp != nullptr;
+    if (sp) r.sp = *sp;
+    r.ids = out_ids;
+    r.scores = out_scores;
+    r.n = out_n;
+    std::unique_lock<std::mutex> lk(ix->b1_mu);
+    ix->b1_pend.push_back(&r);
+    while (!r.done) {
+        if (!r.taken && !ix->b1_exec) {
+            // lead the next batch: the oldest pending request and the later ones it can share a search with
+            std::vector<B1Req*> mine;
+            std::vector<B1Req*> rest;
+            for (B1Req* x : ix->b1_pend)
+                (mine.size() < kB1MaxBatch && x->same_batch(*ix->b1_pend.front()) ? mine : rest).push_back(x);
+            ix->b1_pend.swap(rest);
+            for (B1Req* x : mine) x->taken = true;
+            g_b1_batches.fetch_add(1);
+            g_b1_queries.fetch_add(mine.size());
+            for (uint64_t m = g_b1_max.load(); m < mine.size() && !g_b1_max.compare_exchange_weak(m, mine.size());) {
+            }
+            ix->b1_exec = true;
+            lk.unlock();
+            b1_run_batch(ix, dim, mine);
+            lk.lock();
+            ix->b1_exec = false;
+            for (B1Req* x : mine) x->done = true;
+            ix->b1_cv.notify_all();
+        } else {
+            ix->b1_cv.wait(lk);
+        }
+    }
+    lk.unlock();
+    if (r.st != GVDB_OK) return fail(r.st, r.err);
+    return GVDB_OK;
+}
+
+gvdb_status gvdb_index_search(const gvdb_index* ix, const float* queries, uint64_t B, uint32_t dim, uint64_t k,
+                              const gvdb_search_params* sp, uint64_t* out_ids, float* out_scores, uint32_t* out_n) {
+    gvdb_status st = check_search(ix, dim, B, k);
+    if (st != GVDB_OK) return st;
+    if (B == 0) return GVDB_OK;
+    if (!queries || !out_n || (k && (!out_ids || !out_scores))) return fail(GVDB_ERR_INVALID_ARGUMENT, "null argument");
+    static const bool coalesce = [] {
+        const char* e = getenv("GVDB_B1_COALESCE");
+        return !(e && e[0] == '0');
+    }();
+    if (B == 1 && k > 0 && coalesce) return b1_coalesced(ix, queries, dim, k, sp, out_ids, out_scores, out_n);
+    return index_search_host(ix, queries, B, dim, k, sp, out_ids, out_scores, out_n);
 }
 
 // Filtered search (§8(f) rank 4): the pre-mask of FilterEngine::execute_filter
@@ -2421,6 +2569,12 @@ extern "C" int gvdb_debug_stage1_thresholds(uint32_t* out, uint32_t B) {
     return (int)hipMemcpy(out, debug_thr(), (size_t)B * 4, hipMemcpyDeviceToHost);
 }
 // tests only: 1 if a query of the last GVDB_DEBUG_THR=1 batch took the all-rows rescan
+extern "C" int gvdb_debug_b1_coalesce(uint64_t* out) {  // [0] batches, [1] queries, [2] largest batch
+    out[0] = g_b1_batches.load();
+    out[1] = g_b1_queries.load();
+    out[2] = g_b1_max.load();
+    return 0;
+}
 extern "C" int gvdb_debug_deep_cert(uint64_t* out) {  // [0] certified batches, [1] sent to the rerank path
     if (!out) return 1;
     tier_poll(true);

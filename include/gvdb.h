@@ -176,22 +176,38 @@ gvdb_status gvdb_index_build(gvdb_index* index);
 /* search (index.rs:212-231) for a batch of B queries (B x dim, host memory).
  * Per query q, up to k results: out_ids[q*k + i], out_scores[q*k + i],
  * count out_n[q]; slots i >= out_n[q] are zero-filled.  IndexNotBuilt when
- * the index is empty (index.rs:213). */
+ * the index is empty (index.rs:213).  Synchronous: returns when the results
+ * are in the caller's buffers.  Reentrant (many concurrent readers, the
+ * reference's Arc<RwLock<dyn VectorIndex>>, lib.rs:238): concurrent B = 1
+ * calls are coalesced inside the library -- whenever no coalesced batch is
+ * executing, the waiting calls with the same k and params run as ONE batched
+ * search (up to 256 queries) and each caller gets exactly the results its own
+ * call would have returned (every mode is exact); a lone caller runs at once.
+ * GVDB_B1_COALESCE=0 disables it.  A query with a NaN score fails only its
+ * own call (GVDB_ERR_QUANTIZATION). */
 gvdb_status gvdb_index_search(const gvdb_index* index, const float* queries, uint64_t B, uint32_t dim,
                               uint64_t k, const gvdb_search_params* sp, uint64_t* out_ids,
                               float* out_scores, uint32_t* out_n);
 /* Same with queries and outputs in HBM.  out_n may be NULL.  The work is
- * enqueued on `stream`: results are ready once the caller synchronises that
- * stream (BQ mode returns without any host sync; FLAT mode synchronises
- * internally because its tier decision reads a device flag, and so does BQ mode
- * at the reference's default depth -- R > 8192 with R >= N / 64, cosine, k <= 32,
- * N >= 65536, no orphan rows -- which answers from a certified exact cosine
- * top-64 list filtered by the stage-1 membership rule instead of reranking
- * B x R rows, the regular rerank whenever the list cannot certify).  A query whose
- * top-R holds a NaN score (the reference's partial_cmp().unwrap() sort would
- * panic) is reported ONLY through out_n[q] = GVDB_N_POISONED: callers that need
- * the reference's failure must pass out_n (with out_n == NULL such a query's
- * order is unspecified). */
+ * ENQUEUED on `stream` and the call returns without any host synchronisation
+ * in every mode: results are ready once the caller synchronises that stream
+ * (or waits on an event recorded on it after the call).  Modes with tiers
+ * decide them on the device: FLAT runs its MFMA candidate tier (i8, or bf16
+ * while the index skips i8) and then the exact scan GATED by that tier's
+ * certificate word (the scan's kernels exit at once when the tier certified);
+ * BQ at the reference's default depth (R > 8192 with R >= N / 64, cosine,
+ * k <= 32, N >= 65536, no orphan rows) answers from a certified exact cosine
+ * top-32/64 list filtered by the stage-1 membership rule and enqueues the
+ * B x R rerank behind it gated by the certificate.  Either way the results are
+ * exact.  Tier outcomes are copied to pinned host words behind the search and
+ * polled by later calls (they drive the adaptive i8 skip and the counters
+ * gvdb_flat_fallback_count / gvdb_flat_i8_fallback_count); nothing waits for
+ * them.  A query whose top-R holds a NaN score (the reference's
+ * partial_cmp().unwrap() sort would panic) is reported ONLY through
+ * out_n[q] = GVDB_N_POISONED: callers that need the reference's failure must
+ * pass out_n and check it after the stream (with out_n == NULL such a query's
+ * order is unspecified).  Argument and allocation errors are returned by the
+ * call itself, before anything is enqueued. */
 gvdb_status gvdb_index_search_device(const gvdb_index* index, const float* d_queries, uint64_t B,
                                      uint32_t dim, uint64_t k, const gvdb_search_params* sp,
                                      uint64_t* d_out_ids, float* d_out_scores, uint32_t* d_out_n,
@@ -387,8 +403,9 @@ gvdb_status gvdb_shard_stage1_device(const gvdb_index* shard, const float* d_que
  * 2 only reads its member lists, so it may run again on them).  Deep form on a
  * shard of >= 65536 rows without orphan rows, k <= 32: the rank's local top-k
  * comes from its certified exact cosine top-32 / 64 filtered by its owned-row
- * rule (no rerank of the ~R / G owned rows); this synchronises the host, and
- * falls back to the rerank when the list cannot certify. */
+ * rule (no rerank of the ~R / G owned rows); the owned-row rerank is enqueued
+ * behind it, gated on the device by the certificate word, for a list that
+ * cannot certify.  No host synchronisation in either form. */
 gvdb_status gvdb_shard_rerank_device(const gvdb_index* shard, const float* d_queries, uint64_t B, uint32_t dim,
                                      uint64_t R, uint64_t k, const uint32_t* d_gathered1, uint64_t G, uint64_t rank,
                                      void* d_scratch, uint32_t* d_block2, void* stream);

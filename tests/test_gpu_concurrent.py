@@ -94,3 +94,111 @@ def test_concurrent_readers_equal_serial(g):
     # the last mutations are visible: the added rows are found
     ids, _, _ = ix.search_batch(Q256[16:24], 1, sp)
     assert set(int(v) for v in ids[:, 0]) <= set(range(N, next_id))
+
+
+def test_concurrent_default_depth_device_searches_equal_serial(g):
+    """The async certified default depth (R = 0.1 N, quantization.rs:27,178) runs
+    its flat pass on a second pooled workspace whose failure word the certify
+    pass reads later on the caller's stream (the word is now copied
+    into the caller's own workspace before the pooled one is released).  Four
+    threads, each on its own stream, interleave default-depth and FLAT-mode
+    _device searches (the FLAT calls take pooled workspaces and clear their
+    words) with no sync between enqueues; every result equals the serial
+    host-buffer search bit for bit."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    N, D, B, T, k = 200_000, 768, 64, 4, 10
+    x = rng.standard_normal((N, D)).astype(np.float32)
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    Q = rng.standard_normal((T, B, D)).astype(np.float32)
+    deep = g.SearchParams()  # mode BQ_RERANK, rescore_ratio 0.1 -> R = 20000
+    flat = g.SearchParams(mode=g._ffi.GVDB_SEARCH_FLAT)
+    ref = {(t, m): ix.search_batch(Q[t], k, sp) for t in range(T) for m, sp in (("deep", deep), ("flat", flat))}
+    errors = []
+    barrier = threading.Barrier(T)
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream()
+            outs = []
+            with torch.cuda.stream(s):  # inputs, outputs and searches all ordered on s
+                q = torch.from_numpy(Q[t]).cuda()
+                s.synchronize()
+                barrier.wait()
+                for it in range(8):
+                    m = "deep" if (t + it) % 2 == 0 else "flat"
+                    oi = torch.zeros((B, k), dtype=torch.int64, device="cuda")
+                    osc = torch.zeros((B, k), dtype=torch.float32, device="cuda")
+                    on = torch.zeros(B, dtype=torch.int32, device="cuda")
+                    ix.search_device(q, k, oi, osc, on, deep if m == "deep" else flat, stream=s.cuda_stream)
+                    outs.append((m, oi, osc, on))
+            s.synchronize()
+            for m, oi, osc, on in outs:
+                want = ref[(t, m)]
+                got = (oi.cpu().numpy().view(np.uint64), osc.cpu().numpy(), on.cpu().numpy().view(np.uint32))
+                if not ((got[0] == want[0]).all() and got[1].tobytes() == want[1].tobytes()
+                        and (got[2] == want[2]).all()):
+                    errors.append((t, m))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_concurrent_batch1_callers_coalesce_and_equal_serial(g):
+    """Raw gvdb_index_search with B = 1 from many threads (the reference's
+    concurrent readers, lib.rs:238 + index.rs:212-231) is coalesced inside the
+    library: batches form while one executes, requests with a different k or
+    params never share a batch, and every answer equals the serial call's."""
+    import ctypes as C
+
+    rng = np.random.default_rng(4242)
+    N, D, T, per = 400_000, 768, 48, 6
+    x = rng.standard_normal((N, D)).astype(np.float32)
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    Q = rng.standard_normal((T * per, D)).astype(np.float32)
+    Q[7] = x[123]
+    sps = [g.SearchParams(rescore_count=100), g.SearchParams(rescore_count=300),
+           g.SearchParams(mode=g._ffi.GVDB_SEARCH_FLAT)]
+    ks = [10, 10, 5]
+    ref = [ix.search_batch(Q[i:i + 1], ks[i % 3], sps[i % 3]) for i in range(T * per)]
+    L = g.lib()
+    L.gvdb_debug_b1_coalesce.argtypes = [C.POINTER(C.c_uint64)]
+    before = (C.c_uint64 * 3)()
+    L.gvdb_debug_b1_coalesce(before)
+    errors = []
+    barrier = threading.Barrier(T)
+
+    def worker(t):
+        try:
+            barrier.wait()
+            for j in range(per):
+                i = t * per + j
+                got = ix.search_batch(Q[i:i + 1], ks[i % 3], sps[i % 3])
+                want = ref[i]
+                if not ((got[0] == want[0]).all() and got[1].tobytes() == want[1].tobytes()
+                        and (got[2] == want[2]).all()):
+                    errors.append(i)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+    after = (C.c_uint64 * 3)()
+    L.gvdb_debug_b1_coalesce(after)
+    nq = after[1] - before[1]
+    assert nq == T * per
+    assert after[0] - before[0] < nq  # some searches were shared
+    assert int(ref[7][0][0, 0]) == 123
