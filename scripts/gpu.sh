@@ -254,6 +254,20 @@ for t in "${TASKS[@]}"; do
                 DIM=3072 GVDB_LIB_PATH=$lib TAG=$v run 600 gpurun_out/mx4var_$v.log python3 -u scripts/b256_timing.py
                 grep "scan" gpurun_out/mx4var_$v.log | tail -1
             done ;;
+        bm25ab)  # BM25 leg at 5M docs, one box: VARIANTS (abl/libgvdb_NAME.so, "base" = product) alternating twice
+            for v in ${VARIANTS:-base} ${VARIANTS:-base}; do
+                lib=""; [ "$v" != base ] && lib=grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib run 300 gpurun_out/bm25ab_$v.log python3 -u scripts/bm25_timing.py --check --steps 20
+                echo "$v $(tail -1 gpurun_out/bm25ab_$v.log)"
+            done ;;
+        bm25prof)  # BM25 leg at 5M docs under rocprofv3 (kernel trace) and the phase clocks, per VARIANT
+            for v in ${VARIANTS:-base}; do
+                lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib run 300 gpurun_out/bm25prof_$v.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bm25_$v -o run -- python3 scripts/bm25_timing.py --steps 10
+                python3 scripts/trace_summary.py gpurun_out/prof_bm25_$v/run_kernel_trace.csv > gpurun_out/bm25_kernels_$v.txt; echo "== $v"; head -8 gpurun_out/bm25_kernels_$v.txt
+                GVDB_LIB_PATH=$lib GVDB_BM25_ABL=8 run 300 gpurun_out/bm25clk_$v.log python3 -u scripts/bm25_timing.py --steps 2
+                grep "bm25 prof" gpurun_out/bm25clk_$v.log | tail -1
+            done ;;
         bm25clk)  # BM25 leg at 5M docs: timing, then the per-phase shader clocks (GVDB_BM25_ABL=8)
             run 600 gpurun_out/bm25t.log python3 -u scripts/bm25_timing.py --check
             tail -3 gpurun_out/bm25t.log
