@@ -197,9 +197,10 @@ struct TaArgs {
 //      (per wave: ballot + one counter add) and an LDS (group term x slot) map
 //      of u16 stage offsets (0 = no posting; the first entry of a re-added
 //      document's run) points at them -- 512 rows x 128 slots in 128 KB, so
-//      one group holds up to 511 distinct terms.  The queries' bits (host mask
-//      per group term) are OR-ed into the slot's LDS hit mask: the documents
-//      each query matches;
+//      one group holds up to 511 distinct terms.  (Which documents each query
+//      matches comes from the rounds' own map reads: no per-posting LDS hit mask
+//      -- round 6: the 64-bit LDS atomic OR per posting was ~2 of the build's 5
+//      LDS operations);
 //   2. rounds: wave w owns 4 queries (host-balanced), accumulators in
 //      registers.  Query q's terms in order: a map read, two stage reads,
 //      acc = acc + q_tf * tfc * idf -- per document exactly the reference's
@@ -225,8 +226,6 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
     constexpr uint32_t SPL = kTaSpl, kCh = kTaCh * SPL, kRows = kTaRows, kEmpty = kRows - 1;
     __shared__ __attribute__((aligned(16))) uint16_t s_tmap[kRows * kCh];  // stage byte offset per (term, slot)
     __shared__ __attribute__((aligned(16))) float s_tfc[kTaStaged];
-    __shared__ uint64_t s_qmask[kRows];  // group term index -> the group's queries holding it
-    __shared__ uint64_t s_hit[kCh];      // per slot of the chunk: the queries it matches
     __shared__ __attribute__((aligned(4))) uint8_t s_present[kRows];  // group terms with a posting in the chunk
     __shared__ uint32_t s_cptr[(SPL + 1) * (kTaCptrLds + 1)];  // the block's chunk (sub-)ranges, from cbase
     __shared__ uint32_t s_slow, s_nst, s_npool;
@@ -246,7 +245,6 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         s_tfc[0] = 0.0f;
         s_npool = 0;
     }
-    if (tid < nu) s_qmask[tid] = a.qmask[tid];
     auto tfc_at = [&](uint32_t off) { return *(const float*)((const char*)s_tfc + off); };
     // group term index of a gmap word, kEmpty for a term outside the group
     auto group_of = [&](uint32_t gv) { return (gv >> kGmapShift) == a.epoch ? gv & ((1u << kGmapShift) - 1) : kEmpty; };
@@ -354,7 +352,6 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
             for (uint32_t k = 0; k < kPer; ++k)
                 if (cell[k] != 0xffffffffu) s_tmap[cell[k]] = 0;
         }
-        if (tid < kCh) s_hit[tid] = 0ull;
         if (tid < kRows / 4) ((uint32_t*)s_present)[tid] = 0u;
         if (tid == 0) {
             s_slow = 0;
@@ -400,7 +397,6 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     s_tmap[cell[k]] = kTaUnstaged;
                     slow = true;
                 }
-                atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
                 s_present[g] = 1;
             }
             for (uint64_t i = ce0 + kTaStage + tid; i < ce1; i += kTaThreads) {  // past the register stage
@@ -420,7 +416,6 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                     s_tmap[g * kCh + sl] = kTaUnstaged;
                     slow = true;
                 }
-                atomicOr((unsigned long long*)&s_hit[sl], (unsigned long long)s_qmask[g]);
                 s_present[g] = 1;
                 slow = slow || (i + 1 < ce1 && a.cterm[i + 1] == a.cterm[i] && a.cslot[i + 1] == s);
             }
@@ -433,10 +428,16 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         mark(4);
         // 2. rounds, per query m in its term order; lane holds slots SPL*lane + h
         float acc[kTaQW][SPL];
+        // the documents each query matches (a posting of one of its terms: the reference's
+        // scores.entry(id)), from the map reads themselves -- OR of the 16-bit offsets per
+        // (query, slot half); no LDS hit mask built per posting
+        uint32_t orv[kTaQW];
 #pragma unroll
-        for (uint32_t m = 0; m < kTaQW; ++m)
+        for (uint32_t m = 0; m < kTaQW; ++m) {
+            orv[m] = 0u;
 #pragma unroll
             for (uint32_t h = 0; h < SPL; ++h) acc[m][h] = 0.0f;
+        }
         // Only the query terms with a posting in the chunk (a term without one adds +-0.0, or is
         // skipped by the select: either way acc is unchanged), in term order, N <= 4 at a time:
         // the map reads issued together, then the stage reads, then the folds in order.
@@ -460,6 +461,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                 for (uint32_t k = 0; k < N; ++k) {
                     tf[k][0] = tfc_at(off[k] & 0xffffu);
                     tf[k][1] = tfc_at(off[k] >> 16);
+                    orv[m] |= off[k];
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < N; ++k) {
@@ -502,6 +504,7 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
                         const uint32_t sl = SPL * lane + h;  // slot within the chunk
                         const uint32_t off = s_tmap[rec.x * kCh + sl];
                         if (off == 0u) continue;  // no posting
+                        orv[m] |= 1u << (16 * h);
                         if (!s_slow) {
                             acc[m][h] = acc[m][h] + v * tfc_at(off) * idf;
                             continue;
@@ -523,16 +526,13 @@ __global__ __launch_bounds__(kTaThreads, 1) void k_bm25_taat(TaArgs a) {
         }
         mark(2);
         // 3. selection: (query qid[m], slot c0 + SPL lane + h)
-        uint64_t hm[SPL];
-#pragma unroll
-        for (uint32_t h = 0; h < SPL; ++h) hm[h] = s_hit[SPL * lane + h];
 #pragma unroll
         for (uint32_t m = 0; m < kTaQW; ++m) {
             const uint32_t q = qid[m];
             if (q == 0xffffffffu) continue;
             bool hb[SPL];
 #pragma unroll
-            for (uint32_t h = 0; h < SPL; ++h) hb[h] = (hm[h] >> q) & 1ull;
+            for (uint32_t h = 0; h < SPL; ++h) hb[h] = ((orv[m] >> (16 * h)) & 0xffffu) != 0u;
             if constexpr (MODE == 1) {
                 bool pass[SPL], any = false;
 #pragma unroll

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--ef", type=int, nargs="+", default=[10, 50, 100, 200, 400, 1000, 2000, 5000])
     ap.add_argument("--out", default="")
+    ap.add_argument("--unit-only", action="store_true", help="only the unit-row corpus (the bench's data)")
     a = ap.parse_args()
     rng = np.random.default_rng(a.n)
     raw = rng.standard_normal((a.n, a.dim)).astype(np.float32)
@@ -41,7 +42,8 @@ def main():
     noise = unit(rng.standard_normal((a.queries, a.dim)).astype(np.float32))
     res = {"n": a.n, "dim": a.dim, "queries": a.queries, "threads": a.threads, "M": 32, "ef_construction": 100,
            "corpora": []}
-    for name in ("unit rows (cosine = L2 order)", "un-normalised rows (L2 order)"):
+    names = ["unit rows (cosine = L2 order)"] + ([] if a.unit_only else ["un-normalised rows (L2 order)"])
+    for name in names:
         unit_rows = name.startswith("unit")
         x = unit(raw) if unit_rows else raw
         q = unit(qr) if unit_rows else qr
