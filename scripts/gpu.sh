@@ -254,6 +254,12 @@ for t in "${TASKS[@]}"; do
                 DIM=3072 GVDB_LIB_PATH=$lib TAG=$v run 600 gpurun_out/mx4var_$v.log python3 -u scripts/b256_timing.py
                 grep "scan" gpurun_out/mx4var_$v.log | tail -1
             done ;;
+        flatvar)  # exact flat timing at 10M x 768 (BS, default 256,64), VARIANTS (abl/libgvdb_NAME.so, "base" = product) alternating
+            for v in ${VARIANTS:-base}; do
+                lib=""; [ "$v" != base ] && lib=$PWD/grape-vector-db_amd/abl/libgvdb_$v.so
+                GVDB_LIB_PATH=$lib BS=${BS:-256,64} FLAT_REPS=10 run 600 gpurun_out/flatvar_$v.log python3 -u scripts/flat_timing.py
+                echo "== $v"; grep -E "B=|emit" gpurun_out/flatvar_$v.log | tail -4
+            done ;;
         bm25ab)  # BM25 leg at 5M docs, one box: VARIANTS (abl/libgvdb_NAME.so, "base" = product) alternating twice
             for v in ${VARIANTS:-base} ${VARIANTS:-base}; do
                 lib=""; [ "$v" != base ] && lib=grape-vector-db_amd/abl/libgvdb_$v.so
