@@ -317,6 +317,7 @@ def main():
         run_point("bq R=0.1 N (reference default rescore_ratio, certified)", gvdb.SearchParams(rescore_ratio=0.1))
         c1 = deep_cert_counts(L)
         points[-1]["certified_batches"], points[-1]["rerank_batches"] = c1[0] - c0[0], c1[1] - c0[1]
+        points[-1]["rooflines"] = deep_rooflines(L, ix, q, k, n_local, D)
         run_point("exact flat (i8/bf16-MFMA certified candidates + exact f32 rerank)", gvdb.SearchParams(mode=1))
         points[-1]["emit_roofline"] = flat_emit_roofline(L, ix, q, k, n_local, D)
         if planted:
@@ -723,6 +724,56 @@ def deep_cert_counts(L):
     out = (ctypes.c_uint64 * 2)()
     L.gvdb_debug_deep_cert(out)
     return int(out[0]), int(out[1])
+
+
+def deep_rooflines(L, ix, q, k, n_local, D):
+    """The reference default depth's two big kernels (certified search): the
+    dense FP4 stage-1 scan (k_scan_mx7<DENSE>: every Hamming dot of the 256-slot query
+    tile written as f16 -- HBM-bound on its writes) and the flat pass's i8 candidate
+    kernel (k_flat_i8q, HBM-bound on the i8 mirror).  HIP events around each launch
+    (gvdb_timing slots 1 and 7) over 3 searches."""
+    B = q.shape[0]
+    oi = torch.zeros((B, k), dtype=torch.int64, device=q.device)
+    osc = torch.zeros((B, k), dtype=torch.float32, device=q.device)
+    prm = gvdb.SearchParams(rescore_ratio=0.1)
+    ix.search_device(q, k, oi, osc, None, prm)
+    torch.cuda.synchronize()
+    L.gvdb_timing_reset()
+    L.gvdb_timing_enable(1)
+    for _ in range(3):
+        ix.search_device(q, k, oi, osc, None, prm)
+    torch.cuda.synchronize()
+    L.gvdb_timing_enable(0)
+    sm, sn = timing_slot(L, 1)
+    em, en = timing_slot(L, 7)
+    L.gvdb_timing_reset()
+    out = {}
+    w4 = gvdb_code_w4(D)
+    if sn:
+        ms = sm / sn
+        groups = -(-B // 256)
+        wr = 256 * groups * (-(-n_local // 32) * 32) * 2  # the f16 dot block
+        rd = n_local * w4 * 16 * groups + wr  # the codes, and the block again by the rule's segment histograms
+        ops = float(n_local) * 256 * groups * w4 * 128 * 2
+        out["dense_scan"] = {
+            "kernel": "dense stage 1: k_scan_mx7<DENSE> (every FP4-MFMA Hamming dot of the 256-slot tile stored as "
+                      "f16) + the membership rule over that block (k_dense_seg_hist, k_dense_rule)",
+            "bound": "hbm", "achieved": (rd + wr) / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": (rd + wr) / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None, "avg_launch_ms": ms,
+            "algorithmic_bytes_per_launch": rd + wr, "reads": rd, "writes": wr,
+            "mfma_frac": ops / (ms * 1e-3) / 1e12 / PEAK_FP4_TFLOPS,
+            "source": "avg_launch_ms: HIP events around the dense scan + rule launches (gvdb_timing slot 1), "
+                      "3 searches"}
+    if en:
+        ms = em / en
+        algo = n_local * ((D + 127) // 128) * 128
+        out["flat_pass"] = {
+            "kernel": "k_flat_i8q (the certified list's i8 MFMA candidate pass over the int8 mirror)",
+            "bound": "hbm", "achieved": algo / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": algo / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None, "avg_launch_ms": ms,
+            "algorithmic_bytes_per_launch": algo,
+            "source": "avg_launch_ms: HIP events around each emit launch (gvdb_timing slot 7), 3 searches"}
+    return out or None
 
 
 def flat_emit_roofline(L, ix, q, k, n_local, D):

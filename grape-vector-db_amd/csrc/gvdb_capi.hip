@@ -1550,7 +1550,18 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
         HIP_TRY(hipStreamWaitEvent(s2, e_in.e, 0), "stream wait");
     }
     UseGuard ug2{ix, s2};
+    bool timed = false;
+    {
+        std::lock_guard<std::mutex> g(timing().mu);
+        timed = timing().on;
+    }
+    EvSet* tev = timed ? timing_events() : nullptr;  // timing mode: the dense scan in the scan slot
+    s1.ev = tev ? tev->e : nullptr;
     HIP_TRY(launch_stage1_fast(s1, s), "certified depth: stage 1");
+    if (tev) {
+        HIP_TRY(hipEventRecord(tev->e[5], s), "event");
+        timing_submit(tev);
+    }
     bool cert = false, i8_tier = false;
     uint32_t* flat_fail = nullptr;
     gvdb_status st;
