@@ -480,11 +480,15 @@ def main():
         # exact top-k of the prefix on the GPU (f32; a CPU argsort of B x 1M scores took ~15 s)
         xt = torch.from_numpy(xs).to(dev)
         sub_truth = torch.topk(q @ xt.T, k, dim=1).indices.cpu().numpy()
-        # planted queries (x_j + 0.1 n, rows j of the first chunk, inside the prefix): their own truth
-        use_planted = planted and ns >= min(N, CHUNK)
+        # planted queries (x_j + 0.1 n) whose row j lies in the prefix: their own truth
+        use_planted = planted
         if use_planted:
-            qpn = qp.cpu().numpy()
-            sub_ptruth = torch.topk(qp @ xt.T, k, dim=1).indices.cpu().numpy()
+            keep = torch.nonzero(pj < ns).flatten()
+            qps_ = qp[keep.to(dev)].contiguous()
+            use_planted = qps_.shape[0] > 0
+        if use_planted:
+            qpn = qps_.cpu().numpy()
+            sub_ptruth = torch.topk(qps_ @ xt.T, k, dim=1).indices.cpu().numpy()
         log(f"[bench] CPU-HNSW leg: building M=32 ef_construction=100 on {ns} rows ({threads} threads)")
         tb = time.perf_counter()
         h = oracle.Hnsw(xs, threads=threads)
@@ -531,20 +535,23 @@ def main():
              ("exact flat", gvdb.SearchParams(mode=1))]
 
         def gpu_point(name, prm, qq, tr, label):
-            sub_ix.search_device(qq, k, osi, oss, None, prm)
+            nq = qq.shape[0]
+            oi_ = osi if nq == B else torch.zeros((nq, k), dtype=torch.int64, device=dev)
+            os_ = oss if nq == B else torch.zeros((nq, k), dtype=torch.float32, device=dev)
+            sub_ix.search_device(qq, k, oi_, os_, None, prm)
             torch.cuda.synchronize()
             reps = 5
             tp = time.perf_counter()
             for _ in range(reps):
-                sub_ix.search_device(qq, k, osi, oss, None, prm)
+                sub_ix.search_device(qq, k, oi_, os_, None, prm)
             torch.cuda.synchronize()
             tp = time.perf_counter() - tp
-            f = osi.cpu().numpy()
-            return {"search": name, "queries": label, "qps": B * reps / tp, "batch": B,
+            f = oi_.cpu().numpy()
+            return {"search": name, "queries": label, "qps": nq * reps / tp, "batch": nq,
                     "recall_at_10": recall_at(f, tr), "recall_at_1": float(np.mean(f[:, 0] == tr[:, 0]))}
 
         gpts = [gpu_point(nm, prm, q, sub_truth, "iid") for nm, prm in searches]
-        gpl = [gpu_point(nm, prm, qp, sub_ptruth, "planted") for nm, prm in searches[:3] + searches[-1:]] \
+        gpl = [gpu_point(nm, prm, qps_, sub_ptruth, "planted") for nm, prm in searches[:3] + searches[-1:]] \
             if use_planted else []
         # batch 1: one query per call over the benchmark queries (host sync per call excluded:
         # calls queue back to back on the stream, as a serving loop would)
