@@ -669,7 +669,7 @@ def main():
         dist.destroy_process_group()
 
 
-PMC_FILE = "profiles/r05/pmc_bench_10M.json"
+PMC_FILE = "profiles/r06/pmc_bench_10M.json"
 PMC_FLAT_FILE = PMC_FILE  # the same passes cover k_flat_i8q (bench.py operating points, 10M x 768, B = 256)
 
 
