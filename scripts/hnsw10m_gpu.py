@@ -34,7 +34,8 @@ def recall(found, truth):
 
 def main():
     N, D, B, k = 10_000_000, 768, 256, 10
-    gt = np.load(os.path.join(ROOT, "profiles", "r03", "hnsw10M_gt.npz"))
+    # HNSW10M_GT: the ground truth the CPU side wrote (default: round 3's)
+    gt = np.load(os.environ.get("HNSW10M_GT", os.path.join(ROOT, "profiles", "r03", "hnsw10M_gt.npz")))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     ix = gvdb.GpuVectorIndex(dimension=D, capacity_hint=N)
@@ -64,7 +65,8 @@ def main():
         osc = torch.zeros((B, k), dtype=torch.float32, device=dev)
         for label, prm in [(f"bq R={r}", gvdb.SearchParams(rescore_count=r))
                            for r in (10, 30, 100, 300, 1000, 3000, 8000)] + \
-                          [("exact flat", gvdb.SearchParams(mode=1))]:
+                          [("bq R=0.1 N (reference default, certified)", gvdb.SearchParams(rescore_ratio=0.1)),
+                           ("exact flat", gvdb.SearchParams(mode=1))]:
             found = np.zeros((nq, k), np.int64)
             ix.search_device(qd[:B], k, oi, osc, None, prm)  # warm
             torch.cuda.synchronize()
@@ -98,6 +100,15 @@ def main():
             pts.append({"search": f"bq R={r}", "queries": name, "batch": 1, "qps": n1 / t,
                         "recall_at_10": recall(found, truth[:n1]),
                         "recall_at_1": float(np.mean(found[:, 0] == truth[:n1, 0]))})
+            log(pts[-1])
+        # 64 concurrent single-query callers through the C ABI (bench.py's driver, library-coalesced)
+        from bench import concurrent_b1_points
+        for p in concurrent_b1_points(ix, D, k, Q[:nq], truth[:nq], None, None,
+                                      [("bq R=100", gvdb.SearchParams(rescore_count=100)),
+                                       ("exact flat", gvdb.SearchParams(mode=1))], threads=64):
+            p["queries"] = name
+            p["batch"] = "concurrent64"
+            pts.append(p)
             log(pts[-1])
     out = {"rows": N, "dim": D, "points": pts,
            "note": "same rows / queries / ground truth as profiles/r03/hnsw10M_cpu.json (scripts/hnsw10m_data.py); "

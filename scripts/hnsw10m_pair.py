@@ -26,13 +26,13 @@ def best(gpu_pts, qset, batch, need):
 
 
 def main():
-    d = os.path.join(ROOT, "profiles", "r03")
+    d = os.environ.get("HNSW10M_DIR", os.path.join(ROOT, "profiles", "r03"))
     cpu = json.load(open(sys.argv[1] if len(sys.argv) > 1 else os.path.join(d, "hnsw10M_cpu.json")))
     gpu = json.load(open(sys.argv[2] if len(sys.argv) > 2 else os.path.join(d, "hnsw10M_gpu.json")))
     pairs = []
     for c in cpu["points"]:
         row = {"cpu": c}
-        for batch in (256, 1):
+        for batch in (256, 1, "concurrent64"):
             for tag, need in (("strict", c["recall_at_10"]), ("minus_0.02", c["recall_at_10"] - 0.02)):
                 g = best(gpu["points"], c["queries"], batch, need)
                 row[f"gpu_b{batch}_{tag}"] = None if g is None else {
