@@ -1122,6 +1122,14 @@ hipError_t launch_queries_to_i8(const float* q, uint32_t B, uint32_t D, const fl
 // wave's 6 row pieces of sub-tile i+2 one per 2 k-steps of step i's MFMAs
 // instead of all after the barrier saved 7 % (every 1, 2, 3 or 4 k-steps, at
 // any offset: the same within noise).
+// GVDB_I8Q_T (experimental, default 0): the MFMA operands swapped -- rows as A, queries
+// as B -- so a lane's 16 accumulators are ONE query against 16 rows (k_scan_mx7's trick),
+// and the candidate test starts from a per-lane bound (largest dot x the rows' largest
+// qinv * rinv against thr - qa * the rows' largest rho; both monotone in f32, so no pair
+// the exact test nominates is missed).  GVDB_I8Q_NOPASS: timing probe, bound never passes.
+#ifndef GVDB_I8Q_T
+#define GVDB_I8Q_T 0
+#endif
 constexpr int kI8qBr = 4;           // B-fragment ring depth in k-steps
 constexpr int kI8qSpread = 2;       // a row piece of the sub-tile two ahead every kI8qSpread k-steps
 constexpr uint32_t kI8qSub = 2;     // 32-row groups per LDS sub-tile
@@ -1138,13 +1146,17 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     constexpr uint32_t kPerWave = kPieces / 8;          // row DMAs per wave per sub-tile
     constexpr uint32_t kSubBytes = kPieces * 1024u;
     constexpr uint32_t kRows = kI8qSub * 32u;           // rows per sub-tile (one per lane)
-    constexpr uint32_t kBufBytes = kSubBytes + 2u * kRows * 4u;  // + the rows' s_x/|x| and rho_x
+    constexpr uint32_t kBufBytes = kSubBytes;
     constexpr uint32_t kOps = kPerWave + 1u;            // vector-memory ops per stage of a wave with an operand DMA
     constexpr uint32_t kOpsWaves = kRows == 64 ? 2u : 1u;  // waves that DMA the rows' s_x/|x| and rho_x
     static_assert((kPerWave - 1u) * kI8qSpread < (uint32_t)KS, "every row piece issued within its step");
     static_assert(kPieces % 8 == 0, "pieces split evenly over the waves");
     static_assert(kRows == 64 || kRows == 32, "one operand word per lane");
     __shared__ __attribute__((aligned(16))) char Bs[kI8qBufs][kBufBytes];
+    // the rows' s_x/|x| and rho_x of sub-tile i, in a ring one deeper than the row buffers (the
+    // transposed form's late waves read step i-1's after the barrier of step i)
+    constexpr uint32_t kOpsRing = kI8qBufs + 1u;
+    __shared__ __attribute__((aligned(16))) float opsr[kOpsRing][2u * kRows];
     // nomination (slot q, block step i, row group gi, row j) as q << 24 | i << 6 | gi << 5 | j
     __shared__ uint32_t cl[kI8qCl];
     __shared__ float cs[kI8qCl];  // their approx scores
@@ -1181,7 +1193,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     auto stage_ops = [&](uint32_t i) __attribute__((always_inline)) {
         uint32_t t, u;
         sub_of(i, t, u);
-        const uint32_t l0 = (uint32_t)(uintptr_t)Bs[i % kI8qBufs];
+        const uint32_t l0 = (uint32_t)(uintptr_t)opsr[i % kOpsRing];
         if (wv < kOpsWaves) {
             // 64 rows: wave 0 s_x/|x|, wave 1 rho_x; 32 rows: wave 0, lanes 0-31 / 32-63
             const uint32_t r = kRows == 64 ? lane : (lane & 31u);
@@ -1189,7 +1201,7 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             const bool rho = kRows == 64 ? wv == 1 : lane >= 32u;
             const float* src = (rho ? a.rrho : a.rscale) + n;
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src),
-                         "s"(l0 + kSubBytes + (kRows == 64 ? wv * kRows * 4u : 0u))
+                         "s"(l0 + (kRows == 64 ? wv * kRows * 4u : 0u))
                          : "memory");
         }
     };
@@ -1217,6 +1229,10 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     }
     if (tid == 0) cl_n = 0;
     __syncthreads();  // the compiler-visible loads above are complete from here on
+    constexpr bool kT = GVDB_I8Q_T != 0;
+    // transposed: this lane's query slot and its epilogue operands, for the whole launch
+    const uint32_t lq = qtile * 32u + (lane & 31u);
+    const float lqinv = qinv_l[lq], lthr = thr_l[lq], lqa = qa_l[lq];
     if (ns)
 #pragma unroll
         for (uint32_t j = 0; j + 1 < kI8qBufs; ++j) stage(j);
@@ -1310,11 +1326,71 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
             }
         }
     };
+    auto set_stats = [&](const float* ops, float* rmx, float* rmn, float* pmx) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t ga = 0; ga < NGI; ++ga) {
+            const uint32_t b = (gi0 + ga) * 32u + 4u * (lane >> 5);
+            float hi = 0.0f, lo = __builtin_inff(), ph = 0.0f;
+#pragma unroll
+            for (uint32_t g = 0; g < 4; ++g) {
+                const float4 r = *(const float4*)(ops + b + 8u * g);
+                const float4 h = *(const float4*)(ops + kRows + b + 8u * g);
+                hi = fmaxf(fmaxf(hi, fmaxf(r.x, r.y)), fmaxf(r.z, r.w));
+                lo = fminf(fminf(lo, fminf(r.x, r.y)), fminf(r.z, r.w));
+                ph = fmaxf(fmaxf(ph, fmaxf(h.x, h.y)), fmaxf(h.z, h.w));
+            }
+            rmx[ga] = hi;
+            rmn[ga] = lo;
+            pmx[ga] = ph;
+        }
+    };
+    auto epilogue_t = [&](uint32_t i, uint32_t t, uint32_t u, const float* rmx, const float* rmn, const float* pmx,
+                          const float* ops) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t ga = 0; ga < NGI; ++ga) {
+            const uint32_t gi = gi0 + ga;
+            int m = acc[ga][0];
+#pragma unroll
+            for (int e = 1; e < 16; ++e) m = max(m, acc[ga][e]);
+            const float bnd = (float)m * (m >= 0 ? lqinv * rmx[ga] : lqinv * rmn[ga]);
+            const float tmin = lthr - lqa * pmx[ga];
+#ifdef GVDB_I8Q_NOPASS
+            const bool pass = bnd >= tmin && bnd < -1.0e30f;
+#else
+            const bool pass = bnd >= tmin;
+#endif
+            if (!__ballot(pass)) continue;
+            if (!pass) continue;
+            const uint32_t r0 = 4u * (lane >> 5), nb = t * kFxRows + (kI8qSub * u + gi) * 32u + r0;
+            const float* ro = ops + gi * 32u + r0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const uint32_t rr = (uint32_t)(e & 3) + 8u * (uint32_t)(e >> 2);
+                const uint32_t n = nb + rr;
+                if (n >= N) continue;
+                const float v = (float)acc[ga][e] * (lqinv * ro[rr]);
+                if (v >= lthr - lqa * ro[kRows + rr]) {
+                    const uint32_t li = atomicAdd(&cl_n, 1u);
+                    if (li < kI8qCl) {
+                        cl[li] = (lq << 24) | (i << 6) | (gi << 5) | (r0 + rr);
+                        cs[li] = v;
+                    } else {
+                        const uint32_t pos = atomicAdd(&a.counts[lq], 1u);
+                        if (pos < a.candcap) {
+                            a.cand[(uint64_t)lq * a.candcap + pos] = n;
+                            if (a.cscore) a.cscore[(uint64_t)lq * a.candcap + pos] = v;
+                        }
+                    }
+                }
+            }
+        }
+    };
     // Waves 4..7 (the second wave of each SIMD) run step i-1's epilogue right after the
     // barrier of step i, before step i's MFMAs: on every SIMD one wave's candidate test
     // overlaps the other wave's MFMAs instead of both testing while the matrix core idles.
     const bool late = wv >= 4;
     float lrv[NGI] = {}, lrh[NGI] = {};  // step i-1's row operands (late waves)
+    float lmx[NGI] = {}, lmn[NGI] = {}, lpx[NGI] = {};  // transposed: step i-1's bound operands
     for (uint32_t i = 0; i < ns; ++i) {
         // stage i landed (stages i+1 .. i+kI8qBufs-2 are the younger ops), then every wave's part
         if (wv < kOpsWaves)
@@ -1336,11 +1412,14 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
         uint32_t t, u;
         sub_of(i, t, u);
         const char* Bb = Bs[i % kI8qBufs] + lane * 16u;
-        const float* ops = (const float*)(Bs[i % kI8qBufs] + kSubBytes);
+        const float* ops = opsr[i % kOpsRing];
         if (late && i > 0) {
             uint32_t tp, up;
             sub_of(i - 1, tp, up);
-            epilogue(i - 1, tp, up, lrv, lrh);
+            if constexpr (kT)
+                epilogue_t(i - 1, tp, up, lmx, lmn, lpx, opsr[(i - 1) % kOpsRing]);
+            else
+                epilogue(i - 1, tp, up, lrv, lrh);
         }
 #pragma unroll
         for (uint32_t ga = 0; ga < NGI; ++ga)
@@ -1372,11 +1451,22 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
                 piece(i + kI8qBufs - 1u, (uint32_t)(s / kI8qSpread));
 #pragma unroll
             for (uint32_t ga = 0; ga < NGI; ++ga) {
-                acc[ga] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][ga], acc[ga], 0, 0, 0);
+                if constexpr (kT)  // rows x queries: lane = one query, 16 rows
+                    acc[ga] = __builtin_amdgcn_mfma_i32_32x32x32_i8(bf[s % BR][ga], A[s], acc[ga], 0, 0, 0);
+                else
+                    acc[ga] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], bf[s % BR][ga], acc[ga], 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (!late) {
+        if constexpr (kT) {
+            if (!late) {
+                float mx[NGI], mn[NGI], px[NGI];
+                set_stats(ops, mx, mn, px);
+                epilogue_t(i, t, u, mx, mn, px, ops);
+            } else {
+                set_stats(ops, lmx, lmn, lpx);
+            }
+        } else if (!late) {
             float rv[NGI], rh[NGI];
 #pragma unroll
             for (uint32_t ga = 0; ga < NGI; ++ga) {
@@ -1395,7 +1485,10 @@ __global__ __launch_bounds__(kFxThreads, 1) void k_flat_i8q(FlatMxArgs a) {
     if (late && ns) {
         uint32_t t, u;
         sub_of(ns - 1, t, u);
-        epilogue(ns - 1, t, u, lrv, lrh);
+        if constexpr (kT)
+            epilogue_t(ns - 1, t, u, lmx, lmn, lpx, opsr[(ns - 1) % kOpsRing]);
+        else
+            epilogue(ns - 1, t, u, lrv, lrh);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped prefetches land before exit
     __syncthreads();
