@@ -151,3 +151,27 @@ def test_bq_device_search_no_host_sync(g, oracle_mod):
         hi, hs, hn = ix.search_batch(Q, k, sp)
         di, ds, dn, busy = device_search_async(g, ix, Q, k, sp)
         assert busy and (dn == hn).all() and (di == hi).all() and same_f32(ds, hs)
+
+
+def test_default_depth_device_with_large_r_path_off(g, oracle_mod, monkeypatch):
+    """with the batched large-R path disabled (GVDB_BIGR_OFF), a gated
+    fallback could not honour its gate, so the async default depth must not take
+    the certified form at all: the _device search runs the plain R = 0.1 N
+    multi-stage search and still equals the host form and the oracle."""
+    monkeypatch.setenv("GVDB_BIGR_OFF", "1")
+    N, D, B, k = 90_000, 256, 3, 10
+    x = rng_rows(811, N, D, dup=30)
+    Q = rng_rows(812, B, D)
+    Q[0] = x[17]
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    sp = g.SearchParams(rescore_ratio=0.1)
+    c0 = counts(g)
+    di, ds, dn, _ = device_search_async(g, ix, Q, k, sp)
+    c1 = counts(g)
+    assert (c1["cert"], c1["rerank"]) == (c0["cert"], c0["rerank"])  # the certified form was not entered
+    R = int(np.float32(N) * np.float32(0.1))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (dn == k).all() and (di == ri[:, :k]).all() and same_f32(ds, rs[:, :k])
+    hi, hs, hn = ix.search_batch(Q, k, sp)
+    assert (hn == dn).all() and (hi == di).all() and same_f32(hs, ds)
