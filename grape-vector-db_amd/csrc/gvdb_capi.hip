@@ -255,6 +255,11 @@ struct ShardView {
 
 constexpr uint32_t kExactN = 262144;  // below this the "sample" is the whole shard
 constexpr uint64_t kFlatScoreBytes = 1ull << 30;  // dense score block cap of the exact flat scan
+// ... and of its device-gated form (the _device FLAT search's last tier, enqueued behind every
+// batch and skipped on the device when the candidate tier certified): a skipped launch still
+// costs its dispatch (~7 us with the gap), so fewer, larger query groups -- 4 GiB: 107 queries
+// per group at 10M rows, 8 launches per batch of 256 instead of 22 (round 6)
+constexpr uint64_t kFlatScoreBytesGated = 4ull << 30;
 
 // Stage-1 sampling plan: S rows in 4096-row chunks spread over the shard.
 // sample_div: the sample is ~N/sample_div rows (32; 64 for large batches,
@@ -1636,7 +1641,8 @@ static gvdb_status flat_exact(const gvdb_index* ix, const float* d_q, uint64_t B
                               int descending, uint64_t* d_ids, float* d_scores, uint32_t* d_n, Workspace& ws,
                               hipStream_t s, const uint32_t* gate) {
     const uint64_t per_q = std::max<uint64_t>(ix->n * 4, 1);
-    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(B, kFlatScoreBytes / per_q));
+    const uint64_t cap_bytes = gate ? kFlatScoreBytesGated : kFlatScoreBytes;
+    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(B, cap_bytes / per_q));
     HIP_TRY(ws.qnorm.ensure(B * 4), "alloc qnorm");
     HIP_TRY(ws.scores.ensure(G * per_q), "alloc flat scores");
     HIP_TRY(ws.flags.ensure(16), "alloc flags");
