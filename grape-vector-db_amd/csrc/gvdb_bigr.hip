@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "gvdb_device.h"
 #include "gvdb_internal.h"
@@ -482,9 +483,213 @@ void dense_segments(uint32_t N, uint32_t smax, uint32_t* S, uint32_t* L) {
     *S = std::max<uint32_t>(1u, (N + l - 1u) / l);
 }
 
+// ---- the byte form of the parallel rule (round 6, Stage1Args::dense8) ----------
+// The f16 dense block of the certified default depth (B x N x 2 B: 5.1 GB per batch of
+// 256 at 10M rows) was written by the scan at ~2.5 TB/s and read back by the segment
+// histograms: 3 of the 5.7 ms step.  The rule only needs the distances near T, so a
+// pair is stored as one byte b = clamp(d - base, 0, 255) around a per-query window:
+//   k_dense_base      one block per query: the Hamming histogram of an 8192-row strided
+//                     sample, its quantile at R / N -> t_est; base = t_est - 127 (>= 0),
+//                     hi = the sample's quantile at target + 6 sqrt(target) + 16 (at least
+//                     t_est + 2, at most base + 254): the histograms count d <= hi only;
+//   k_dense_seg_hist8 the segment histograms over bytes <= hi - base (d-space bins
+//                     [base, hi] of seg_hist; no other bin is written or read);
+//   k_dense_rule8     T and the tie cut from them as k_dense_rule, or -- when T is not
+//                     strictly inside the window (cum(hi) < R, or T == base > 0: rows
+//                     below base share byte 0) -- rule mode 5: k_deep_certify then fails
+//                     the batch and the exact fallback (gated bq_search) answers it.
+// Exact whenever it certifies: inside the window every byte is d - base exactly.
+constexpr uint32_t kBaseThreads = 256;
+constexpr uint32_t kBaseSample = 8192;
+constexpr uint32_t kRuleInvalid = 5u;  // tcut mode: no rule (the window missed T)
+__global__ __launch_bounds__(kBaseThreads) void k_dense_base(const uint4* __restrict__ codes, uint64_t cap,
+                                                             uint32_t W4, uint32_t N, uint32_t D, uint32_t R,
+                                                             const uint4* __restrict__ qcodes, uint32_t B,
+                                                             uint32_t* __restrict__ qwin, int shift,
+                                                             const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    extern __shared__ uint32_t hist[];  // [D + 1]
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, H = D + 1u;
+    for (uint32_t t = tid; t < H; t += kBaseThreads) hist[t] = 0u;
+    __syncthreads();
+    const uint32_t S = min(N, kBaseSample);  // N <= S: every row (t_est = T)
+    const uint4* qc = qcodes + (uint64_t)q * W4;
+    for (uint32_t i = tid; i < S; i += kBaseThreads) {
+        const uint64_t n = (uint64_t)i * N / S;
+        atomicAdd(&hist[min(big_dist(codes, cap, W4, qc, n), D)], 1u);
+    }
+    __syncthreads();
+    if (tid < 64u) {
+        const uint32_t target = max(1u, (uint32_t)(((uint64_t)R * S + N - 1u) / N));
+        // shift (tests, GVDB_DENSE8_SHIFT): a deliberately wrong estimate -- the rule must then fail
+        const uint32_t t = (uint32_t)min(max((int)wave_find_cum(hist, H, target) + shift, 0), (int)D);
+        const uint32_t tgt_hi = min(S, target + (uint32_t)(6.0f * sqrtf((float)target)) + 16u);
+        const uint32_t th = (uint32_t)min(max((int)wave_find_cum(hist, H, tgt_hi) + shift, 0), (int)D);
+        if (tid == 0) {
+            const uint32_t base = t > 127u ? t - 127u : 0u;
+            const uint32_t hi = min(min(max(th, t + 2u), base + 254u), D);
+            qwin[q] = base;
+            qwin[B + q] = hi;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* __restrict__ dense, uint32_t np,
+                                                                 uint32_t N, uint32_t D,
+                                                                 const uint32_t* __restrict__ qwin, uint32_t Bt,
+                                                                 uint32_t S, uint32_t L,
+                                                                 uint32_t* __restrict__ seg_hist,
+                                                                 const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    __shared__ uint32_t wh_all[4][256];  // one histogram of bytes per wave
+    const uint32_t sg = blockIdx.x, q = blockIdx.y, tid = threadIdx.x, H = D + 1u;
+    const uint32_t wv = tid >> 6;
+    for (uint32_t i = tid; i < 4u * 256u; i += kSegThreads) (&wh_all[0][0])[i] = 0u;
+    __syncthreads();
+    const uint32_t base = qwin[q], hb = qwin[Bt + q] - base;  // bytes 0 .. hb are counted (hb <= 254)
+    const uint32_t r0 = sg * L, r1 = min(N, r0 + L);  // L % 256 == 0
+    const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);  // 16 rows per 16-B load (np % 32 == 0)
+    uint32_t* wh = wh_all[wv];
+    const uint32_t v0 = r0 / 16u, v1 = (r1 + 15u) / 16u;
+    constexpr uint32_t kU = 4;  // 16-B loads in flight per thread
+    for (uint32_t v = v0 + tid; v < v1; v += kSegThreads * kU) {
+        uint4 w[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t vv = v + kSegThreads * u;
+            w[u] = vv < v1 ? dq[vv] : make_uint4(~0u, ~0u, ~0u, ~0u);  // 255: never counted
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t vv = v + kSegThreads * u;
+            const uint32_t ws[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t b = (ws[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                if (b <= hb && 16u * vv + (uint32_t)j < r1) atomicAdd(&wh[b], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t* out = seg_hist + ((uint64_t)q * S + sg) * H + base;  // d-space bins base .. base + hb
+    for (uint32_t t = tid; t <= hb; t += kSegThreads) out[t] = wh_all[0][t] + wh_all[1][t] + wh_all[2][t] + wh_all[3][t];
+}
+
+__global__ __launch_bounds__(kBigThreads) void k_dense_rule8(const uint32_t* __restrict__ seg_hist, uint32_t S,
+                                                             uint32_t L, const uint8_t* __restrict__ dense,
+                                                             uint32_t np, uint32_t N, uint32_t D, uint32_t R,
+                                                             const uint32_t* __restrict__ qwin, uint32_t Bt,
+                                                             uint32_t* __restrict__ tcut,
+                                                             const uint32_t* __restrict__ gate) {
+    if (gate_closed(gate)) return;
+    __shared__ uint32_t hist[256];  // the window's bins (byte b = distance base + b)
+    __shared__ uint32_t s_T, s_lt, s_seg, s_left, s_cut, wsum[kBigThreads / 64];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, H = D + 1u;
+    const uint32_t base = qwin[q], hw = qwin[Bt + q] - base + 1u;  // bins 0 .. hw - 1
+    const uint32_t* sh = seg_hist + (uint64_t)q * S * H + base;
+    for (uint32_t t = tid; t < hw; t += kBigThreads) {
+        uint32_t c = 0u;
+        for (uint32_t sg = 0; sg < S; ++sg) c += sh[(uint64_t)sg * H + t];
+        hist[t] = c;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t t = wave_find_cum(hist, hw, R);
+        const uint32_t lt = wave_sum_below(hist, t);
+        if (tid == 0) {
+            s_T = t;
+            s_lt = lt;
+        }
+    }
+    __syncthreads();
+    const uint32_t tb = s_T, lt = s_lt;
+    // T strictly inside the window: cum(hi) reaches R, and byte 0 (d <= base) is exact or below T
+    if (lt + hist[tb] < R || (tb == 0u && base > 0u)) {
+        if (tid == 0) {
+            tcut[4u * q] = 0u;
+            tcut[4u * q + 1u] = 0u;
+            tcut[4u * q + 2u] = 0u;
+            tcut[4u * q + 3u] = kRuleInvalid;
+        }
+        return;
+    }
+    const uint32_t need = R - lt;
+    uint32_t cut = ~0u;
+    if (hist[tb] > need) {  // block-uniform: the segment holding the need-th tied row, and its rank there
+        if (tid == 0) {
+            uint32_t c = 0u, sg = 0u;
+            for (; sg + 1u < S; ++sg) {
+                const uint32_t w = sh[(uint64_t)sg * H + tb];
+                if (c + w >= need) break;
+                c += w;
+            }
+            s_seg = sg;
+            s_left = need - c;
+            s_cut = ~0u;
+        }
+        __syncthreads();
+        const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);
+        const uint32_t r0 = s_seg * L, r1 = min(N, r0 + L), left = s_left;
+        const uint32_t sv0 = r0 / 16u, sv1 = (r1 + 15u) / 16u;
+        uint32_t done = 0u;
+        for (uint32_t it = sv0; it < sv1; it += kBigThreads) {  // block-uniform rounds, rows in order
+            const uint32_t v = it + tid;
+            uint32_t tm = 0u;  // this thread's 16 rows tied at T
+            if (v < sv1) {
+                const uint4 w = dq[v];
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (16u * v + (uint32_t)j < r1 && ((ws[j >> 2] >> (8 * (j & 3))) & 0xffu) == tb) tm |= 1u << j;
+            }
+            uint32_t total;
+            const uint32_t excl = done + block_scan_u32((uint32_t)__popc(tm), wsum, &total);
+            const uint32_t cnt = (uint32_t)__popc(tm);
+            if (cnt && excl < left && left <= excl + cnt) {
+                uint32_t r = left - excl, bits = tm;
+                while (--r) bits &= bits - 1u;
+                s_cut = 16u * v + (uint32_t)__builtin_ctz(bits);
+            }
+            done += total;
+            if (done >= left) break;
+        }
+        __syncthreads();
+        cut = s_cut;
+    }
+    if (tid == 0) {
+        tcut[4u * q] = base + tb;
+        tcut[4u * q + 1u] = cut;
+        tcut[4u * q + 2u] = need;
+        tcut[4u * q + 3u] = 0u;
+    }
+}
+
+hipError_t launch_dense_base(const Stage1Args& a, hipStream_t s) {
+    if (a.B == 0) return hipSuccess;
+    if (!a.qwin || !a.qcodes || a.D >= 4096u) return hipErrorInvalidValue;
+    const char* sh = getenv("GVDB_DENSE8_SHIFT");
+    hipLaunchKernelGGL(k_dense_base, dim3(a.B), dim3(kBaseThreads), (size_t)(a.D + 1u) * 4u, s, a.codes, a.cap,
+                       code_w4(a.D), a.N, a.D, a.R, a.qcodes, a.B, a.qwin, sh ? atoi(sh) : 0, a.gate);
+    GVDB_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hipStream_t s) {
     if (bg == 0) return hipSuccess;
     if (a.R > a.N || !a.dense) return hipErrorInvalidValue;  // every list slot must be filled
+    if (a.dense8) {  // the byte form (rule only)
+        if (!a.seg_hist || !a.tcut || !a.qwin || a.mhist || a.dense_keep) return hipErrorInvalidValue;
+        const uint32_t H = a.D + 1u;
+        const uint8_t* dn = (const uint8_t*)a.dense;
+        uint32_t* sh = a.seg_hist + (uint64_t)g0 * a.seg_n * H;
+        hipLaunchKernelGGL(k_dense_seg_hist8, dim3(a.seg_n, bg), dim3(kSegThreads), 0, s, dn, a.dense_np, a.N, a.D,
+                           a.qwin + g0, a.B, a.seg_n, a.seg_len, sh, a.gate);
+        GVDB_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_dense_rule8, dim3(bg), dim3(kBigThreads), 0, s, sh, a.seg_n, a.seg_len, dn, a.dense_np,
+                           a.N, a.D, a.R, a.qwin + g0, a.B, a.tcut + 4ull * g0, a.gate);
+        GVDB_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     if (a.seg_hist && a.tcut) {  // the parallel rule form
         const uint32_t H = a.D + 1u;
         const uint16_t* dn = a.dense + (a.dense_keep ? (uint64_t)g0 * a.dense_np : 0ull);
@@ -546,6 +751,10 @@ __global__ __launch_bounds__(kCertThreads) void k_deep_certify(
     const uint32_t T = tcut[4u * q], cut = tcut[4u * q + 1u], need = tcut[4u * q + 2u];
     // 0: cut, 2: no tied member, 3: the tie rank counted in the member list (deep sharded phase 2)
     const uint32_t mode = tcut[4u * q + 3u];
+    if (mode == kRuleInvalid) {  // the byte form's window missed T: no rule, the batch takes the fallback
+        if (tid == 0) atomicOr(fail, 1u);
+        return;
+    }
     const bool lazy = mode == 3u && (m_rows || seg_hist);
     bool mem = false, tied = false;
     uint32_t row = 0u, d = 0u, o = ~0u;  // o: ascending = cosine descending

@@ -1509,7 +1509,7 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     // rerank of 64 (the i8 pass nominates by the K2-th score)
     const uint32_t K2 = k <= 16u ? 32u : kDeepK2;
     HIP_TRY(ws.qcodes.ensure((size_t)B * W4 * 16), "alloc qcodes");
-    HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 20 + 16), "alloc certified-depth lists");
+    HIP_TRY(ws.deep.ensure((size_t)B * K2 * 12 + (size_t)B * 28 + 32), "alloc certified-depth lists");
     if (!sync) {  // the gated fallback's buffers, sized before anything is enqueued (no reallocation under it)
         HIP_TRY(ws.s1_rows.ensure((size_t)B * R * 4), "alloc s1_rows");
         HIP_TRY(ws.s1_dist.ensure((size_t)B * R * 4), "alloc s1_dist");
@@ -1521,7 +1521,13 @@ static gvdb_status deep_cert_search(const gvdb_index* ix, const float* d_q, uint
     float* fsc = (float*)(p + (size_t)B * K2 * 8);
     uint32_t* tcut = (uint32_t*)(p + (size_t)B * K2 * 12);
     uint32_t* fn = tcut + 4ull * B;
-    uint32_t* dfail = fn + B;
+    uint32_t* dfail = fn + B;  // [4]: the certify word, the flat tier's word (async), 2 spare
+    // the byte form of the dense rule (GVDB_DENSE8=0: the f16 form): its windows after the words
+    {
+        const char* e8 = getenv("GVDB_DENSE8");
+        s1.dense8 = !(e8 && e8[0] == '0');
+    }
+    s1.qwin = dfail + 4;  // [2][B]
     s1.qf32 = d_q;  // k_qprep packs the query codes (the certify pass reads them)
     s1.qthr = ix->thr;
     s1.codes = ix->codes;

@@ -112,6 +112,9 @@ struct Stage1Args {
     int dense_keep;          // dense_sel: `dense` holds every query's row ([B][dense_np], caller memory) instead
                              // of one 256-query group's
     uint32_t* pc_out;        // optional, the parallel rule form: |q| per query [B] (kept for a later call)
+    int dense8;              // the parallel rule form only (tcut + seg_hist, no mhist / dense_keep): one byte
+    uint32_t* qwin;          //   per pair, clamp(d - base, 0, 255); qwin [2][B]: base[B] then hi[B], from
+                             //   k_dense_base (hi: the largest distance the histograms count); `dense` holds bytes
 };
 constexpr uint32_t kDenseSegs = 64;  // row segments of the parallel dense rule
 // S segments of L rows (L % 256 == 0) covering N rows, S <= min(smax, kDenseSegs)
@@ -127,6 +130,8 @@ constexpr uint32_t kBigRMax = 1u << 20;
 hipError_t launch_select_big(const Stage1Args& a, hipStream_t s);
 // dense_sel: the members of queries [g0, g0 + bg) from their dense f16 dots (gvdb_bigr.hip)
 hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hipStream_t s);
+// dense8: every query's byte window (base, hi) into a.qwin from a strided sample (gvdb_bigr.hip)
+hipError_t launch_dense_base(const Stage1Args& a, hipStream_t s);
 // certified default-depth search (gvdb_bigr.hip): the first min(k, R) members of the exact top-K2 cosine
 // list (rows + scores, (cos desc, row) order, fn[q] entries) under the membership rule tcut; fail[0] |= 1
 // for a query the list cannot certify

@@ -1054,7 +1054,11 @@ __device__ unsigned long long g_mx7_clk[4096][6];
 // four consecutive rows per 8-byte store; the select reads d = |q| - dot.
 // QT: query tiles of 32 per launch (8 = a full 256-query group; smaller batches take
 // 1 / 2 / 4 instead of multiplying padded slots: the MFMAs per row scale with QT).
-template <int W4, bool DENSE, int QT = 8>
+// D8 (with DENSE, round 6: the certified default depth's rule form): one BYTE per pair
+// instead of an f16 -- b = clamp(d - base[q], 0, 255) with the query's window base
+// passed in `thr` (k_dense_base) -- half the dense block's writes and its histogram
+// pass's reads; the rule (k_dense_rule8) checks that T lies strictly inside the window.
+template <int W4, bool DENSE, int QT = 8, bool D8 = false>
 __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const v4i_t* __restrict__ qfrag_g,
                                                            const uint32_t* __restrict__ qpc,
@@ -1123,7 +1127,9 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     if (tid < QT * 32) {
         const uint32_t q = tid;
         const uint32_t pc = qpc[q];
-        cq_lds[q] = DENSE ? 0.0f : q < B ? (float)pc - (float)min(thr[q], kPadBits) : 1.0e9f;
+        // D8: |q| - base (the byte of a pair is |q| - base - dot, clamped)
+        cq_lds[q] = DENSE ? (D8 && q < B ? (float)pc - (float)thr[q] : 0.0f)
+                          : q < B ? (float)pc - (float)min(thr[q], kPadBits) : 1.0e9f;
         pc_lds[q] = (float)pc;
         qcnt[q] = 0u;
     }
@@ -1193,7 +1199,41 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     // loop over the groups of 4 registers (4 consecutive rows) that hold a hit.
     // Register r holds row 8 (r / 4) + 4 h + (r % 4) of the sub-tile at n0.
     auto test = [&](const v16f_t& A, uint32_t qt, uint32_t n0) __attribute__((always_inline)) {
-        if constexpr (DENSE) {
+        if constexpr (DENSE && D8) {
+            // the tile's 32 x 32 bytes through the wave's LDS scratch ([query][4-row word],
+            // padded) so that lane L stores rows 16 (L & 1) .. +15 of query L / 2 as one
+            // 16-B store: 32-B segments per query and sub-tile
+            if (qt < nqt) {
+                constexpr uint32_t kLd = 9;  // u32 per query row of the scratch (8 + 1 pad)
+                uint32_t* tw = (uint32_t*)tscr[wv];
+                const uint32_t j = lane & 31u;
+                const float cb = cq[qt];  // |q| - base: the byte is cb - dot (an exact integer)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {  // rows 8g + 4h .. +3: word 2g + h
+                    uint32_t x = 0u;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        x = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(cb - A[4 * g + r], 0.0f, 255.0f),
+                                                           (uint32_t)r, x);
+                    tw[j * kLd + 2u * (uint32_t)g + h] = x;
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const uint32_t qo = lane >> 1, half = lane & 1u;
+                const uint32_t* src = tw + qo * kLd + 4u * half;
+                typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+                const u4v_t v0 = {src[0], src[1], src[2], src[3]};
+                const uint32_t qi = qt * 32u + qo;
+                if (qi < B) {
+                    typedef __attribute__((address_space(1))) u4v_t g_u4;
+                    g_u4* dst = (g_u4*)((uint8_t*)dense + (uint64_t)qi * dense_np + n0 + 16u * half);
+                    dst[0] = v0;
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            return;
+        } else if constexpr (DENSE) {
             // the tile's 32 x 32 f16 dots go through the wave's LDS scratch ([query][row
             // pair], padded rows) so that lane L stores rows 16 (L & 1) .. +15 of query
             // L / 2 as 32 contiguous bytes: 64-B segments per query instead of 8-B pieces
@@ -1560,13 +1600,16 @@ static hipError_t launch_scan_mx7_t(const Stage1Args& a, hipStream_t s) {
         // the query tiles this group needs (a batch of 64 pays 2 tiles' MFMAs, not 8)
         const uint32_t qt = bg <= 32u ? 1u : bg <= 64u ? 2u : bg <= 128u ? 4u : 8u;
         if (a.dense_sel) {  // every distance of the group, then its members (the dense block is reused per group)
-            auto kern = qt == 1 ? k_scan_mx7<W4, true, 1> : qt == 2 ? k_scan_mx7<W4, true, 2>
-                      : qt == 4 ? k_scan_mx7<W4, true, 4> : k_scan_mx7<W4, true, 8>;
+            auto kern = a.dense8 ? (qt == 1 ? k_scan_mx7<W4, true, 1, true> : qt == 2 ? k_scan_mx7<W4, true, 2, true>
+                                  : qt == 4 ? k_scan_mx7<W4, true, 4, true> : k_scan_mx7<W4, true, 8, true>)
+                                 : (qt == 1 ? k_scan_mx7<W4, true, 1> : qt == 2 ? k_scan_mx7<W4, true, 2>
+                                  : qt == 4 ? k_scan_mx7<W4, true, 4> : k_scan_mx7<W4, true, 8>);
             // few tiles: little MFMA work per code load, two blocks per CU keep more loads in flight
             uint16_t* dn = a.dense + (a.dense_keep ? (uint64_t)g * a.dense_np : 0ull);
+            // dense8: the window bases in the threshold slot
+            const uint32_t* th = a.dense8 ? a.qwin + g : a.thr + g;
             hipLaunchKernelGGL(kern, dim3(cu_count() * (qt <= 2u ? 2u : 1u)), dim3(kMx7Threads), 0, s, a.codes, a.cap,
-                               a.N, qf, a.qpc + g, a.thr + g, bg, a.counts + g, a.buf, a.bufcap, dn, a.dense_np,
-                               a.gate);
+                               a.N, qf, a.qpc + g, th, bg, a.counts + g, a.buf, a.bufcap, dn, a.dense_np, a.gate);
             GVDB_LAUNCH_CHECK();
             const hipError_t e = launch_select_dense(a, g, bg, s);
             if (e != hipSuccess) return e;
@@ -2639,8 +2682,9 @@ hipError_t launch_stage1_fast(const Stage1Args& a, hipStream_t s) {
     }
     if (a.dense_sel) {
         // no threshold: every distance is written and selected exactly (the scan below)
-        if (a.ev) (void)hipEventRecord(a.ev[1], s);
         hipError_t e = hipSuccess;
+        if (a.dense8 && (e = launch_dense_base(a, s)) != hipSuccess) return e;  // the byte windows
+        if (a.ev) (void)hipEventRecord(a.ev[1], s);
         switch (W4) {
             case 2: e = launch_scan_mx7_t<2>(a, s); break;
             case 3: e = launch_scan_mx7_t<3>(a, s); break;

@@ -139,6 +139,35 @@ def test_default_depth_device_gated_rerank(g, oracle_mod):
         assert (dn == k).all() and (di == ri[o:, :k]).all() and same_f32(ds, rs[o:, :k])
 
 
+@pytest.mark.parametrize("shift", [0, 300])
+def test_default_depth_device_byte_window(g, oracle_mod, monkeypatch, shift):
+    """The byte form of the dense rule through gvdb_index_search_device: with
+    the window on T the batch certifies on the device; with a window shifted
+    off T (GVDB_DENSE8_SHIFT) the rule reports no rule, k_deep_certify fails
+    the batch and the GATED rerank answers it -- no host sync either way, and
+    both equal the host form and the oracle."""
+    if shift:
+        monkeypatch.setenv("GVDB_DENSE8_SHIFT", str(shift))
+    N, D, B, k = 100_003, 768, 5, 10
+    x = rng_rows(821, N, D, dup=60)
+    Q = rng_rows(822, B, D)
+    Q[0] = x[N - 1]
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    sp = g.SearchParams(rescore_ratio=0.1)
+    c0 = counts(g)
+    di, ds, dn, busy = device_search_async(g, ix, Q, k, sp)
+    c1 = counts(g)
+    assert busy, "gvdb_index_search_device (default depth) waited for the stream"
+    assert (c1["cert"] - c0["cert"], c1["rerank"] - c0["rerank"]) == ((0, 2) if shift else (2, 0))
+    R = int(np.float32(N) * np.float32(0.1))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (dn == k).all() and (di == ri[:, :k]).all() and same_f32(ds, rs[:, :k])
+    assert di[0, 0] == N - 1
+    hi, hs, hn = ix.search_batch(Q, k, sp)
+    assert (hn == dn).all() and (hi == di).all() and same_f32(hs, ds)
+
+
 def test_bq_device_search_no_host_sync(g, oracle_mod):
     """BQ R = 100 (the bench's mode) at batch 256 and batch 1: no host sync."""
     N, D, k = 150_000, 768, 10

@@ -322,6 +322,37 @@ def test_default_depth_certificate_falls_back_to_rerank(g, oracle_mod):
     assert not planted & set(ids[:2].ravel().tolist())
 
 
+@pytest.mark.parametrize("form,shift,D", [("8", 0, 768), ("0", 0, 768), ("8", 0, 256), ("8", 300, 768),
+                                          ("8", -300, 768), ("8", 0, 200)])
+def test_default_depth_byte_rule_matches_oracle(g, oracle_mod, monkeypatch, form, shift, D):
+    """The certified default depth's dense rule in its byte form (round 6,
+    GVDB_DENSE8, default on: one byte per pair around a per-query window from
+    k_dense_base) and in the f16 form (GVDB_DENSE8=0): ids and cosine bits equal
+    the oracle, the batch certifies, duplicate rows make ties at T (the tie cut
+    comes from the bytes).  D = 256 / 200: the window starts at 0 (exact bytes).
+    A window shifted off T (GVDB_DENSE8_SHIFT = +-300: T below base, or above the
+    counted range) must not certify: the rule reports no rule, the batch takes
+    the B x R rerank, and the answer is still the oracle's."""
+    monkeypatch.setenv("GVDB_DENSE8", form)
+    if shift:
+        monkeypatch.setenv("GVDB_DENSE8_SHIFT", str(shift))
+    N, B, k = 131_077, 40, 10
+    x = rng_rows(N + D + 5, N, D, dup=400)
+    Q = rng_rows(D + 61, B, D)
+    Q[0] = x[N - 3]
+    Q[1] = x[(7 * 5 + 11) % N]  # a duplicated row: Hamming and cosine ties
+    ix = g.GpuVectorIndex(dimension=D, capacity_hint=N)
+    ix.add_batch(np.arange(N, dtype=np.uint64), x)
+    c0 = deep_cert_counts(g)
+    ids, sc, n = ix.search_batch(Q, k, g.SearchParams(rescore_ratio=0.1))
+    c1 = deep_cert_counts(g)
+    R = int(np.float32(N) * np.float32(0.1))
+    ri, rs = oracle_mod.multi_stage_search_batch_r(oracle_mod.quantize(Q), oracle_mod.quantize(x), Q, x, R)
+    assert (n == k).all() and (ids == ri[:, :k]).all() and same_f32(sc, rs[:, :k])
+    assert ids[0, 0] == N - 3
+    assert (c1[0] - c0[0], c1[1] - c0[1]) == ((0, 1) if shift else (1, 0))
+
+
 def test_dense_select_query_groups_match_oracle(g, oracle_mod):
     """Dense large-R stage 1 over more than one 256-query group (B = 300: the
     dense block is reused by the second group of 44 queries), D = 256."""
