@@ -1203,6 +1203,9 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
             // the tile's 32 x 32 bytes through the wave's LDS scratch ([query][4-row word],
             // padded) so that lane L stores rows 16 (L & 1) .. +15 of query L / 2 as one
             // 16-B store: 32-B segments per query and sub-tile
+#ifdef GVDB_D8_NOEPI
+            return;  // timing probe (variant builds only): the MFMA stream without the epilogue
+#endif
             if (qt < nqt) {
                 constexpr uint32_t kLd = 9;  // u32 per query row of the scratch (8 + 1 pad)
                 uint32_t* tw = (uint32_t*)tscr[wv];
@@ -1227,7 +1230,9 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
                 if (qi < B) {
                     typedef __attribute__((address_space(1))) u4v_t g_u4;
                     g_u4* dst = (g_u4*)((uint8_t*)dense + (uint64_t)qi * dense_np + n0 + 16u * half);
+#ifndef GVDB_D8_NOSTORE  // timing probe (variant builds only): the epilogue without its stores
                     dst[0] = v0;
+#endif
                 }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
