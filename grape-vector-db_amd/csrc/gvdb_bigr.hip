@@ -488,8 +488,8 @@ void dense_segments(uint32_t N, uint32_t smax, uint32_t* S, uint32_t* L) {
 // 256 at 10M rows) was written by the scan at ~2.5 TB/s and read back by the segment
 // histograms: 3 of the 5.7 ms step.  The rule only needs the distances near T, so a
 // pair is stored as one byte b = clamp(d - base, 0, 255) around a per-query window:
-//   k_dense_base      one block per query: the Hamming histogram of an 8192-row strided
-//                     sample, its quantile at R / N -> t_est; base = t_est - 127 (>= 0),
+//   k_dense_base      one block per query: the Hamming histogram of an 8192-row sample (64
+//                     spread chunks of 128 consecutive rows), its quantile at R / N -> t_est; base = t_est - 127 (>= 0),
 //                     hi = the sample's quantile at target + 6 sqrt(target) + 16 (at least
 //                     t_est + 2, at most base + 254): the histograms count d <= hi only;
 //   k_dense_seg_hist8 the segment histograms over bytes <= hi - base (d-space bins
@@ -499,25 +499,43 @@ void dense_segments(uint32_t N, uint32_t smax, uint32_t* S, uint32_t* L) {
 //                     below base share byte 0) -- rule mode 5: k_deep_certify then fails
 //                     the batch and the exact fallback (gated bq_search) answers it.
 // Exact whenever it certifies: inside the window every byte is d - base exactly.
-constexpr uint32_t kBaseThreads = 256;
-constexpr uint32_t kBaseSample = 8192;
-constexpr uint32_t kRuleInvalid = 5u;  // tcut mode: no rule (the window missed T)
-__global__ __launch_bounds__(kBaseThreads) void k_dense_base(const uint4* __restrict__ codes, uint64_t cap,
-                                                             uint32_t W4, uint32_t N, uint32_t D, uint32_t R,
-                                                             const uint4* __restrict__ qcodes, uint32_t B,
-                                                             uint32_t* __restrict__ qwin, int shift,
+constexpr uint32_t kBaseThreads = 1024;
+constexpr uint32_t kBaseSample = 8192;  // 64 chunks of 128 consecutive rows (coalesced plane loads)
+constexpr uint32_t kRuleInvalid = 5u;   // tcut mode: no rule (the window missed T)
+template <int W4>
+__global__ __launch_bounds__(kBaseThreads) void k_dense_base(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
+                                                             uint32_t D, uint32_t R, const uint4* __restrict__ qcodes,
+                                                             uint32_t B, uint32_t* __restrict__ qwin, int shift,
                                                              const uint32_t* __restrict__ gate) {
     if (gate_closed(gate)) return;
     extern __shared__ uint32_t hist[];  // [D + 1]
     const uint32_t q = blockIdx.x, tid = threadIdx.x, H = D + 1u;
     for (uint32_t t = tid; t < H; t += kBaseThreads) hist[t] = 0u;
+    uint4 qc[W4];
+#pragma unroll
+    for (int p = 0; p < W4; ++p) qc[p] = qcodes[(uint64_t)q * W4 + p];
     __syncthreads();
     const uint32_t S = min(N, kBaseSample);  // N <= S: every row (t_est = T)
-    const uint4* qc = qcodes + (uint64_t)q * W4;
-    for (uint32_t i = tid; i < S; i += kBaseThreads) {
-        const uint64_t n = (uint64_t)i * N / S;
-        atomicAdd(&hist[min(big_dist(codes, cap, W4, qc, n), D)], 1u);
+    constexpr uint32_t kPer = kBaseSample / kBaseThreads;
+    uint32_t dv[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {  // every load of the thread in flight together
+        const uint32_t i = tid + k * kBaseThreads;
+        const uint32_t n = N <= kBaseSample ? min(i, N - 1u)
+                                            : (uint32_t)((uint64_t)(i >> 7) * (N - 128u) / 63u) + (i & 127u);
+        uint4 c[W4];
+#pragma unroll
+        for (int p = 0; p < W4; ++p) c[p] = codes[(uint64_t)p * cap + n];
+        uint32_t d = 0;
+#pragma unroll
+        for (int p = 0; p < W4; ++p)
+            d += __popc(c[p].x ^ qc[p].x) + __popc(c[p].y ^ qc[p].y) + __popc(c[p].z ^ qc[p].z) +
+                 __popc(c[p].w ^ qc[p].w);
+        dv[k] = d;
     }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k)
+        if (tid + k * kBaseThreads < S) atomicAdd(&hist[min(dv[k], D)], 1u);
     __syncthreads();
     if (tid < 64u) {
         const uint32_t target = max(1u, (uint32_t)(((uint64_t)R * S + N - 1u) / N));
@@ -534,7 +552,12 @@ __global__ __launch_bounds__(kBaseThreads) void k_dense_base(const uint4* __rest
     }
 }
 
-__global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* __restrict__ dense, uint32_t np,
+// the blocked byte layout (k_scan_mx7<..., D8>): rows 16v .. 16v + 15 of query q as one uint4
+__device__ __forceinline__ const uint4* d8_at(const uint8_t* dense, uint32_t bg, uint32_t q, uint32_t v) {
+    return (const uint4*)(dense + ((uint64_t)(v >> 4) * bg + q) * 256u + 16u * (v & 15u));
+}
+
+__global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* __restrict__ dense, uint32_t bg,
                                                                  uint32_t N, uint32_t D,
                                                                  const uint32_t* __restrict__ qwin, uint32_t Bt,
                                                                  uint32_t S, uint32_t L,
@@ -542,13 +565,13 @@ __global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* 
                                                                  const uint32_t* __restrict__ gate) {
     if (gate_closed(gate)) return;
     __shared__ uint32_t wh_all[4][256];  // one histogram of bytes per wave
-    const uint32_t sg = blockIdx.x, q = blockIdx.y, tid = threadIdx.x, H = D + 1u;
+    // grid (query, segment): consecutive blocks read neighbouring 256-B pieces of one region
+    const uint32_t q = blockIdx.x, sg = blockIdx.y, tid = threadIdx.x, H = D + 1u;
     const uint32_t wv = tid >> 6;
     for (uint32_t i = tid; i < 4u * 256u; i += kSegThreads) (&wh_all[0][0])[i] = 0u;
     __syncthreads();
     const uint32_t base = qwin[q], hb = qwin[Bt + q] - base;  // bytes 0 .. hb are counted (hb <= 254)
     const uint32_t r0 = sg * L, r1 = min(N, r0 + L);  // L % 256 == 0
-    const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);  // 16 rows per 16-B load (np % 32 == 0)
     uint32_t* wh = wh_all[wv];
     const uint32_t v0 = r0 / 16u, v1 = (r1 + 15u) / 16u;
     constexpr uint32_t kU = 4;  // 16-B loads in flight per thread
@@ -557,7 +580,7 @@ __global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* 
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
             const uint32_t vv = v + kSegThreads * u;
-            w[u] = vv < v1 ? dq[vv] : make_uint4(~0u, ~0u, ~0u, ~0u);  // 255: never counted
+            w[u] = vv < v1 ? *d8_at(dense, bg, q, vv) : make_uint4(~0u, ~0u, ~0u, ~0u);  // 255: never counted
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
@@ -577,7 +600,7 @@ __global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* 
 
 __global__ __launch_bounds__(kBigThreads) void k_dense_rule8(const uint32_t* __restrict__ seg_hist, uint32_t S,
                                                              uint32_t L, const uint8_t* __restrict__ dense,
-                                                             uint32_t np, uint32_t N, uint32_t D, uint32_t R,
+                                                             uint32_t bg, uint32_t N, uint32_t D, uint32_t R,
                                                              const uint32_t* __restrict__ qwin, uint32_t Bt,
                                                              uint32_t* __restrict__ tcut,
                                                              const uint32_t* __restrict__ gate) {
@@ -628,7 +651,6 @@ __global__ __launch_bounds__(kBigThreads) void k_dense_rule8(const uint32_t* __r
             s_cut = ~0u;
         }
         __syncthreads();
-        const uint4* dq = (const uint4*)(dense + (uint64_t)q * np);
         const uint32_t r0 = s_seg * L, r1 = min(N, r0 + L), left = s_left;
         const uint32_t sv0 = r0 / 16u, sv1 = (r1 + 15u) / 16u;
         uint32_t done = 0u;
@@ -636,7 +658,7 @@ __global__ __launch_bounds__(kBigThreads) void k_dense_rule8(const uint32_t* __r
             const uint32_t v = it + tid;
             uint32_t tm = 0u;  // this thread's 16 rows tied at T
             if (v < sv1) {
-                const uint4 w = dq[v];
+                const uint4 w = *d8_at(dense, bg, q, v);
                 const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
@@ -668,8 +690,12 @@ hipError_t launch_dense_base(const Stage1Args& a, hipStream_t s) {
     if (a.B == 0) return hipSuccess;
     if (!a.qwin || !a.qcodes || a.D >= 4096u) return hipErrorInvalidValue;
     const char* sh = getenv("GVDB_DENSE8_SHIFT");
-    hipLaunchKernelGGL(k_dense_base, dim3(a.B), dim3(kBaseThreads), (size_t)(a.D + 1u) * 4u, s, a.codes, a.cap,
-                       code_w4(a.D), a.N, a.D, a.R, a.qcodes, a.B, a.qwin, sh ? atoi(sh) : 0, a.gate);
+    const int shift = sh ? atoi(sh) : 0;
+    const uint32_t W4 = code_w4(a.D);
+    auto kern = W4 == 2 ? k_dense_base<2> : W4 == 3 ? k_dense_base<3> : W4 == 4 ? k_dense_base<4> : k_dense_base<6>;
+    if (W4 != 2 && W4 != 3 && W4 != 4 && W4 != 6) return hipErrorInvalidValue;  // the FP4 scan's widths
+    hipLaunchKernelGGL(kern, dim3(a.B), dim3(kBaseThreads), (size_t)(a.D + 1u) * 4u, s, a.codes, a.cap, a.N, a.D,
+                       a.R, a.qcodes, a.B, a.qwin, shift, a.gate);
     GVDB_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -682,11 +708,12 @@ hipError_t launch_select_dense(const Stage1Args& a, uint32_t g0, uint32_t bg, hi
         const uint32_t H = a.D + 1u;
         const uint8_t* dn = (const uint8_t*)a.dense;
         uint32_t* sh = a.seg_hist + (uint64_t)g0 * a.seg_n * H;
-        hipLaunchKernelGGL(k_dense_seg_hist8, dim3(a.seg_n, bg), dim3(kSegThreads), 0, s, dn, a.dense_np, a.N, a.D,
+        if (a.seg_len % 256u) return hipErrorInvalidValue;  // segments of whole 256-row regions
+        hipLaunchKernelGGL(k_dense_seg_hist8, dim3(bg, a.seg_n), dim3(kSegThreads), 0, s, dn, bg, a.N, a.D,
                            a.qwin + g0, a.B, a.seg_n, a.seg_len, sh, a.gate);
         GVDB_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_dense_rule8, dim3(bg), dim3(kBigThreads), 0, s, sh, a.seg_n, a.seg_len, dn, a.dense_np,
-                           a.N, a.D, a.R, a.qwin + g0, a.B, a.tcut + 4ull * g0, a.gate);
+        hipLaunchKernelGGL(k_dense_rule8, dim3(bg), dim3(kBigThreads), 0, s, sh, a.seg_n, a.seg_len, dn, bg, a.N, a.D,
+                           a.R, a.qwin + g0, a.B, a.tcut + 4ull * g0, a.gate);
         GVDB_LAUNCH_CHECK();
         return hipSuccess;
     }

@@ -1058,6 +1058,7 @@ __device__ unsigned long long g_mx7_clk[4096][6];
 // instead of an f16 -- b = clamp(d - base[q], 0, 255) with the query's window base
 // passed in `thr` (k_dense_base) -- half the dense block's writes and its histogram
 // pass's reads; the rule (k_dense_rule8) checks that T lies strictly inside the window.
+// The bytes are BLOCKED: pair (q, n) at ((n / 256) * B + q) * 256 + n % 256.
 template <int W4, bool DENSE, int QT = 8, bool D8 = false>
 __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const v4i_t* __restrict__ qfrag_g,
@@ -1229,7 +1230,10 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
                 const uint32_t qi = qt * 32u + qo;
                 if (qi < B) {
                     typedef __attribute__((address_space(1))) u4v_t g_u4;
-                    g_u4* dst = (g_u4*)((uint8_t*)dense + (uint64_t)qi * dense_np + n0 + 16u * half);
+                    // blocked layout [row / 256][query][row % 256]: a block's 8 consecutive sub-tiles
+                    // fill one 64-KiB region (B = 256) instead of 256 pieces np bytes apart
+                    g_u4* dst = (g_u4*)((uint8_t*)dense + ((uint64_t)(n0 >> 8) * B + qi) * 256u + (n0 & 255u) +
+                                        16u * half);
 #ifndef GVDB_D8_NOSTORE  // timing probe (variant builds only): the epilogue without its stores
                     dst[0] = v0;
 #endif
