@@ -772,11 +772,18 @@ def deep_rooflines(L, ix, q, k, n_local, D):
     if sn:
         ms = sm / sn
         groups = -(-B // 256)
-        wr = 256 * groups * (-(-n_local // 32) * 32) * 2  # the f16 dot block
+        byte_form = os.environ.get("GVDB_DENSE8", "1") != "0"  # round 6: one byte per pair
+        if byte_form:
+            wr = B * n_local  # the byte block: clamp(d - base, 0, 255) per (query, row)
+        else:
+            wr = 256 * groups * (-(-n_local // 32) * 32) * 2  # the f16 dot block
         rd = n_local * w4 * 16 * groups + wr  # the codes, and the block again by the rule's segment histograms
         ops = float(n_local) * 256 * groups * w4 * 128 * 2
         out["dense_scan"] = {
-            "kernel": "dense stage 1: k_scan_mx7<DENSE> (every FP4-MFMA Hamming dot of the 256-slot tile stored as "
+            "kernel": ("dense stage 1, byte form: k_dense_base (per-query window) + k_scan_mx7<DENSE, D8> (every "
+                       "FP4-MFMA Hamming distance stored as one byte around the window) + the rule over that block "
+                       "(k_dense_seg_hist8, k_dense_rule8)") if byte_form else
+                      "dense stage 1: k_scan_mx7<DENSE> (every FP4-MFMA Hamming dot of the 256-slot tile stored as "
                       "f16) + the membership rule over that block (k_dense_seg_hist, k_dense_rule)",
             "bound": "hbm", "achieved": (rd + wr) / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": (rd + wr) / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None, "avg_launch_ms": ms,
