@@ -552,10 +552,12 @@ __global__ __launch_bounds__(kBaseThreads) void k_dense_base(const uint4* __rest
     }
 }
 
-// the blocked byte layout (k_scan_mx7<..., D8>): rows 16v .. 16v + 15 of query q as one uint4
+// the blocked byte layout (k_scan_mx7<..., D8>): unit v = half v & 1 of sub-tile v / 2 of query q
+// as one uint4; its byte j is row 32 (v / 2) + d8_row(v & 1, j)
 __device__ __forceinline__ const uint4* d8_at(const uint8_t* dense, uint32_t bg, uint32_t q, uint32_t v) {
     return (const uint4*)(dense + ((uint64_t)(v >> 4) * bg + q) * 256u + 16u * (v & 15u));
 }
+__device__ __forceinline__ uint32_t d8_row(uint32_t h, uint32_t j) { return 8u * (j >> 2) + 4u * h + (j & 3u); }
 
 __global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* __restrict__ dense, uint32_t bg,
                                                                  uint32_t N, uint32_t D,
@@ -573,7 +575,8 @@ __global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* 
     const uint32_t base = qwin[q], hb = qwin[Bt + q] - base;  // bytes 0 .. hb are counted (hb <= 254)
     const uint32_t r0 = sg * L, r1 = min(N, r0 + L);  // L % 256 == 0
     uint32_t* wh = wh_all[wv];
-    const uint32_t v0 = r0 / 16u, v1 = (r1 + 15u) / 16u;
+    // 16-byte units of whole sub-tiles (a sub-tile's two units interleave its rows)
+    const uint32_t v0 = r0 / 16u, v1 = 2u * ((r1 + 31u) / 32u);
     constexpr uint32_t kU = 4;  // 16-B loads in flight per thread
     for (uint32_t v = v0 + tid; v < v1; v += kSegThreads * kU) {
         uint4 w[kU];
@@ -589,7 +592,7 @@ __global__ __launch_bounds__(kSegThreads) void k_dense_seg_hist8(const uint8_t* 
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const uint32_t b = (ws[j >> 2] >> (8 * (j & 3))) & 0xffu;
-                if (b <= hb && 16u * vv + (uint32_t)j < r1) atomicAdd(&wh[b], 1u);
+                if (b <= hb && 32u * (vv >> 1) + d8_row(vv & 1u, (uint32_t)j) < r1) atomicAdd(&wh[b], 1u);
             }
         }
     }
@@ -652,17 +655,22 @@ __global__ __launch_bounds__(kBigThreads) void k_dense_rule8(const uint32_t* __r
         }
         __syncthreads();
         const uint32_t r0 = s_seg * L, r1 = min(N, r0 + L), left = s_left;
-        const uint32_t sv0 = r0 / 16u, sv1 = (r1 + 15u) / 16u;
+        const uint32_t st0 = r0 / 32u, st1 = (r1 + 31u) / 32u;  // sub-tiles: one per thread per round
         uint32_t done = 0u;
-        for (uint32_t it = sv0; it < sv1; it += kBigThreads) {  // block-uniform rounds, rows in order
-            const uint32_t v = it + tid;
-            uint32_t tm = 0u;  // this thread's 16 rows tied at T
-            if (v < sv1) {
-                const uint4 w = *d8_at(dense, bg, q, v);
-                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        for (uint32_t it = st0; it < st1; it += kBigThreads) {  // block-uniform rounds, rows in order
+            const uint32_t t = it + tid;
+            uint32_t tm = 0u;  // this thread's 32 rows tied at T, bit = row within the sub-tile
+            if (t < st1) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (16u * v + (uint32_t)j < r1 && ((ws[j >> 2] >> (8 * (j & 3))) & 0xffu) == tb) tm |= 1u << j;
+                for (uint32_t hh = 0; hh < 2; ++hh) {
+                    const uint4 w = *d8_at(dense, bg, q, 2u * t + hh);
+                    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const uint32_t rr = d8_row(hh, (uint32_t)j);
+                        if (32u * t + rr < r1 && ((ws[j >> 2] >> (8 * (j & 3))) & 0xffu) == tb) tm |= 1u << rr;
+                    }
+                }
             }
             uint32_t total;
             const uint32_t excl = done + block_scan_u32((uint32_t)__popc(tm), wsum, &total);
@@ -670,7 +678,7 @@ __global__ __launch_bounds__(kBigThreads) void k_dense_rule8(const uint32_t* __r
             if (cnt && excl < left && left <= excl + cnt) {
                 uint32_t r = left - excl, bits = tm;
                 while (--r) bits &= bits - 1u;
-                s_cut = 16u * v + (uint32_t)__builtin_ctz(bits);
+                s_cut = 32u * t + (uint32_t)__builtin_ctz(bits);
             }
             done += total;
             if (done >= left) break;

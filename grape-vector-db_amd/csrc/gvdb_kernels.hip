@@ -1058,7 +1058,8 @@ __device__ unsigned long long g_mx7_clk[4096][6];
 // instead of an f16 -- b = clamp(d - base[q], 0, 255) with the query's window base
 // passed in `thr` (k_dense_base) -- half the dense block's writes and its histogram
 // pass's reads; the rule (k_dense_rule8) checks that T lies strictly inside the window.
-// The bytes are BLOCKED: pair (q, n) at ((n / 256) * B + q) * 256 + n % 256.
+// The bytes are BLOCKED: pair (q, n) at ((n / 256) * B + q) * 256 + 32 (n % 256 / 32) + the
+// position of row n % 32 within its sub-tile (16 h + 4 g + r for row 8 g + 4 h + r).
 template <int W4, bool DENSE, int QT = 8, bool D8 = false>
 __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __restrict__ codes, uint64_t cap, uint32_t N,
                                                            const v4i_t* __restrict__ qfrag_g,
@@ -1201,45 +1202,35 @@ __global__ __launch_bounds__(kMx7Threads, 1) void k_scan_mx7(const uint4* __rest
     // Register r holds row 8 (r / 4) + 4 h + (r % 4) of the sub-tile at n0.
     auto test = [&](const v16f_t& A, uint32_t qt, uint32_t n0) __attribute__((always_inline)) {
         if constexpr (DENSE && D8) {
-            // the tile's 32 x 32 bytes through the wave's LDS scratch ([query][4-row word],
-            // padded) so that lane L stores rows 16 (L & 1) .. +15 of query L / 2 as one
-            // 16-B store: 32-B segments per query and sub-tile
+            // no transpose: within each 32-row sub-tile the bytes are stored PERMUTED --
+            // position 16 h + 4 g + r holds row 8 g + 4 h + r (register 4 g + r of lane half h)
+            // -- so a lane's 16 bytes (one query) are one contiguous 16-B store, with no LDS
+            // round trip or wave barrier in the MFMA stream; the readers (k_dense_seg_hist8,
+            // k_dense_rule8) undo the permutation
 #ifdef GVDB_D8_NOEPI
             return;  // timing probe (variant builds only): the MFMA stream without the epilogue
 #endif
-            if (qt < nqt) {
-                constexpr uint32_t kLd = 9;  // u32 per query row of the scratch (8 + 1 pad)
-                uint32_t* tw = (uint32_t*)tscr[wv];
-                const uint32_t j = lane & 31u;
+            const uint32_t qi = qt * 32u + (lane & 31u);
+            if (qt < nqt && qi < B) {
                 const float cb = cq[qt];  // |q| - base: the byte is cb - dot (an exact integer)
+                typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+                u4v_t v0;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {  // rows 8g + 4h .. +3: word 2g + h
+                for (int g = 0; g < 4; ++g) {  // word g: rows 8g + 4h .. +3
                     uint32_t x = 0u;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
                         x = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(cb - A[4 * g + r], 0.0f, 255.0f),
                                                            (uint32_t)r, x);
-                    tw[j * kLd + 2u * (uint32_t)g + h] = x;
+                    v0[g] = x;
                 }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                const uint32_t qo = lane >> 1, half = lane & 1u;
-                const uint32_t* src = tw + qo * kLd + 4u * half;
-                typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
-                const u4v_t v0 = {src[0], src[1], src[2], src[3]};
-                const uint32_t qi = qt * 32u + qo;
-                if (qi < B) {
-                    typedef __attribute__((address_space(1))) u4v_t g_u4;
-                    // blocked layout [row / 256][query][row % 256]: a block's 8 consecutive sub-tiles
-                    // fill one 64-KiB region (B = 256) instead of 256 pieces np bytes apart
-                    g_u4* dst = (g_u4*)((uint8_t*)dense + ((uint64_t)(n0 >> 8) * B + qi) * 256u + (n0 & 255u) +
-                                        16u * half);
+                typedef __attribute__((address_space(1))) u4v_t g_u4;
+                // blocked layout [row / 256][query][row % 256 (permuted per sub-tile)]: a block's 8
+                // consecutive sub-tiles fill one 64-KiB region (B = 256)
+                g_u4* dst = (g_u4*)((uint8_t*)dense + ((uint64_t)(n0 >> 8) * B + qi) * 256u + (n0 & 255u) + 16u * h);
 #ifndef GVDB_D8_NOSTORE  // timing probe (variant builds only): the epilogue without its stores
-                    dst[0] = v0;
+                dst[0] = v0;
 #endif
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
             return;
         } else if constexpr (DENSE) {
